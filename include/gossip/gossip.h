@@ -1,0 +1,188 @@
+/*
+ * gossip.h -- C-ABI of libgossip_hip, the MI355X (gfx950) gossip-propagation
+ * engine.  This is the drop-in boundary for the reference's hot path:
+ * plain C types, caller-owned host buffers, no C++ types, never throws.
+ *
+ * Each entry point replaces one piece of the reference's per-process,
+ * thread-per-connection C++ (PareenShah27/P2P-GossipProtocol @ 2025-02-25;
+ * file:line below).  One gossip_ctx simulates ALL peers of one vertex
+ * partition: a reference PeerNode becomes a peer id inside the ctx.
+ *
+ * Threading: a ctx is single-caller-thread.  Device work is issued on the
+ * ctx's HIP stream (its own, or the one given to gossip_set_stream).
+ * Errors: every call returns gossip_status (0 = OK, < 0 = error);
+ * gossip_last_error() gives the message of the last failure on this thread.
+ */
+#ifndef GOSSIP_GOSSIP_H
+#define GOSSIP_GOSSIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct gossip_ctx gossip_ctx;
+typedef int gossip_status;
+
+#define GOSSIP_OK 0
+#define GOSSIP_EINVAL (-1)  /* bad argument */
+#define GOSSIP_ENOMEM (-2)  /* host or device allocation failed */
+#define GOSSIP_EHIP (-3)    /* HIP runtime error */
+#define GOSSIP_ESTATE (-4)  /* call out of order (e.g. step before graph) */
+#define GOSSIP_ENODEV (-5)  /* no gfx950 device visible */
+#define GOSSIP_EOVERFLOW (-6) /* report buffer overflowed (reports dropped) */
+
+/* Overlay models. */
+#define GOSSIP_GRAPH_POWERLAW 1      /* scale overlay: power-law pick (peer.cpp:219-222), skewed
+                                        candidates, symmetrised */
+#define GOSSIP_GRAPH_REF_BOOTSTRAP 2 /* literal bootstrap DAG (peer.cpp:63-72,214-253; seed.cpp:117), n <= 4096 */
+
+/* gossip_config.flags */
+#define GOSSIP_FLAG_COVERAGE_HISTORY 1u /* keep per-message coverage for every round */
+
+/*
+ * Replaces: NetworkConfig's parsed values (config.cpp:31-42,93-96) plus the
+ * constants PeerNode hard-codes (peer.cpp:219,330,337,353,358,377).
+ */
+typedef struct gossip_config {
+    uint64_t n_peers;         /* global peer count (< 2^31) */
+    uint64_t part_begin;      /* owned peer range [part_begin, part_end); both 0 = all */
+    uint64_t part_end;
+    uint32_t n_msgs;          /* M concurrent messages; W = ceil(M/64) 64-bit words per peer (M <= 512) */
+    uint32_t rng_seed;        /* Philox key word 0 (overlay, churn, origins) */
+    uint32_t graph_model;     /* GOSSIP_GRAPH_* */
+    uint32_t list_len;        /* powerlaw: candidates per seed response (default 6) */
+    uint32_t n_seeds;         /* ref_bootstrap: seeds in network.txt (quorum = n_seeds/2+1) */
+    uint32_t churn_threshold; /* peer dies in round r iff philox.x < threshold; 0 = none */
+    uint32_t ping_every;      /* liveness every k rounds (ping_interval gate, peer.cpp:329-330); 0 = none */
+    uint32_t max_missed;      /* max_missed_pings (peer.cpp:337); default 3 */
+    uint32_t max_rounds;      /* hard stop (default 4096) */
+    uint32_t min_rounds;      /* run at least this many rounds (liveness demos) */
+    int32_t device;           /* HIP device ordinal; -1 = current */
+    uint32_t flags;           /* GOSSIP_FLAG_* */
+    uint64_t report_capacity; /* dead-node report buffer entries (0 = default) */
+} gossip_config;
+
+/*
+ * One round's statistics.  Replaces the observable side effects of one hop
+ * of broadcastMessage (peer.cpp:310-316: a successful send adds to
+ * MessageTracker.sentTo) and handleClient (peer.cpp:277-285: new message ->
+ * "Received new message", duplicate -> dropped).
+ */
+typedef struct gossip_round_stats {
+    uint32_t round;
+    uint32_t flags;         /* bit0: liveness (ping) round */
+    uint64_t frontier;      /* peers with new messages at push start */
+    uint64_t traversals;    /* live out-edges scanned from the frontier */
+    uint64_t deliveries;    /* sum popcount(new[u]) over traversed edges with alive target (= sentTo inserts) */
+    uint64_t undelivered;   /* same for dead targets (send attempted, peer.cpp:312 fails) */
+    uint64_t new_receipts;  /* (peer, message) pairs received for the first time */
+    uint64_t duplicates;    /* deliveries - new_receipts (dropped by the Message-List check) */
+    uint64_t injected;      /* messages generated this round (messageGenerationLoop) */
+    uint64_t died;          /* peers that died this round */
+    uint64_t reports;       /* dead-node reports emitted this round */
+    uint64_t seed_removals; /* seed-registry entries removed (first report of a peer) */
+    uint64_t digest;        /* sum_v,w g(v*W+w) * seen[v][w] mod 2^64 at push start */
+    uint64_t covered;       /* sum popcount(seen) at push start */
+} gossip_round_stats;
+
+/* A dead-node report: reporter u detected dead peer v in round r
+ * (handleDeadPeer peer.cpp:381-397 -> the seed's dead_node handler seed.cpp:130-138). */
+typedef struct gossip_dead_report {
+    uint32_t round;
+    uint32_t reporter;
+    uint32_t dead;
+} gossip_dead_report;
+
+/* ---- lifecycle ---------------------------------------------------------- */
+/* Replaces PeerNode::PeerNode (peer.cpp:19-22) for all peers of a partition. */
+gossip_status gossip_create(const gossip_config* cfg, gossip_ctx** out);
+/* Replaces PeerNode::~PeerNode / stop (peer.cpp:24-26,106-123). */
+void gossip_destroy(gossip_ctx* ctx);
+const char* gossip_strerror(gossip_status s);
+const char* gossip_last_error(void);
+/* Sets the HIP stream (hipStream_t passed as void*) the ctx issues work on. */
+gossip_status gossip_set_stream(gossip_ctx* ctx, void* hip_stream);
+/* Shape: W = ceil(M/64) words per peer in host buffers; exchange_words = the
+ * (padded) words per peer of the device exchange buffers; owned peers; edges. */
+gossip_status gossip_get_shape(gossip_ctx* ctx, uint32_t* words, uint32_t* exchange_words, uint64_t* n_local,
+                               uint64_t* n_edges);
+
+/* ---- overlay ------------------------------------------------------------ */
+/* Replaces the seed bootstrap + selectAndConnectPeers (peer.cpp:63-72,161-253;
+ * seed.cpp:109-129,153-178): builds the CSR overlay of the owned rows on the
+ * device (Philox-keyed, deterministic). */
+gossip_status gossip_build_graph(gossip_ctx* ctx);
+/* Loads a caller-built CSR of the owned rows (row_ptr[n_local+1] local offsets,
+ * col[n_edges] global ids, rows sorted, no self loops).  Copied; caller keeps ownership. */
+gossip_status gossip_load_csr(gossip_ctx* ctx, const uint64_t* row_ptr, const uint32_t* col, uint64_t n_rows,
+                              uint64_t n_edges);
+/* Copies the owned CSR back (row_ptr: n_local+1, col: n_edges; masked edges have bit 31 set). */
+gossip_status gossip_read_csr(gossip_ctx* ctx, uint64_t* row_ptr, uint32_t* col);
+
+/* ---- schedule ------------------------------------------------------------ */
+/* Replaces messageGenerationLoop (peer.cpp:357-379): message m (msgNumber of
+ * origin[m]) is generated by origin[m] in round inject_round[m]. n_msgs == cfg.n_msgs. */
+gossip_status gossip_inject(gossip_ctx* ctx, const uint32_t* origin, const uint32_t* inject_round, uint32_t n_msgs);
+/* Fault injection (README.md:6 "Ctrl+C to kill any peer"): peer kill_peer[i] dies in kill_round[i]. */
+gossip_status gossip_schedule_kills(gossip_ctx* ctx, const uint32_t* kill_peer, const uint32_t* kill_round,
+                                    uint32_t n_kills);
+/* Philox-chosen distinct origins (host helper; same draw on every rank). */
+gossip_status gossip_pick_origins(uint64_t n_peers, uint32_t rng_seed, uint32_t count, uint32_t* out);
+
+/* ---- rounds (single partition) ------------------------------------------ */
+/* Clears all dynamic state (seen/new, alive, edge masks, miss counters,
+ * registry, reports) back to round 0; keeps overlay and schedule. */
+gossip_status gossip_reset(gossip_ctx* ctx);
+/* One round: churn -> liveness (if due) -> injection -> push -> advance.
+ * Returns 1 when the run is finished after this round, 0 if not, < 0 on error. */
+gossip_status gossip_step(gossip_ctx* ctx, gossip_round_stats* out);
+/* Steps until finished or max_rounds; per_round (may be NULL) receives up to cap entries. */
+gossip_status gossip_run(gossip_ctx* ctx, gossip_round_stats* per_round, uint32_t cap, uint32_t* rounds);
+
+/* ---- rounds (vertex-partitioned, one process per GPU) --------------------- */
+/* The caller owns the exchange: send = device buffer of n_peers*X u64 (dense,
+ * indexed by global peer; X = exchange_words of gossip_get_shape), recv =
+ * device buffer of world*n_local*X u64 (rank p's slice for this partition at
+ * offset p*n_local*X).
+ * Per round: gossip_round_push -> all-to-all(send slices -> recv) -> gossip_round_finish
+ * -> all-reduce of the stats -> gossip_round_commit(new_receipts_global). */
+gossip_status gossip_set_exchange(gossip_ctx* ctx, void* send_dev, void* recv_dev, uint32_t world,
+                                  const uint64_t* part_begins /* world+1 */);
+gossip_status gossip_round_push(gossip_ctx* ctx);
+gossip_status gossip_round_finish(gossip_ctx* ctx, gossip_round_stats* local_out);
+gossip_status gossip_round_commit(gossip_ctx* ctx, uint64_t global_new_receipts, int* finished);
+
+/* ---- results ------------------------------------------------------------- */
+/* Owned seen words (n_local * W): bit m of peer v = v's Message-List holds m (peer.hpp:52). */
+gossip_status gossip_read_seen(gossip_ctx* ctx, uint64_t* host_seen);
+/* Per-message coverage over owned peers (M counts). */
+gossip_status gossip_read_coverage(gossip_ctx* ctx, uint64_t* counts);
+/* Per-message coverage at push start of every executed round ([rounds][M]);
+ * needs GOSSIP_FLAG_COVERAGE_HISTORY. */
+gossip_status gossip_read_coverage_history(gossip_ctx* ctx, uint64_t* buf, uint32_t max_rounds, uint32_t* rounds);
+/* Dead-node reports sorted by (round, reporter, dead). */
+gossip_status gossip_read_reports(gossip_ctx* ctx, gossip_dead_report* buf, uint64_t cap, uint64_t* count);
+/* Alive flags of all n_peers peers (1 byte each). */
+gossip_status gossip_read_alive(gossip_ctx* ctx, uint8_t* out);
+/* Seed-registry membership of all n_peers peers (seed.cpp peerList; 1 byte each). */
+gossip_status gossip_read_registered(gossip_ctx* ctx, uint8_t* out);
+
+/* ---- measurement ----------------------------------------------------------- */
+/* Per-kernel device time (ms) accumulated since timing was last enabled, by kernel name
+ * ("push_light", "push_heavy", "liveness", "churn", "inject", "apply_remote"),
+ * measured with HIP events on the ctx stream.  enable != 0 turns timing on. */
+gossip_status gossip_enable_timing(gossip_ctx* ctx, int enable);
+gossip_status gossip_kernel_time(gossip_ctx* ctx, const char* kernel, double* ms, uint64_t* launches);
+/* Algorithmic HBM bytes of the same kernels over the same
+ * interval: push = 32 B per frontier peer + 20 B per edge traversal (light
+ * rows to "push_light", heavy rows to "push_heavy"); liveness = 6.125 B per
+ * live edge checked. */
+gossip_status gossip_kernel_bytes(gossip_ctx* ctx, const char* kernel, double* bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

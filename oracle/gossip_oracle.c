@@ -1,0 +1,689 @@
+/*
+ * gossip_oracle.c -- CPU restatement of the reference gossip hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see gossip_oracle.h).  Never linked into the
+ * product.  Restates the intended semantics of:
+ *   peer.cpp:214-253  selectAndConnectPeers   (overlay construction)
+ *   peer.cpp:255-295  handleClient            (receive + Message-List dedup)
+ *   peer.cpp:297-318  broadcastMessage        (push to every out-neighbour; F9)
+ *   peer.cpp:320-355  pingLoop                (miss counters, 3 misses -> dead)
+ *   peer.cpp:357-379  messageGenerationLoop   (origination)
+ *   peer.cpp:381-405  handleDeadPeer          (drop edge)
+ *   seed.cpp:130-138,158-167 handleDeadNode   (registry removal on report)
+ * as the deterministic round model of DESIGN.md section 2.
+ */
+#include "gossip_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+typedef unsigned __int128 u128;
+
+/* ------------------------------------------------------------------------ */
+/* Philox4x32-10                                                            */
+/* ------------------------------------------------------------------------ */
+#define PHILOX_M0 0xD2511F53u
+#define PHILOX_M1 0xCD9E8D57u
+#define PHILOX_W0 0x9E3779B9u
+#define PHILOX_W1 0xBB67AE85u
+
+void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
+    uint32_t k0 = key[0], k1 = key[1];
+    for (int r = 0; r < 10; ++r) {
+        uint64_t p0 = (uint64_t)PHILOX_M0 * c0;
+        uint64_t p1 = (uint64_t)PHILOX_M1 * c2;
+        uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        uint32_t n0 = hi1 ^ c1 ^ k0;
+        uint32_t n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += PHILOX_W0; k1 += PHILOX_W1;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+static inline uint32_t philox_x(uint32_t seed, uint32_t peer, uint32_t a, uint32_t b, uint32_t c,
+                                uint32_t d, int lane) {
+    uint32_t ctr[4] = {a, b, c, d}, key[2] = {seed, peer}, out[4];
+    oracle_philox4x32_10(ctr, key, out);
+    return out[lane];
+}
+
+/* ------------------------------------------------------------------------ */
+/* Power-law pick thresholds (peer.cpp:219-222)                             */
+/* ------------------------------------------------------------------------ */
+static int thr_ok(uint64_t x, uint32_t j, uint32_t L) {
+    u128 l5 = (u128)L * L * L * L * L;
+    u128 j5 = (u128)j * j * j * j * j;
+    return (u128)x * x * l5 >= (j5 << 64);
+}
+
+uint64_t oracle_threshold(uint32_t j, uint32_t L) {
+    if (j >= L) return (uint64_t)1 << 32;
+    if (j == 0) return 0;
+    double est = ldexp(pow((double)j / (double)L, 2.5), 32);
+    uint64_t x = (uint64_t)ceil(est);
+    if (x > ((uint64_t)1 << 32)) x = (uint64_t)1 << 32;
+    while (x > 0 && thr_ok(x - 1, j, L)) --x;
+    while (!thr_ok(x, j, L)) ++x;
+    return x;
+}
+
+/* k = floor(L * U^(1/2.5)) with U = x/2^32, via the exact thresholds. */
+static uint32_t pick_count(uint32_t x, uint32_t L, const uint64_t* thr) {
+    uint32_t k = 0;
+    for (uint32_t j = 1; j < L; ++j) k += ((uint64_t)x >= thr[j]);
+    return k;
+}
+
+uint32_t oracle_skew_pick(uint32_t x, uint64_t n) {
+    uint64_t a = ((uint64_t)x * x) >> 32;
+    uint64_t b = (a * x) >> 32;
+    return (uint32_t)((n * b) >> 32);
+}
+
+uint64_t oracle_digest_weight(uint64_t idx) {
+    uint64_t z = (idx + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return z | 1ull;
+}
+
+void oracle_free(void* p) { free(p); }
+
+/* ------------------------------------------------------------------------ */
+/* CSR assembly: sort rows, drop duplicates and self loops                  */
+/* ------------------------------------------------------------------------ */
+static int cmp_u32(const void* a, const void* b) {
+    uint32_t x = *(const uint32_t*)a, y = *(const uint32_t*)b;
+    return (x > y) - (x < y);
+}
+
+static void sort_row(uint32_t* a, uint64_t len) {
+    if (len < 32) {
+        for (uint64_t i = 1; i < len; ++i) {
+            uint32_t v = a[i];
+            uint64_t j = i;
+            while (j > 0 && a[j - 1] > v) { a[j] = a[j - 1]; --j; }
+            a[j] = v;
+        }
+    } else {
+        qsort(a, len, sizeof(uint32_t), cmp_u32);
+    }
+}
+
+/* raw rows [rp_raw[v], rp_raw[v+1]) of col_raw -> sorted unique CSR without self loops */
+static int finish_csr(uint64_t n, uint64_t* rp_raw, uint32_t* col_raw, int threads,
+                      uint64_t** row_ptr, uint32_t** col, uint64_t* n_edges) {
+    (void)threads;
+    uint64_t* cnt = (uint64_t*)malloc((n + 1) * sizeof(uint64_t));
+    if (!cnt) return -1;
+#pragma omp parallel for schedule(dynamic, 1024) num_threads(threads)
+    for (int64_t v = 0; v < (int64_t)n; ++v) {
+        uint32_t* a = col_raw + rp_raw[v];
+        uint64_t len = rp_raw[v + 1] - rp_raw[v];
+        sort_row(a, len);
+        uint64_t m = 0;
+        for (uint64_t i = 0; i < len; ++i) {
+            if (a[i] == (uint32_t)v) continue;
+            if (m > 0 && a[m - 1] == a[i]) continue;
+            a[m++] = a[i];
+        }
+        cnt[v] = m;
+    }
+    uint64_t* rp = (uint64_t*)malloc((n + 1) * sizeof(uint64_t));
+    if (!rp) { free(cnt); return -1; }
+    rp[0] = 0;
+    for (uint64_t v = 0; v < n; ++v) rp[v + 1] = rp[v] + cnt[v];
+    uint32_t* c = (uint32_t*)malloc((rp[n] ? rp[n] : 1) * sizeof(uint32_t));
+    if (!c) { free(cnt); free(rp); return -1; }
+#pragma omp parallel for schedule(dynamic, 1024) num_threads(threads)
+    for (int64_t v = 0; v < (int64_t)n; ++v)
+        memcpy(c + rp[v], col_raw + rp_raw[v], cnt[v] * sizeof(uint32_t));
+    free(cnt);
+    *row_ptr = rp;
+    *col = c;
+    *n_edges = rp[n];
+    return 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* ref_bootstrap: literal F8 overlay (peer.cpp:63-72, 214-253; seed.cpp:117) */
+/* ------------------------------------------------------------------------ */
+int oracle_gen_ref_bootstrap(uint32_t n, uint32_t n_seeds, uint32_t seed, uint64_t** row_ptr,
+                             uint32_t** col, uint64_t* n_edges) {
+    if (n == 0 || n > 4096 || n_seeds == 0) return -1;
+    uint32_t q = n_seeds / 2 + 1; /* quorum, peer.cpp:64 / config.cpp:76 */
+    uint64_t cap = (uint64_t)n * n;
+    uint64_t* rp_raw = (uint64_t*)calloc((size_t)n + 1, sizeof(uint64_t));
+    uint32_t* col_raw = (uint32_t*)malloc(cap * sizeof(uint32_t) + 4);
+    uint32_t* perm = (uint32_t*)malloc((size_t)n * sizeof(uint32_t));
+    uint8_t* chosen = (uint8_t*)malloc(n);
+    uint64_t* thr = (uint64_t*)malloc((size_t)(n + 1) * sizeof(uint64_t));
+    if (!rp_raw || !col_raw || !perm || !chosen || !thr) return -1;
+    uint64_t w = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        uint32_t L = i + 1; /* registry {0..i}, self included (seed.cpp:117-122) */
+        for (uint32_t j = 0; j < L; ++j) thr[j] = oracle_threshold(j, L);
+        memset(chosen, 0, L);
+        for (uint32_t s = 0; s < q; ++s) {
+            uint32_t x = philox_x(seed, i, ORACLE_P_DEGREE, s, 0, 0, 0);
+            uint32_t k = pick_count(x, L, thr);
+            for (uint32_t j = 0; j < L; ++j) perm[j] = j; /* list in registration order */
+            uint32_t d = 0;
+            for (uint32_t idx = L - 1; idx >= 1; --idx, ++d) { /* Fisher-Yates, peer.cpp:224-225 */
+                uint32_t r = philox_x(seed, i, ORACLE_P_SHUFFLE, s, d >> 2, 0, (int)(d & 3));
+                uint32_t jj = (uint32_t)(((uint64_t)r * (idx + 1)) >> 32);
+                uint32_t t = perm[idx]; perm[idx] = perm[jj]; perm[jj] = t;
+            }
+            for (uint32_t t = 0; t < k; ++t) {          /* peer.cpp:227-230 */
+                uint32_t c = perm[t];
+                if (c == i) continue;                    /* self still consumes a slot */
+                chosen[c] = 1;                           /* peer.cpp:242 map overwrite = union */
+            }
+        }
+        rp_raw[i] = w;
+        for (uint32_t c = 0; c < L; ++c)
+            if (chosen[c]) col_raw[w++] = c;
+    }
+    rp_raw[n] = w;
+    free(perm); free(chosen); free(thr);
+    int rc = finish_csr(n, rp_raw, col_raw, 1, row_ptr, col, n_edges);
+    free(rp_raw); free(col_raw);
+    return rc;
+}
+
+/* ------------------------------------------------------------------------ */
+/* powerlaw: scale overlay, symmetrised                                     */
+/* ------------------------------------------------------------------------ */
+int oracle_gen_powerlaw(uint64_t n, uint32_t list_len, uint32_t seed, int threads, uint64_t** row_ptr,
+                        uint32_t** col, uint64_t* n_edges) {
+    if (n < 2 || n > 0x80000000ull || list_len < 2 || list_len > 64) return -1;
+    if (threads <= 0) threads = 1;
+    uint64_t thr[65];
+    for (uint32_t j = 0; j <= list_len; ++j) thr[j] = oracle_threshold(j, list_len);
+    uint64_t* deg = (uint64_t*)calloc(n + 1, sizeof(uint64_t));
+    if (!deg) return -1;
+    /* pass 1: count (u->c and c->u) */
+#pragma omp parallel for schedule(static, 4096) num_threads(threads)
+    for (int64_t u = 0; u < (int64_t)n; ++u) {
+        uint32_t x = philox_x(seed, (uint32_t)u, ORACLE_P_DEGREE, 0, 0, 0, 0);
+        uint32_t k = pick_count(x, list_len, thr);
+        uint64_t mine = 0;
+        for (uint32_t i = 0; i < k; ++i) {
+            uint32_t t = philox_x(seed, (uint32_t)u, ORACLE_P_TARGET, 0, i >> 2, 0, (int)(i & 3));
+            uint32_t c = oracle_skew_pick(t, n);
+            if (c == (uint32_t)u) continue;
+            ++mine;
+            __atomic_fetch_add(&deg[c], 1, __ATOMIC_RELAXED);
+        }
+        __atomic_fetch_add(&deg[u], mine, __ATOMIC_RELAXED);
+    }
+    uint64_t* rp_raw = (uint64_t*)malloc((n + 1) * sizeof(uint64_t));
+    if (!rp_raw) { free(deg); return -1; }
+    rp_raw[0] = 0;
+    for (uint64_t v = 0; v < n; ++v) rp_raw[v + 1] = rp_raw[v] + deg[v];
+    uint32_t* col_raw = (uint32_t*)malloc((rp_raw[n] ? rp_raw[n] : 1) * sizeof(uint32_t));
+    if (!col_raw) { free(deg); free(rp_raw); return -1; }
+    for (uint64_t v = 0; v < n; ++v) deg[v] = rp_raw[v]; /* cursors */
+#pragma omp parallel for schedule(static, 4096) num_threads(threads)
+    for (int64_t u = 0; u < (int64_t)n; ++u) {
+        uint32_t x = philox_x(seed, (uint32_t)u, ORACLE_P_DEGREE, 0, 0, 0, 0);
+        uint32_t k = pick_count(x, list_len, thr);
+        for (uint32_t i = 0; i < k; ++i) {
+            uint32_t t = philox_x(seed, (uint32_t)u, ORACLE_P_TARGET, 0, i >> 2, 0, (int)(i & 3));
+            uint32_t c = oracle_skew_pick(t, n);
+            if (c == (uint32_t)u) continue;
+            uint64_t a = __atomic_fetch_add(&deg[u], 1, __ATOMIC_RELAXED);
+            col_raw[a] = c;
+            uint64_t b = __atomic_fetch_add(&deg[c], 1, __ATOMIC_RELAXED);
+            col_raw[b] = (uint32_t)u;
+        }
+    }
+    free(deg);
+    int rc = finish_csr(n, rp_raw, col_raw, threads, row_ptr, col, n_edges);
+    free(rp_raw); free(col_raw);
+    return rc;
+}
+
+void oracle_pick_origins(uint64_t n, uint32_t seed, uint32_t count, uint32_t* out) {
+    for (uint32_t k = 0; k < count; ++k) {
+        for (uint32_t attempt = 0;; ++attempt) {
+            uint32_t x = philox_x(seed, 0xFFFFFFFFu, ORACLE_P_ORIGIN, k, attempt, 0, 0);
+            uint32_t o = (uint32_t)(((uint64_t)x * n) >> 32);
+            int dup = 0;
+            for (uint32_t i = 0; i < k; ++i) dup |= (out[i] == o);
+            if (!dup || (uint64_t)k >= n) { out[k] = o; break; }
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Round driver                                                             */
+/* ------------------------------------------------------------------------ */
+/* literal variant: per-peer Message-List (peer.hpp:52) keyed by message id,
+ * with the MessageTracker.sentTo count (peer.hpp:23-26). */
+typedef struct msg_list {
+    uint32_t cap, size;
+    uint32_t* key;     /* 0xFFFFFFFF = empty */
+    uint64_t* sent_to; /* |sentTo| per message */
+} msg_list;
+
+struct oracle_sim {
+    oracle_sim_cfg cfg;
+    uint64_t n, e;
+    uint32_t W, M;
+    const uint64_t* rp;
+    const uint32_t* col;
+    uint8_t* alive;
+    uint8_t* registered;
+    uint8_t* masked; /* per edge */
+    uint8_t* miss;   /* per edge, saturating */
+    uint32_t round;
+    int finished;
+    /* schedule */
+    uint32_t* origin;
+    uint32_t* inject_round;
+    uint32_t n_kills;
+    uint32_t* kill_peer;
+    uint32_t* kill_round;
+    /* reports */
+    oracle_report* rep;
+    uint64_t n_rep, cap_rep;
+    /* fast variant */
+    uint64_t *seen, *nw, *nx;
+    /* literal variant */
+    msg_list* lists;
+    uint32_t** outbox;   /* per peer: message ids to broadcast this round */
+    uint32_t* outbox_n;
+    uint32_t** nextbox;
+    uint32_t* nextbox_n;
+};
+
+static int ml_find(const msg_list* l, uint32_t m) {
+    if (!l->cap) return -1;
+    uint32_t mask = l->cap - 1, h = (m * 0x9E3779B1u) & mask;
+    for (;;) {
+        if (l->key[h] == 0xFFFFFFFFu) return -1;
+        if (l->key[h] == m) return (int)h;
+        h = (h + 1) & mask;
+    }
+}
+
+static int ml_insert(msg_list* l, uint32_t m) {
+    if ((l->size + 1) * 2 > l->cap) {
+        uint32_t ncap = l->cap ? l->cap * 2 : 8;
+        uint32_t* nk = (uint32_t*)malloc(ncap * sizeof(uint32_t));
+        uint64_t* ns = (uint64_t*)calloc(ncap, sizeof(uint64_t));
+        memset(nk, 0xFF, ncap * sizeof(uint32_t));
+        for (uint32_t i = 0; i < l->cap; ++i) {
+            if (l->key[i] == 0xFFFFFFFFu) continue;
+            uint32_t h = (l->key[i] * 0x9E3779B1u) & (ncap - 1);
+            while (nk[h] != 0xFFFFFFFFu) h = (h + 1) & (ncap - 1);
+            nk[h] = l->key[i];
+            ns[h] = l->sent_to[i];
+        }
+        free(l->key); free(l->sent_to);
+        l->key = nk; l->sent_to = ns; l->cap = ncap;
+    }
+    uint32_t h = (m * 0x9E3779B1u) & (l->cap - 1);
+    while (l->key[h] != 0xFFFFFFFFu) h = (h + 1) & (l->cap - 1);
+    l->key[h] = m;
+    l->sent_to[h] = 0;
+    l->size++;
+    return (int)h;
+}
+
+oracle_sim* oracle_sim_create(const oracle_sim_cfg* cfg, const uint64_t* row_ptr, const uint32_t* col) {
+    if (!cfg || cfg->n == 0 || cfg->n_msgs == 0) return NULL;
+    oracle_sim* s = (oracle_sim*)calloc(1, sizeof(oracle_sim));
+    s->cfg = *cfg;
+    if (s->cfg.threads <= 0) s->cfg.threads = 1;
+    if (s->cfg.max_rounds == 0) s->cfg.max_rounds = 1u << 20;
+    s->n = cfg->n;
+    s->e = row_ptr[cfg->n];
+    s->M = cfg->n_msgs;
+    s->W = (cfg->n_msgs + 63) / 64;
+    s->rp = row_ptr;
+    s->col = col;
+    s->alive = (uint8_t*)malloc(s->n);
+    s->registered = (uint8_t*)malloc(s->n);
+    memset(s->alive, 1, s->n);
+    memset(s->registered, 1, s->n);
+    s->masked = (uint8_t*)calloc(s->e + 1, 1);
+    s->miss = (uint8_t*)calloc(s->e + 1, 1);
+    s->origin = (uint32_t*)calloc(s->M, sizeof(uint32_t));
+    s->inject_round = (uint32_t*)malloc(s->M * sizeof(uint32_t));
+    for (uint32_t m = 0; m < s->M; ++m) s->inject_round[m] = 0xFFFFFFFFu; /* unscheduled */
+    if (cfg->variant == 0) {
+        s->seen = (uint64_t*)calloc(s->n * s->W, sizeof(uint64_t));
+        s->nw = (uint64_t*)calloc(s->n * s->W, sizeof(uint64_t));
+        s->nx = (uint64_t*)calloc(s->n * s->W, sizeof(uint64_t));
+    } else {
+        s->lists = (msg_list*)calloc(s->n, sizeof(msg_list));
+        s->outbox = (uint32_t**)calloc(s->n, sizeof(uint32_t*));
+        s->nextbox = (uint32_t**)calloc(s->n, sizeof(uint32_t*));
+        s->outbox_n = (uint32_t*)calloc(s->n, sizeof(uint32_t));
+        s->nextbox_n = (uint32_t*)calloc(s->n, sizeof(uint32_t));
+        for (uint64_t v = 0; v < s->n; ++v) {
+            s->outbox[v] = (uint32_t*)malloc(s->M * sizeof(uint32_t));
+            s->nextbox[v] = (uint32_t*)malloc(s->M * sizeof(uint32_t));
+        }
+    }
+    return s;
+}
+
+void oracle_sim_destroy(oracle_sim* s) {
+    if (!s) return;
+    free(s->alive); free(s->registered); free(s->masked); free(s->miss);
+    free(s->origin); free(s->inject_round); free(s->kill_peer); free(s->kill_round);
+    free(s->rep); free(s->seen); free(s->nw); free(s->nx);
+    if (s->lists) {
+        for (uint64_t v = 0; v < s->n; ++v) {
+            free(s->lists[v].key); free(s->lists[v].sent_to);
+            free(s->outbox[v]); free(s->nextbox[v]);
+        }
+        free(s->lists); free(s->outbox); free(s->nextbox); free(s->outbox_n); free(s->nextbox_n);
+    }
+    free(s);
+}
+
+int oracle_sim_schedule(oracle_sim* s, const uint32_t* origin, const uint32_t* inject_round, uint32_t n_kills,
+                        const uint32_t* kill_peer, const uint32_t* kill_round) {
+    for (uint32_t m = 0; m < s->M; ++m) {
+        if (origin[m] >= s->n) return -1;
+        s->origin[m] = origin[m];
+        s->inject_round[m] = inject_round[m];
+    }
+    free(s->kill_peer); free(s->kill_round);
+    s->n_kills = n_kills;
+    s->kill_peer = (uint32_t*)malloc((n_kills + 1) * sizeof(uint32_t));
+    s->kill_round = (uint32_t*)malloc((n_kills + 1) * sizeof(uint32_t));
+    for (uint32_t i = 0; i < n_kills; ++i) {
+        if (kill_peer[i] >= s->n) return -1;
+        s->kill_peer[i] = kill_peer[i];
+        s->kill_round[i] = kill_round[i];
+    }
+    return 0;
+}
+
+static void push_report(oracle_sim* s, uint32_t r, uint32_t u, uint32_t v) {
+    if (s->n_rep == s->cap_rep) {
+        s->cap_rep = s->cap_rep ? s->cap_rep * 2 : 1024;
+        s->rep = (oracle_report*)realloc(s->rep, s->cap_rep * sizeof(oracle_report));
+    }
+    s->rep[s->n_rep].round = r;
+    s->rep[s->n_rep].reporter = u;
+    s->rep[s->n_rep].dead = v;
+    s->n_rep++;
+}
+
+static int has_bit_fast(const oracle_sim* s, uint64_t v, uint32_t m) {
+    return (int)((s->seen[v * s->W + (m >> 6)] >> (m & 63)) & 1u);
+}
+
+/* step 1: churn (A11) + kill list -- a dead peer stops receiving, forwarding, pinging */
+static uint64_t do_churn(oracle_sim* s, uint32_t r) {
+    uint64_t died = 0;
+    for (uint32_t i = 0; i < s->n_kills; ++i) {
+        uint32_t v = s->kill_peer[i];
+        if (s->kill_round[i] == r && s->alive[v]) {
+            s->alive[v] = 0;
+            ++died;
+        }
+    }
+    if (s->cfg.churn_threshold) {
+        for (uint64_t v = 0; v < s->n; ++v) {
+            if (!s->alive[v]) continue;
+            uint32_t x = philox_x(s->cfg.seed, (uint32_t)v, ORACLE_P_CHURN, r, 0, 0, 0);
+            if (x < s->cfg.churn_threshold) { s->alive[v] = 0; ++died; }
+        }
+    }
+    if (died) {
+        for (uint64_t v = 0; v < s->n; ++v) {
+            if (s->alive[v]) continue;
+            if (s->cfg.variant == 0) memset(s->nw + v * s->W, 0, s->W * sizeof(uint64_t));
+            else s->outbox_n[v] = 0;
+        }
+    }
+    return died;
+}
+
+/* step 2: liveness (pingLoop peer.cpp:328-346 + handleDeadPeer :383-397 + seed :158-167) */
+static void do_liveness(oracle_sim* s, uint32_t r, oracle_stats* st) {
+    for (uint64_t u = 0; u < s->n; ++u) {
+        if (!s->alive[u]) continue;
+        for (uint64_t e = s->rp[u]; e < s->rp[u + 1]; ++e) {
+            if (s->masked[e]) continue;
+            uint32_t v = s->col[e];
+            if (s->alive[v]) { s->miss[e] = 0; continue; }      /* ping ok -> reset (:340-341) */
+            if (s->miss[e] < 255) s->miss[e]++;                  /* failedAttempts++ (:336) */
+            if (s->miss[e] >= s->cfg.max_missed) {               /* >= 3 -> dead (:337-338) */
+                s->masked[e] = 1;                                /* connectedPeers.erase (:388) */
+                push_report(s, r, (uint32_t)u, v);
+                st->reports++;
+                if (s->registered[v]) { s->registered[v] = 0; st->seed_removals++; } /* seed.cpp:162 */
+            }
+        }
+    }
+}
+
+static void stats_start_fast(oracle_sim* s, oracle_stats* st) {
+    uint64_t frontier = 0, digest = 0, covered = 0;
+    const uint32_t W = s->W;
+    int T = s->cfg.threads;
+    (void)T;
+#pragma omp parallel for reduction(+ : frontier, digest, covered) schedule(static, 8192) num_threads(T)
+    for (int64_t v = 0; v < (int64_t)s->n; ++v) {
+        int act = 0;
+        for (uint32_t w = 0; w < W; ++w) {
+            uint64_t x = s->seen[v * W + w];
+            act |= s->nw[v * W + w] != 0;
+            covered += (uint64_t)__builtin_popcountll(x);
+            digest += oracle_digest_weight((uint64_t)v * W + w) * x;
+        }
+        frontier += (uint64_t)act;
+    }
+    st->frontier = frontier;
+    st->digest = digest;
+    st->covered = covered;
+}
+
+static int step_fast(oracle_sim* s, oracle_stats* st) {
+    const uint32_t W = s->W;
+    const uint32_t r = s->round;
+    /* 3: injection (messageGenerationLoop peer.cpp:359-374) */
+    for (uint32_t m = 0; m < s->M; ++m) {
+        if (s->inject_round[m] != r) continue;
+        uint32_t o = s->origin[m];
+        if (!s->alive[o]) continue;
+        s->seen[o * W + (m >> 6)] |= 1ull << (m & 63);
+        s->nw[o * W + (m >> 6)] |= 1ull << (m & 63);
+        st->injected++;
+    }
+    stats_start_fast(s, st);
+    /* 4: push (broadcastMessage :310-316 -> handleClient :277-285) */
+    uint64_t trav = 0, deliv = 0, undeliv = 0, fresh_bits = 0;
+    int T = s->cfg.threads;
+    (void)T;
+#pragma omp parallel for reduction(+ : trav, deliv, undeliv, fresh_bits) schedule(dynamic, 256) num_threads(T)
+    for (int64_t u = 0; u < (int64_t)s->n; ++u) {
+        const uint64_t* mk = s->nw + (uint64_t)u * W;
+        int act = 0;
+        uint64_t pc = 0;
+        for (uint32_t w = 0; w < W; ++w) { act |= mk[w] != 0; pc += (uint64_t)__builtin_popcountll(mk[w]); }
+        if (!act) continue;
+        for (uint64_t e = s->rp[u]; e < s->rp[u + 1]; ++e) {
+            if (s->masked[e]) continue;
+            ++trav;
+            uint32_t v = s->col[e];
+            if (!s->alive[v]) { undeliv += pc; continue; }
+            deliv += pc;
+            for (uint32_t w = 0; w < W; ++w) {
+                if (!mk[w]) continue;
+                uint64_t old = __atomic_fetch_or(&s->seen[(uint64_t)v * W + w], mk[w], __ATOMIC_RELAXED);
+                uint64_t fr = mk[w] & ~old;
+                if (fr) {
+                    __atomic_fetch_or(&s->nx[(uint64_t)v * W + w], fr, __ATOMIC_RELAXED);
+                    fresh_bits += (uint64_t)__builtin_popcountll(fr);
+                }
+            }
+        }
+    }
+    st->traversals = trav;
+    st->deliveries = deliv;
+    st->undelivered = undeliv;
+    st->new_receipts = fresh_bits;
+    st->duplicates = deliv - fresh_bits;
+    /* 5: advance */
+    uint64_t* t = s->nw; s->nw = s->nx; s->nx = t;
+    memset(s->nx, 0, s->n * W * sizeof(uint64_t));
+    return 0;
+}
+
+static int step_literal(oracle_sim* s, oracle_stats* st) {
+    const uint32_t r = s->round;
+    const uint32_t W = s->W;
+    for (uint32_t m = 0; m < s->M; ++m) {
+        if (s->inject_round[m] != r) continue;
+        uint32_t o = s->origin[m];
+        if (!s->alive[o]) continue;
+        if (ml_find(&s->lists[o], m) < 0) ml_insert(&s->lists[o], m); /* messageList[hash] = {msg,{}} (:371) */
+        s->outbox[o][s->outbox_n[o]++] = m;                           /* broadcastMessage(msg) (:374) */
+        st->injected++;
+    }
+    /* stats at push start, from the message lists */
+    for (uint64_t v = 0; v < s->n; ++v) {
+        const msg_list* l = &s->lists[v];
+        st->frontier += s->outbox_n[v] > 0;
+        for (uint32_t i = 0; i < l->cap; ++i) {
+            uint32_t m = l->key[i];
+            if (m == 0xFFFFFFFFu) continue;
+            st->covered++;
+            st->digest += oracle_digest_weight(v * W + (m >> 6)) * (1ull << (m & 63));
+        }
+    }
+    /* push: every sender broadcasts every outbox message to every live out-edge */
+    for (uint64_t u = 0; u < s->n; ++u) {
+        if (!s->outbox_n[u]) continue;
+        for (uint64_t e = s->rp[u]; e < s->rp[u + 1]; ++e) {
+            if (s->masked[e]) continue;
+            st->traversals++;
+            uint32_t v = s->col[e];
+            for (uint32_t i = 0; i < s->outbox_n[u]; ++i) {
+                uint32_t m = s->outbox[u][i];
+                if (!s->alive[v]) { st->undelivered++; continue; } /* send() fails: not in sentTo */
+                st->deliveries++;
+                int h = ml_find(&s->lists[u], m);
+                s->lists[u].sent_to[h]++;                           /* sentTo.insert(peer) (:314) */
+                /* receiver: handleClient dedup (:281-285) */
+                if (ml_find(&s->lists[v], m) < 0) {
+                    ml_insert(&s->lists[v], m);
+                    s->nextbox[v][s->nextbox_n[v]++] = m;
+                    st->new_receipts++;
+                } else {
+                    st->duplicates++;
+                }
+            }
+        }
+    }
+    for (uint64_t v = 0; v < s->n; ++v) {
+        uint32_t* t = s->outbox[v]; s->outbox[v] = s->nextbox[v]; s->nextbox[v] = t;
+        s->outbox_n[v] = s->nextbox_n[v];
+        s->nextbox_n[v] = 0;
+    }
+    return 0;
+}
+
+int oracle_sim_step(oracle_sim* s, oracle_stats* out) {
+    if (s->finished) return 1;
+    oracle_stats st;
+    memset(&st, 0, sizeof(st));
+    uint32_t r = s->round;
+    st.round = r;
+    st.died = do_churn(s, r);
+    if (s->cfg.ping_every && r % s->cfg.ping_every == 0) {
+        st.flags |= 1;
+        do_liveness(s, r, &st);
+    }
+    if (s->cfg.variant == 0) step_fast(s, &st);
+    else step_literal(s, &st);
+    if (out) *out = st;
+    s->round++;
+    int pending = 0;
+    for (uint32_t m = 0; m < s->M; ++m) pending |= (s->inject_round[m] != 0xFFFFFFFFu && s->inject_round[m] > r);
+    if ((st.new_receipts == 0 && !pending && s->round >= s->cfg.min_rounds) || s->round >= s->cfg.max_rounds)
+        s->finished = 1;
+    return s->finished;
+}
+
+int oracle_sim_run(oracle_sim* s, oracle_stats* per_round, uint32_t cap) {
+    int rounds = 0;
+    while (!s->finished) {
+        oracle_stats st;
+        int rc = oracle_sim_step(s, &st);
+        if (rc < 0) return rc;
+        if (per_round && (uint32_t)rounds < cap) per_round[rounds] = st;
+        ++rounds;
+    }
+    return rounds;
+}
+
+void oracle_sim_seen(const oracle_sim* s, uint64_t* out) {
+    if (s->cfg.variant == 0) {
+        memcpy(out, s->seen, s->n * s->W * sizeof(uint64_t));
+        return;
+    }
+    memset(out, 0, s->n * s->W * sizeof(uint64_t));
+    for (uint64_t v = 0; v < s->n; ++v) {
+        const msg_list* l = &s->lists[v];
+        for (uint32_t i = 0; i < l->cap; ++i) {
+            uint32_t m = l->key[i];
+            if (m != 0xFFFFFFFFu) out[v * s->W + (m >> 6)] |= 1ull << (m & 63);
+        }
+    }
+}
+
+void oracle_sim_coverage(const oracle_sim* s, uint64_t* out) {
+    memset(out, 0, s->M * sizeof(uint64_t));
+    for (uint64_t v = 0; v < s->n; ++v) {
+        for (uint32_t m = 0; m < s->M; ++m) {
+            if (s->cfg.variant == 0) out[m] += (uint64_t)has_bit_fast(s, v, m);
+            else out[m] += ml_find(&s->lists[v], m) >= 0;
+        }
+    }
+}
+
+static int cmp_rep(const void* a, const void* b) {
+    const oracle_report* x = (const oracle_report*)a;
+    const oracle_report* y = (const oracle_report*)b;
+    if (x->round != y->round) return x->round < y->round ? -1 : 1;
+    if (x->reporter != y->reporter) return x->reporter < y->reporter ? -1 : 1;
+    if (x->dead != y->dead) return x->dead < y->dead ? -1 : 1;
+    return 0;
+}
+
+uint64_t oracle_sim_reports(const oracle_sim* s, oracle_report* buf, uint64_t cap) {
+    qsort(s->rep, s->n_rep, sizeof(oracle_report), cmp_rep);
+    uint64_t k = s->n_rep < cap ? s->n_rep : cap;
+    if (buf && k) memcpy(buf, s->rep, k * sizeof(oracle_report));
+    return s->n_rep;
+}
+
+void oracle_sim_alive(const oracle_sim* s, uint8_t* out) { memcpy(out, s->alive, s->n); }
+void oracle_sim_registered(const oracle_sim* s, uint8_t* out) { memcpy(out, s->registered, s->n); }
+
+uint64_t oracle_sim_sent_to_total(const oracle_sim* s) {
+    if (!s->lists) return 0;
+    uint64_t t = 0;
+    for (uint64_t v = 0; v < s->n; ++v)
+        for (uint32_t i = 0; i < s->lists[v].cap; ++i)
+            if (s->lists[v].key[i] != 0xFFFFFFFFu) t += s->lists[v].sent_to[i];
+    return t;
+}

@@ -1,0 +1,838 @@
+// gossip_engine.hip -- C-ABI of libgossip_hip (include/gossip/gossip.h).
+//
+// Host orchestration of the round kernels.  One gossip_ctx owns one vertex
+// partition of the overlay in HBM; each round is a short chain of kernels on
+// the ctx stream (kills -> churn -> liveness -> inject -> push heavy -> push
+// light) followed by one 128-byte stats read-back that decides termination.
+// No exception crosses the ABI; all errors become gossip_status codes.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/gossip/gossip.h"
+#include "gossip_internal.hpp"
+#include "philox.hpp"
+
+using namespace gossip;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+gossip_status fail(gossip_status s, const std::string& msg) {
+    g_last_error = msg;
+    return s;
+}
+
+#define HIPCHK(call)                                                                              \
+    do {                                                                                          \
+        hipError_t e_ = (call);                                                                   \
+        if (e_ != hipSuccess)                                                                     \
+            return fail(GOSSIP_EHIP, std::string(#call) + " failed: " + hipGetErrorString(e_));   \
+    } while (0)
+
+__global__ void k_unmask(uint32_t* col, uint64_t m) {
+    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (uint64_t)gridDim.x * blockDim.x)
+        col[e] &= ~kMaskedEdge;
+}
+
+struct TimerRec {
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+    double ms = 0.0;
+    uint64_t launches = 0;
+};
+
+}  // namespace
+
+struct gossip_ctx {
+    gossip_config cfg{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    uint64_t n = 0, begin = 0, end = 0, n_local = 0;
+    uint32_t M = 0, W = 0, Wp = 0;
+
+    // overlay
+    uint64_t* rp = nullptr;
+    uint32_t* col = nullptr;
+    uint64_t n_edges = 0;
+    HeavyChunk* chunks = nullptr;
+    uint64_t n_chunks = 0;
+    bool graph_ready = false;
+
+    // dynamic state
+    uint64_t *seen = nullptr, *nw = nullptr, *nx = nullptr;
+    uint32_t* alive = nullptr;
+    uint32_t* registered = nullptr;
+    uint8_t* miss = nullptr;
+    DevStats* st = nullptr;
+    DevStats* h_st = nullptr;  // pinned
+    unsigned long long* cov_hist = nullptr;
+    DeadReport* reports = nullptr;
+    unsigned long long* n_reports = nullptr;
+    uint64_t report_cap = 0;
+    bool any_masked = false;
+
+    // schedule
+    std::vector<uint32_t> origin, inject_round;
+    std::vector<uint32_t> inj_round_sorted;  // per sorted entry
+    uint32_t* d_inj_origin = nullptr;
+    uint32_t* d_inj_msg = nullptr;
+    std::vector<uint32_t> kill_round_sorted;
+    uint32_t* d_kill_peer = nullptr;
+    uint32_t last_inject_round = 0;
+    bool has_schedule = false;
+
+    // run state
+    uint32_t round = 0;
+    bool finished = false;
+    bool any_dead = false;
+    uint64_t cum_digest = 0, cum_covered = 0;
+
+    // partitioned exchange
+    uint64_t* send = nullptr;
+    const uint64_t* recv = nullptr;
+    uint32_t world = 1;
+    std::vector<uint64_t> part_begins;
+
+    // timing
+    bool timing = false;
+    std::map<std::string, TimerRec> timers;
+    std::map<std::string, double> kbytes;
+};
+
+namespace {
+
+uint32_t pad_words(uint32_t w) {
+    if (w <= 1) return 1;
+    if (w <= 2) return 2;
+    if (w <= 4) return 4;
+    return 8;
+}
+
+uint32_t pack_w(const gossip_ctx* c) { return (c->W << 16) | c->Wp; }
+
+gossip_status set_dev(gossip_ctx* c) {
+    HIPCHK(hipSetDevice(c->device));
+    return GOSSIP_OK;
+}
+
+template <class F>
+hipError_t timed(gossip_ctx* c, const char* name, F&& launch) {
+    if (!c->timing) return launch();
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    hipEventRecord(a, c->stream);
+    hipError_t e = launch();
+    hipEventRecord(b, c->stream);
+    c->timers[name].pending.emplace_back(a, b);
+    return e;
+}
+
+void drain_timers(gossip_ctx* c) {
+    for (auto& kv : c->timers) {
+        for (auto& ev : kv.second.pending) {
+            float ms = 0.f;
+            hipEventSynchronize(ev.second);
+            hipEventElapsedTime(&ms, ev.first, ev.second);
+            kv.second.ms += ms;
+            kv.second.launches++;
+            hipEventDestroy(ev.first);
+            hipEventDestroy(ev.second);
+        }
+        kv.second.pending.clear();
+    }
+}
+
+void free_state(gossip_ctx* c) {
+    hipFree(c->seen);
+    hipFree(c->nw);
+    hipFree(c->nx);
+    hipFree(c->alive);
+    hipFree(c->registered);
+    hipFree(c->miss);
+    hipFree(c->st);
+    if (c->h_st) hipHostFree(c->h_st);
+    hipFree(c->cov_hist);
+    hipFree(c->reports);
+    hipFree(c->n_reports);
+    c->seen = c->nw = c->nx = nullptr;
+    c->alive = c->registered = nullptr;
+    c->miss = nullptr;
+    c->st = c->h_st = nullptr;
+    c->cov_hist = nullptr;
+    c->reports = nullptr;
+    c->n_reports = nullptr;
+}
+
+void free_graph(gossip_ctx* c) {
+    hipFree(c->rp);
+    hipFree(c->col);
+    hipFree(c->chunks);
+    c->rp = nullptr;
+    c->col = nullptr;
+    c->chunks = nullptr;
+    c->n_edges = c->n_chunks = 0;
+    c->graph_ready = false;
+}
+
+RoundArgs make_args(gossip_ctx* c) {
+    RoundArgs a{};
+    a.rp = c->rp;
+    a.col = c->col;
+    a.alive = c->alive;
+    a.registered = c->registered;
+    a.seen = c->seen;
+    a.nw = c->nw;
+    a.nx = c->nx;
+    a.send = c->send;
+    a.miss = c->miss;
+    a.st = c->st + c->round;
+    a.cov = c->cov_hist ? c->cov_hist + (uint64_t)c->round * 64 * c->Wp : nullptr;
+    a.chunks = c->chunks;
+    a.n_chunks = c->n_chunks;
+    a.n_local = c->n_local;
+    a.begin = c->begin;
+    a.end = c->end;
+    a.n_global = c->n;
+    a.reports = c->reports;
+    a.n_reports = c->n_reports;
+    a.report_cap = c->report_cap;
+    a.round = c->round;
+    a.max_missed = c->cfg.max_missed;
+    return a;
+}
+
+// Upload a host-built CSR and derive the heavy-row chunk list.
+gossip_status install_graph(gossip_ctx* c, uint64_t* d_rp, uint32_t* d_col, uint64_t m) {
+    free_graph(c);
+    c->rp = d_rp;
+    c->col = d_col;
+    c->n_edges = m;
+    unsigned long long* d_cnt = nullptr;
+    HIPCHK(hipMalloc((void**)&d_cnt, 2 * sizeof(unsigned long long)));
+    HIPCHK(hipMemsetAsync(d_cnt, 0, 2 * sizeof(unsigned long long), c->stream));
+    HIPCHK(launch_heavy_count(c->rp, c->n_local, d_cnt, c->stream));
+    unsigned long long nch = 0;
+    HIPCHK(hipMemcpyAsync(&nch, d_cnt, sizeof(nch), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->n_chunks = nch;
+    if (nch) {
+        HIPCHK(hipMalloc((void**)&c->chunks, nch * sizeof(HeavyChunk)));
+        HIPCHK(launch_heavy_fill(c->rp, c->n_local, c->chunks, d_cnt + 1, c->stream));
+    }
+    HIPCHK(hipStreamSynchronize(c->stream));
+    hipFree(d_cnt);
+    if (c->cfg.ping_every && !c->reports) {
+        uint64_t cap = c->cfg.report_capacity ? c->cfg.report_capacity : std::min<uint64_t>(m + (1u << 20), 1ull << 28);
+        c->report_cap = cap;
+        HIPCHK(hipMalloc((void**)&c->reports, cap * sizeof(DeadReport)));
+    }
+    if (c->cfg.ping_every) {
+        hipFree(c->miss);
+        HIPCHK(hipMalloc((void**)&c->miss, m + 1));
+    }
+    c->graph_ready = true;
+    return GOSSIP_OK;
+}
+
+// Literal bootstrap (peer.cpp:63-72,214-253; seed.cpp:117-125): peer i
+// registers with seeds 0..q-1 in file order; each returns the registry
+// {0..i}; power-law k, Fisher-Yates shuffle, first k, skip self; union.
+void host_ref_bootstrap(uint32_t n, uint32_t n_seeds, uint32_t seed, std::vector<uint64_t>& rp,
+                        std::vector<uint32_t>& col) {
+    const uint32_t q = n_seeds / 2 + 1;
+    rp.assign(n + 1, 0);
+    col.clear();
+    std::vector<uint32_t> perm(n);
+    std::vector<uint8_t> chosen(n);
+    std::vector<uint64_t> thr(n + 1);
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t L = i + 1;
+        for (uint32_t j = 0; j < L; ++j) thr[j] = pick_threshold(j, L);
+        std::fill(chosen.begin(), chosen.begin() + L, 0);
+        for (uint32_t s = 0; s < q; ++s) {
+            const uint32_t x = philox4x32_10(P_DEGREE, s, 0, 0, seed, i).x;
+            uint32_t k = 0;
+            for (uint32_t j = 1; j < L; ++j) k += (uint64_t)x >= thr[j];
+            for (uint32_t j = 0; j < L; ++j) perm[j] = j;
+            uint32_t d = 0;
+            for (uint32_t idx = L - 1; idx >= 1; --idx, ++d) {
+                const uint32_t r = lane_of(philox4x32_10(P_SHUFFLE, s, d >> 2, 0, seed, i), d & 3);
+                const uint32_t jj = (uint32_t)(((uint64_t)r * (idx + 1)) >> 32);
+                std::swap(perm[idx], perm[jj]);
+            }
+            for (uint32_t t = 0; t < k; ++t)
+                if (perm[t] != i) chosen[perm[t]] = 1;
+        }
+        rp[i] = col.size();
+        for (uint32_t c = 0; c < L; ++c)
+            if (chosen[c]) col.push_back(c);
+    }
+    rp[n] = col.size();
+}
+
+gossip_status upload_csr(gossip_ctx* c, const uint64_t* rp, const uint32_t* col, uint64_t m) {
+    uint64_t* d_rp = nullptr;
+    uint32_t* d_col = nullptr;
+    HIPCHK(hipMalloc((void**)&d_rp, (c->n_local + 1) * sizeof(uint64_t)));
+    HIPCHK(hipMalloc((void**)&d_col, (m + 1) * sizeof(uint32_t)));
+    HIPCHK(hipMemcpy(d_rp, rp, (c->n_local + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
+    if (m) HIPCHK(hipMemcpy(d_col, col, m * sizeof(uint32_t), hipMemcpyHostToDevice));
+    return install_graph(c, d_rp, d_col, m);
+}
+
+uint32_t kills_in_round(const gossip_ctx* c, uint32_t r, uint32_t* first) {
+    auto lo = std::lower_bound(c->kill_round_sorted.begin(), c->kill_round_sorted.end(), r);
+    auto hi = std::upper_bound(c->kill_round_sorted.begin(), c->kill_round_sorted.end(), r);
+    *first = (uint32_t)(lo - c->kill_round_sorted.begin());
+    return (uint32_t)(hi - lo);
+}
+
+uint32_t injections_in_round(const gossip_ctx* c, uint32_t r, uint32_t* first) {
+    auto lo = std::lower_bound(c->inj_round_sorted.begin(), c->inj_round_sorted.end(), r);
+    auto hi = std::upper_bound(c->inj_round_sorted.begin(), c->inj_round_sorted.end(), r);
+    *first = (uint32_t)(lo - c->inj_round_sorted.begin());
+    return (uint32_t)(hi - lo);
+}
+
+// Round phases up to and including the push.
+gossip_status round_push(gossip_ctx* c, bool remote) {
+    if (!c->graph_ready) return fail(GOSSIP_ESTATE, "no overlay: call gossip_build_graph or gossip_load_csr");
+    if (!c->has_schedule) return fail(GOSSIP_ESTATE, "no schedule: call gossip_inject");
+    if (c->finished) return fail(GOSSIP_ESTATE, "run finished: call gossip_reset");
+    if (c->round >= c->cfg.max_rounds) return fail(GOSSIP_ESTATE, "max_rounds reached");
+    RoundArgs a = make_args(c);
+    const uint32_t pw = pack_w(c);
+    uint32_t first = 0, cnt = kills_in_round(c, c->round, &first);
+    if (cnt) {
+        c->any_dead = true;
+        HIPCHK(timed(c, "kills", [&] { return launch_kills(a, pw, c->d_kill_peer + first, cnt, c->stream); }));
+    }
+    if (c->cfg.churn_threshold) {
+        c->any_dead = true;
+        HIPCHK(timed(c, "churn", [&] { return launch_churn(a, pw, c->cfg.rng_seed, c->cfg.churn_threshold, c->stream); }));
+    }
+    if (c->cfg.ping_every && c->round % c->cfg.ping_every == 0) {
+        HIPCHK(timed(c, "liveness", [&] {
+            hipError_t e = launch_liveness(a, c->stream, 1);
+            return e != hipSuccess ? e : launch_liveness(a, c->stream, 0);
+        }));
+        c->any_masked = true;
+    }
+    cnt = injections_in_round(c, c->round, &first);
+    if (cnt)
+        HIPCHK(timed(c, "inject", [&] {
+            return launch_inject(a, pw, c->d_inj_origin + first, c->d_inj_msg + first, cnt, c->stream);
+        }));
+    if (remote) HIPCHK(hipMemsetAsync(c->send, 0, c->n * c->Wp * sizeof(uint64_t), c->stream));
+    HIPCHK(timed(c, "push_heavy", [&] { return launch_push_heavy(a, pw, c->any_dead, remote, c->stream); }));
+    HIPCHK(timed(c, "push_light", [&] { return launch_push_light(a, pw, c->any_dead, remote, c->stream); }));
+    return GOSSIP_OK;
+}
+
+gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative) {
+    HIPCHK(hipMemcpyAsync(c->h_st, c->st + c->round, sizeof(DevStats), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const DevStats& d = *c->h_st;
+    if (c->timing) {
+        c->kbytes["push_light"] += 32.0 * d.frontier + 20.0 * (double)(d.traversals - d.heavy_traversals);
+        c->kbytes["push_heavy"] += 20.0 * (double)d.heavy_traversals;
+        c->kbytes["liveness"] += 6.125 * (double)d.live_checked;
+    }
+    gossip_round_stats s{};
+    s.round = c->round;
+    s.flags = (c->cfg.ping_every && c->round % c->cfg.ping_every == 0) ? 1u : 0u;
+    s.frontier = d.frontier;
+    s.traversals = d.traversals;
+    s.deliveries = d.deliveries;
+    s.undelivered = d.undelivered;
+    s.new_receipts = d.new_receipts;
+    s.duplicates = d.deliveries - d.new_receipts;
+    s.injected = d.injected;
+    s.died = d.died;
+    s.reports = d.reports;
+    s.seed_removals = d.seed_removals;
+    if (cumulative) {
+        c->cum_digest += d.digest;
+        c->cum_covered += d.covered;
+        s.digest = c->cum_digest;
+        s.covered = c->cum_covered;
+    } else {
+        s.digest = d.digest;
+        s.covered = d.covered;
+    }
+    if (out) *out = s;
+    return GOSSIP_OK;
+}
+
+void advance(gossip_ctx* c, uint64_t fresh_global) {
+    std::swap(c->nw, c->nx);  // nw was cleared by push_light; nx holds the fresh words
+    const uint32_t r = c->round;
+    c->round++;
+    const bool pending = c->has_schedule && c->last_inject_round > r;
+    if ((fresh_global == 0 && !pending && c->round >= c->cfg.min_rounds) || c->round >= c->cfg.max_rounds)
+        c->finished = true;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* gossip_strerror(gossip_status s) {
+    switch (s) {
+        case GOSSIP_OK: return "ok";
+        case GOSSIP_EINVAL: return "invalid argument";
+        case GOSSIP_ENOMEM: return "out of memory";
+        case GOSSIP_EHIP: return "HIP runtime error";
+        case GOSSIP_ESTATE: return "call out of order";
+        case GOSSIP_ENODEV: return "no gfx950 device";
+        case GOSSIP_EOVERFLOW: return "report buffer overflow";
+        default: return "unknown status";
+    }
+}
+
+const char* gossip_last_error(void) { return g_last_error.c_str(); }
+
+gossip_status gossip_create(const gossip_config* cfg, gossip_ctx** out) {
+    if (!cfg || !out) return fail(GOSSIP_EINVAL, "null argument");
+    *out = nullptr;
+    if (cfg->n_peers < 1 || cfg->n_peers > 0x7FFFFFFFull) return fail(GOSSIP_EINVAL, "n_peers out of range");
+    if (cfg->n_msgs < 1 || cfg->n_msgs > 64u * kMaxWords) return fail(GOSSIP_EINVAL, "n_msgs must be 1..512");
+    uint64_t b = cfg->part_begin, e = cfg->part_end;
+    if (b == 0 && e == 0) e = cfg->n_peers;
+    if (b >= e || e > cfg->n_peers) return fail(GOSSIP_EINVAL, "bad partition range");
+    if (cfg->graph_model == GOSSIP_GRAPH_REF_BOOTSTRAP && cfg->n_peers > 4096)
+        return fail(GOSSIP_EINVAL, "ref_bootstrap supports n_peers <= 4096");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(GOSSIP_ENODEV, "no HIP device visible");
+    int dev = cfg->device;
+    if (dev < 0) hipGetDevice(&dev);
+    if (dev >= ndev) return fail(GOSSIP_ENODEV, "device ordinal out of range");
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return fail(GOSSIP_ENODEV, "hipGetDeviceProperties failed");
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(GOSSIP_ENODEV, std::string("libgossip_hip is built for gfx950, device is ") + prop.gcnArchName);
+
+    gossip_ctx* c = new (std::nothrow) gossip_ctx();
+    if (!c) return fail(GOSSIP_ENOMEM, "ctx allocation");
+    c->cfg = *cfg;
+    if (!c->cfg.max_missed) c->cfg.max_missed = 3;
+    if (!c->cfg.max_rounds) c->cfg.max_rounds = 4096;
+    if (!c->cfg.list_len) c->cfg.list_len = 6;
+    if (!c->cfg.n_seeds) c->cfg.n_seeds = 20;
+    if (!c->cfg.graph_model) c->cfg.graph_model = GOSSIP_GRAPH_POWERLAW;
+    c->device = dev;
+    c->n = cfg->n_peers;
+    c->begin = b;
+    c->end = e;
+    c->n_local = e - b;
+    c->M = cfg->n_msgs;
+    c->W = (cfg->n_msgs + 63) / 64;
+    c->Wp = pad_words(c->W);
+    auto bail = [&](const char* what, hipError_t err) {
+        std::string m = std::string(what) + ": " + hipGetErrorString(err);
+        free_state(c);
+        if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
+        delete c;
+        return fail(err == hipErrorOutOfMemory ? GOSSIP_ENOMEM : GOSSIP_EHIP, m);
+    };
+    hipError_t err;
+    if ((err = hipSetDevice(dev)) != hipSuccess) return bail("hipSetDevice", err);
+    if ((err = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) return bail("stream", err);
+    c->own_stream = true;
+    const uint64_t words = c->n_local * c->Wp;
+    const uint64_t bitwords = (c->n + 31) / 32;
+    if ((err = hipMalloc((void**)&c->seen, words * 8)) != hipSuccess) return bail("seen", err);
+    if ((err = hipMalloc((void**)&c->nw, words * 8)) != hipSuccess) return bail("new", err);
+    if ((err = hipMalloc((void**)&c->nx, words * 8)) != hipSuccess) return bail("next", err);
+    if ((err = hipMalloc((void**)&c->alive, bitwords * 4)) != hipSuccess) return bail("alive", err);
+    if ((err = hipMalloc((void**)&c->registered, bitwords * 4)) != hipSuccess) return bail("registry", err);
+    if ((err = hipMalloc((void**)&c->st, (uint64_t)c->cfg.max_rounds * sizeof(DevStats))) != hipSuccess)
+        return bail("stats", err);
+    if ((err = hipHostMalloc((void**)&c->h_st, sizeof(DevStats))) != hipSuccess) return bail("pinned stats", err);
+    if ((err = hipMalloc((void**)&c->n_reports, sizeof(unsigned long long))) != hipSuccess) return bail("nrep", err);
+    if (c->cfg.flags & GOSSIP_FLAG_COVERAGE_HISTORY) {
+        if ((err = hipMalloc((void**)&c->cov_hist, (uint64_t)c->cfg.max_rounds * 64 * c->Wp * 8)) != hipSuccess)
+            return bail("coverage history", err);
+    }
+    *out = c;
+    return gossip_reset(c);
+}
+
+void gossip_destroy(gossip_ctx* c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    drain_timers(c);
+    free_state(c);
+    free_graph(c);
+    hipFree(c->d_inj_origin);
+    hipFree(c->d_inj_msg);
+    hipFree(c->d_kill_peer);
+    if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
+    delete c;
+}
+
+gossip_status gossip_set_stream(gossip_ctx* c, void* s) {
+    if (!c) return fail(GOSSIP_EINVAL, "null ctx");
+    if (set_dev(c)) return GOSSIP_EHIP;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->own_stream) hipStreamDestroy(c->stream);
+    c->stream = (hipStream_t)s;
+    c->own_stream = false;
+    return GOSSIP_OK;
+}
+
+gossip_status gossip_get_shape(gossip_ctx* c, uint32_t* words, uint32_t* exchange_words, uint64_t* n_local,
+                               uint64_t* n_edges) {
+    if (!c) return fail(GOSSIP_EINVAL, "null ctx");
+    if (words) *words = c->W;
+    if (exchange_words) *exchange_words = c->Wp;
+    if (n_local) *n_local = c->n_local;
+    if (n_edges) *n_edges = c->n_edges;
+    return GOSSIP_OK;
+}
+
+gossip_status gossip_build_graph(gossip_ctx* c) {
+    if (!c) return fail(GOSSIP_EINVAL, "null ctx");
+    if (set_dev(c)) return GOSSIP_EHIP;
+    if (c->cfg.graph_model == GOSSIP_GRAPH_REF_BOOTSTRAP) {
+        if (c->n_local != c->n) return fail(GOSSIP_EINVAL, "ref_bootstrap is single-partition");
+        std::vector<uint64_t> rp;
+        std::vector<uint32_t> col;
+        host_ref_bootstrap((uint32_t)c->n, c->cfg.n_seeds, c->cfg.rng_seed, rp, col);
+        return upload_csr(c, rp.data(), col.data(), col.size());
+    }
+    if (c->cfg.graph_model != GOSSIP_GRAPH_POWERLAW) return fail(GOSSIP_EINVAL, "unknown graph_model");
+    if (c->cfg.list_len < 2 || c->cfg.list_len > 64) return fail(GOSSIP_EINVAL, "list_len must be 2..64");
+    if (c->n < 2) return fail(GOSSIP_EINVAL, "powerlaw needs n_peers >= 2");
+    uint64_t* rp = nullptr;
+    uint32_t* col = nullptr;
+    uint64_t m = 0;
+    std::string err;
+    if (build_powerlaw_device(c->n, c->begin, c->end, c->cfg.list_len, c->cfg.rng_seed, &rp, &col, &m, c->stream,
+                              &err) != hipSuccess)
+        return fail(GOSSIP_EHIP, "overlay generator: " + err);
+    return install_graph(c, rp, col, m);
+}
+
+gossip_status gossip_load_csr(gossip_ctx* c, const uint64_t* rp, const uint32_t* col, uint64_t n_rows,
+                              uint64_t n_edges) {
+    if (!c || !rp || (n_edges && !col)) return fail(GOSSIP_EINVAL, "null argument");
+    if (n_rows != c->n_local) return fail(GOSSIP_EINVAL, "n_rows must equal the owned peer count");
+    if (rp[0] != 0 || rp[n_rows] != n_edges) return fail(GOSSIP_EINVAL, "row_ptr must start at 0 and end at n_edges");
+    for (uint64_t v = 0; v < n_rows; ++v) {
+        if (rp[v + 1] < rp[v]) return fail(GOSSIP_EINVAL, "row_ptr not monotone");
+        for (uint64_t e = rp[v]; e < rp[v + 1]; ++e) {
+            if (col[e] >= c->n) return fail(GOSSIP_EINVAL, "col entry out of range");
+            if (col[e] == c->begin + v) return fail(GOSSIP_EINVAL, "self loop");
+            if (e > rp[v] && col[e] <= col[e - 1]) return fail(GOSSIP_EINVAL, "row not sorted/unique");
+        }
+    }
+    if (set_dev(c)) return GOSSIP_EHIP;
+    return upload_csr(c, rp, col, n_edges);
+}
+
+gossip_status gossip_read_csr(gossip_ctx* c, uint64_t* rp, uint32_t* col) {
+    if (!c || !rp || !col) return fail(GOSSIP_EINVAL, "null argument");
+    if (!c->graph_ready) return fail(GOSSIP_ESTATE, "no overlay");
+    if (set_dev(c)) return GOSSIP_EHIP;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipMemcpy(rp, c->rp, (c->n_local + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    if (c->n_edges) HIPCHK(hipMemcpy(col, c->col, c->n_edges * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return GOSSIP_OK;
+}
+
+gossip_status gossip_inject(gossip_ctx* c, const uint32_t* origin, const uint32_t* inject_round, uint32_t n_msgs) {
+    if (!c || !origin || !inject_round) return fail(GOSSIP_EINVAL, "null argument");
+    if (n_msgs != c->M) return fail(GOSSIP_EINVAL, "n_msgs must equal cfg.n_msgs");
+    std::vector<uint32_t> idx(n_msgs);
+    for (uint32_t m = 0; m < n_msgs; ++m) {
+        if (origin[m] >= c->n) return fail(GOSSIP_EINVAL, "origin out of range");
+        idx[m] = m;
+    }
+    std::stable_sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return inject_round[a] < inject_round[b]; });
+    std::vector<uint32_t> o(n_msgs), mid(n_msgs);
+    c->inj_round_sorted.resize(n_msgs);
+    c->last_inject_round = 0;
+    for (uint32_t i = 0; i < n_msgs; ++i) {
+        o[i] = origin[idx[i]];
+        mid[i] = idx[i];
+        c->inj_round_sorted[i] = inject_round[idx[i]];
+        c->last_inject_round = std::max(c->last_inject_round, inject_round[idx[i]]);
+    }
+    c->origin.assign(origin, origin + n_msgs);
+    c->inject_round.assign(inject_round, inject_round + n_msgs);
+    if (set_dev(c)) return GOSSIP_EHIP;
+    hipFree(c->d_inj_origin);
+    hipFree(c->d_inj_msg);
+    c->d_inj_origin = c->d_inj_msg = nullptr;
+    HIPCHK(hipMalloc((void**)&c->d_inj_origin, n_msgs * sizeof(uint32_t)));
+    HIPCHK(hipMalloc((void**)&c->d_inj_msg, n_msgs * sizeof(uint32_t)));
+    HIPCHK(hipMemcpy(c->d_inj_origin, o.data(), n_msgs * sizeof(uint32_t), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d_inj_msg, mid.data(), n_msgs * sizeof(uint32_t), hipMemcpyHostToDevice));
+    c->has_schedule = true;
+    return GOSSIP_OK;
+}
+
+gossip_status gossip_schedule_kills(gossip_ctx* c, const uint32_t* peer, const uint32_t* round, uint32_t n) {
+    if (!c || (n && (!peer || !round))) return fail(GOSSIP_EINVAL, "null argument");
+    std::vector<std::pair<uint32_t, uint32_t>> k(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        if (peer[i] >= c->n) return fail(GOSSIP_EINVAL, "kill peer out of range");
+        k[i] = {round[i], peer[i]};
+    }
+    std::sort(k.begin(), k.end());
+    c->kill_round_sorted.resize(n);
+    std::vector<uint32_t> p(n + 1);
+    for (uint32_t i = 0; i < n; ++i) {
+        c->kill_round_sorted[i] = k[i].first;
+        p[i] = k[i].second;
+    }
+    if (set_dev(c)) return GOSSIP_EHIP;
+    hipFree(c->d_kill_peer);
+    c->d_kill_peer = nullptr;
+    HIPCHK(hipMalloc((void**)&c->d_kill_peer, (n + 1) * sizeof(uint32_t)));
+    HIPCHK(hipMemcpy(c->d_kill_peer, p.data(), (n + 1) * sizeof(uint32_t), hipMemcpyHostToDevice));
+    return GOSSIP_OK;
+}
+
+gossip_status gossip_pick_origins(uint64_t n, uint32_t seed, uint32_t count, uint32_t* out) {
+    if (!out || n == 0) return fail(GOSSIP_EINVAL, "bad argument");
+    for (uint32_t k = 0; k < count; ++k) {
+        for (uint32_t attempt = 0;; ++attempt) {
+            const uint32_t x = philox4x32_10(P_ORIGIN, k, attempt, 0, seed, 0xFFFFFFFFu).x;
+            const uint32_t o = (uint32_t)(((uint64_t)x * n) >> 32);
+            bool dup = false;
+            for (uint32_t i = 0; i < k; ++i) dup |= out[i] == o;
+            if (!dup || (uint64_t)k >= n) {
+                out[k] = o;
+                break;
+            }
+        }
+    }
+    return GOSSIP_OK;
+}
+
+gossip_status gossip_reset(gossip_ctx* c) {
+    if (!c) return fail(GOSSIP_EINVAL, "null ctx");
+    if (set_dev(c)) return GOSSIP_EHIP;
+    hipStream_t s = c->stream;
+    const uint64_t words = c->n_local * c->Wp;
+    const uint64_t bitwords = (c->n + 31) / 32;
+    HIPCHK(hipMemsetAsync(c->seen, 0, words * 8, s));
+    HIPCHK(hipMemsetAsync(c->nw, 0, words * 8, s));
+    HIPCHK(hipMemsetAsync(c->nx, 0, words * 8, s));
+    HIPCHK(hipMemsetAsync(c->alive, 0xFF, bitwords * 4, s));
+    HIPCHK(hipMemsetAsync(c->registered, 0xFF, bitwords * 4, s));
+    if (c->n % 32) {
+        static thread_local uint32_t tail;
+        tail = (1u << (c->n % 32)) - 1u;
+        HIPCHK(hipMemcpyAsync(c->alive + bitwords - 1, &tail, 4, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(c->registered + bitwords - 1, &tail, 4, hipMemcpyHostToDevice, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    HIPCHK(hipMemsetAsync(c->st, 0, (uint64_t)c->cfg.max_rounds * sizeof(DevStats), s));
+    HIPCHK(hipMemsetAsync(c->n_reports, 0, sizeof(unsigned long long), s));
+    if (c->cov_hist) HIPCHK(hipMemsetAsync(c->cov_hist, 0, (uint64_t)c->cfg.max_rounds * 64 * c->Wp * 8, s));
+    if (c->miss) HIPCHK(hipMemsetAsync(c->miss, 0, c->n_edges + 1, s));
+    if (c->any_masked && c->col && c->n_edges) {
+        hipLaunchKernelGGL(k_unmask, dim3(2048), dim3(256), 0, s, c->col, c->n_edges);
+        HIPCHK(hipGetLastError());
+    }
+    c->any_masked = false;
+    c->round = 0;
+    c->finished = false;
+    c->any_dead = false;
+    c->cum_digest = c->cum_covered = 0;
+    HIPCHK(hipStreamSynchronize(s));
+    return GOSSIP_OK;
+}
+
+gossip_status gossip_step(gossip_ctx* c, gossip_round_stats* out) {
+    if (!c) return fail(GOSSIP_EINVAL, "null ctx");
+    if (set_dev(c)) return GOSSIP_EHIP;
+    if (c->world > 1) return fail(GOSSIP_ESTATE, "partitioned ctx: use gossip_round_push/finish/commit");
+    gossip_status s = round_push(c, false);
+    if (s) return s;
+    gossip_round_stats st;
+    if ((s = read_slot(c, &st, true))) return s;
+    if (out) *out = st;
+    advance(c, st.new_receipts);
+    return c->finished ? 1 : 0;
+}
+
+gossip_status gossip_run(gossip_ctx* c, gossip_round_stats* per_round, uint32_t cap, uint32_t* rounds) {
+    if (!c) return fail(GOSSIP_EINVAL, "null ctx");
+    uint32_t k = 0;
+    while (!c->finished) {
+        gossip_round_stats st;
+        gossip_status s = gossip_step(c, &st);
+        if (s < 0) return s;
+        if (per_round && k < cap) per_round[k] = st;
+        ++k;
+    }
+    if (rounds) *rounds = k;
+    return GOSSIP_OK;
+}
+
+gossip_status gossip_set_exchange(gossip_ctx* c, void* send, void* recv, uint32_t world, const uint64_t* pb) {
+    if (!c || !send || !recv || !pb || world < 1) return fail(GOSSIP_EINVAL, "null argument");
+    bool found = false;
+    for (uint32_t p = 0; p < world; ++p) {
+        if (pb[p + 1] < pb[p]) return fail(GOSSIP_EINVAL, "part_begins not monotone");
+        found |= (pb[p] == c->begin && pb[p + 1] == c->end);
+    }
+    if (pb[0] != 0 || pb[world] != c->n || !found) return fail(GOSSIP_EINVAL, "partition table does not match ctx");
+    c->send = (uint64_t*)send;
+    c->recv = (const uint64_t*)recv;
+    c->world = world;
+    c->part_begins.assign(pb, pb + world + 1);
+    return GOSSIP_OK;
+}
+
+gossip_status gossip_round_push(gossip_ctx* c) {
+    if (!c) return fail(GOSSIP_EINVAL, "null ctx");
+    if (!c->send) return fail(GOSSIP_ESTATE, "call gossip_set_exchange first");
+    if (set_dev(c)) return GOSSIP_EHIP;
+    return round_push(c, true);
+}
+
+gossip_status gossip_round_finish(gossip_ctx* c, gossip_round_stats* out) {
+    if (!c) return fail(GOSSIP_EINVAL, "null ctx");
+    if (!c->recv) return fail(GOSSIP_ESTATE, "call gossip_set_exchange first");
+    if (set_dev(c)) return GOSSIP_EHIP;
+    RoundArgs a = make_args(c);
+    HIPCHK(timed(c, "apply_remote",
+                 [&] { return launch_apply_remote(a, pack_w(c), c->recv, c->world, c->n_local, c->stream); }));
+    return read_slot(c, out, false);
+}
+
+gossip_status gossip_round_commit(gossip_ctx* c, uint64_t global_new_receipts, int* finished) {
+    if (!c) return fail(GOSSIP_EINVAL, "null ctx");
+    advance(c, global_new_receipts);
+    if (finished) *finished = c->finished ? 1 : 0;
+    return GOSSIP_OK;
+}
+
+gossip_status gossip_read_seen(gossip_ctx* c, uint64_t* out) {
+    if (!c || !out) return fail(GOSSIP_EINVAL, "null argument");
+    if (set_dev(c)) return GOSSIP_EHIP;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->W == c->Wp) {
+        HIPCHK(hipMemcpy(out, c->seen, c->n_local * c->W * 8, hipMemcpyDeviceToHost));
+        return GOSSIP_OK;
+    }
+    std::vector<uint64_t> tmp(c->n_local * c->Wp);
+    HIPCHK(hipMemcpy(tmp.data(), c->seen, tmp.size() * 8, hipMemcpyDeviceToHost));
+    for (uint64_t v = 0; v < c->n_local; ++v)
+        for (uint32_t w = 0; w < c->W; ++w) out[v * c->W + w] = tmp[v * c->Wp + w];
+    return GOSSIP_OK;
+}
+
+gossip_status gossip_read_coverage(gossip_ctx* c, uint64_t* counts) {
+    if (!c || !counts) return fail(GOSSIP_EINVAL, "null argument");
+    if (set_dev(c)) return GOSSIP_EHIP;
+    unsigned long long* d = nullptr;
+    HIPCHK(hipMalloc((void**)&d, 64 * c->Wp * 8));
+    HIPCHK(hipMemsetAsync(d, 0, 64 * c->Wp * 8, c->stream));
+    HIPCHK(launch_coverage(c->seen, c->n_local, pack_w(c), d, c->stream));
+    std::vector<uint64_t> h(64 * c->Wp);
+    HIPCHK(hipMemcpyAsync(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    hipFree(d);
+    std::memcpy(counts, h.data(), c->M * 8);
+    return GOSSIP_OK;
+}
+
+gossip_status gossip_read_coverage_history(gossip_ctx* c, uint64_t* buf, uint32_t max_rounds, uint32_t* rounds) {
+    if (!c || !buf) return fail(GOSSIP_EINVAL, "null argument");
+    if (!c->cov_hist) return fail(GOSSIP_ESTATE, "ctx created without GOSSIP_FLAG_COVERAGE_HISTORY");
+    if (set_dev(c)) return GOSSIP_EHIP;
+    const uint32_t R = std::min(c->round, max_rounds);
+    std::vector<uint64_t> h((uint64_t)R * 64 * c->Wp);
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (R) HIPCHK(hipMemcpy(h.data(), c->cov_hist, h.size() * 8, hipMemcpyDeviceToHost));
+    std::vector<uint64_t> acc(c->M, 0);
+    for (uint32_t r = 0; r < R; ++r)
+        for (uint32_t m = 0; m < c->M; ++m) {
+            acc[m] += h[(uint64_t)r * 64 * c->Wp + m];
+            buf[(uint64_t)r * c->M + m] = acc[m];
+        }
+    if (rounds) *rounds = R;
+    return GOSSIP_OK;
+}
+
+gossip_status gossip_read_reports(gossip_ctx* c, gossip_dead_report* buf, uint64_t cap, uint64_t* count) {
+    if (!c || !count) return fail(GOSSIP_EINVAL, "null argument");
+    if (set_dev(c)) return GOSSIP_EHIP;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    unsigned long long n = 0;
+    HIPCHK(hipMemcpy(&n, c->n_reports, sizeof(n), hipMemcpyDeviceToHost));
+    *count = n;
+    if (n > c->report_cap) return fail(GOSSIP_EOVERFLOW, "report buffer overflowed");
+    if (!buf || !n) return GOSSIP_OK;
+    std::vector<DeadReport> h(n);
+    HIPCHK(hipMemcpy(h.data(), c->reports, n * sizeof(DeadReport), hipMemcpyDeviceToHost));
+    std::sort(h.begin(), h.end(), [](const DeadReport& x, const DeadReport& y) {
+        if (x.round != y.round) return x.round < y.round;
+        if (x.reporter != y.reporter) return x.reporter < y.reporter;
+        return x.dead < y.dead;
+    });
+    const uint64_t k = std::min<uint64_t>(n, cap);
+    for (uint64_t i = 0; i < k; ++i) buf[i] = gossip_dead_report{h[i].round, h[i].reporter, h[i].dead};
+    return GOSSIP_OK;
+}
+
+static gossip_status read_bits(gossip_ctx* c, const uint32_t* d, uint8_t* out) {
+    if (!c || !out) return fail(GOSSIP_EINVAL, "null argument");
+    if (set_dev(c)) return GOSSIP_EHIP;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    std::vector<uint32_t> h((c->n + 31) / 32);
+    HIPCHK(hipMemcpy(h.data(), d, h.size() * 4, hipMemcpyDeviceToHost));
+    for (uint64_t v = 0; v < c->n; ++v) out[v] = (h[v >> 5] >> (v & 31)) & 1u;
+    return GOSSIP_OK;
+}
+
+gossip_status gossip_read_alive(gossip_ctx* c, uint8_t* out) { return read_bits(c, c ? c->alive : nullptr, out); }
+gossip_status gossip_read_registered(gossip_ctx* c, uint8_t* out) {
+    return read_bits(c, c ? c->registered : nullptr, out);
+}
+
+gossip_status gossip_enable_timing(gossip_ctx* c, int enable) {
+    if (!c) return fail(GOSSIP_EINVAL, "null ctx");
+    if (set_dev(c)) return GOSSIP_EHIP;
+    drain_timers(c);
+    c->timers.clear();
+    c->kbytes.clear();
+    c->timing = enable != 0;
+    return GOSSIP_OK;
+}
+
+gossip_status gossip_kernel_time(gossip_ctx* c, const char* kernel, double* ms, uint64_t* launches) {
+    if (!c || !kernel) return fail(GOSSIP_EINVAL, "null argument");
+    if (set_dev(c)) return GOSSIP_EHIP;
+    drain_timers(c);
+    auto it = c->timers.find(kernel);
+    if (ms) *ms = it == c->timers.end() ? 0.0 : it->second.ms;
+    if (launches) *launches = it == c->timers.end() ? 0 : it->second.launches;
+    return GOSSIP_OK;
+}
+
+gossip_status gossip_kernel_bytes(gossip_ctx* c, const char* kernel, double* bytes) {
+    if (!c || !kernel || !bytes) return fail(GOSSIP_EINVAL, "null argument");
+    auto it = c->kbytes.find(kernel);
+    *bytes = it == c->kbytes.end() ? 0.0 : it->second;
+    return GOSSIP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,81 @@
+// gossip_internal.hpp -- internal (non-ABI) declarations of libgossip_hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+namespace gossip {
+
+constexpr uint32_t kMaskedEdge = 0x80000000u;  // col[e] bit 31: edge dropped by liveness (peer.cpp:388)
+constexpr uint32_t kHeavyDegree = 256;         // rows longer than this go to the edge-chunked kernel
+constexpr uint32_t kHeavyChunk = 2048;         // edges per heavy chunk (one workgroup)
+constexpr int kBlock = 256;                    // 4 waves of 64
+constexpr int kMaxWords = 8;                   // M <= 512 concurrent messages
+
+// Per-round device counters (all integer; order-independent sums).
+struct DevStats {
+    unsigned long long frontier, traversals, deliveries, undelivered, new_receipts, injected, died, reports,
+        seed_removals, digest, covered, heavy_traversals, live_checked, pad[3];
+};
+static_assert(sizeof(DevStats) == 128, "DevStats layout");
+
+struct HeavyChunk {
+    uint32_t v;    // local row
+    uint32_t pad;
+    uint64_t e0, e1;
+};
+
+struct DeadReport {
+    uint32_t round, reporter, dead;
+};
+
+// Everything a round kernel needs; passed by value.
+struct RoundArgs {
+    const uint64_t* rp;     // n_local + 1 local offsets
+    uint32_t* col;          // global ids, bit 31 = masked
+    uint32_t* alive;        // global bitset (n_global bits)
+    uint32_t* registered;   // global bitset (seed registry view)
+    uint64_t* seen;         // n_local * W
+    uint64_t* nw;           // this round's new words (sources); cleared by push_light
+    uint64_t* nx;           // next round's new words (fresh)
+    uint64_t* send;         // dense remote staging (n_global * W) or null
+    uint8_t* miss;          // per-edge miss counters
+    DevStats* st;           // this round's slot
+    unsigned long long* cov;  // per-message coverage increments of this round (history) or null
+    const HeavyChunk* chunks;
+    uint64_t n_chunks;
+    uint64_t n_local, begin, end, n_global;
+    DeadReport* reports;
+    unsigned long long* n_reports;
+    uint64_t report_cap;
+    uint32_t round;
+    uint32_t max_missed;
+};
+
+// ---- launchers (gossip_kernels.hip) ----
+hipError_t launch_churn(const RoundArgs& a, uint32_t W, uint32_t seed, uint32_t threshold, hipStream_t s);
+hipError_t launch_kills(const RoundArgs& a, uint32_t W, const uint32_t* kill_peers, uint32_t n, hipStream_t s);
+hipError_t launch_liveness(const RoundArgs& a, hipStream_t s, int heavy);
+hipError_t launch_inject(const RoundArgs& a, uint32_t W, const uint32_t* origin, const uint32_t* msg_id, uint32_t n,
+                         hipStream_t s);
+hipError_t launch_push_heavy(const RoundArgs& a, uint32_t W, bool check_alive, bool remote, hipStream_t s);
+hipError_t launch_push_light(const RoundArgs& a, uint32_t W, bool check_alive, bool remote, hipStream_t s);
+hipError_t launch_apply_remote(const RoundArgs& a, uint32_t W, const uint64_t* recv, uint32_t world,
+                               uint64_t part_stride, hipStream_t s);
+hipError_t launch_coverage(const uint64_t* words, uint64_t n_local, uint32_t W, unsigned long long* counts,
+                           hipStream_t s);
+hipError_t launch_heavy_count(const uint64_t* rp, uint64_t n_local, unsigned long long* n_chunks, hipStream_t s);
+hipError_t launch_heavy_fill(const uint64_t* rp, uint64_t n_local, HeavyChunk* chunks, unsigned long long* cursor,
+                             hipStream_t s);
+
+// ---- overlay generator (gossip_graph.hip) ----
+// Builds the owned rows of the powerlaw overlay on the device.  On success
+// *rp (n_local+1) and *col (n_edges) are device allocations owned by the caller.
+hipError_t build_powerlaw_device(uint64_t n_global, uint64_t begin, uint64_t end, uint32_t list_len, uint32_t seed,
+                                 uint64_t** rp, uint32_t** col, uint64_t* n_edges, hipStream_t s, std::string* err);
+
+// Exact integer threshold ceil(2^32 (j/L)^2.5) (host only).
+uint64_t pick_threshold(uint32_t j, uint32_t L);
+
+}  // namespace gossip

@@ -1,0 +1,569 @@
+// gossip_kernels.hip -- round kernels of libgossip_hip for gfx950 (CDNA4).
+//
+// One round of the reference's recursion
+//   broadcastMessage (peer.cpp:297-318) -> handleClient (peer.cpp:255-295)
+// over ALL peers at once, plus liveness (peer.cpp:320-355, 381-405) and
+// churn.  Everything is integer; results do not depend on atomic order.
+//
+// Layout: CSR rows of the owned peers (row_ptr u64,
+// col u32 global ids, bit 31 = edge masked by liveness); seen/new/next as
+// Wp u64 words per peer (bit m = message m); alive and registry as global
+// bitsets.  Work mapping: one wave64 per tile of 64 consecutive peers with
+// an in-wave prefix sum over row lengths ("edge-space expansion"), so the
+// wave's lanes walk consecutive col entries of the tile -- one contiguous
+// span when the tile's rows are all active; rows longer than kHeavyDegree
+// are cut into kHeavyChunk-edge chunks, one workgroup each.
+#include <hip/hip_runtime.h>
+
+#include "gossip_internal.hpp"
+#include "philox.hpp"
+
+namespace gossip {
+
+namespace {
+
+constexpr int kWavesPerBlock = kBlock / 64;
+constexpr unsigned kMaxGrid = 2048;  // 256 CUs x 8 blocks of 256 threads
+
+__device__ __forceinline__ bool bit_alive(const uint32_t* bits, uint32_t v) { return (bits[v >> 5] >> (v & 31)) & 1u; }
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+    return x;
+}
+
+__device__ __forceinline__ uint32_t lane_rank(unsigned long long mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+struct Acc {
+    unsigned long long frontier = 0, trav = 0, deliv = 0, undeliv = 0, fresh = 0, digest = 0, covered = 0, died = 0,
+                       reports = 0, removals = 0, injected = 0, htrav = 0, checked = 0;
+};
+
+// One atomic per nonzero field per wave.
+__device__ __forceinline__ void flush(Acc& acc, DevStats* st) {
+    const int lane = threadIdx.x & 63;
+#define GOSSIP_FLUSH(field, dst)                                   \
+    {                                                              \
+        const unsigned long long s_ = wave_sum(acc.field);         \
+        if (lane == 0 && s_) atomicAdd(&st->dst, s_);              \
+    }
+    GOSSIP_FLUSH(frontier, frontier)
+    GOSSIP_FLUSH(trav, traversals)
+    GOSSIP_FLUSH(deliv, deliveries)
+    GOSSIP_FLUSH(undeliv, undelivered)
+    GOSSIP_FLUSH(fresh, new_receipts)
+    GOSSIP_FLUSH(digest, digest)
+    GOSSIP_FLUSH(covered, covered)
+    GOSSIP_FLUSH(died, died)
+    GOSSIP_FLUSH(reports, reports)
+    GOSSIP_FLUSH(removals, seed_removals)
+    GOSSIP_FLUSH(injected, injected)
+    GOSSIP_FLUSH(htrav, heavy_traversals)
+    GOSSIP_FLUSH(checked, live_checked)
+#undef GOSSIP_FLUSH
+}
+
+// Edge-space expansion of one tile (64 rows, one wave).  deg = this lane's
+// row length (0 = skip), rb = its row begin.  f(src_lane, valid, e) runs once
+// per 64-edge batch in every lane (so it may shuffle); valid lanes own edge e.
+template <class F>
+__device__ __forceinline__ void tile_edges(uint32_t deg, uint64_t rb, F&& f) {
+    const int lane = threadIdx.x & 63;
+    uint32_t incl = deg;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off);
+        if (lane >= off) incl += y;
+    }
+    const uint32_t excl = incl - deg;
+    const uint32_t total = __shfl(incl, 63);
+    for (uint32_t base = 0; base < total; base += 64) {
+        const uint32_t p = base + lane;
+        int s = 0;  // number of rows whose inclusive end <= p  == source lane
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1) {
+            const uint32_t val = __shfl(incl, s + step - 1);
+            if (val <= p) s += step;
+        }
+        const uint32_t ex = __shfl(excl, s);
+        const uint64_t rbs = __shfl(rb, s);
+        f(s, p < total, rbs + (uint64_t)(p - ex));
+    }
+}
+
+// handleClient's dedup (peer.cpp:277-285) as a 64-bit test-and-set: deliver
+// the source's new words m to peer c.  A plain read first: seen only grows
+// within a round, so a stale read can only cost an extra atomic, never a
+// wrong answer.
+template <int W, bool CA, bool RM>
+__device__ __forceinline__ void deliver(const RoundArgs& a, uint32_t c, const uint64_t (&m)[W], uint32_t pc,
+                                        Acc& acc) {
+    if (c & kMaskedEdge) return;  // connectedPeers.erase'd (peer.cpp:388)
+    acc.trav++;
+    if (CA && !bit_alive(a.alive, c)) {  // send() to a dead peer fails (peer.cpp:312)
+        acc.undeliv += pc;
+        return;
+    }
+    acc.deliv += pc;  // sentTo.insert (peer.cpp:314)
+    if (RM && (c < a.begin || c >= a.end)) {
+        unsigned long long* dst = reinterpret_cast<unsigned long long*>(a.send) + (uint64_t)c * W;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            if (!m[w]) continue;
+            const unsigned long long cur = dst[w];
+            if ((cur & m[w]) != m[w]) atomicOr(dst + w, (unsigned long long)m[w]);
+        }
+        return;
+    }
+    const uint64_t lv = (uint64_t)(c - (uint32_t)a.begin);
+    unsigned long long* sp = reinterpret_cast<unsigned long long*>(a.seen) + lv * W;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        if (!m[w]) continue;
+        const unsigned long long cur = sp[w];
+        if (!(m[w] & ~cur)) continue;  // all duplicates: dropped (peer.cpp:281)
+        const unsigned long long old = atomicOr(sp + w, (unsigned long long)m[w]);
+        const unsigned long long fr = m[w] & ~old;
+        if (fr) {
+            atomicOr(reinterpret_cast<unsigned long long*>(a.nx) + lv * W + w, fr);
+            acc.fresh += (unsigned long long)__popcll(fr);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// push: light rows (<= kHeavyDegree), one wave per 64-peer tile.  Also the
+// round's push-start bookkeeping: frontier, digest and coverage increments
+// (the new words ARE the bits added to seen since the last push start).
+// ---------------------------------------------------------------------------
+template <int W, bool CA, bool RM, bool COV>
+__global__ __launch_bounds__(kBlock) void k_push_light(RoundArgs a, uint32_t wd) {
+    __shared__ unsigned int cov_s[COV ? 64 * W : 1];
+    if (COV) {
+        for (int i = threadIdx.x; i < 64 * W; i += kBlock) cov_s[i] = 0;
+        __syncthreads();
+    }
+    Acc acc;
+    const int lane = threadIdx.x & 63;
+    const uint64_t n_tiles = (a.n_local + 63) >> 6;
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); t < n_tiles; t += nwaves) {
+        const uint64_t v = (t << 6) + lane;
+        uint64_t m[W];
+        bool act = false;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            m[w] = v < a.n_local ? a.nw[v * W + w] : 0ull;
+            act |= m[w] != 0;
+        }
+        if (!__any(act)) continue;
+        uint32_t pc = 0, deg = 0;
+        uint64_t rb = 0;
+        if (act) {
+            acc.frontier++;
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                pc += (uint32_t)__popcll(m[w]);
+                if (w < (int)wd) acc.digest += digest_weight((a.begin + v) * wd + w) * m[w];
+                a.nw[v * W + w] = 0ull;  // consumed: this buffer is next round's accumulator
+                if (COV) {
+                    for (uint64_t x = m[w]; x; x &= x - 1) atomicAdd(&cov_s[w * 64 + __builtin_ctzll(x)], 1u);
+                }
+            }
+            acc.covered += pc;
+            rb = a.rp[v];
+            const uint64_t d = a.rp[v + 1] - rb;
+            deg = d <= kHeavyDegree ? (uint32_t)d : 0u;
+        }
+        tile_edges(deg, rb, [&](int s, bool valid, uint64_t e) {
+            uint64_t ms[W];
+#pragma unroll
+            for (int w = 0; w < W; ++w) ms[w] = __shfl(m[w], s);
+            const uint32_t pcs = __shfl(pc, s);
+            if (valid) deliver<W, CA, RM>(a, a.col[e], ms, pcs, acc);
+        });
+    }
+    flush(acc, a.st);
+    if (COV) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < 64 * W; i += kBlock)
+            if (cov_s[i]) atomicAdd(&a.cov[i], (unsigned long long)cov_s[i]);
+    }
+}
+
+// push: heavy rows, one workgroup per kHeavyChunk-edge chunk; runs before
+// k_push_light (which clears the new words).
+template <int W, bool CA, bool RM>
+__global__ __launch_bounds__(kBlock) void k_push_heavy(RoundArgs a) {
+    Acc acc;
+    for (uint64_t ci = blockIdx.x; ci < a.n_chunks; ci += gridDim.x) {
+        const HeavyChunk ch = a.chunks[ci];
+        uint64_t m[W];
+        bool act = false;
+        uint32_t pc = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            m[w] = a.nw[(uint64_t)ch.v * W + w];
+            act |= m[w] != 0;
+            pc += (uint32_t)__popcll(m[w]);
+        }
+        if (!act) continue;  // uniform over the workgroup
+        for (uint64_t e = ch.e0 + threadIdx.x; e < ch.e1; e += kBlock) deliver<W, CA, RM>(a, a.col[e], m, pc, acc);
+    }
+    acc.htrav = acc.trav;
+    flush(acc, a.st);
+}
+
+// ---------------------------------------------------------------------------
+// liveness (pingLoop peer.cpp:328-346 -> handleDeadPeer :383-397 ->
+// SeedNode::handleDeadNode seed.cpp:158-167)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void ping_edge(const RoundArgs& a, bool valid, uint64_t e, bool& emit, uint32_t& dead,
+                                          unsigned long long& checked) {
+    emit = false;
+    dead = 0;
+    if (!valid) return;
+    const uint32_t c = a.col[e];
+    if (c & kMaskedEdge) return;
+    checked++;
+    if (bit_alive(a.alive, c)) {  // ping ok: failedAttempts = 0 (:340-341)
+        if (a.miss[e]) a.miss[e] = 0;
+        return;
+    }
+    uint32_t mm = a.miss[e];
+    if (mm < 255) ++mm;  // failedAttempts++ (:336)
+    a.miss[e] = (uint8_t)mm;
+    if (mm >= a.max_missed) {  // >= 3 -> dead (:337)
+        a.col[e] = c | kMaskedEdge;
+        emit = true;
+        dead = c;
+    }
+}
+
+// Wave-aggregated append of dead-node reports + registry removal.
+__device__ __forceinline__ void emit_reports(const RoundArgs& a, bool emit, uint32_t reporter, uint32_t dead,
+                                             Acc& acc) {
+    const unsigned long long mask = __ballot(emit);
+    if (!mask) return;
+    const int lane = threadIdx.x & 63;
+    const int leader = __builtin_ctzll(mask);
+    unsigned long long base = 0;
+    if (lane == leader) base = atomicAdd(a.n_reports, (unsigned long long)__popcll(mask));
+    base = __shfl(base, leader);
+    if (emit) {
+        const unsigned long long idx = base + lane_rank(mask);
+        if (idx < a.report_cap) a.reports[idx] = DeadReport{a.round, reporter, dead};
+        acc.reports++;
+        const uint32_t bit = 1u << (dead & 31);
+        const uint32_t old = atomicAnd(&a.registered[dead >> 5], ~bit);
+        if (old & bit) acc.removals++;  // peerList.erase > 0 (seed.cpp:162)
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_liveness_light(RoundArgs a) {
+    Acc acc;
+    const int lane = threadIdx.x & 63;
+    const uint64_t n_tiles = (a.n_local + 63) >> 6;
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); t < n_tiles; t += nwaves) {
+        const uint64_t v = (t << 6) + lane;
+        const bool act = v < a.n_local && bit_alive(a.alive, (uint32_t)(a.begin + v));
+        if (!__any(act)) continue;
+        uint32_t deg = 0;
+        uint64_t rb = 0;
+        if (act) {
+            rb = a.rp[v];
+            const uint64_t d = a.rp[v + 1] - rb;
+            deg = d <= kHeavyDegree ? (uint32_t)d : 0u;
+        }
+        const uint32_t tile_base = (uint32_t)(a.begin + (t << 6));
+        tile_edges(deg, rb, [&](int s, bool valid, uint64_t e) {
+            bool emit;
+            uint32_t dead;
+            ping_edge(a, valid, e, emit, dead, acc.checked);
+            emit_reports(a, emit, tile_base + (uint32_t)s, dead, acc);
+        });
+    }
+    flush(acc, a.st);
+}
+
+__global__ __launch_bounds__(kBlock) void k_liveness_heavy(RoundArgs a) {
+    Acc acc;
+    for (uint64_t ci = blockIdx.x; ci < a.n_chunks; ci += gridDim.x) {
+        const HeavyChunk ch = a.chunks[ci];
+        const uint32_t u = (uint32_t)(a.begin + ch.v);
+        if (!bit_alive(a.alive, u)) continue;
+        for (uint64_t base = ch.e0; base < ch.e1; base += kBlock) {
+            const uint64_t e = base + threadIdx.x;
+            bool emit;
+            uint32_t dead;
+            ping_edge(a, e < ch.e1, e, emit, dead, acc.checked);
+            emit_reports(a, emit, u, dead, acc);
+        }
+    }
+    flush(acc, a.st);
+}
+
+// ---------------------------------------------------------------------------
+// churn / kills: a dead peer stops receiving, forwarding and pinging.  Its
+// pending new words are dropped, but they are already in seen, so their
+// digest/coverage contribution is booked here.
+// ---------------------------------------------------------------------------
+template <int W>
+__device__ __forceinline__ void retire_peer(const RoundArgs& a, uint32_t v, uint32_t wd, Acc& acc) {
+    if (v < a.begin || v >= a.end) return;
+    acc.died++;
+    const uint64_t lv = v - a.begin;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        const uint64_t mm = a.nw[lv * W + w];
+        if (!mm) continue;
+        if (w < (int)wd) acc.digest += digest_weight((uint64_t)v * wd + w) * mm;
+        acc.covered += (unsigned long long)__popcll(mm);
+        if (a.cov)
+            for (uint64_t x = mm; x; x &= x - 1) atomicAdd(&a.cov[w * 64 + __builtin_ctzll(x)], 1ull);
+        a.nw[lv * W + w] = 0ull;
+    }
+}
+
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_churn(RoundArgs a, uint32_t wd, uint32_t seed, uint32_t thr) {
+    Acc acc;
+    const uint64_t n_words = (a.n_global + 31) >> 5;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n_words; i += (uint64_t)gridDim.x * kBlock) {
+        const uint32_t word = a.alive[i];
+        if (!word) continue;
+        uint32_t dead = 0;
+        for (uint32_t x = word; x; x &= x - 1) {
+            const uint32_t b = (uint32_t)__builtin_ctz(x);
+            const uint32_t v = (uint32_t)(i * 32 + b);
+            if (philox4x32_10(P_CHURN, a.round, 0, 0, seed, v).x < thr) dead |= 1u << b;
+        }
+        if (!dead) continue;
+        a.alive[i] = word & ~dead;
+        for (uint32_t x = dead; x; x &= x - 1) retire_peer<W>(a, (uint32_t)(i * 32 + __builtin_ctz(x)), wd, acc);
+    }
+    flush(acc, a.st);
+}
+
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_kills(RoundArgs a, uint32_t wd, const uint32_t* peers, uint32_t n) {
+    Acc acc;
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    bool died = false;
+    uint32_t v = 0;
+    if (i < n) {
+        v = peers[i];
+        const uint32_t bit = 1u << (v & 31);
+        died = (atomicAnd(&a.alive[v >> 5], ~bit) & bit) != 0;
+    }
+    if (died) retire_peer<W>(a, v, wd, acc);
+    flush(acc, a.st);
+}
+
+// messageGenerationLoop (peer.cpp:359-374): origin marks the message seen and
+// will push it this round.
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_inject(RoundArgs a, const uint32_t* origin, const uint32_t* msg_id,
+                                                    uint32_t n) {
+    Acc acc;
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) {
+        const uint32_t o = origin[i];
+        if (o >= a.begin && o < a.end && bit_alive(a.alive, o)) {
+            const uint32_t m = msg_id[i];
+            const uint64_t idx = (uint64_t)(o - a.begin) * W + (m >> 6);
+            const unsigned long long bit = 1ull << (m & 63);
+            atomicOr(reinterpret_cast<unsigned long long*>(a.seen) + idx, bit);
+            atomicOr(reinterpret_cast<unsigned long long*>(a.nw) + idx, bit);
+            acc.injected++;
+        }
+    }
+    flush(acc, a.st);
+}
+
+// Partitioned rounds: OR the masks received from every rank into the owned
+// peers (test-and-set without atomics: this kernel is the only writer).
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_apply_remote(RoundArgs a, const uint64_t* recv, uint32_t world,
+                                                         uint64_t stride) {
+    Acc acc;
+    for (uint64_t v = (uint64_t)blockIdx.x * kBlock + threadIdx.x; v < a.n_local; v += (uint64_t)gridDim.x * kBlock) {
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            uint64_t inc = 0;
+            for (uint32_t p = 0; p < world; ++p) inc |= recv[((uint64_t)p * stride + v) * W + w];
+            if (!inc) continue;
+            const uint64_t cur = a.seen[v * W + w];
+            const uint64_t fr = inc & ~cur;
+            if (!fr) continue;
+            a.seen[v * W + w] = cur | fr;
+            a.nx[v * W + w] |= fr;
+            acc.fresh += (unsigned long long)__popcll(fr);
+        }
+    }
+    flush(acc, a.st);
+}
+
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_coverage(const uint64_t* words, uint64_t n, unsigned long long* counts) {
+    __shared__ unsigned int cnt[64 * W];
+    for (int i = threadIdx.x; i < 64 * W; i += kBlock) cnt[i] = 0;
+    __syncthreads();
+    for (uint64_t v = (uint64_t)blockIdx.x * kBlock + threadIdx.x; v < n; v += (uint64_t)gridDim.x * kBlock) {
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+            for (uint64_t x = words[v * W + w]; x; x &= x - 1) atomicAdd(&cnt[w * 64 + __builtin_ctzll(x)], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 64 * W; i += kBlock)
+        if (cnt[i]) atomicAdd(&counts[i], (unsigned long long)cnt[i]);
+}
+
+__global__ void k_heavy_count(const uint64_t* rp, uint64_t n, unsigned long long* n_chunks) {
+    unsigned long long mine = 0;
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t d = rp[v + 1] - rp[v];
+        if (d > kHeavyDegree) mine += (d + kHeavyChunk - 1) / kHeavyChunk;
+    }
+    mine = wave_sum(mine);
+    if ((threadIdx.x & 63) == 0 && mine) atomicAdd(n_chunks, mine);
+}
+
+__global__ void k_heavy_fill(const uint64_t* rp, uint64_t n, HeavyChunk* chunks, unsigned long long* cursor) {
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t b = rp[v], e = rp[v + 1];
+        if (e - b <= kHeavyDegree) continue;
+        const uint64_t nc = (e - b + kHeavyChunk - 1) / kHeavyChunk;
+        const unsigned long long at = atomicAdd(cursor, (unsigned long long)nc);
+        for (uint64_t k = 0; k < nc; ++k) {
+            const uint64_t e0 = b + k * kHeavyChunk;
+            chunks[at + k] = HeavyChunk{(uint32_t)v, 0u, e0, e0 + kHeavyChunk < e ? e0 + kHeavyChunk : e};
+        }
+    }
+}
+
+unsigned grid_for(uint64_t items, uint64_t per_block) {
+    uint64_t g = (items + per_block - 1) / per_block;
+    if (g < 1) g = 1;
+    if (g > kMaxGrid) g = kMaxGrid;
+    return (unsigned)g;
+}
+
+
+}  // namespace
+
+// ---- launchers: dispatch the padded word count Wp in {1,2,4,8} ------------
+#define GOSSIP_DISPATCH_W(Wp, CALL)                     \
+    switch (Wp) {                                       \
+        case 1: { constexpr int W = 1; CALL; } break;   \
+        case 2: { constexpr int W = 2; CALL; } break;   \
+        case 4: { constexpr int W = 4; CALL; } break;   \
+        case 8: { constexpr int W = 8; CALL; } break;   \
+        default: return hipErrorInvalidValue;           \
+    }
+
+// Wp is the padded storage stride; the digest uses the unpadded W carried in
+// the upper 16 bits of the W argument (see gossip_engine.hip: pack_w).
+static inline uint32_t wp_of(uint32_t w) { return w & 0xFFFFu; }
+static inline uint32_t wd_of(uint32_t w) { return w >> 16; }
+
+hipError_t launch_churn(const RoundArgs& a, uint32_t W_, uint32_t seed, uint32_t threshold, hipStream_t s) {
+    const unsigned g = grid_for((a.n_global + 31) / 32, kBlock);
+    GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_churn<W>, dim3(g), dim3(kBlock), 0, s, a, wd_of(W_), seed,
+                                                   threshold));
+    return hipGetLastError();
+}
+
+hipError_t launch_kills(const RoundArgs& a, uint32_t W_, const uint32_t* peers, uint32_t n, hipStream_t s) {
+    if (!n) return hipSuccess;
+    const unsigned g = (n + kBlock - 1) / kBlock;
+    GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_kills<W>, dim3(g), dim3(kBlock), 0, s, a, wd_of(W_), peers, n));
+    return hipGetLastError();
+}
+
+hipError_t launch_liveness(const RoundArgs& a, hipStream_t s, int heavy) {
+    if (heavy) {
+        if (!a.n_chunks) return hipSuccess;
+        hipLaunchKernelGGL(k_liveness_heavy, dim3(grid_for(a.n_chunks, 1)), dim3(kBlock), 0, s, a);
+    } else {
+        const uint64_t tiles = (a.n_local + 63) / 64;
+        hipLaunchKernelGGL(k_liveness_light, dim3(grid_for(tiles, kWavesPerBlock)), dim3(kBlock), 0, s, a);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_inject(const RoundArgs& a, uint32_t W_, const uint32_t* origin, const uint32_t* msg_id, uint32_t n,
+                         hipStream_t s) {
+    if (!n) return hipSuccess;
+    const unsigned g = (n + kBlock - 1) / kBlock;
+    GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_inject<W>, dim3(g), dim3(kBlock), 0, s, a, origin, msg_id, n));
+    return hipGetLastError();
+}
+
+hipError_t launch_push_heavy(const RoundArgs& a, uint32_t W_, bool check_alive, bool remote, hipStream_t s) {
+    if (!a.n_chunks) return hipSuccess;
+    const unsigned g = grid_for(a.n_chunks, 1);
+#define GOSSIP_HEAVY(CA, RM) hipLaunchKernelGGL((k_push_heavy<W, CA, RM>), dim3(g), dim3(kBlock), 0, s, a)
+    GOSSIP_DISPATCH_W(wp_of(W_), {
+        if (check_alive) {
+            if (remote) GOSSIP_HEAVY(true, true); else GOSSIP_HEAVY(true, false);
+        } else {
+            if (remote) GOSSIP_HEAVY(false, true); else GOSSIP_HEAVY(false, false);
+        }
+    });
+#undef GOSSIP_HEAVY
+    return hipGetLastError();
+}
+
+hipError_t launch_push_light(const RoundArgs& a, uint32_t W_, bool check_alive, bool remote, hipStream_t s) {
+    const uint64_t tiles = (a.n_local + 63) / 64;
+    const unsigned g = grid_for(tiles, kWavesPerBlock);
+    const uint32_t wd = wd_of(W_);
+    const bool cov = a.cov != nullptr;
+#define GOSSIP_LIGHT(CA, RM, COV) \
+    hipLaunchKernelGGL((k_push_light<W, CA, RM, COV>), dim3(g), dim3(kBlock), 0, s, a, wd)
+    GOSSIP_DISPATCH_W(wp_of(W_), {
+        if (cov) {
+            if (check_alive) { if (remote) GOSSIP_LIGHT(true, true, true); else GOSSIP_LIGHT(true, false, true); }
+            else { if (remote) GOSSIP_LIGHT(false, true, true); else GOSSIP_LIGHT(false, false, true); }
+        } else {
+            if (check_alive) { if (remote) GOSSIP_LIGHT(true, true, false); else GOSSIP_LIGHT(true, false, false); }
+            else { if (remote) GOSSIP_LIGHT(false, true, false); else GOSSIP_LIGHT(false, false, false); }
+        }
+    });
+#undef GOSSIP_LIGHT
+    return hipGetLastError();
+}
+
+hipError_t launch_apply_remote(const RoundArgs& a, uint32_t W_, const uint64_t* recv, uint32_t world,
+                               uint64_t part_stride, hipStream_t s) {
+    const unsigned g = grid_for(a.n_local, kBlock);
+    GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_apply_remote<W>, dim3(g), dim3(kBlock), 0, s, a, recv, world,
+                                                   part_stride));
+    return hipGetLastError();
+}
+
+hipError_t launch_coverage(const uint64_t* words, uint64_t n_local, uint32_t W_, unsigned long long* counts,
+                           hipStream_t s) {
+    const unsigned g = grid_for(n_local, kBlock);
+    GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_coverage<W>, dim3(g), dim3(kBlock), 0, s, words, n_local,
+                                                   counts));
+    return hipGetLastError();
+}
+
+hipError_t launch_heavy_count(const uint64_t* rp, uint64_t n_local, unsigned long long* n_chunks, hipStream_t s) {
+    hipLaunchKernelGGL(k_heavy_count, dim3(grid_for(n_local, kBlock)), dim3(kBlock), 0, s, rp, n_local, n_chunks);
+    return hipGetLastError();
+}
+
+hipError_t launch_heavy_fill(const uint64_t* rp, uint64_t n_local, HeavyChunk* chunks, unsigned long long* cursor,
+                             hipStream_t s) {
+    hipLaunchKernelGGL(k_heavy_fill, dim3(grid_for(n_local, kBlock)), dim3(kBlock), 0, s, rp, n_local, chunks, cursor);
+    return hipGetLastError();
+}
+
+}  // namespace gossip

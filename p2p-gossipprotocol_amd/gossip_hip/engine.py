@@ -1,0 +1,212 @@
+"""Engine: a thin owner of one gossip_ctx (one vertex partition in HBM).
+
+Mirrors the reference's per-peer surface at simulation scale: the overlay
+(selectAndConnectPeers, peer.cpp:214-253), message generation
+(messageGenerationLoop, peer.cpp:357-379), forwarding + Message-List dedup
+(broadcastMessage/handleClient, peer.cpp:255-318) and liveness
+(pingLoop/handleDeadPeer, peer.cpp:320-405) all run inside libgossip_hip.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _abi
+from ._abi import DeadReport, GossipConfig, RoundStats, check
+
+_GRAPHS = {"powerlaw": _abi.GRAPH_POWERLAW, "ref_bootstrap": _abi.GRAPH_REF_BOOTSTRAP}
+KERNELS = ("push_light", "push_heavy", "liveness", "churn", "kills", "inject", "apply_remote")
+
+
+def _u32(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.uint32))
+
+
+def _ptr(a: np.ndarray, ctype):
+    return a.ctypes.data_as(C.POINTER(ctype))
+
+
+def pick_origins(n_peers: int, rng_seed: int, count: int) -> np.ndarray:
+    out = np.zeros(max(count, 1), dtype=np.uint32)
+    check(_abi.lib().gossip_pick_origins(n_peers, rng_seed, count, _ptr(out, C.c_uint32)), "gossip_pick_origins")
+    return out[:count]
+
+
+class Engine:
+    def __init__(self, n_peers: int, n_msgs: int, *, rng_seed: int = 0, graph: str = "powerlaw", list_len: int = 6,
+                 n_seeds: int = 20, churn_threshold: int = 0, ping_every: int = 0, max_missed: int = 3,
+                 max_rounds: int = 4096, min_rounds: int = 0, device: int = -1, coverage_history: bool = False,
+                 part: tuple[int, int] = (0, 0), report_capacity: int = 0):
+        self._L = _abi.lib()
+        cfg = GossipConfig()
+        cfg.n_peers = n_peers
+        cfg.part_begin, cfg.part_end = part
+        cfg.n_msgs = n_msgs
+        cfg.rng_seed = rng_seed
+        cfg.graph_model = _GRAPHS[graph]
+        cfg.list_len = list_len
+        cfg.n_seeds = n_seeds
+        cfg.churn_threshold = churn_threshold
+        cfg.ping_every = ping_every
+        cfg.max_missed = max_missed
+        cfg.max_rounds = max_rounds
+        cfg.min_rounds = min_rounds
+        cfg.device = device
+        cfg.flags = _abi.FLAG_COVERAGE_HISTORY if coverage_history else 0
+        cfg.report_capacity = report_capacity
+        self.cfg = cfg
+        ctx = C.c_void_p()
+        check(self._L.gossip_create(C.byref(cfg), C.byref(ctx)), "gossip_create")
+        self._ctx = ctx
+        self.n_peers = n_peers
+        self.n_msgs = n_msgs
+        self.begin, self.end = (part if part != (0, 0) else (0, n_peers))
+
+    # -- lifecycle ----------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_ctx", None) and self._ctx.value:
+            self._L.gossip_destroy(self._ctx)
+            self._ctx = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def ctx(self):
+        return self._ctx
+
+    def shape(self) -> dict:
+        w, x, nl, ne = C.c_uint32(), C.c_uint32(), C.c_uint64(), C.c_uint64()
+        check(self._L.gossip_get_shape(self._ctx, C.byref(w), C.byref(x), C.byref(nl), C.byref(ne)), "get_shape")
+        return {"words": w.value, "exchange_words": x.value, "n_local": nl.value, "n_edges": ne.value}
+
+    def set_stream(self, stream_handle: int) -> None:
+        check(self._L.gossip_set_stream(self._ctx, C.c_void_p(stream_handle)), "gossip_set_stream")
+
+    # -- overlay --------------------------------------------------------------
+    def build_graph(self) -> None:
+        check(self._L.gossip_build_graph(self._ctx), "gossip_build_graph")
+
+    def load_csr(self, row_ptr: np.ndarray, col: np.ndarray) -> None:
+        rp = np.ascontiguousarray(row_ptr, dtype=np.uint64)
+        cl = np.ascontiguousarray(col, dtype=np.uint32)
+        if cl.size == 0:
+            cl = np.zeros(1, dtype=np.uint32)
+        check(self._L.gossip_load_csr(self._ctx, _ptr(rp, C.c_uint64), _ptr(cl, C.c_uint32), rp.size - 1,
+                                      int(rp[-1])), "gossip_load_csr")
+
+    def read_csr(self) -> tuple[np.ndarray, np.ndarray]:
+        s = self.shape()
+        rp = np.zeros(s["n_local"] + 1, dtype=np.uint64)
+        col = np.zeros(max(s["n_edges"], 1), dtype=np.uint32)
+        check(self._L.gossip_read_csr(self._ctx, _ptr(rp, C.c_uint64), _ptr(col, C.c_uint32)), "gossip_read_csr")
+        return rp, col[: s["n_edges"]]
+
+    # -- schedule ---------------------------------------------------------------
+    def inject(self, origin, inject_round) -> None:
+        o, r = _u32(origin), _u32(inject_round)
+        check(self._L.gossip_inject(self._ctx, _ptr(o, C.c_uint32), _ptr(r, C.c_uint32), o.size), "gossip_inject")
+
+    def schedule_kills(self, peers, rounds) -> None:
+        p, r = _u32(peers), _u32(rounds)
+        n = p.size
+        if n == 0:
+            p = r = np.zeros(1, dtype=np.uint32)
+        check(self._L.gossip_schedule_kills(self._ctx, _ptr(p, C.c_uint32), _ptr(r, C.c_uint32), n),
+              "gossip_schedule_kills")
+
+    # -- rounds -----------------------------------------------------------------
+    def reset(self) -> None:
+        check(self._L.gossip_reset(self._ctx), "gossip_reset")
+
+    def step(self) -> tuple[dict, bool]:
+        st = RoundStats()
+        rc = check(self._L.gossip_step(self._ctx, C.byref(st)), "gossip_step")
+        return st.as_dict(), rc == 1
+
+    def run(self, cap: int = 4096) -> list[dict]:
+        buf = (RoundStats * cap)()
+        rounds = C.c_uint32()
+        check(self._L.gossip_run(self._ctx, buf, cap, C.byref(rounds)), "gossip_run")
+        return [buf[i].as_dict() for i in range(min(rounds.value, cap))]
+
+    # partitioned phases (see distributed.py)
+    def set_exchange(self, send_ptr: int, recv_ptr: int, part_begins) -> None:
+        pb = np.ascontiguousarray(part_begins, dtype=np.uint64)
+        check(self._L.gossip_set_exchange(self._ctx, C.c_void_p(send_ptr), C.c_void_p(recv_ptr), pb.size - 1,
+                                          _ptr(pb, C.c_uint64)), "gossip_set_exchange")
+
+    def round_push(self) -> None:
+        check(self._L.gossip_round_push(self._ctx), "gossip_round_push")
+
+    def round_finish(self) -> dict:
+        st = RoundStats()
+        check(self._L.gossip_round_finish(self._ctx, C.byref(st)), "gossip_round_finish")
+        return st.as_dict()
+
+    def round_commit(self, global_new_receipts: int) -> bool:
+        fin = C.c_int()
+        check(self._L.gossip_round_commit(self._ctx, global_new_receipts, C.byref(fin)), "gossip_round_commit")
+        return bool(fin.value)
+
+    # -- results ----------------------------------------------------------------
+    def read_seen(self) -> np.ndarray:
+        s = self.shape()
+        out = np.zeros((s["n_local"], s["words"]), dtype=np.uint64)
+        check(self._L.gossip_read_seen(self._ctx, _ptr(out, C.c_uint64)), "gossip_read_seen")
+        return out
+
+    def coverage(self) -> np.ndarray:
+        out = np.zeros(self.n_msgs, dtype=np.uint64)
+        check(self._L.gossip_read_coverage(self._ctx, _ptr(out, C.c_uint64)), "gossip_read_coverage")
+        return out
+
+    def coverage_history(self, max_rounds: int = 4096) -> np.ndarray:
+        buf = np.zeros((max_rounds, self.n_msgs), dtype=np.uint64)
+        r = C.c_uint32()
+        check(self._L.gossip_read_coverage_history(self._ctx, _ptr(buf, C.c_uint64), max_rounds, C.byref(r)),
+              "gossip_read_coverage_history")
+        return buf[: r.value]
+
+    def reports(self) -> np.ndarray:
+        cnt = C.c_uint64()
+        check(self._L.gossip_read_reports(self._ctx, None, 0, C.byref(cnt)), "gossip_read_reports")
+        n = cnt.value
+        buf = (DeadReport * max(n, 1))()
+        check(self._L.gossip_read_reports(self._ctx, buf, n, C.byref(cnt)), "gossip_read_reports")
+        return np.array([(buf[i].round, buf[i].reporter, buf[i].dead) for i in range(n)],
+                        dtype=np.uint32).reshape(n, 3)
+
+    def alive(self) -> np.ndarray:
+        out = np.zeros(self.n_peers, dtype=np.uint8)
+        check(self._L.gossip_read_alive(self._ctx, _ptr(out, C.c_uint8)), "gossip_read_alive")
+        return out
+
+    def registered(self) -> np.ndarray:
+        out = np.zeros(self.n_peers, dtype=np.uint8)
+        check(self._L.gossip_read_registered(self._ctx, _ptr(out, C.c_uint8)), "gossip_read_registered")
+        return out
+
+    # -- measurement ------------------------------------------------------------
+    def enable_timing(self, on: bool = True) -> None:
+        check(self._L.gossip_enable_timing(self._ctx, 1 if on else 0), "gossip_enable_timing")
+
+    def kernel_time(self, name: str) -> tuple[float, int]:
+        ms, n = C.c_double(), C.c_uint64()
+        check(self._L.gossip_kernel_time(self._ctx, name.encode(), C.byref(ms), C.byref(n)), "gossip_kernel_time")
+        return ms.value, n.value
+
+    def kernel_bytes(self, name: str) -> float:
+        b = C.c_double()
+        check(self._L.gossip_kernel_bytes(self._ctx, name.encode(), C.byref(b)), "gossip_kernel_bytes")
+        return b.value

@@ -1,0 +1,129 @@
+"""ctypes binding of oracle/libgossip_oracle.so -- TEST INFRASTRUCTURE ONLY.
+
+The oracle is the checker: tests compare libgossip_hip against it, never the
+other way round, and nothing in the product imports this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+import numpy as np
+
+STAT_FIELDS = ("frontier", "traversals", "deliveries", "undelivered", "new_receipts", "duplicates", "injected",
+               "died", "reports", "seed_removals", "digest", "covered")
+
+
+class OStats(C.Structure):
+    _fields_ = [("round", C.c_uint32), ("flags", C.c_uint32)] + [(f, C.c_uint64) for f in STAT_FIELDS]
+
+    def as_dict(self):
+        return {f: int(getattr(self, f)) for f, _ in self._fields_}
+
+
+class OCfg(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("n_msgs", C.c_uint32), ("seed", C.c_uint32), ("churn_threshold", C.c_uint32),
+                ("ping_every", C.c_uint32), ("max_missed", C.c_uint32), ("max_rounds", C.c_uint32),
+                ("min_rounds", C.c_uint32), ("threads", C.c_int), ("variant", C.c_int)]
+
+
+class OReport(C.Structure):
+    _fields_ = [("round", C.c_uint32), ("reporter", C.c_uint32), ("dead", C.c_uint32)]
+
+
+def _p(a, t):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+class Oracle:
+    def __init__(self, so: Path):
+        L = C.CDLL(str(so))
+        L.oracle_threshold.restype = C.c_uint64
+        L.oracle_skew_pick.restype = C.c_uint32
+        L.oracle_skew_pick.argtypes = [C.c_uint32, C.c_uint64]
+        L.oracle_digest_weight.restype = C.c_uint64
+        L.oracle_digest_weight.argtypes = [C.c_uint64]
+        L.oracle_sim_create.restype = C.c_void_p
+        L.oracle_sim_reports.restype = C.c_uint64
+        L.oracle_sim_sent_to_total.restype = C.c_uint64
+        for name in ("oracle_sim_step", "oracle_sim_run", "oracle_sim_schedule"):
+            getattr(L, name).restype = C.c_int
+        self.L = L
+
+    def philox(self, ctr, key):
+        out = (C.c_uint32 * 4)()
+        self.L.oracle_philox4x32_10((C.c_uint32 * 4)(*ctr), (C.c_uint32 * 2)(*key), out)
+        return [int(x) for x in out]
+
+    def threshold(self, j, L):
+        return int(self.L.oracle_threshold(C.c_uint32(j), C.c_uint32(L)))
+
+    def pick_origins(self, n, seed, count):
+        out = (C.c_uint32 * max(count, 1))()
+        self.L.oracle_pick_origins(C.c_uint64(n), C.c_uint32(seed), C.c_uint32(count), out)
+        return np.array(list(out)[:count], dtype=np.uint32)
+
+    def gen(self, kind, n, arg, seed, threads=8):
+        rp = C.POINTER(C.c_uint64)()
+        col = C.POINTER(C.c_uint32)()
+        e = C.c_uint64()
+        if kind == "ref_bootstrap":
+            rc = self.L.oracle_gen_ref_bootstrap(C.c_uint32(n), C.c_uint32(arg), C.c_uint32(seed), C.byref(rp),
+                                                 C.byref(col), C.byref(e))
+        else:
+            rc = self.L.oracle_gen_powerlaw(C.c_uint64(n), C.c_uint32(arg), C.c_uint32(seed), C.c_int(threads),
+                                            C.byref(rp), C.byref(col), C.byref(e))
+        assert rc == 0, "oracle generator failed"
+        R = np.ctypeslib.as_array(rp, (n + 1,)).copy()
+        Cc = np.ctypeslib.as_array(col, (max(e.value, 1),)).copy()[: e.value]
+        self.L.oracle_free(C.cast(rp, C.c_void_p))
+        self.L.oracle_free(C.cast(col, C.c_void_p))
+        return R, Cc
+
+    def gen_workload(self, w, threads=8):
+        arg = w.n_seeds if w.graph == "ref_bootstrap" else w.list_len
+        return self.gen(w.graph, w.n, arg, w.rng_seed, threads)
+
+    def simulate(self, rp, col, n, n_msgs, origins, inject_rounds, *, seed=0, churn_threshold=0, ping_every=0,
+                 max_missed=3, max_rounds=4096, min_rounds=0, kills=(), variant=0, threads=8):
+        rp = np.ascontiguousarray(rp, dtype=np.uint64)
+        col = np.ascontiguousarray(col if len(col) else np.zeros(1), dtype=np.uint32)
+        cfg = OCfg(n, n_msgs, seed, churn_threshold, ping_every, max_missed, max_rounds, min_rounds, threads, variant)
+        s = self.L.oracle_sim_create(C.byref(cfg), _p(rp, C.c_uint64), _p(col, C.c_uint32))
+        assert s, "oracle_sim_create failed"
+        s = C.c_void_p(s)
+        try:
+            o = np.ascontiguousarray(origins, dtype=np.uint32)
+            r = np.ascontiguousarray(inject_rounds, dtype=np.uint32)
+            kp = np.array([k[0] for k in kills] + [0], dtype=np.uint32)
+            kr = np.array([k[1] for k in kills] + [0], dtype=np.uint32)
+            assert self.L.oracle_sim_schedule(s, _p(o, C.c_uint32), _p(r, C.c_uint32), C.c_uint32(len(kills)),
+                                              _p(kp, C.c_uint32), _p(kr, C.c_uint32)) == 0
+            buf = (OStats * max_rounds)()
+            nr = self.L.oracle_sim_run(s, buf, C.c_uint32(max_rounds))
+            stats = [buf[i].as_dict() for i in range(nr)]
+            W = (n_msgs + 63) // 64
+            seen = np.zeros((n, W), dtype=np.uint64)
+            self.L.oracle_sim_seen(s, _p(seen, C.c_uint64))
+            cov = np.zeros(n_msgs, dtype=np.uint64)
+            self.L.oracle_sim_coverage(s, _p(cov, C.c_uint64))
+            nrep = self.L.oracle_sim_reports(s, None, C.c_uint64(0))
+            rb = (OReport * max(int(nrep), 1))()
+            self.L.oracle_sim_reports(s, rb, C.c_uint64(nrep))
+            reps = np.array([(rb[i].round, rb[i].reporter, rb[i].dead) for i in range(int(nrep))],
+                            dtype=np.uint32).reshape(int(nrep), 3)
+            alive = np.zeros(n, dtype=np.uint8)
+            self.L.oracle_sim_alive(s, _p(alive, C.c_uint8))
+            reg = np.zeros(n, dtype=np.uint8)
+            self.L.oracle_sim_registered(s, _p(reg, C.c_uint8))
+            sent = int(self.L.oracle_sim_sent_to_total(s))
+            return dict(stats=stats, seen=seen, coverage=cov, reports=reps, alive=alive, registered=reg,
+                        sent_to_total=sent)
+        finally:
+            self.L.oracle_sim_destroy(s)
+
+    def simulate_workload(self, w, rp, col, variant=0, threads=8, max_rounds=4096):
+        return self.simulate(rp, col, w.n, w.n_msgs, w.origins, w.inject_rounds, seed=w.rng_seed,
+                             churn_threshold=w.churn_threshold, ping_every=w.ping_every, max_missed=w.max_missed,
+                             min_rounds=w.min_rounds, kills=w.kills, variant=variant, threads=threads,
+                             max_rounds=max_rounds)

@@ -1,0 +1,150 @@
+"""GPU parity: libgossip_hip (through its C-ABI) vs the CPU oracle on the
+same seeded inputs -- bit-exact stats, seen sets, reports, alive/registry --
+plus size-independent properties at BASELINE.json's full sizes."""
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from gossip_hip import Engine
+from gossip_hip.workloads import config, run_engine
+
+pytestmark = pytest.mark.gpu
+GOLDEN = Path(__file__).resolve().parent / "golden"
+
+
+def _engine(w, **kw):
+    return Engine(w.n, w.n_msgs, **w.engine_kwargs(), **kw)
+
+
+def _hand_csr(case):
+    rows = case["rows"]
+    rp = np.zeros(len(rows) + 1, dtype=np.uint64)
+    rp[1:] = np.cumsum([len(r) for r in rows])
+    return rp, np.array([c for r in rows for c in r], dtype=np.uint32)
+
+
+@pytest.mark.parametrize("case", json.loads((GOLDEN / "hand_graphs.json").read_text())["cases"],
+                         ids=lambda c: c["name"])
+def test_hand_graphs(case):
+    fields = json.loads((GOLDEN / "hand_graphs.json").read_text())["fields"]
+    with Engine(case["n"], len(case["origins"]), ping_every=case.get("ping_every", 0),
+                max_missed=case.get("max_missed", 3), min_rounds=case.get("min_rounds", 0)) as e:
+        e.load_csr(*_hand_csr(case))
+        e.inject(case["origins"], case["inject_rounds"])
+        kills = case.get("kills", [])
+        if kills:
+            e.schedule_kills([k[0] for k in kills], [k[1] for k in kills])
+        e.reset()
+        stats = e.run()
+        assert [[s[f] for f in fields] for s in stats] == case["expect"]
+        assert e.coverage().tolist() == case["coverage"]
+        assert e.reports().tolist() == case.get("reports", [])
+
+
+@pytest.mark.parametrize("kind,n,arg,seed", [("ref_bootstrap", 8, 20, 0x5EED0001), ("ref_bootstrap", 300, 20, 5),
+                                             ("powerlaw", 1 << 12, 6, 3), ("powerlaw", 1 << 18, 6, 0x5EED0002),
+                                             ("powerlaw", 100_003, 11, 9)])
+def test_overlay_generator_matches_oracle(oracle, kind, n, arg, seed):
+    kw = dict(n_seeds=arg) if kind == "ref_bootstrap" else dict(list_len=arg)
+    with Engine(n, 64, rng_seed=seed, graph=kind, **kw) as e:
+        e.build_graph()
+        rp, col = e.read_csr()
+    orp, ocol = oracle.gen(kind, n, arg, seed)
+    assert np.array_equal(rp, orp)
+    assert np.array_equal(col, ocol)
+
+
+def _compare(e, ref, w):
+    got = e.run()
+    assert len(got) == len(ref["stats"])
+    for g, r in zip(got, ref["stats"]):
+        assert g == r, (g, r)
+    assert np.array_equal(e.read_seen(), ref["seen"])
+    assert np.array_equal(e.coverage(), ref["coverage"])
+    assert np.array_equal(e.reports(), ref["reports"])
+    assert np.array_equal(e.alive(), ref["alive"])
+    assert np.array_equal(e.registered(), ref["registered"])
+    return got
+
+
+@pytest.mark.parametrize("idx,n", [(1, None), (2, 1 << 16), (3, 1 << 18), (5, 1 << 16), (5, 50_000)])
+def test_workload_parity(oracle, idx, n):
+    w = config(idx, n, pick=oracle.pick_origins)
+    rp, col = oracle.gen_workload(w)
+    ref = oracle.simulate_workload(w, rp, col)
+    with _engine(w) as e:
+        e.build_graph()
+        e.inject(w.origins, w.inject_rounds)
+        if w.kills:
+            e.schedule_kills([k[0] for k in w.kills], [k[1] for k in w.kills])
+        e.reset()
+        first = _compare(e, ref, w)
+        e.reset()  # a second run from reset is identical
+        assert e.run() == first
+
+
+@pytest.mark.parametrize("M", [65, 130, 300, 512])
+def test_multiword_messages(oracle, M):
+    n = 1 << 14
+    rng = np.random.default_rng(M)
+    origins = rng.integers(0, n, M).astype(np.uint32)
+    rounds = rng.integers(0, 4, M).astype(np.uint32)
+    rp, col = oracle.gen("powerlaw", n, 6, 77)
+    ref = oracle.simulate(rp, col, n, M, origins, rounds, seed=77, churn_threshold=42949673 * 2, ping_every=2,
+                          max_missed=2)
+    with Engine(n, M, rng_seed=77, churn_threshold=42949673 * 2, ping_every=2, max_missed=2) as e:
+        e.load_csr(rp, col)
+        e.inject(origins, rounds)
+        e.reset()
+        _compare(e, ref, None)
+
+
+def test_coverage_history_last_row_is_final(oracle):
+    w = config(3, 1 << 14, pick=oracle.pick_origins)
+    with _engine(w, coverage_history=True) as e:
+        stats = run_engine(e, w)
+        hist = e.coverage_history()
+        assert hist.shape[0] == len(stats)
+        assert np.array_equal(hist[-1], e.coverage())
+        assert [int(h.sum()) for h in hist] == [s["covered"] for s in stats]
+
+
+def _digest(seen):
+    n, W = seen.shape
+    idx = np.arange(n * W, dtype=np.uint64) + np.uint64(1)
+    z = idx * np.uint64(0x9E3779B97F4A7C15)
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    z = (z ^ (z >> np.uint64(31))) | np.uint64(1)
+    return int(np.sum(z * seen.reshape(-1), dtype=np.uint64))
+
+
+@pytest.mark.parametrize("idx", [3, 5])
+def test_full_size_properties(idx):
+    """BASELINE sizes (config 3: 2^24 peers; config 5: 2^26 with churn):
+    checksum-of-state, conservation and determinism."""
+    w = config(idx)
+    with _engine(w) as e:
+        stats = run_engine(e, w)
+        last = stats[-1]
+        assert last["new_receipts"] == 0
+        seen = e.read_seen()
+        assert _digest(seen) == last["digest"]
+        covered = int(np.bitwise_count(seen).sum())
+        assert covered == last["covered"] == sum(s["new_receipts"] + s["injected"] for s in stats)
+        assert int(e.coverage().sum()) == covered
+        for s in stats:
+            assert s["duplicates"] == s["deliveries"] - s["new_receipts"]
+        if idx == 3:   # no churn: every message reaches its origin's whole component
+            assert stats[0]["injected"] == 64
+        else:
+            alive = e.alive()
+            assert int(alive.sum()) == w.n - sum(s["died"] for s in stats)
+            reps = e.reports()
+            assert len(reps) == sum(s["reports"] for s in stats)
+            assert np.all(alive[reps[:, 2]] == 0)      # only dead peers are reported
+            assert np.all(e.registered()[reps[:, 2]] == 0)
+        e.reset()
+        assert e.run() == stats
