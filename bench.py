@@ -36,7 +36,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", type=int, default=4, help="BASELINE.json config index (1-5)")
     ap.add_argument("--n", type=int, default=0, help="override peer count")
-    ap.add_argument("--cpu-sample-n", type=int, default=1 << 22)
+    ap.add_argument("--cpu-sample-n", type=int, default=1 << 25)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP event timing")
@@ -147,8 +147,9 @@ def main():
     value = args.steps * deliveries / dt / 1e9
     roofline = None
     if not args.no_timing:
-        k_ms = {k: eng.kernel_time(k) for k in ("push_light", "push_heavy", "liveness")}
-        k_b = {k: eng.kernel_bytes(k) for k in ("push_light", "push_heavy", "liveness")}
+        from gossip_hip.engine import KERNELS
+        k_ms = {k: eng.kernel_time(k) for k in KERNELS}
+        k_b = {k: eng.kernel_bytes(k) for k in KERNELS}
         dom = max(k_ms, key=lambda k: k_ms[k][0])
         ms, launches = k_ms[dom]
         if ms > 0 and launches:
@@ -159,7 +160,9 @@ def main():
                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                         "avg_launch_ms": round(ms / launches, 4), "launches": launches,
                         "alg_bytes_per_launch": round(per_launch_bytes),
-                        "kernel_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in k_ms.items()}}
+                        "kernel_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in k_ms.items() if v[1]},
+                        "kernel_frac": {k: round(k_b[k] / (v[0] / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
+                                        for k, v in k_ms.items() if v[0] > 0 and k_b[k] > 0}}
 
     if rank == 0:
         line = {

@@ -41,6 +41,8 @@ typedef int gossip_status;
 
 /* gossip_config.flags */
 #define GOSSIP_FLAG_COVERAGE_HISTORY 1u /* keep per-message coverage for every round */
+#define GOSSIP_FLAG_FORCE_PUSH 2u       /* never use pull rounds */
+#define GOSSIP_FLAG_FORCE_PULL 4u       /* pull every eligible round (symmetric overlay, nobody dead, P = 1) */
 
 /*
  * Replaces: NetworkConfig's parsed values (config.cpp:31-42,93-96) plus the
@@ -63,6 +65,8 @@ typedef struct gossip_config {
     int32_t device;           /* HIP device ordinal; -1 = current */
     uint32_t flags;           /* GOSSIP_FLAG_* */
     uint64_t report_capacity; /* dead-node report buffer entries (0 = default) */
+    uint32_t pull_permille;   /* pull when the frontier estimate >= this per-mille of the owned peers (0 = 50) */
+    uint32_t reserved;
 } gossip_config;
 
 /*
@@ -136,7 +140,8 @@ gossip_status gossip_pick_origins(uint64_t n_peers, uint32_t rng_seed, uint32_t 
 /* Clears all dynamic state (seen/new, alive, edge masks, miss counters,
  * registry, reports) back to round 0; keeps overlay and schedule. */
 gossip_status gossip_reset(gossip_ctx* ctx);
-/* One round: churn -> liveness (if due) -> injection -> push -> advance.
+/* One round: churn -> liveness (if due) -> injection -> push (or, on dense
+ * rounds of a symmetric overlay with nobody dead, the equivalent pull) -> advance.
  * Returns 1 when the run is finished after this round, 0 if not, < 0 on error. */
 gossip_status gossip_step(gossip_ctx* ctx, gossip_round_stats* out);
 /* Steps until finished or max_rounds; per_round (may be NULL) receives up to cap entries. */
@@ -179,7 +184,8 @@ gossip_status gossip_kernel_time(gossip_ctx* ctx, const char* kernel, double* ms
 /* Algorithmic HBM bytes of the same kernels over the same
  * interval: push = 32 B per frontier peer + 20 B per edge traversal (light
  * rows to "push_light", heavy rows to "push_heavy"); liveness = 6.125 B per
- * live edge checked. */
+ * live edge checked; pull = 40 B per owned peer + 12 B per edge scanned
+ * ("pull_light") and 12 B per heavy-row edge scanned ("pull_heavy"). */
 gossip_status gossip_kernel_bytes(gossip_ctx* ctx, const char* kernel, double* bytes);
 
 #ifdef __cplusplus

@@ -94,6 +94,11 @@ struct gossip_ctx {
     uint32_t round = 0;
     bool finished = false;
     bool any_dead = false;
+    bool symmetric = false;      // overlay is symmetric (pull rounds allowed)
+    bool nx_dirty = false;       // nx holds stale words (after a pull round)
+    bool last_pull = false;      // mode of the round in flight
+    uint64_t frontier_est = 0;   // activated peers of the previous round
+    std::vector<uint64_t> inj_prefix;  // per sorted injection: cumulative mask words
     uint64_t cum_digest = 0, cum_covered = 0;
 
     // partitioned exchange
@@ -333,6 +338,27 @@ gossip_status round_push(gossip_ctx* c, bool remote) {
         HIPCHK(timed(c, "inject", [&] {
             return launch_inject(a, pw, c->d_inj_origin + first, c->d_inj_msg + first, cnt, c->stream);
         }));
+    // messages injected up to and including this round (what a peer can still learn)
+    {
+        uint32_t hi = (uint32_t)(std::upper_bound(c->inj_round_sorted.begin(), c->inj_round_sorted.end(), c->round) -
+                                 c->inj_round_sorted.begin());
+        for (int w = 0; w < kMaxWords; ++w) a.inj_mask[w] = hi ? c->inj_prefix[(uint64_t)(hi - 1) * kMaxWords + w] : 0;
+    }
+    const uint32_t permille = c->cfg.pull_permille ? c->cfg.pull_permille : 50;
+    const bool pull_ok = !remote && c->symmetric && !c->any_dead && !(c->cfg.flags & GOSSIP_FLAG_FORCE_PUSH);
+    const bool pull = pull_ok && ((c->cfg.flags & GOSSIP_FLAG_FORCE_PULL) ||
+                                  (c->frontier_est + cnt) * 1000 >= c->n_local * (uint64_t)permille);
+    c->last_pull = pull;
+    if (pull) {
+        // nx is written whole by pull_light; heavy rows are OR-ed in afterwards
+        HIPCHK(timed(c, "pull_light", [&] { return launch_pull_light(a, pw, c->stream); }));
+        HIPCHK(timed(c, "pull_heavy", [&] { return launch_pull_heavy(a, pw, c->stream); }));
+        return GOSSIP_OK;
+    }
+    if (c->nx_dirty) {
+        HIPCHK(hipMemsetAsync(c->nx, 0, c->n_local * c->Wp * sizeof(uint64_t), c->stream));
+        c->nx_dirty = false;
+    }
     if (remote) HIPCHK(hipMemsetAsync(c->send, 0, c->n * c->Wp * sizeof(uint64_t), c->stream));
     HIPCHK(timed(c, "push_heavy", [&] { return launch_push_heavy(a, pw, c->any_dead, remote, c->stream); }));
     HIPCHK(timed(c, "push_light", [&] { return launch_push_light(a, pw, c->any_dead, remote, c->stream); }));
@@ -343,9 +369,15 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
     HIPCHK(hipMemcpyAsync(c->h_st, c->st + c->round, sizeof(DevStats), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     const DevStats& d = *c->h_st;
+    c->frontier_est = d.activated;
     if (c->timing) {
-        c->kbytes["push_light"] += 32.0 * d.frontier + 20.0 * (double)(d.traversals - d.heavy_traversals);
-        c->kbytes["push_heavy"] += 20.0 * (double)d.heavy_traversals;
+        if (c->last_pull) {
+            c->kbytes["pull_light"] += 40.0 * c->n_local + 12.0 * (double)d.pull_edges;
+            c->kbytes["pull_heavy"] += 12.0 * (double)d.heavy_traversals;
+        } else {
+            c->kbytes["push_light"] += 32.0 * d.frontier + 20.0 * (double)(d.traversals - d.heavy_traversals);
+            c->kbytes["push_heavy"] += 20.0 * (double)d.heavy_traversals;
+        }
         c->kbytes["liveness"] += 6.125 * (double)d.live_checked;
     }
     gossip_round_stats s{};
@@ -375,7 +407,8 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
 }
 
 void advance(gossip_ctx* c, uint64_t fresh_global) {
-    std::swap(c->nw, c->nx);  // nw was cleared by push_light; nx holds the fresh words
+    std::swap(c->nw, c->nx);  // push: nw was cleared by push_light; pull: the old nw is stale
+    c->nx_dirty = c->last_pull;
     const uint32_t r = c->round;
     c->round++;
     const bool pending = c->has_schedule && c->last_inject_round > r;
@@ -510,7 +543,9 @@ gossip_status gossip_build_graph(gossip_ctx* c) {
         std::vector<uint64_t> rp;
         std::vector<uint32_t> col;
         host_ref_bootstrap((uint32_t)c->n, c->cfg.n_seeds, c->cfg.rng_seed, rp, col);
-        return upload_csr(c, rp.data(), col.data(), col.size());
+        gossip_status st = upload_csr(c, rp.data(), col.data(), col.size());
+        c->symmetric = false;  // the literal bootstrap overlay is a DAG (F8)
+        return st;
     }
     if (c->cfg.graph_model != GOSSIP_GRAPH_POWERLAW) return fail(GOSSIP_EINVAL, "unknown graph_model");
     if (c->cfg.list_len < 2 || c->cfg.list_len > 64) return fail(GOSSIP_EINVAL, "list_len must be 2..64");
@@ -522,7 +557,9 @@ gossip_status gossip_build_graph(gossip_ctx* c) {
     if (build_powerlaw_device(c->n, c->begin, c->end, c->cfg.list_len, c->cfg.rng_seed, &rp, &col, &m, c->stream,
                               &err) != hipSuccess)
         return fail(GOSSIP_EHIP, "overlay generator: " + err);
-    return install_graph(c, rp, col, m);
+    gossip_status st = install_graph(c, rp, col, m);
+    c->symmetric = true;  // powerlaw overlay is symmetrised by construction
+    return st;
 }
 
 gossip_status gossip_load_csr(gossip_ctx* c, const uint64_t* rp, const uint32_t* col, uint64_t n_rows,
@@ -538,8 +575,18 @@ gossip_status gossip_load_csr(gossip_ctx* c, const uint64_t* rp, const uint32_t*
             if (e > rp[v] && col[e] <= col[e - 1]) return fail(GOSSIP_EINVAL, "row not sorted/unique");
         }
     }
+    // symmetric iff every edge v->c has its reverse (rows are sorted): enables pull rounds
+    bool sym = c->n_local == c->n;
+    for (uint64_t v = 0; sym && v < n_rows; ++v)
+        for (uint64_t e = rp[v]; sym && e < rp[v + 1]; ++e) {
+            const uint32_t* b = col + rp[col[e]];
+            const uint32_t* x = col + rp[col[e] + 1];
+            sym = std::binary_search(b, x, (uint32_t)v);
+        }
     if (set_dev(c)) return GOSSIP_EHIP;
-    return upload_csr(c, rp, col, n_edges);
+    gossip_status st = upload_csr(c, rp, col, n_edges);
+    c->symmetric = sym;
+    return st;
 }
 
 gossip_status gossip_read_csr(gossip_ctx* c, uint64_t* rp, uint32_t* col) {
@@ -569,6 +616,11 @@ gossip_status gossip_inject(gossip_ctx* c, const uint32_t* origin, const uint32_
         mid[i] = idx[i];
         c->inj_round_sorted[i] = inject_round[idx[i]];
         c->last_inject_round = std::max(c->last_inject_round, inject_round[idx[i]]);
+    }
+    c->inj_prefix.assign((uint64_t)n_msgs * kMaxWords, 0);
+    for (uint32_t i = 0; i < n_msgs; ++i) {
+        for (int w = 0; w < kMaxWords; ++w) c->inj_prefix[(uint64_t)i * kMaxWords + w] = i ? c->inj_prefix[(uint64_t)(i - 1) * kMaxWords + w] : 0;
+        c->inj_prefix[(uint64_t)i * kMaxWords + (mid[i] >> 6)] |= 1ull << (mid[i] & 63);
     }
     c->origin.assign(origin, origin + n_msgs);
     c->inject_round.assign(inject_round, inject_round + n_msgs);
@@ -650,6 +702,9 @@ gossip_status gossip_reset(gossip_ctx* c) {
         HIPCHK(hipGetLastError());
     }
     c->any_masked = false;
+    c->nx_dirty = false;
+    c->last_pull = false;
+    c->frontier_est = 0;
     c->round = 0;
     c->finished = false;
     c->any_dead = false;

@@ -16,7 +16,7 @@ constexpr int kMaxWords = 8;                   // M <= 512 concurrent messages
 // Per-round device counters (all integer; order-independent sums).
 struct DevStats {
     unsigned long long frontier, traversals, deliveries, undelivered, new_receipts, injected, died, reports,
-        seed_removals, digest, covered, heavy_traversals, live_checked, pad[3];
+        seed_removals, digest, covered, heavy_traversals, live_checked, activated, pull_edges, pad[1];
 };
 static_assert(sizeof(DevStats) == 128, "DevStats layout");
 
@@ -51,6 +51,7 @@ struct RoundArgs {
     uint64_t report_cap;
     uint32_t round;
     uint32_t max_missed;
+    uint64_t inj_mask[kMaxWords];  // messages injected so far (pull: bits a peer can still learn)
 };
 
 // ---- launchers (gossip_kernels.hip) ----
@@ -61,6 +62,8 @@ hipError_t launch_inject(const RoundArgs& a, uint32_t W, const uint32_t* origin,
                          hipStream_t s);
 hipError_t launch_push_heavy(const RoundArgs& a, uint32_t W, bool check_alive, bool remote, hipStream_t s);
 hipError_t launch_push_light(const RoundArgs& a, uint32_t W, bool check_alive, bool remote, hipStream_t s);
+hipError_t launch_pull_light(const RoundArgs& a, uint32_t W, hipStream_t s);
+hipError_t launch_pull_heavy(const RoundArgs& a, uint32_t W, hipStream_t s);
 hipError_t launch_apply_remote(const RoundArgs& a, uint32_t W, const uint64_t* recv, uint32_t world,
                                uint64_t part_stride, hipStream_t s);
 hipError_t launch_coverage(const uint64_t* words, uint64_t n_local, uint32_t W, unsigned long long* counts,

@@ -39,7 +39,8 @@ __device__ __forceinline__ uint32_t lane_rank(unsigned long long mask) {
 
 struct Acc {
     unsigned long long frontier = 0, trav = 0, deliv = 0, undeliv = 0, fresh = 0, digest = 0, covered = 0, died = 0,
-                       reports = 0, removals = 0, injected = 0, htrav = 0, checked = 0;
+                       reports = 0, removals = 0, injected = 0, htrav = 0, checked = 0,
+                       activated = 0, pulled = 0;
 };
 
 // One atomic per nonzero field per wave.
@@ -63,6 +64,8 @@ __device__ __forceinline__ void flush(Acc& acc, DevStats* st) {
     GOSSIP_FLUSH(injected, injected)
     GOSSIP_FLUSH(htrav, heavy_traversals)
     GOSSIP_FLUSH(checked, live_checked)
+    GOSSIP_FLUSH(activated, activated)
+    GOSSIP_FLUSH(pulled, pull_edges)
 #undef GOSSIP_FLUSH
 }
 
@@ -128,7 +131,8 @@ __device__ __forceinline__ void deliver(const RoundArgs& a, uint32_t c, const ui
         const unsigned long long old = atomicOr(sp + w, (unsigned long long)m[w]);
         const unsigned long long fr = m[w] & ~old;
         if (fr) {
-            atomicOr(reinterpret_cast<unsigned long long*>(a.nx) + lv * W + w, fr);
+            const unsigned long long onx = atomicOr(reinterpret_cast<unsigned long long*>(a.nx) + lv * W + w, fr);
+            acc.activated += onx == 0;
             acc.fresh += (unsigned long long)__popcll(fr);
         }
     }
@@ -214,6 +218,172 @@ __global__ __launch_bounds__(kBlock) void k_push_heavy(RoundArgs a) {
         for (uint64_t e = ch.e0 + threadIdx.x; e < ch.e1; e += kBlock) deliver<W, CA, RM>(a, a.col[e], m, pc, acc);
     }
     acc.htrav = acc.trav;
+    flush(acc, a.st);
+}
+
+
+// ---------------------------------------------------------------------------
+// pull (direction-optimised dense rounds): every peer that can still learn a
+// message ORs the new words of its neighbours into a wave-private LDS
+// accumulator, then applies its own test-and-set with plain stores -- no
+// global atomics.  Same round contract as push: on a symmetric overlay with
+// no dead peers and no masked edges, edge u->v is traversed iff u is in the
+// frontier, so traversals/deliveries are summed on the source side
+// (deg(u), popcount(new[u]) * deg(u)) and new_receipts on the receiving side.
+// Rows longer than kHeavyDegree are pulled by k_pull_heavy (one workgroup per
+// chunk, one atomicOr per chunk).  P = 1 only (col ids index nw directly).
+// ---------------------------------------------------------------------------
+template <int W, bool COV>
+__global__ __launch_bounds__(kBlock) void k_pull_light(RoundArgs a, uint32_t wd) {
+    __shared__ unsigned int cov_s[COV ? 64 * W : 1];
+    __shared__ unsigned long long acc_s[kWavesPerBlock][64 * W];
+    if (COV) {
+        for (int i = threadIdx.x; i < 64 * W; i += kBlock) cov_s[i] = 0;
+        __syncthreads();
+    }
+    Acc acc;
+    const int lane = threadIdx.x & 63;
+    unsigned long long* my = acc_s[threadIdx.x >> 6];
+    const uint64_t n_tiles = (a.n_local + 63) >> 6;
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); t < n_tiles; t += nwaves) {
+        const uint64_t v = (t << 6) + lane;
+        const bool vv = v < a.n_local;
+        uint64_t m[W], need[W], sv[W];
+        bool act = false, needy = false;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            m[w] = vv ? a.nw[v * W + w] : 0ull;
+            sv[w] = vv ? a.seen[v * W + w] : ~0ull;
+            need[w] = a.inj_mask[w] & ~sv[w];
+            act |= m[w] != 0;
+            needy |= need[w] != 0;
+        }
+        if (!__any(act || needy)) {
+            if (vv)
+#pragma unroll
+                for (int w = 0; w < W; ++w) a.nx[v * W + w] = 0ull;  // nx is written whole in a pull round
+            continue;
+        }
+        uint64_t rb = 0, d = 0;
+        if (vv) {
+            rb = a.rp[v];
+            d = a.rp[v + 1] - rb;
+        }
+        if (act) {  // source side of this peer's pushes (broadcastMessage, peer.cpp:310-316)
+            uint32_t pc = 0;
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                pc += (uint32_t)__popcll(m[w]);
+                if (w < (int)wd) acc.digest += digest_weight((a.begin + v) * wd + w) * m[w];
+                if (COV)
+                    for (uint64_t x = m[w]; x; x &= x - 1) atomicAdd(&cov_s[w * 64 + __builtin_ctzll(x)], 1u);
+            }
+            acc.frontier++;
+            acc.covered += pc;
+            acc.trav += d;
+            acc.deliv += (unsigned long long)pc * d;
+        }
+        const bool light = d <= kHeavyDegree;
+#pragma unroll
+        for (int w = 0; w < W; ++w) my[lane * W + w] = 0ull;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        tile_edges(needy && light ? (uint32_t)d : 0u, rb, [&](int s, bool valid, uint64_t e) {
+            uint64_t ns[W];
+#pragma unroll
+            for (int w = 0; w < W; ++w) ns[w] = __shfl(need[w], s);
+            if (!valid) return;
+            bool want = false;
+#pragma unroll
+            for (int w = 0; w < W; ++w) want |= (ns[w] & ~my[s * W + w]) != 0;  // stale read: only extra loads
+            if (!want) return;  // peer s already collected everything it can learn
+            acc.pulled++;
+            const uint32_t u = a.col[e];
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                const uint64_t x = a.nw[(uint64_t)u * W + w] & ns[w];
+                if (x) atomicOr(&my[s * W + w], (unsigned long long)x);  // LDS ds_or_b64
+            }
+        });
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (vv) {
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                const uint64_t fr = light ? (my[lane * W + w] & need[w]) : 0ull;
+                if (fr) {  // handleClient: new -> Message-List insert (peer.cpp:281-282)
+                    a.seen[v * W + w] = sv[w] | fr;
+                    acc.fresh += (unsigned long long)__popcll(fr);
+                    acc.activated++;
+                }
+                a.nx[v * W + w] = fr;  // heavy rows: 0 here, OR-ed by k_pull_heavy afterwards
+            }
+        }
+    }
+    flush(acc, a.st);
+    if (COV) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < 64 * W; i += kBlock)
+            if (cov_s[i]) atomicAdd(&a.cov[i], (unsigned long long)cov_s[i]);
+    }
+}
+
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_pull_heavy(RoundArgs a) {
+    __shared__ unsigned long long need_s[W];
+    __shared__ unsigned long long red[kWavesPerBlock][W];
+    Acc acc;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (uint64_t ci = blockIdx.x; ci < a.n_chunks; ci += gridDim.x) {
+        const HeavyChunk ch = a.chunks[ci];
+        if (threadIdx.x < W) need_s[threadIdx.x] = a.inj_mask[threadIdx.x] & ~a.seen[(uint64_t)ch.v * W + threadIdx.x];
+        __syncthreads();
+        uint64_t need[W], part[W];
+        bool any = false;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            need[w] = need_s[w];
+            part[w] = 0;
+            any |= need[w] != 0;
+        }
+        if (any) {  // uniform: every thread read the same need_s
+            for (uint64_t e = ch.e0 + threadIdx.x; e < ch.e1; e += kBlock) {
+                const uint32_t u = a.col[e];
+                acc.pulled++;
+#pragma unroll
+                for (int w = 0; w < W; ++w)
+                    if (need[w]) part[w] |= a.nw[(uint64_t)u * W + w] & need[w];
+            }
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) part[w] |= __shfl_xor(part[w], off);
+                if (lane == 0) red[wid][w] = part[w];
+            }
+            __syncthreads();
+            if (threadIdx.x < W) {
+                const int w = threadIdx.x;
+                uint64_t tot = 0;
+                for (int k = 0; k < kWavesPerBlock; ++k) tot |= red[k][w];
+                if (tot) {
+                    unsigned long long* sp = reinterpret_cast<unsigned long long*>(a.seen) + (uint64_t)ch.v * W + w;
+                    const unsigned long long fr = tot & ~atomicOr(sp, (unsigned long long)tot);
+                    if (fr) {
+                        const unsigned long long onx =
+                            atomicOr(reinterpret_cast<unsigned long long*>(a.nx) + (uint64_t)ch.v * W + w, fr);
+                        acc.activated += onx == 0;
+                        acc.fresh += (unsigned long long)__popcll(fr);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+    acc.htrav = acc.pulled;  // heavy-row edges scanned
+    acc.pulled = 0;
     flush(acc, a.st);
 }
 
@@ -536,6 +706,25 @@ hipError_t launch_push_light(const RoundArgs& a, uint32_t W_, bool check_alive, 
         }
     });
 #undef GOSSIP_LIGHT
+    return hipGetLastError();
+}
+
+hipError_t launch_pull_light(const RoundArgs& a, uint32_t W_, hipStream_t s) {
+    const uint64_t tiles = (a.n_local + 63) / 64;
+    const unsigned g = grid_for(tiles, kWavesPerBlock);
+    const uint32_t wd = wd_of(W_);
+    if (a.cov) {
+        GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_pull_light<W, true>), dim3(g), dim3(kBlock), 0, s, a, wd));
+    } else {
+        GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_pull_light<W, false>), dim3(g), dim3(kBlock), 0, s, a, wd));
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_pull_heavy(const RoundArgs& a, uint32_t W_, hipStream_t s) {
+    if (!a.n_chunks) return hipSuccess;
+    GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_pull_heavy<W>, dim3(grid_for(a.n_chunks, 1)), dim3(kBlock), 0, s,
+                                                   a));
     return hipGetLastError();
 }
 

@@ -25,6 +25,8 @@ GOSSIP_EOVERFLOW = -6
 GRAPH_POWERLAW = 1
 GRAPH_REF_BOOTSTRAP = 2
 FLAG_COVERAGE_HISTORY = 1
+FLAG_FORCE_PUSH = 2
+FLAG_FORCE_PULL = 4
 
 
 class GossipConfig(C.Structure):
@@ -45,6 +47,8 @@ class GossipConfig(C.Structure):
         ("device", C.c_int32),
         ("flags", C.c_uint32),
         ("report_capacity", C.c_uint64),
+        ("pull_permille", C.c_uint32),
+        ("reserved", C.c_uint32),
     ]
 
 

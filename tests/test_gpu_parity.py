@@ -25,12 +25,13 @@ def _hand_csr(case):
     return rp, np.array([c for r in rows for c in r], dtype=np.uint32)
 
 
+@pytest.mark.parametrize("mode", ["push", "pull"])
 @pytest.mark.parametrize("case", json.loads((GOLDEN / "hand_graphs.json").read_text())["cases"],
                          ids=lambda c: c["name"])
-def test_hand_graphs(case):
+def test_hand_graphs(case, mode):
     fields = json.loads((GOLDEN / "hand_graphs.json").read_text())["fields"]
     with Engine(case["n"], len(case["origins"]), ping_every=case.get("ping_every", 0),
-                max_missed=case.get("max_missed", 3), min_rounds=case.get("min_rounds", 0)) as e:
+                max_missed=case.get("max_missed", 3), min_rounds=case.get("min_rounds", 0), mode=mode) as e:
         e.load_csr(*_hand_csr(case))
         e.inject(case["origins"], case["inject_rounds"])
         kills = case.get("kills", [])
@@ -69,12 +70,13 @@ def _compare(e, ref, w):
     return got
 
 
+@pytest.mark.parametrize("mode", ["auto", "push", "pull"])
 @pytest.mark.parametrize("idx,n", [(1, None), (2, 1 << 16), (3, 1 << 18), (5, 1 << 16), (5, 50_000)])
-def test_workload_parity(oracle, idx, n):
+def test_workload_parity(oracle, idx, n, mode):
     w = config(idx, n, pick=oracle.pick_origins)
     rp, col = oracle.gen_workload(w)
     ref = oracle.simulate_workload(w, rp, col)
-    with _engine(w) as e:
+    with _engine(w, mode=mode) as e:
         e.build_graph()
         e.inject(w.origins, w.inject_rounds)
         if w.kills:
@@ -85,16 +87,18 @@ def test_workload_parity(oracle, idx, n):
         assert e.run() == first
 
 
+@pytest.mark.parametrize("mode", ["push", "pull"])
 @pytest.mark.parametrize("M", [65, 130, 300, 512])
-def test_multiword_messages(oracle, M):
+def test_multiword_messages(oracle, M, mode):
     n = 1 << 14
     rng = np.random.default_rng(M)
     origins = rng.integers(0, n, M).astype(np.uint32)
     rounds = rng.integers(0, 4, M).astype(np.uint32)
     rp, col = oracle.gen("powerlaw", n, 6, 77)
-    ref = oracle.simulate(rp, col, n, M, origins, rounds, seed=77, churn_threshold=42949673 * 2, ping_every=2,
+    churn = 42949673 * 2 if mode == "push" else 0   # pull rounds need a churn-free run
+    ref = oracle.simulate(rp, col, n, M, origins, rounds, seed=77, churn_threshold=churn, ping_every=2,
                           max_missed=2)
-    with Engine(n, M, rng_seed=77, churn_threshold=42949673 * 2, ping_every=2, max_missed=2) as e:
+    with Engine(n, M, rng_seed=77, churn_threshold=churn, ping_every=2, max_missed=2, mode=mode) as e:
         e.load_csr(rp, col)
         e.inject(origins, rounds)
         e.reset()
@@ -121,12 +125,12 @@ def _digest(seen):
     return int(np.sum(z * seen.reshape(-1), dtype=np.uint64))
 
 
-@pytest.mark.parametrize("idx", [3, 5])
-def test_full_size_properties(idx):
-    """BASELINE sizes (config 3: 2^24 peers; config 5: 2^26 with churn):
-    checksum-of-state, conservation and determinism."""
+@pytest.mark.parametrize("idx,mode", [(3, "auto"), (3, "push"), (5, "auto"), (4, "auto")])
+def test_full_size_properties(idx, mode):
+    """BASELINE sizes (config 3: 2^24 peers; config 4: 2^28; config 5: 2^26
+    with churn): checksum-of-state, conservation, push == pull, determinism."""
     w = config(idx)
-    with _engine(w) as e:
+    with _engine(w, mode=mode) as e:
         stats = run_engine(e, w)
         last = stats[-1]
         assert last["new_receipts"] == 0
@@ -148,3 +152,15 @@ def test_full_size_properties(idx):
             assert np.all(e.registered()[reps[:, 2]] == 0)
         e.reset()
         assert e.run() == stats
+
+
+def test_push_equals_pull_at_full_size():
+    """config 3 at its full 2^24 peers: the direction-optimised schedule and the
+    push-only schedule produce identical rounds and seen sets."""
+    w = config(3)
+    out = {}
+    for mode in ("push", "auto"):
+        with _engine(w, mode=mode) as e:
+            out[mode] = (run_engine(e, w), e.read_seen())
+    assert out["push"][0] == out["auto"][0]
+    assert np.array_equal(out["push"][1], out["auto"][1])
