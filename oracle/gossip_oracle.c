@@ -687,3 +687,212 @@ uint64_t oracle_sim_sent_to_total(const oracle_sim* s) {
             if (s->lists[v].key[i] != 0xFFFFFFFFu) t += s->lists[v].sent_to[i];
     return t;
 }
+
+/* ------------------------------------------------------------------------ */
+/* Partition emulation: the same round model over one vertex block          */
+/* [b, e) of a P-way 1D partition, with an explicit exchange step, so that  */
+/* the multi-rank driver can be tested on CPU (gloo).  State that the       */
+/* engine keeps globally (alive, registry view) is global here too.         */
+/* ------------------------------------------------------------------------ */
+struct oracle_part {
+    oracle_sim_cfg cfg;
+    uint64_t n, b, e, nl, E;
+    uint32_t W, M;
+    const uint64_t* rp;
+    const uint32_t* col;
+    uint8_t *alive, *registered, *masked, *miss;
+    uint64_t *seen, *nw, *nx;
+    uint32_t *origin, *inject_round, n_kills, *kill_peer, *kill_round;
+    oracle_report* rep;
+    uint64_t n_rep, cap_rep;
+    uint32_t round;
+    int finished;
+    uint64_t prev_digest, prev_covered;
+    oracle_stats cur;
+};
+
+oracle_part* oracle_part_create(const oracle_sim_cfg* cfg, uint64_t b, uint64_t e, const uint64_t* row_ptr,
+                                const uint32_t* col) {
+    if (!cfg || b >= e || e > cfg->n) return NULL;
+    oracle_part* p = (oracle_part*)calloc(1, sizeof(oracle_part));
+    p->cfg = *cfg;
+    if (p->cfg.max_rounds == 0) p->cfg.max_rounds = 1u << 20;
+    p->n = cfg->n; p->b = b; p->e = e; p->nl = e - b;
+    p->E = row_ptr[p->nl];
+    p->M = cfg->n_msgs; p->W = (cfg->n_msgs + 63) / 64;
+    p->rp = row_ptr; p->col = col;
+    p->alive = (uint8_t*)malloc(p->n); memset(p->alive, 1, p->n);
+    p->registered = (uint8_t*)malloc(p->n); memset(p->registered, 1, p->n);
+    p->masked = (uint8_t*)calloc(p->E + 1, 1);
+    p->miss = (uint8_t*)calloc(p->E + 1, 1);
+    p->seen = (uint64_t*)calloc(p->nl * p->W, 8);
+    p->nw = (uint64_t*)calloc(p->nl * p->W, 8);
+    p->nx = (uint64_t*)calloc(p->nl * p->W, 8);
+    p->origin = (uint32_t*)calloc(p->M, 4);
+    p->inject_round = (uint32_t*)malloc(p->M * 4);
+    for (uint32_t m = 0; m < p->M; ++m) p->inject_round[m] = 0xFFFFFFFFu;
+    return p;
+}
+
+void oracle_part_destroy(oracle_part* p) {
+    if (!p) return;
+    free(p->alive); free(p->registered); free(p->masked); free(p->miss);
+    free(p->seen); free(p->nw); free(p->nx); free(p->origin); free(p->inject_round);
+    free(p->kill_peer); free(p->kill_round); free(p->rep);
+    free(p);
+}
+
+int oracle_part_schedule(oracle_part* p, const uint32_t* origin, const uint32_t* inject_round, uint32_t n_kills,
+                         const uint32_t* kill_peer, const uint32_t* kill_round) {
+    for (uint32_t m = 0; m < p->M; ++m) { p->origin[m] = origin[m]; p->inject_round[m] = inject_round[m]; }
+    free(p->kill_peer); free(p->kill_round);
+    p->n_kills = n_kills;
+    p->kill_peer = (uint32_t*)malloc((n_kills + 1) * 4);
+    p->kill_round = (uint32_t*)malloc((n_kills + 1) * 4);
+    for (uint32_t i = 0; i < n_kills; ++i) { p->kill_peer[i] = kill_peer[i]; p->kill_round[i] = kill_round[i]; }
+    return 0;
+}
+
+static int owned(const oracle_part* p, uint64_t v) { return v >= p->b && v < p->e; }
+
+/* churn, liveness, injection, push-start stats, local push; masks for peers
+ * of other blocks are OR-ed into send[v * W + w] (dense, global index). */
+int oracle_part_push(oracle_part* p, uint64_t* send) {
+    const uint32_t W = p->W, r = p->round;
+    oracle_stats* st = &p->cur;
+    memset(st, 0, sizeof(*st));
+    st->round = r;
+    /* churn + kills over every peer (alive state is global) */
+    for (uint32_t i = 0; i < p->n_kills; ++i) {
+        uint32_t v = p->kill_peer[i];
+        if (p->kill_round[i] == r && p->alive[v]) { p->alive[v] = 0; if (owned(p, v)) st->died++; }
+    }
+    if (p->cfg.churn_threshold) {
+        for (uint64_t v = 0; v < p->n; ++v) {
+            if (!p->alive[v]) continue;
+            if (philox_x(p->cfg.seed, (uint32_t)v, ORACLE_P_CHURN, r, 0, 0, 0) < p->cfg.churn_threshold) {
+                p->alive[v] = 0;
+                if (owned(p, v)) st->died++;
+            }
+        }
+    }
+    for (uint64_t lv = 0; lv < p->nl; ++lv)
+        if (!p->alive[p->b + lv]) memset(p->nw + lv * W, 0, W * 8);
+    if (p->cfg.ping_every && r % p->cfg.ping_every == 0) {
+        st->flags |= 1;
+        for (uint64_t lu = 0; lu < p->nl; ++lu) {
+            uint64_t u = p->b + lu;
+            if (!p->alive[u]) continue;
+            for (uint64_t e = p->rp[lu]; e < p->rp[lu + 1]; ++e) {
+                if (p->masked[e]) continue;
+                uint32_t v = p->col[e];
+                if (p->alive[v]) { p->miss[e] = 0; continue; }
+                if (p->miss[e] < 255) p->miss[e]++;
+                if (p->miss[e] >= p->cfg.max_missed) {
+                    p->masked[e] = 1;
+                    if (p->n_rep == p->cap_rep) {
+                        p->cap_rep = p->cap_rep ? 2 * p->cap_rep : 1024;
+                        p->rep = (oracle_report*)realloc(p->rep, p->cap_rep * sizeof(oracle_report));
+                    }
+                    p->rep[p->n_rep].round = r; p->rep[p->n_rep].reporter = (uint32_t)u; p->rep[p->n_rep].dead = v;
+                    p->n_rep++;
+                    st->reports++;
+                    if (p->registered[v]) { p->registered[v] = 0; st->seed_removals++; }
+                }
+            }
+        }
+    }
+    for (uint32_t m = 0; m < p->M; ++m) {
+        uint32_t o = p->origin[m];
+        if (p->inject_round[m] != r || !owned(p, o) || !p->alive[o]) continue;
+        p->seen[(o - p->b) * W + (m >> 6)] |= 1ull << (m & 63);
+        p->nw[(o - p->b) * W + (m >> 6)] |= 1ull << (m & 63);
+        st->injected++;
+    }
+    uint64_t digest = 0, covered = 0;
+    for (uint64_t lv = 0; lv < p->nl; ++lv) {
+        int act = 0;
+        for (uint32_t w = 0; w < W; ++w) {
+            uint64_t x = p->seen[lv * W + w];
+            act |= p->nw[lv * W + w] != 0;
+            covered += (uint64_t)__builtin_popcountll(x);
+            digest += oracle_digest_weight((p->b + lv) * W + w) * x;
+        }
+        st->frontier += (uint64_t)act;
+    }
+    st->digest = digest - p->prev_digest;  /* increments, summed over ranks by the driver */
+    st->covered = covered - p->prev_covered;
+    p->prev_digest = digest;
+    p->prev_covered = covered;
+    for (uint64_t lu = 0; lu < p->nl; ++lu) {
+        const uint64_t* mk = p->nw + lu * W;
+        uint64_t pc = 0;
+        int act = 0;
+        for (uint32_t w = 0; w < W; ++w) { act |= mk[w] != 0; pc += (uint64_t)__builtin_popcountll(mk[w]); }
+        if (!act) continue;
+        for (uint64_t e = p->rp[lu]; e < p->rp[lu + 1]; ++e) {
+            if (p->masked[e]) continue;
+            st->traversals++;
+            uint32_t v = p->col[e];
+            if (!p->alive[v]) { st->undelivered += pc; continue; }
+            st->deliveries += pc;
+            if (!owned(p, v)) {
+                for (uint32_t w = 0; w < W; ++w) send[(uint64_t)v * W + w] |= mk[w];
+                continue;
+            }
+            for (uint32_t w = 0; w < W; ++w) {
+                uint64_t* s = &p->seen[(v - p->b) * W + w];
+                uint64_t fr = mk[w] & ~*s;
+                *s |= mk[w];
+                if (fr) { p->nx[(v - p->b) * W + w] |= fr; st->new_receipts += (uint64_t)__builtin_popcountll(fr); }
+            }
+        }
+    }
+    return 0;
+}
+
+/* test-and-set of the masks received from every block (recv: world x nl x W) */
+int oracle_part_finish(oracle_part* p, const uint64_t* recv, uint32_t world, oracle_stats* out) {
+    const uint32_t W = p->W;
+    for (uint64_t lv = 0; lv < p->nl; ++lv) {
+        for (uint32_t w = 0; w < W; ++w) {
+            uint64_t inc = 0;
+            for (uint32_t q = 0; q < world; ++q) inc |= recv[((uint64_t)q * p->nl + lv) * W + w];
+            uint64_t fr = inc & ~p->seen[lv * W + w];
+            if (!fr) continue;
+            p->seen[lv * W + w] |= fr;
+            p->nx[lv * W + w] |= fr;
+            p->cur.new_receipts += (uint64_t)__builtin_popcountll(fr);
+        }
+    }
+    p->cur.duplicates = p->cur.deliveries - p->cur.new_receipts;
+    if (out) *out = p->cur;
+    return 0;
+}
+
+int oracle_part_commit(oracle_part* p, uint64_t global_new_receipts) {
+    uint64_t* t = p->nw; p->nw = p->nx; p->nx = t;
+    memset(p->nx, 0, p->nl * p->W * 8);
+    uint32_t r = p->round++;
+    int pending = 0;
+    for (uint32_t m = 0; m < p->M; ++m) pending |= (p->inject_round[m] != 0xFFFFFFFFu && p->inject_round[m] > r);
+    if ((global_new_receipts == 0 && !pending && p->round >= p->cfg.min_rounds) || p->round >= p->cfg.max_rounds)
+        p->finished = 1;
+    return p->finished;
+}
+
+void oracle_part_reset(oracle_part* p) {
+    memset(p->alive, 1, p->n); memset(p->registered, 1, p->n);
+    memset(p->masked, 0, p->E + 1); memset(p->miss, 0, p->E + 1);
+    memset(p->seen, 0, p->nl * p->W * 8); memset(p->nw, 0, p->nl * p->W * 8); memset(p->nx, 0, p->nl * p->W * 8);
+    p->n_rep = 0; p->round = 0; p->finished = 0; p->prev_digest = p->prev_covered = 0;
+}
+
+void oracle_part_seen(const oracle_part* p, uint64_t* out) { memcpy(out, p->seen, p->nl * p->W * 8); }
+
+uint64_t oracle_part_reports(const oracle_part* p, oracle_report* buf, uint64_t cap) {
+    qsort(p->rep, p->n_rep, sizeof(oracle_report), cmp_rep);
+    uint64_t k = p->n_rep < cap ? p->n_rep : cap;
+    if (buf && k) memcpy(buf, p->rep, k * sizeof(oracle_report));
+    return p->n_rep;
+}

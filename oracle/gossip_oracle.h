@@ -130,6 +130,24 @@ void oracle_sim_alive(const oracle_sim* s, uint8_t* out);          /* n bytes */
 void oracle_sim_registered(const oracle_sim* s, uint8_t* out);     /* n bytes */
 uint64_t oracle_sim_sent_to_total(const oracle_sim* s);             /* literal variant: sum sentTo */
 
+/* ---- partition emulation (multi-rank driver tests on CPU) --------------- */
+/* One block [b, e) of a 1D partition: row_ptr is local (e-b+1 entries),
+ * col holds global ids.  Per round: part_push(send) -> exchange ->
+ * part_finish(recv) -> sum of the ranks' stats -> part_commit(global fresh).
+ * part_finish's digest/covered are per-round increments. */
+typedef struct oracle_part oracle_part;
+oracle_part* oracle_part_create(const oracle_sim_cfg* cfg, uint64_t b, uint64_t e, const uint64_t* row_ptr,
+                                const uint32_t* col);
+void oracle_part_destroy(oracle_part* p);
+int oracle_part_schedule(oracle_part* p, const uint32_t* origin, const uint32_t* inject_round, uint32_t n_kills,
+                         const uint32_t* kill_peer, const uint32_t* kill_round);
+int oracle_part_push(oracle_part* p, uint64_t* send);
+int oracle_part_finish(oracle_part* p, const uint64_t* recv, uint32_t world, oracle_stats* out);
+int oracle_part_commit(oracle_part* p, uint64_t global_new_receipts);
+void oracle_part_reset(oracle_part* p);
+void oracle_part_seen(const oracle_part* p, uint64_t* out);
+uint64_t oracle_part_reports(const oracle_part* p, oracle_report* buf, uint64_t cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -127,3 +127,76 @@ class Oracle:
                              churn_threshold=w.churn_threshold, ping_every=w.ping_every, max_missed=w.max_missed,
                              min_rounds=w.min_rounds, kills=w.kills, variant=variant, threads=threads,
                              max_rounds=max_rounds)
+
+
+class OraclePartition:
+    """One rank's block of the oracle's partition emulation, with the same
+    phase API the multi-rank driver (gossip_hip.distributed) drives on a
+    libgossip_hip Engine.  CPU tests only."""
+
+    def __init__(self, orc: Oracle, w, rp_global, col_global, begin, end, threads=1):
+        L = orc.L
+        L.oracle_part_create.restype = C.c_void_p
+        L.oracle_part_reports.restype = C.c_uint64
+        self.L, self.w = L, w
+        self.begin, self.end = begin, end
+        self.n_local = end - begin
+        self.W = (w.n_msgs + 63) // 64
+        base = int(rp_global[begin])
+        self.rp = np.ascontiguousarray(rp_global[begin:end + 1] - np.uint64(base), dtype=np.uint64)
+        self.col = np.ascontiguousarray(col_global[base:int(rp_global[end])], dtype=np.uint32)
+        if self.col.size == 0:
+            self.col = np.zeros(1, dtype=np.uint32)
+        cfg = OCfg(w.n, w.n_msgs, w.rng_seed, w.churn_threshold, w.ping_every, w.max_missed, 4096, w.min_rounds,
+                   threads, 0)
+        self.p = C.c_void_p(L.oracle_part_create(C.byref(cfg), C.c_uint64(begin), C.c_uint64(end),
+                                                  _p(self.rp, C.c_uint64), _p(self.col, C.c_uint32)))
+        o = np.ascontiguousarray(w.origins, dtype=np.uint32)
+        r = np.ascontiguousarray(w.inject_rounds, dtype=np.uint32)
+        kp = np.array([k[0] for k in w.kills] + [0], dtype=np.uint32)
+        kr = np.array([k[1] for k in w.kills] + [0], dtype=np.uint32)
+        L.oracle_part_schedule(self.p, _p(o, C.c_uint32), _p(r, C.c_uint32), C.c_uint32(len(w.kills)),
+                               _p(kp, C.c_uint32), _p(kr, C.c_uint32))
+        self._send = self._recv = None
+        self.world = 1
+
+    def shape(self):
+        return {"words": self.W, "exchange_words": self.W, "n_local": self.n_local, "n_edges": int(self.rp[-1])}
+
+    def set_exchange(self, send_ptr, recv_ptr, part):
+        self._send = C.cast(C.c_void_p(send_ptr), C.POINTER(C.c_uint64))
+        self._recv = C.cast(C.c_void_p(recv_ptr), C.POINTER(C.c_uint64))
+        self.world = len(part) - 1
+        self._send_words = self.w.n * self.W
+
+    def reset(self):
+        self.L.oracle_part_reset(self.p)
+
+    def round_push(self):
+        C.memset(self._send, 0, self._send_words * 8)
+        self.L.oracle_part_push(self.p, self._send)
+
+    def round_finish(self):
+        st = OStats()
+        self.L.oracle_part_finish(self.p, self._recv, C.c_uint32(self.world), C.byref(st))
+        return st.as_dict()
+
+    def round_commit(self, global_new_receipts):
+        return bool(self.L.oracle_part_commit(self.p, C.c_uint64(global_new_receipts)))
+
+    def read_seen(self):
+        out = np.zeros((self.n_local, self.W), dtype=np.uint64)
+        self.L.oracle_part_seen(self.p, _p(out, C.c_uint64))
+        return out
+
+    def reports(self):
+        n = int(self.L.oracle_part_reports(self.p, None, C.c_uint64(0)))
+        buf = (OReport * max(n, 1))()
+        self.L.oracle_part_reports(self.p, buf, C.c_uint64(n))
+        return np.array([(buf[i].round, buf[i].reporter, buf[i].dead) for i in range(n)],
+                        dtype=np.uint32).reshape(n, 3)
+
+    def close(self):
+        if self.p:
+            self.L.oracle_part_destroy(self.p)
+            self.p = None
