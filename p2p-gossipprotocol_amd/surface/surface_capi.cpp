@@ -1,0 +1,70 @@
+// surface_capi.cpp -- extern "C" probes of the drop-in surface for the test
+// harness (ctypes): NetworkConfig outcomes and the reference string formats.
+#include <cstring>
+#include <exception>
+#include <string>
+
+#include "gossip/config.hpp"
+#include "gossip/formats.hpp"
+
+namespace {
+
+int put(const std::string& s, char* out, size_t cap) {
+    if (!out || cap == 0) return -1;
+    const size_t k = std::min(cap - 1, s.size());
+    std::memcpy(out, s.data(), k);
+    out[k] = 0;
+    return s.size() < cap ? 0 : -1;
+}
+
+}  // namespace
+
+extern "C" {
+
+// JSON object in the shape of oracle/ref_config_driver's output.
+int gossip_surface_netcfg(const char* path, char* out, size_t cap) {
+    std::string js;
+    try {
+        NetworkConfig c(path);
+        std::string seeds;
+        for (const auto& s : c.getSeedNodes()) seeds += (seeds.empty() ? "" : ",") + gossip::json_escape(s.toString());
+        js = "{\"ok\":true,\"seeds\":[" + seeds + "],\"min_seeds\":" + std::to_string(c.getMinRequiredSeeds()) +
+             ",\"ping_interval\":" + std::to_string(c.getPingInterval()) +
+             ",\"message_interval\":" + std::to_string(c.getMessageInterval()) +
+             ",\"max_messages\":" + std::to_string(c.getMaxMessages()) +
+             ",\"max_missed_pings\":" + std::to_string(c.getMaxMissedPings()) +
+             ",\"local_ip\":" + gossip::json_escape(c.getLocalIP()) + ",\"local_port\":" + std::to_string(c.getLocalPort()) +
+             ",\"to_string\":" + gossip::json_escape(c.toString()) + "}";
+    } catch (const NetworkConfig::ConfigException& e) {
+        js = "{\"ok\":false,\"kind\":\"ConfigException\",\"what\":" + gossip::json_escape(e.what()) + "}";
+    } catch (const std::exception& e) {
+        js = "{\"ok\":false,\"kind\":\"std::exception\",\"what\":" + gossip::json_escape(e.what()) + "}";
+    }
+    return put(js, out, cap);
+}
+
+int gossip_surface_message(const char* ip, int port, unsigned round, int msg_number, char* out, size_t cap) {
+    const std::string content = gossip::message_content({ip, port});
+    const std::string ts = gossip::message_timestamp(round);
+    const std::string h = gossip::message_hash(content, ts, ip);
+    return put(gossip::gossip_json(content, h, msg_number, ip, port, ts), out, cap);
+}
+
+int gossip_surface_hash(const char* content, const char* timestamp, const char* ip, char* out, size_t cap) {
+    return put(gossip::message_hash(content, timestamp, ip), out, cap);
+}
+
+int gossip_surface_register(const char* ip, int port, char* out, size_t cap) {
+    return put(gossip::register_json(ip, port), out, cap);
+}
+
+int gossip_surface_dead_node(const char* ip, int port, char* out, size_t cap) {
+    return put(gossip::dead_node_json(ip, port), out, cap);
+}
+
+int gossip_surface_log(int seed_style, long long t, const char* msg, char* out, size_t cap) {
+    return put(seed_style ? gossip::seed_log_line((std::time_t)t, msg) : gossip::peer_log_line((std::time_t)t, msg), out,
+               cap);
+}
+
+}  // extern "C"

@@ -1,0 +1,51 @@
+"""The drop-in surface on the GPU: `gossip_peer_network network.txt` with the
+reference's 20 seeds, 8 peers, 10 messages each, peer 3 killed at round 12
+(BASELINE.json configs[0]) -- stats equal the oracle's, and the per-peer /
+per-seed log files say what the reference would have logged."""
+import json
+import subprocess
+from pathlib import Path
+
+import pytest
+
+from gossip_hip.workloads import config
+
+pytestmark = pytest.mark.gpu
+REPO = Path(__file__).resolve().parent.parent
+EXE = REPO / "p2p-gossipprotocol_amd" / "build" / "gossip_peer_network"
+
+
+def test_cli_reference_run(oracle, tmp_path):
+    cfg = tmp_path / "network.txt"
+    cfg.write_text((REPO / "tests" / "golden" / "network.txt").read_text() +
+                   "n_peers=8\nrng_seed=0x5EED0001\nkills=3@12\nmin_rounds=46\n")
+    logs = tmp_path / "logs"
+    logs.mkdir()
+    r = subprocess.run([str(EXE), str(cfg), "--logs", str(logs)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "Minimum Required Seeds: 11" in r.stdout
+    rounds = [json.loads(l) for l in r.stdout.splitlines() if l.startswith('{"round"')]
+    w = config(1, pick=oracle.pick_origins)
+    rp, col = oracle.gen_workload(w)
+    ref = oracle.simulate_workload(w, rp, col)
+    assert [(x["round"], x["frontier"], x["deliveries"], x["new_receipts"], x["died"], x["reports"], x["covered"])
+            for x in rounds] == [(s["round"], s["frontier"], s["deliveries"], s["new_receipts"], s["died"],
+                                  s["reports"], s["covered"]) for s in ref["stats"]]
+    # F8: peer 0 connects to nobody; peer 7 to everyone before it
+    p0 = (logs / "peer_5000_output.txt").read_text()
+    p7 = (logs / "peer_5007_output.txt").read_text()
+    assert "Connected to peer" not in p0
+    assert p7.count("Connected to peer: 127.0.0.1:") == 7
+    assert p7.count("Generated message: Message from 127.0.0.1:5007") == 10
+    assert "Received new message" not in p7          # nobody pushes to the last arrival
+    assert p0.count("Received new message: Message from 127.0.0.1:5007") == 10
+    # peer 3 died at round 12: it generated messages 0..2 only; 4..7 report it at round 45
+    p3 = (logs / "peer_5003_output.txt").read_text()
+    assert p3.count("Generated message") == 3
+    for u in range(4, 8):
+        assert "Peer disconnected: 127.0.0.1:5003" in (logs / f"peer_{5000 + u}_output.txt").read_text()
+    s0 = (logs / "seed_8000_output.txt").read_text()
+    assert s0.count("Registered new peer") == 8
+    assert s0.count("Received dead node notification for: 127.0.0.1:5003") == 4
+    assert s0.count("Removed dead peer: 127.0.0.1:5003") == 1
+    assert "Registered new peer" not in (logs / "seed_8019_output.txt").read_text()  # quorum reached at seed 10
