@@ -9,14 +9,20 @@
 // messageList with sentTo).
 #pragma once
 
+#include <chrono>
+#include <condition_variable>
 #include <memory>
+#include <mutex>
+#include <queue>
 #include <set>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <utility>
 #include <vector>
 
 #include "gossip/info.hpp"
+#include "gossip/seed.hpp"  // the reference's peer.hpp pulls PeerInfo in through seed.hpp
 
 struct Message {
     std::string content;

@@ -92,3 +92,17 @@ def test_cli_config_error_and_usage(tmp_path):
     assert "Configuration error: Configuration Error: Ping interval must be positive" in r.stderr
     r = subprocess.run([exe, str(tmp_path / "nope.txt")], capture_output=True, text=True)
     assert r.returncode == 1 and "Unable to open config file" in r.stderr
+
+
+@pytest.mark.skipif(not Path("/root/reference/main.cpp").exists(), reason="reference sources only in the build container")
+def test_reference_main_compiles_against_dropin_headers(tmp_path):
+    """The reference's own main.cpp (read from /root/reference, fed on stdin so
+    its directory's headers are not picked up) compiles unchanged against
+    include/gossip/*.hpp and links with libgossip_surface."""
+    exe = tmp_path / "peer_network"
+    src = Path("/root/reference/main.cpp").read_bytes()
+    r = subprocess.run(["g++", "-std=c++17", f"-I{REPO / 'include'}", f"-I{REPO / 'include' / 'gossip'}", "-x", "c++",
+                        "-", "-x", "none", f"-L{BUILD}", "-lgossip_surface", "-lgossip_hip",
+                        f"-Wl,-rpath,{BUILD}", "-o", str(exe)], input=src, capture_output=True)
+    assert r.returncode == 0, r.stderr.decode()
+    assert exe.exists()
