@@ -40,7 +40,33 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP event timing")
+    ap.add_argument("--pull-permille", type=int, default=0, help="push/pull switch point (0 = engine default)")
+    ap.add_argument("--front-permille", type=int, default=0, help="frontier-bitmap switch point (0 = default)")
+    ap.add_argument("--mode", default="auto", choices=["auto", "push", "pull"])
     return ap.parse_args()
+
+
+def pmc_traffic(workload: str, kernel: str, alg_bytes_per_launch: float, n_local: int):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
+    (FETCH_SIZE and WRITE_SIZE, separate runs of this same command) with the
+    gfx950 corrections measured by tools/calib_fetch.hip: FETCH_SIZE counts
+    1/2 of coalesced streamed bytes and one 64-B line per random 8-B gather,
+    so traffic = fetch_counted + streamed_reads / 2 + write_counted."""
+    path = REPO / "profiles" / "r01" / "config4_pmc_summary.json"
+    if not workload.startswith("config4") or not path.exists():
+        return None, None
+    prof = json.loads(path.read_text())
+    key = next((k for k in prof["kernels"] if k.startswith("k_" + kernel)), None)
+    if key is None or "fetch_bytes_per_launch_counted" not in prof["kernels"][key]:
+        return None, None
+    k = prof["kernels"][key]
+    if kernel == "pull_light":
+        scanned = max(alg_bytes_per_launch - 40.0 * n_local, 0.0) / 12.0
+        streamed = 24.0 * n_local + 4.0 * scanned
+    else:
+        streamed = 0.0
+    t = k["fetch_bytes_per_launch_counted"] + streamed / 2 + k.get("write_bytes_per_launch_counted", 0.0)
+    return round(t), f"{path.relative_to(REPO)} ({key}: {k['launches']} launches, avg {k['avg_ms']:.3f} ms)"
 
 
 def rounds_to_full(stats: list[dict]) -> int:
@@ -89,6 +115,7 @@ def main():
     from gossip_hip.workloads import config
 
     w = config(args.config, args.n or None)
+    tune = dict(pull_permille=args.pull_permille, front_permille=args.front_permille, mode=args.mode)
     if world > 1:
         import torch.distributed as dist
 
@@ -96,7 +123,7 @@ def main():
 
         dist.init_process_group("nccl", device_id=dev)
         part = partition(w.n, world)
-        eng = Engine(w.n, w.n_msgs, device=local, part=(part[rank], part[rank + 1]), **w.engine_kwargs())
+        eng = Engine(w.n, w.n_msgs, device=local, part=(part[rank], part[rank + 1]), **tune, **w.engine_kwargs())
         eng.build_graph()
         eng.inject(w.origins, w.inject_rounds)
         if w.kills:
@@ -112,7 +139,7 @@ def main():
             dist.barrier()
             torch.cuda.synchronize()
     else:
-        eng = Engine(w.n, w.n_msgs, device=local, **w.engine_kwargs())
+        eng = Engine(w.n, w.n_msgs, device=local, **tune, **w.engine_kwargs())
         eng.build_graph()
         eng.inject(w.origins, w.inject_rounds)
         if w.kills:
@@ -156,8 +183,10 @@ def main():
             per_launch_bytes = k_b[dom] / launches
             avg_s = ms / launches / 1e3
             ach = per_launch_bytes / avg_s / 1e9
+            traffic, tsrc = pmc_traffic(w.name, dom, per_launch_bytes, shape["n_local"])
             roofline = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
-                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                        "traffic_source": tsrc,
                         "avg_launch_ms": round(ms / launches, 4), "launches": launches,
                         "alg_bytes_per_launch": round(per_launch_bytes),
                         "kernel_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in k_ms.items() if v[1]},

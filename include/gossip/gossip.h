@@ -66,7 +66,7 @@ typedef struct gossip_config {
     uint32_t flags;           /* GOSSIP_FLAG_* */
     uint64_t report_capacity; /* dead-node report buffer entries (0 = default) */
     uint32_t pull_permille;   /* pull when the frontier estimate >= this per-mille of the owned peers (0 = 50) */
-    uint32_t reserved;
+    uint32_t front_permille;  /* pull rounds probe a frontier bitmap below this per-mille (0 = 400; 1000 = always) */
 } gossip_config;
 
 /*
@@ -184,8 +184,9 @@ gossip_status gossip_kernel_time(gossip_ctx* ctx, const char* kernel, double* ms
 /* Algorithmic HBM bytes of the same kernels over the same
  * interval: push = 32 B per frontier peer + 20 B per edge traversal (light
  * rows to "push_light", heavy rows to "push_heavy"); liveness = 6.125 B per
- * live edge checked; pull = 40 B per owned peer + 12 B per edge scanned
- * ("pull_light") and 12 B per heavy-row edge scanned ("pull_heavy"). */
+ * live edge checked; pull = 40 B per owned peer + 4 B per edge scanned + 8 B
+ * per neighbour word gathered ("pull_light"), 12 B per heavy-row edge scanned
+ * ("pull_heavy"), 8.125 B per owned peer ("frontier_bits"). */
 gossip_status gossip_kernel_bytes(gossip_ctx* ctx, const char* kernel, double* bytes);
 
 #ifdef __cplusplus

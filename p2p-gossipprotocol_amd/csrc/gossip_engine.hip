@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <new>
@@ -69,6 +70,7 @@ struct gossip_ctx {
 
     // dynamic state
     uint64_t *seen = nullptr, *nw = nullptr, *nx = nullptr;
+    uint64_t* front = nullptr;  // pull-round frontier bitmap
     uint32_t* alive = nullptr;
     uint32_t* registered = nullptr;
     uint8_t* miss = nullptr;
@@ -97,6 +99,8 @@ struct gossip_ctx {
     bool symmetric = false;      // overlay is symmetric (pull rounds allowed)
     bool nx_dirty = false;       // nx holds stale words (after a pull round)
     bool last_pull = false;      // mode of the round in flight
+    bool last_front = false;     // pull round used the frontier bitmap
+    int pull_unroll = 2;         // 64-edge batches in flight per wave in pull_light (GOSSIP_PULL_UNROLL)
     uint64_t frontier_est = 0;   // activated peers of the previous round
     std::vector<uint64_t> inj_prefix;  // per sorted injection: cumulative mask words
     uint64_t cum_digest = 0, cum_covered = 0;
@@ -161,6 +165,7 @@ void free_state(gossip_ctx* c) {
     hipFree(c->seen);
     hipFree(c->nw);
     hipFree(c->nx);
+    hipFree(c->front);
     hipFree(c->alive);
     hipFree(c->registered);
     hipFree(c->miss);
@@ -198,6 +203,7 @@ RoundArgs make_args(gossip_ctx* c) {
     a.seen = c->seen;
     a.nw = c->nw;
     a.nx = c->nx;
+    a.front = c->front;
     a.send = c->send;
     a.miss = c->miss;
     a.st = c->st + c->round;
@@ -351,7 +357,15 @@ gossip_status round_push(gossip_ctx* c, bool remote) {
     c->last_pull = pull;
     if (pull) {
         // nx is written whole by pull_light; heavy rows are OR-ed in afterwards
-        HIPCHK(timed(c, "pull_light", [&] { return launch_pull_light(a, pw, c->stream); }));
+        // frontier bitmap only when enough neighbours are outside the frontier to pay for the probe
+        const uint32_t fpm = c->cfg.front_permille ? c->cfg.front_permille : 400;
+        if ((c->frontier_est + cnt) * 1000 < c->n_local * (uint64_t)fpm) {
+            HIPCHK(timed(c, "frontier_bits", [&] { return launch_frontier_bits(a, pw, c->stream); }));
+        } else {
+            a.front = nullptr;
+        }
+        c->last_front = a.front != nullptr;
+        HIPCHK(timed(c, "pull_light", [&] { return launch_pull_light(a, pw, c->pull_unroll, c->stream); }));
         HIPCHK(timed(c, "pull_heavy", [&] { return launch_pull_heavy(a, pw, c->stream); }));
         return GOSSIP_OK;
     }
@@ -372,7 +386,8 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
     c->frontier_est = d.activated;
     if (c->timing) {
         if (c->last_pull) {
-            c->kbytes["pull_light"] += 40.0 * c->n_local + 12.0 * (double)d.pull_edges;
+            if (c->last_front) c->kbytes["frontier_bits"] += 8.125 * c->n_local;
+            c->kbytes["pull_light"] += 40.0 * c->n_local + 4.0 * (double)d.pull_edges + 8.0 * (double)d.pull_gathers;
             c->kbytes["pull_heavy"] += 12.0 * (double)d.heavy_traversals;
         } else {
             c->kbytes["push_light"] += 32.0 * d.frontier + 20.0 * (double)(d.traversals - d.heavy_traversals);
@@ -464,6 +479,7 @@ gossip_status gossip_create(const gossip_config* cfg, gossip_ctx** out) {
     if (!c->cfg.n_seeds) c->cfg.n_seeds = 20;
     if (!c->cfg.graph_model) c->cfg.graph_model = GOSSIP_GRAPH_POWERLAW;
     c->device = dev;
+    if (const char* u = std::getenv("GOSSIP_PULL_UNROLL")) c->pull_unroll = std::atoi(u);
     c->n = cfg->n_peers;
     c->begin = b;
     c->end = e;
@@ -487,6 +503,7 @@ gossip_status gossip_create(const gossip_config* cfg, gossip_ctx** out) {
     if ((err = hipMalloc((void**)&c->seen, words * 8)) != hipSuccess) return bail("seen", err);
     if ((err = hipMalloc((void**)&c->nw, words * 8)) != hipSuccess) return bail("new", err);
     if ((err = hipMalloc((void**)&c->nx, words * 8)) != hipSuccess) return bail("next", err);
+    if ((err = hipMalloc((void**)&c->front, ((c->n_local + 63) / 64 + 1) * 8)) != hipSuccess) return bail("front", err);
     if ((err = hipMalloc((void**)&c->alive, bitwords * 4)) != hipSuccess) return bail("alive", err);
     if ((err = hipMalloc((void**)&c->registered, bitwords * 4)) != hipSuccess) return bail("registry", err);
     if ((err = hipMalloc((void**)&c->st, (uint64_t)c->cfg.max_rounds * sizeof(DevStats))) != hipSuccess)

@@ -16,7 +16,7 @@ constexpr int kMaxWords = 8;                   // M <= 512 concurrent messages
 // Per-round device counters (all integer; order-independent sums).
 struct DevStats {
     unsigned long long frontier, traversals, deliveries, undelivered, new_receipts, injected, died, reports,
-        seed_removals, digest, covered, heavy_traversals, live_checked, activated, pull_edges, pad[1];
+        seed_removals, digest, covered, heavy_traversals, live_checked, activated, pull_edges, pull_gathers;
 };
 static_assert(sizeof(DevStats) == 128, "DevStats layout");
 
@@ -52,6 +52,7 @@ struct RoundArgs {
     uint32_t round;
     uint32_t max_missed;
     uint64_t inj_mask[kMaxWords];  // messages injected so far (pull: bits a peer can still learn)
+    uint64_t* front;               // pull rounds: 1 bit per owned peer, set iff its new words are nonzero
 };
 
 // ---- launchers (gossip_kernels.hip) ----
@@ -62,7 +63,8 @@ hipError_t launch_inject(const RoundArgs& a, uint32_t W, const uint32_t* origin,
                          hipStream_t s);
 hipError_t launch_push_heavy(const RoundArgs& a, uint32_t W, bool check_alive, bool remote, hipStream_t s);
 hipError_t launch_push_light(const RoundArgs& a, uint32_t W, bool check_alive, bool remote, hipStream_t s);
-hipError_t launch_pull_light(const RoundArgs& a, uint32_t W, hipStream_t s);
+hipError_t launch_frontier_bits(const RoundArgs& a, uint32_t W, hipStream_t s);
+hipError_t launch_pull_light(const RoundArgs& a, uint32_t W, int unroll, hipStream_t s);
 hipError_t launch_pull_heavy(const RoundArgs& a, uint32_t W, hipStream_t s);
 hipError_t launch_apply_remote(const RoundArgs& a, uint32_t W, const uint64_t* recv, uint32_t world,
                                uint64_t part_stride, hipStream_t s);

@@ -40,7 +40,7 @@ __device__ __forceinline__ uint32_t lane_rank(unsigned long long mask) {
 struct Acc {
     unsigned long long frontier = 0, trav = 0, deliv = 0, undeliv = 0, fresh = 0, digest = 0, covered = 0, died = 0,
                        reports = 0, removals = 0, injected = 0, htrav = 0, checked = 0,
-                       activated = 0, pulled = 0;
+                       activated = 0, pulled = 0, gathered = 0;
 };
 
 // One atomic per nonzero field per wave.
@@ -66,6 +66,7 @@ __device__ __forceinline__ void flush(Acc& acc, DevStats* st) {
     GOSSIP_FLUSH(checked, live_checked)
     GOSSIP_FLUSH(activated, activated)
     GOSSIP_FLUSH(pulled, pull_edges)
+    GOSSIP_FLUSH(gathered, pull_gathers)
 #undef GOSSIP_FLUSH
 }
 
@@ -233,7 +234,38 @@ __global__ __launch_bounds__(kBlock) void k_push_heavy(RoundArgs a) {
 // Rows longer than kHeavyDegree are pulled by k_pull_heavy (one workgroup per
 // chunk, one atomicOr per chunk).  P = 1 only (col ids index nw directly).
 // ---------------------------------------------------------------------------
-template <int W, bool COV>
+// Frontier bitmap for a pull round: one ballot per 64-peer tile, stored by
+// the tile's own wave (no atomics).  n/8 bytes -- cache-resident at 2^28 peers.
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_frontier_bits(RoundArgs a) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t n_tiles = (a.n_local + 63) >> 6;
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); t < n_tiles; t += nwaves) {
+        const uint64_t v = (t << 6) + lane;
+        bool act = false;
+        if (v < a.n_local) {
+#pragma unroll
+            for (int w = 0; w < W; ++w) act |= a.nw[v * W + w] != 0;
+        }
+        const unsigned long long bits = __ballot(act);
+        if (lane == 0) a.front[t] = bits;
+    }
+}
+
+// Source lane of edge position p within a tile: the number of rows whose
+// inclusive end is <= p (incl = in-wave inclusive scan of row lengths).
+__device__ __forceinline__ int src_lane(uint32_t incl, uint32_t p) {
+    int s = 0;
+#pragma unroll
+    for (int step = 32; step > 0; step >>= 1) {
+        const uint32_t val = __shfl(incl, s + step - 1);
+        if (val <= p) s += step;
+    }
+    return s;
+}
+
+template <int W, bool COV, bool FRONT, int kPullUnroll>  // kPullUnroll: 64-edge batches in flight per wave
 __global__ __launch_bounds__(kBlock) void k_pull_light(RoundArgs a, uint32_t wd) {
     __shared__ unsigned int cov_s[COV ? 64 * W : 1];
     __shared__ unsigned long long acc_s[kWavesPerBlock][64 * W];
@@ -290,23 +322,59 @@ __global__ __launch_bounds__(kBlock) void k_pull_light(RoundArgs a, uint32_t wd)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        tile_edges(needy && light ? (uint32_t)d : 0u, rb, [&](int s, bool valid, uint64_t e) {
-            uint64_t ns[W];
+        const uint32_t deg = needy && light ? (uint32_t)d : 0u;
+        uint32_t incl = deg;
 #pragma unroll
-            for (int w = 0; w < W; ++w) ns[w] = __shfl(need[w], s);
-            if (!valid) return;
-            bool want = false;
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(incl, off);
+            if (lane >= off) incl += y;
+        }
+        const uint32_t excl = incl - deg;
+        const uint32_t total = __shfl(incl, 63);
+        for (uint32_t base = 0; base < total; base += 64 * kPullUnroll) {
+            // phase 1: edge positions (and which sources still want anything)
+            int src[kPullUnroll];
+            uint64_t e[kPullUnroll];
+            uint32_t ok = 0;
 #pragma unroll
-            for (int w = 0; w < W; ++w) want |= (ns[w] & ~my[s * W + w]) != 0;  // stale read: only extra loads
-            if (!want) return;  // peer s already collected everything it can learn
-            acc.pulled++;
-            const uint32_t u = a.col[e];
+            for (int j = 0; j < kPullUnroll; ++j) {
+                const uint32_t p = base + j * 64 + lane;
+                src[j] = src_lane(incl, p);
+                e[j] = __shfl(rb, src[j]) + (uint64_t)(p - __shfl(excl, src[j]));
+                bool want = false;
 #pragma unroll
-            for (int w = 0; w < W; ++w) {
-                const uint64_t x = a.nw[(uint64_t)u * W + w] & ns[w];
-                if (x) atomicOr(&my[s * W + w], (unsigned long long)x);  // LDS ds_or_b64
+                for (int w = 0; w < W; ++w)  // stale LDS read: only extra loads
+                    want |= (__shfl(need[w], src[j]) & ~my[src[j] * W + w]) != 0;
+                ok |= (p < total && want) ? 1u << j : 0u;
             }
-        });
+            // phase 2..4: independent loads, kPullUnroll deep
+            uint32_t u[kPullUnroll];
+#pragma unroll
+            for (int j = 0; j < kPullUnroll; ++j) u[j] = (ok >> j) & 1 ? a.col[e[j]] : 0u;
+            acc.pulled += (unsigned)__builtin_popcount(ok);
+            if (FRONT) {
+                uint64_t fb[kPullUnroll];
+#pragma unroll
+                for (int j = 0; j < kPullUnroll; ++j) fb[j] = (ok >> j) & 1 ? a.front[u[j] >> 6] : 0ull;
+#pragma unroll
+                for (int j = 0; j < kPullUnroll; ++j)
+                    if (!((fb[j] >> (u[j] & 63)) & 1ull)) ok &= ~(1u << j);  // u has nothing new: no gather
+            }
+            uint64_t x[kPullUnroll][W];
+#pragma unroll
+            for (int j = 0; j < kPullUnroll; ++j)
+#pragma unroll
+                for (int w = 0; w < W; ++w) x[j][w] = (ok >> j) & 1 ? a.nw[(uint64_t)u[j] * W + w] : 0ull;
+            acc.gathered += (unsigned)__builtin_popcount(ok);
+            // phase 5: fold into the sources' LDS accumulators
+#pragma unroll
+            for (int j = 0; j < kPullUnroll; ++j)
+#pragma unroll
+                for (int w = 0; w < W; ++w) {
+                    const uint64_t y = x[j][w] & __shfl(need[w], src[j]);
+                    if (y) atomicOr(&my[src[j] * W + w], (unsigned long long)y);  // LDS ds_or_b64
+                }
+        }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -353,6 +421,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_heavy(RoundArgs a) {
             for (uint64_t e = ch.e0 + threadIdx.x; e < ch.e1; e += kBlock) {
                 const uint32_t u = a.col[e];
                 acc.pulled++;
+                if (a.front && !((a.front[u >> 6] >> (u & 63)) & 1ull)) continue;
 #pragma unroll
                 for (int w = 0; w < W; ++w)
                     if (need[w]) part[w] |= a.nw[(uint64_t)u * W + w] & need[w];
@@ -709,15 +778,28 @@ hipError_t launch_push_light(const RoundArgs& a, uint32_t W_, bool check_alive, 
     return hipGetLastError();
 }
 
-hipError_t launch_pull_light(const RoundArgs& a, uint32_t W_, hipStream_t s) {
+hipError_t launch_frontier_bits(const RoundArgs& a, uint32_t W_, hipStream_t s) {
+    const uint64_t tiles = (a.n_local + 63) / 64;
+    GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_frontier_bits<W>, dim3(grid_for(tiles, kWavesPerBlock)),
+                                                   dim3(kBlock), 0, s, a));
+    return hipGetLastError();
+}
+
+hipError_t launch_pull_light(const RoundArgs& a, uint32_t W_, int unroll, hipStream_t s) {
     const uint64_t tiles = (a.n_local + 63) / 64;
     const unsigned g = grid_for(tiles, kWavesPerBlock);
     const uint32_t wd = wd_of(W_);
-    if (a.cov) {
-        GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_pull_light<W, true>), dim3(g), dim3(kBlock), 0, s, a, wd));
-    } else {
-        GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_pull_light<W, false>), dim3(g), dim3(kBlock), 0, s, a, wd));
-    }
+#define GOSSIP_PULL(COV, FR)                                                                                 \
+    do {                                                                                                     \
+        if (unroll >= 4) hipLaunchKernelGGL((k_pull_light<W, COV, FR, 4>), dim3(g), dim3(kBlock), 0, s, a, wd); \
+        else if (unroll == 2) hipLaunchKernelGGL((k_pull_light<W, COV, FR, 2>), dim3(g), dim3(kBlock), 0, s, a, wd); \
+        else hipLaunchKernelGGL((k_pull_light<W, COV, FR, 1>), dim3(g), dim3(kBlock), 0, s, a, wd);          \
+    } while (0)
+    GOSSIP_DISPATCH_W(wp_of(W_), {
+        if (a.cov) { if (a.front) GOSSIP_PULL(true, true); else GOSSIP_PULL(true, false); }
+        else { if (a.front) GOSSIP_PULL(false, true); else GOSSIP_PULL(false, false); }
+    });
+#undef GOSSIP_PULL
     return hipGetLastError();
 }
 

@@ -48,7 +48,7 @@ class GossipConfig(C.Structure):
         ("flags", C.c_uint32),
         ("report_capacity", C.c_uint64),
         ("pull_permille", C.c_uint32),
-        ("reserved", C.c_uint32),
+        ("front_permille", C.c_uint32),
     ]
 
 
