@@ -148,14 +148,28 @@ gossip_status gossip_step(gossip_ctx* ctx, gossip_round_stats* out);
 gossip_status gossip_run(gossip_ctx* ctx, gossip_round_stats* per_round, uint32_t cap, uint32_t* rounds);
 
 /* ---- rounds (vertex-partitioned, one process per GPU) --------------------- */
-/* The caller owns the exchange: send = device buffer of n_peers*X u64 (dense,
- * indexed by global peer; X = exchange_words of gossip_get_shape), recv =
- * device buffer of world*n_local*X u64 (rank p's slice for this partition at
- * offset p*n_local*X).
- * Per round: gossip_round_push -> all-to-all(send slices -> recv) -> gossip_round_finish
- * -> all-reduce of the stats -> gossip_round_commit(new_receipts_global). */
+/* The caller owns the exchange buffers (device memory):
+ *   send   n_peers*X u64, dense, indexed by global peer (X = exchange_words of gossip_get_shape)
+ *   recv   world*n_local*X u64; rank p's slice for this block at offset p*n_local*X
+ *   gather (optional, enables pull rounds) world*chunk*X u64, chunk = ceil(n_peers/world);
+ *          needs blocks begins[p] = min(p*chunk, n_peers); rank p's new words at p*chunk*X
+ * Per round:
+ *   gossip_round_begin(mode)            churn, liveness, injection; returns the mode run
+ *   PULL: all-gather(gather)            every rank's new words, before compute
+ *   gossip_round_compute                push (writes send) or pull (reads gather)
+ *   PUSH: all-to-all(send -> recv)
+ *   gossip_round_finish                 applies recv (push); local stats, digest/covered as increments
+ *   all-reduce of the stats; gossip_round_commit(global new_receipts)
+ * The mode must be the same on every rank: choose it from global stats. */
+#define GOSSIP_MODE_AUTO (-1) /* single partition only: the engine decides */
+#define GOSSIP_MODE_PUSH 0
+#define GOSSIP_MODE_PULL 1
 gossip_status gossip_set_exchange(gossip_ctx* ctx, void* send_dev, void* recv_dev, uint32_t world,
                                   const uint64_t* part_begins /* world+1 */);
+gossip_status gossip_set_gather(gossip_ctx* ctx, void* gather_dev);
+gossip_status gossip_round_begin(gossip_ctx* ctx, int requested_mode, int* mode);
+gossip_status gossip_round_compute(gossip_ctx* ctx);
+/* begin(PUSH) + compute: push-only partitioned rounds */
 gossip_status gossip_round_push(gossip_ctx* ctx);
 gossip_status gossip_round_finish(gossip_ctx* ctx, gossip_round_stats* local_out);
 gossip_status gossip_round_commit(gossip_ctx* ctx, uint64_t global_new_receipts, int* finished);

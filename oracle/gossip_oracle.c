@@ -708,6 +708,7 @@ struct oracle_part {
     uint32_t round;
     int finished;
     uint64_t prev_digest, prev_covered;
+    int pull;
     oracle_stats cur;
 };
 
@@ -755,9 +756,10 @@ int oracle_part_schedule(oracle_part* p, const uint32_t* origin, const uint32_t*
 
 static int owned(const oracle_part* p, uint64_t v) { return v >= p->b && v < p->e; }
 
-/* churn, liveness, injection, push-start stats, local push; masks for peers
- * of other blocks are OR-ed into send[v * W + w] (dense, global index). */
-int oracle_part_push(oracle_part* p, uint64_t* send) {
+/* round phase 1: churn, liveness, injection, push-start stats; returns the
+ * mode that will run (pull only if requested and nobody is dead -- the
+ * overlay is assumed symmetric, as the powerlaw model is). */
+int oracle_part_begin(oracle_part* p, int requested_pull) {
     const uint32_t W = p->W, r = p->round;
     oracle_stats* st = &p->cur;
     memset(st, 0, sizeof(*st));
@@ -824,6 +826,49 @@ int oracle_part_push(oracle_part* p, uint64_t* send) {
     st->covered = covered - p->prev_covered;
     p->prev_digest = digest;
     p->prev_covered = covered;
+    int any_dead = 0;
+    for (uint64_t v = 0; v < p->n && !any_dead; ++v) any_dead = !p->alive[v];
+    p->pull = requested_pull && !any_dead;
+    return p->pull;
+}
+
+/* pull: publish this block's new words at gather[b * W] (global peer index) */
+void oracle_part_publish(oracle_part* p, uint64_t* gather) {
+    memcpy(gather + p->b * p->W, p->nw, p->nl * p->W * 8);
+}
+
+/* pull round: every owned peer ORs its neighbours' new words (gather, indexed
+ * by global peer); traversals/deliveries counted on the source side. */
+int oracle_part_pull(oracle_part* p, const uint64_t* gather) {
+    const uint32_t W = p->W;
+    oracle_stats* st = &p->cur;
+    for (uint64_t lu = 0; lu < p->nl; ++lu) {
+        uint64_t pc = 0;
+        for (uint32_t w = 0; w < W; ++w) pc += (uint64_t)__builtin_popcountll(p->nw[lu * W + w]);
+        if (!pc) continue;
+        const uint64_t deg = p->rp[lu + 1] - p->rp[lu];
+        st->traversals += deg;
+        st->deliveries += pc * deg;
+    }
+    for (uint64_t lv = 0; lv < p->nl; ++lv) {
+        for (uint32_t w = 0; w < W; ++w) {
+            uint64_t acc = 0;
+            for (uint64_t e = p->rp[lv]; e < p->rp[lv + 1]; ++e) acc |= gather[(uint64_t)p->col[e] * W + w];
+            const uint64_t fr = acc & ~p->seen[lv * W + w];
+            if (!fr) continue;
+            p->seen[lv * W + w] |= fr;
+            p->nx[lv * W + w] |= fr;
+            st->new_receipts += (uint64_t)__builtin_popcountll(fr);
+        }
+    }
+    return 0;
+}
+
+/* push round: local push; masks for peers of other blocks are OR-ed into
+ * send[v * W + w] (dense, global index). */
+int oracle_part_push_compute(oracle_part* p, uint64_t* send) {
+    const uint32_t W = p->W;
+    oracle_stats* st = &p->cur;
     for (uint64_t lu = 0; lu < p->nl; ++lu) {
         const uint64_t* mk = p->nw + lu * W;
         uint64_t pc = 0;
@@ -851,10 +896,16 @@ int oracle_part_push(oracle_part* p, uint64_t* send) {
     return 0;
 }
 
+int oracle_part_push(oracle_part* p, uint64_t* send) {
+    oracle_part_begin(p, 0);
+    return oracle_part_push_compute(p, send);
+}
+
+
 /* test-and-set of the masks received from every block (recv: world x nl x W) */
 int oracle_part_finish(oracle_part* p, const uint64_t* recv, uint32_t world, oracle_stats* out) {
     const uint32_t W = p->W;
-    for (uint64_t lv = 0; lv < p->nl; ++lv) {
+    for (uint64_t lv = 0; recv && !p->pull && lv < p->nl; ++lv) {
         for (uint32_t w = 0; w < W; ++w) {
             uint64_t inc = 0;
             for (uint32_t q = 0; q < world; ++q) inc |= recv[((uint64_t)q * p->nl + lv) * W + w];

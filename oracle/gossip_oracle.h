@@ -141,7 +141,11 @@ oracle_part* oracle_part_create(const oracle_sim_cfg* cfg, uint64_t b, uint64_t 
 void oracle_part_destroy(oracle_part* p);
 int oracle_part_schedule(oracle_part* p, const uint32_t* origin, const uint32_t* inject_round, uint32_t n_kills,
                          const uint32_t* kill_peer, const uint32_t* kill_round);
-int oracle_part_push(oracle_part* p, uint64_t* send);
+int oracle_part_push(oracle_part* p, uint64_t* send);   /* begin(push) + push_compute */
+int oracle_part_begin(oracle_part* p, int requested_pull); /* returns 1 if this round pulls */
+void oracle_part_publish(oracle_part* p, uint64_t* gather);
+int oracle_part_pull(oracle_part* p, const uint64_t* gather);
+int oracle_part_push_compute(oracle_part* p, uint64_t* send);
 int oracle_part_finish(oracle_part* p, const uint64_t* recv, uint32_t world, oracle_stats* out);
 int oracle_part_commit(oracle_part* p, uint64_t global_new_receipts);
 void oracle_part_reset(oracle_part* p);

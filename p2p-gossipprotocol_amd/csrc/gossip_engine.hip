@@ -100,6 +100,10 @@ struct gossip_ctx {
     bool nx_dirty = false;       // nx holds stale words (after a pull round)
     bool last_pull = false;      // mode of the round in flight
     bool last_front = false;     // pull round used the frontier bitmap
+    bool in_round = false;       // between round_begin and round_compute
+    bool cur_remote = false;
+    RoundArgs cur{};
+    uint64_t* gather = nullptr;  // partitioned pull: every rank's new words, indexed by global peer
     int pull_unroll = 2;         // 64-edge batches in flight per wave in pull_light (GOSSIP_PULL_UNROLL)
     uint64_t frontier_est = 0;   // activated peers of the previous round
     std::vector<uint64_t> inj_prefix;  // per sorted injection: cumulative mask words
@@ -202,6 +206,8 @@ RoundArgs make_args(gossip_ctx* c) {
     a.registered = c->registered;
     a.seen = c->seen;
     a.nw = c->nw;
+    a.nw_src = c->nw;
+    a.n_src = c->n_local;
     a.nx = c->nx;
     a.front = c->front;
     a.send = c->send;
@@ -315,8 +321,12 @@ uint32_t injections_in_round(const gossip_ctx* c, uint32_t r, uint32_t* first) {
     return (uint32_t)(hi - lo);
 }
 
-// Round phases up to and including the push.
-gossip_status round_push(gossip_ctx* c, bool remote) {
+// Round phase 1: churn, kills, liveness, injection; choose push or pull.
+// requested: GOSSIP_MODE_AUTO (P = 1: the engine's frontier estimate decides),
+// GOSSIP_MODE_PUSH or GOSSIP_MODE_PULL (partitioned runs: the driver decides
+// from global stats so every rank agrees; an ineligible pull falls back to
+// push, and eligibility is itself global state, so ranks still agree).
+gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) {
     if (!c->graph_ready) return fail(GOSSIP_ESTATE, "no overlay: call gossip_build_graph or gossip_load_csr");
     if (!c->has_schedule) return fail(GOSSIP_ESTATE, "no schedule: call gossip_inject");
     if (c->finished) return fail(GOSSIP_ESTATE, "run finished: call gossip_reset");
@@ -350,30 +360,64 @@ gossip_status round_push(gossip_ctx* c, bool remote) {
                                  c->inj_round_sorted.begin());
         for (int w = 0; w < kMaxWords; ++w) a.inj_mask[w] = hi ? c->inj_prefix[(uint64_t)(hi - 1) * kMaxWords + w] : 0;
     }
-    const uint32_t permille = c->cfg.pull_permille ? c->cfg.pull_permille : 50;
-    const bool pull_ok = !remote && c->symmetric && !c->any_dead && !(c->cfg.flags & GOSSIP_FLAG_FORCE_PUSH);
-    const bool pull = pull_ok && ((c->cfg.flags & GOSSIP_FLAG_FORCE_PULL) ||
-                                  (c->frontier_est + cnt) * 1000 >= c->n_local * (uint64_t)permille);
+    const bool pull_ok = c->symmetric && !c->any_dead && !(c->cfg.flags & GOSSIP_FLAG_FORCE_PUSH) &&
+                         (!remote || c->gather != nullptr);
+    bool pull;
+    if (requested == GOSSIP_MODE_AUTO) {
+        const uint32_t permille = c->cfg.pull_permille ? c->cfg.pull_permille : 50;
+        pull = !remote && pull_ok &&
+               ((c->cfg.flags & GOSSIP_FLAG_FORCE_PULL) || (c->frontier_est + cnt) * 1000 >= c->n_local * (uint64_t)permille);
+    } else {
+        pull = requested == GOSSIP_MODE_PULL && pull_ok;
+    }
     c->last_pull = pull;
+    c->last_front = false;
     if (pull) {
-        // nx is written whole by pull_light; heavy rows are OR-ed in afterwards
+        a.nw_src = c->nw;
+        a.n_src = c->n_local;
+        if (remote) {  // publish this block's new words; the caller all-gathers c->gather
+            HIPCHK(hipMemcpyAsync(c->gather + c->begin * c->Wp, c->nw, c->n_local * c->Wp * sizeof(uint64_t),
+                                  hipMemcpyDeviceToDevice, c->stream));
+            a.nw_src = c->gather;
+            a.n_src = c->n;
+        }
         // frontier bitmap only when enough neighbours are outside the frontier to pay for the probe
         const uint32_t fpm = c->cfg.front_permille ? c->cfg.front_permille : 400;
-        if ((c->frontier_est + cnt) * 1000 < c->n_local * (uint64_t)fpm) {
-            HIPCHK(timed(c, "frontier_bits", [&] { return launch_frontier_bits(a, pw, c->stream); }));
+        if (requested == GOSSIP_MODE_AUTO && (c->frontier_est + cnt) * 1000 < c->n_local * (uint64_t)fpm) {
+            a.front = c->front;
+            c->last_front = true;
         } else {
             a.front = nullptr;
         }
-        c->last_front = a.front != nullptr;
+    } else {
+        if (c->nx_dirty) {
+            HIPCHK(hipMemsetAsync(c->nx, 0, c->n_local * c->Wp * sizeof(uint64_t), c->stream));
+            c->nx_dirty = false;
+        }
+        if (remote) HIPCHK(hipMemsetAsync(c->send, 0, c->n * c->Wp * sizeof(uint64_t), c->stream));
+    }
+    c->cur = a;
+    c->cur_remote = remote;
+    c->in_round = true;
+    if (mode) *mode = pull ? GOSSIP_MODE_PULL : GOSSIP_MODE_PUSH;
+    return GOSSIP_OK;
+}
+
+// Round phase 2: the push or pull kernels (after the caller's all-gather in a
+// partitioned pull round).
+gossip_status round_compute(gossip_ctx* c) {
+    if (!c->in_round) return fail(GOSSIP_ESTATE, "gossip_round_begin first");
+    RoundArgs a = c->cur;
+    const uint32_t pw = pack_w(c);
+    c->in_round = false;
+    if (c->last_pull) {
+        if (a.front) HIPCHK(timed(c, "frontier_bits", [&] { return launch_frontier_bits(a, pw, c->stream); }));
+        // nx is written whole by pull_light; heavy rows are OR-ed in afterwards
         HIPCHK(timed(c, "pull_light", [&] { return launch_pull_light(a, pw, c->pull_unroll, c->stream); }));
         HIPCHK(timed(c, "pull_heavy", [&] { return launch_pull_heavy(a, pw, c->stream); }));
         return GOSSIP_OK;
     }
-    if (c->nx_dirty) {
-        HIPCHK(hipMemsetAsync(c->nx, 0, c->n_local * c->Wp * sizeof(uint64_t), c->stream));
-        c->nx_dirty = false;
-    }
-    if (remote) HIPCHK(hipMemsetAsync(c->send, 0, c->n * c->Wp * sizeof(uint64_t), c->stream));
+    const bool remote = c->cur_remote;
     HIPCHK(timed(c, "push_heavy", [&] { return launch_push_heavy(a, pw, c->any_dead, remote, c->stream); }));
     HIPCHK(timed(c, "push_light", [&] { return launch_push_light(a, pw, c->any_dead, remote, c->stream); }));
     return GOSSIP_OK;
@@ -386,7 +430,7 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
     c->frontier_est = d.activated;
     if (c->timing) {
         if (c->last_pull) {
-            if (c->last_front) c->kbytes["frontier_bits"] += 8.125 * c->n_local;
+            if (c->last_front) c->kbytes["frontier_bits"] += 8.125 * (c->gather ? c->n : c->n_local);
             c->kbytes["pull_light"] += 40.0 * c->n_local + 4.0 * (double)d.pull_edges + 8.0 * (double)d.pull_gathers;
             c->kbytes["pull_heavy"] += 12.0 * (double)d.heavy_traversals;
         } else {
@@ -734,7 +778,8 @@ gossip_status gossip_step(gossip_ctx* c, gossip_round_stats* out) {
     if (!c) return fail(GOSSIP_EINVAL, "null ctx");
     if (set_dev(c)) return GOSSIP_EHIP;
     if (c->world > 1) return fail(GOSSIP_ESTATE, "partitioned ctx: use gossip_round_push/finish/commit");
-    gossip_status s = round_push(c, false);
+    gossip_status s = round_begin(c, false, GOSSIP_MODE_AUTO, nullptr);
+    if (!s) s = round_compute(c);
     if (s) return s;
     gossip_round_stats st;
     if ((s = read_slot(c, &st, true))) return s;
@@ -772,20 +817,53 @@ gossip_status gossip_set_exchange(gossip_ctx* c, void* send, void* recv, uint32_
     return GOSSIP_OK;
 }
 
+gossip_status gossip_set_gather(gossip_ctx* c, void* gather) {
+    if (!c || !gather) return fail(GOSSIP_EINVAL, "null argument");
+    if (c->part_begins.size() < 2) return fail(GOSSIP_ESTATE, "call gossip_set_exchange first");
+    const uint64_t chunk = c->part_begins[1];
+    for (uint32_t p = 0; p <= c->world; ++p)
+        if (c->part_begins[p] != std::min<uint64_t>((uint64_t)p * chunk, c->n))
+            return fail(GOSSIP_EINVAL, "gather needs blocks of ceil(n/world) peers (begins[p] = p*chunk)");
+    if (set_dev(c)) return GOSSIP_EHIP;
+    hipFree(c->front);
+    c->front = nullptr;
+    HIPCHK(hipMalloc((void**)&c->front, ((c->n + 63) / 64 + 1) * 8));  // bitmap over all peers
+    c->gather = (uint64_t*)gather;
+    return GOSSIP_OK;
+}
+
+gossip_status gossip_round_begin(gossip_ctx* c, int requested_mode, int* mode) {
+    if (!c) return fail(GOSSIP_EINVAL, "null ctx");
+    if (c->world > 1 && !c->send) return fail(GOSSIP_ESTATE, "call gossip_set_exchange first");
+    if (c->world > 1 && requested_mode == GOSSIP_MODE_AUTO)
+        return fail(GOSSIP_EINVAL, "partitioned rounds need an explicit mode (chosen from global stats)");
+    if (set_dev(c)) return GOSSIP_EHIP;
+    return round_begin(c, c->world > 1, requested_mode, mode);
+}
+
+gossip_status gossip_round_compute(gossip_ctx* c) {
+    if (!c) return fail(GOSSIP_EINVAL, "null ctx");
+    if (set_dev(c)) return GOSSIP_EHIP;
+    return round_compute(c);
+}
+
 gossip_status gossip_round_push(gossip_ctx* c) {
     if (!c) return fail(GOSSIP_EINVAL, "null ctx");
     if (!c->send) return fail(GOSSIP_ESTATE, "call gossip_set_exchange first");
     if (set_dev(c)) return GOSSIP_EHIP;
-    return round_push(c, true);
+    gossip_status s = round_begin(c, true, GOSSIP_MODE_PUSH, nullptr);
+    return s ? s : round_compute(c);
 }
 
 gossip_status gossip_round_finish(gossip_ctx* c, gossip_round_stats* out) {
     if (!c) return fail(GOSSIP_EINVAL, "null ctx");
     if (!c->recv) return fail(GOSSIP_ESTATE, "call gossip_set_exchange first");
+    if (c->in_round) return fail(GOSSIP_ESTATE, "gossip_round_compute first");
     if (set_dev(c)) return GOSSIP_EHIP;
     RoundArgs a = make_args(c);
-    HIPCHK(timed(c, "apply_remote",
-                 [&] { return launch_apply_remote(a, pack_w(c), c->recv, c->world, c->n_local, c->stream); }));
+    if (!c->last_pull)  // push round: OR in what the other blocks sent; pull rounds pulled it already
+        HIPCHK(timed(c, "apply_remote",
+                     [&] { return launch_apply_remote(a, pack_w(c), c->recv, c->world, c->n_local, c->stream); }));
     return read_slot(c, out, false);
 }
 

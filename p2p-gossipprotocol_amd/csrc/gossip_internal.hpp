@@ -52,7 +52,9 @@ struct RoundArgs {
     uint32_t round;
     uint32_t max_missed;
     uint64_t inj_mask[kMaxWords];  // messages injected so far (pull: bits a peer can still learn)
-    uint64_t* front;               // pull rounds: 1 bit per owned peer, set iff its new words are nonzero
+    uint64_t* front;               // pull rounds: 1 bit per source peer, set iff its new words are nonzero
+    const uint64_t* nw_src;        // pull rounds: new words of every source, indexed by (global) peer id
+    uint64_t n_src;                // peers covered by nw_src / front
 };
 
 // ---- launchers (gossip_kernels.hip) ----

@@ -239,14 +239,14 @@ __global__ __launch_bounds__(kBlock) void k_push_heavy(RoundArgs a) {
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_frontier_bits(RoundArgs a) {
     const int lane = threadIdx.x & 63;
-    const uint64_t n_tiles = (a.n_local + 63) >> 6;
+    const uint64_t n_tiles = (a.n_src + 63) >> 6;
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
     for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); t < n_tiles; t += nwaves) {
         const uint64_t v = (t << 6) + lane;
         bool act = false;
-        if (v < a.n_local) {
+        if (v < a.n_src) {
 #pragma unroll
-            for (int w = 0; w < W; ++w) act |= a.nw[v * W + w] != 0;
+            for (int w = 0; w < W; ++w) act |= a.nw_src[v * W + w] != 0;
         }
         const unsigned long long bits = __ballot(act);
         if (lane == 0) a.front[t] = bits;
@@ -364,7 +364,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_light(RoundArgs a, uint32_t wd)
 #pragma unroll
             for (int j = 0; j < kPullUnroll; ++j)
 #pragma unroll
-                for (int w = 0; w < W; ++w) x[j][w] = (ok >> j) & 1 ? a.nw[(uint64_t)u[j] * W + w] : 0ull;
+                for (int w = 0; w < W; ++w) x[j][w] = (ok >> j) & 1 ? a.nw_src[(uint64_t)u[j] * W + w] : 0ull;
             acc.gathered += (unsigned)__builtin_popcount(ok);
             // phase 5: fold into the sources' LDS accumulators
 #pragma unroll
@@ -424,7 +424,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_heavy(RoundArgs a) {
                 if (a.front && !((a.front[u >> 6] >> (u & 63)) & 1ull)) continue;
 #pragma unroll
                 for (int w = 0; w < W; ++w)
-                    if (need[w]) part[w] |= a.nw[(uint64_t)u * W + w] & need[w];
+                    if (need[w]) part[w] |= a.nw_src[(uint64_t)u * W + w] & need[w];
             }
 #pragma unroll
             for (int w = 0; w < W; ++w) {
@@ -779,7 +779,7 @@ hipError_t launch_push_light(const RoundArgs& a, uint32_t W_, bool check_alive, 
 }
 
 hipError_t launch_frontier_bits(const RoundArgs& a, uint32_t W_, hipStream_t s) {
-    const uint64_t tiles = (a.n_local + 63) / 64;
+    const uint64_t tiles = (a.n_src + 63) / 64;
     GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_frontier_bits<W>, dim3(grid_for(tiles, kWavesPerBlock)),
                                                    dim3(kBlock), 0, s, a));
     return hipGetLastError();

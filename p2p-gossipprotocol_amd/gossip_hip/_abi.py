@@ -27,6 +27,9 @@ GRAPH_REF_BOOTSTRAP = 2
 FLAG_COVERAGE_HISTORY = 1
 FLAG_FORCE_PUSH = 2
 FLAG_FORCE_PULL = 4
+MODE_AUTO = -1
+MODE_PUSH = 0
+MODE_PULL = 1
 
 
 class GossipConfig(C.Structure):
@@ -105,6 +108,9 @@ def lib() -> C.CDLL:
         "gossip_run": (i32, [P, C.POINTER(RoundStats), u32, pu32]),
         "gossip_set_exchange": (i32, [P, P, P, u32, pu64]),
         "gossip_round_push": (i32, [P]),
+        "gossip_set_gather": (i32, [P, P]),
+        "gossip_round_begin": (i32, [P, i32, C.POINTER(C.c_int)]),
+        "gossip_round_compute": (i32, [P]),
         "gossip_round_finish": (i32, [P, C.POINTER(RoundStats)]),
         "gossip_round_commit": (i32, [P, u64, C.POINTER(C.c_int)]),
         "gossip_read_seen": (i32, [P, pu64]),

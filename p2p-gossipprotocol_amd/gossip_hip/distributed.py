@@ -1,18 +1,26 @@
 """Vertex-partitioned gossip over torch.distributed (RCCL over xGMI on MI355X).
 
 One process per GPU.  Peers are 1D-partitioned into contiguous blocks
-[p*n/P, (p+1)*n/P); each rank owns the CSR rows, seen/new words and miss
+[p*c, min((p+1)*c, n)), c = ceil(n/P); each rank owns the CSR rows, seen/new words and miss
 counters of its block (alive state is global and computed redundantly by
 every rank from the same Philox draws, so churn needs no collective).
 
 Per round (the reference's hop broadcastMessage -> handleClient, peer.cpp:
-297-318 / 255-295, with the TCP send replaced by one exchange):
-  1. engine.round_push()      churn, liveness, injection, local push; masks for
-                              remote peers are OR-ed into a dense send buffer
-  2. all_to_all_single        rank p's slice of every send buffer -> rank p
-  3. engine.round_finish()    test-and-set of the received masks (no atomics)
-  4. all_reduce(stats)        one int64 vector; drives the common termination
-  5. engine.round_commit()
+297-318 / 255-295, with the TCP send replaced by one collective):
+  1. engine.round_begin(mode)  churn, liveness, injection.  The mode is chosen
+                               here from the previous round's GLOBAL new-receipt
+                               count, so every rank runs the same one.
+  PULL (dense rounds):
+  2. all_gather_into_tensor    every rank's new words -> one buffer indexed by
+                               global peer (blocks are ceil(n/P) peers)
+  3. engine.round_compute()    each peer ORs its neighbours' words (no atomics)
+  PUSH (sparse rounds):
+  2. engine.round_compute()    local push; remote masks OR-ed into a dense
+                               send buffer indexed by global peer
+  3. all_to_all_single         rank p's slice of every send buffer -> rank p
+  4. engine.round_finish()     (push: test-and-set of the received masks)
+  5. all_reduce(stats)         one int64 vector; drives the common termination
+  6. engine.round_commit()
 
 The driver is generic over the engine: libgossip_hip on cuda tensors (the
 product) or, in the CPU tests only, a gloo-backed partition emulation with
@@ -31,13 +39,22 @@ MASK32 = (1 << 32) - 1
 MASK64 = (1 << 64) - 1
 
 
+MODE_PUSH, MODE_PULL = 0, 1
+
+
 def partition(n: int, world: int) -> list[int]:
-    """Contiguous, balanced vertex blocks: begins[p] = floor(p*n/P)."""
-    return [(p * n) // world for p in range(world + 1)]
+    """Contiguous vertex blocks of ceil(n/P) peers: begins[p] = min(p*chunk, n),
+    so a buffer of P chunks is indexed directly by global peer id."""
+    chunk = -(-n // world)
+    begins = [min(p * chunk, n) for p in range(world + 1)]
+    if any(begins[p + 1] <= begins[p] for p in range(world)):
+        raise ValueError(f"{n} peers cannot be split into {world} non-empty blocks of {chunk}")
+    return begins
 
 
 class PartitionedRun:
-    def __init__(self, engine, n: int, rank: int, world: int, device: torch.device, group=None):
+    def __init__(self, engine, n: int, rank: int, world: int, device: torch.device, group=None,
+                 pull_permille: int = 50, pull: bool = True):
         self.engine = engine
         self.n, self.rank, self.world = n, rank, world
         self.device = device
@@ -54,6 +71,15 @@ class PartitionedRun:
         if device.type == "cuda":
             engine.set_stream(torch.cuda.current_stream(device).cuda_stream)
         engine.set_exchange(self.send.data_ptr(), self.recv.data_ptr(), self.part)
+        self.chunk = self.part[1]
+        self.pull = pull
+        self.pull_permille = pull_permille
+        if pull:
+            self.gather = torch.zeros(world * self.chunk * X, dtype=torch.int64, device=device)
+            self.gather_mine = self.gather[rank * self.chunk * X:(rank + 1) * self.chunk * X]
+            engine.set_gather(self.gather.data_ptr())
+        self.prev_new = 0
+        self.modes = []
         self.cum_digest = 0
         self.cum_covered = 0
 
@@ -74,10 +100,18 @@ class PartitionedRun:
 
     def step(self) -> tuple[dict, bool]:
         e = self.engine
-        e.round_push()
-        dist.all_to_all_single(self.recv, self.send, self.out_splits, self.in_splits, group=self.group)
+        want = MODE_PULL if self.pull and self.prev_new * 1000 >= self.pull_permille * self.n else MODE_PUSH
+        mode = e.round_begin(want)
+        if mode == MODE_PULL:
+            dist.all_gather_into_tensor(self.gather, self.gather_mine, group=self.group)
+            e.round_compute()
+        else:
+            e.round_compute()
+            dist.all_to_all_single(self.recv, self.send, self.out_splits, self.in_splits, group=self.group)
+        self.modes.append(mode)
         local = e.round_finish()
         g = self._allreduce(local)
+        self.prev_new = g["new_receipts"]
         out = {"round": local["round"], "flags": local["flags"]}
         for f in STAT_FIELDS:
             out[f] = g.get(f, 0)
@@ -88,6 +122,8 @@ class PartitionedRun:
 
     def run(self, max_rounds: int = 4096) -> list[dict]:
         self.cum_digest = self.cum_covered = 0
+        self.prev_new = 0
+        self.modes = []
         rounds = []
         for _ in range(max_rounds):
             st, fin = self.step()

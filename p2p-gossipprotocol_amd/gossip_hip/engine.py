@@ -151,6 +151,18 @@ class Engine:
         check(self._L.gossip_set_exchange(self._ctx, C.c_void_p(send_ptr), C.c_void_p(recv_ptr), pb.size - 1,
                                           _ptr(pb, C.c_uint64)), "gossip_set_exchange")
 
+    def set_gather(self, gather_ptr: int) -> None:
+        check(self._L.gossip_set_gather(self._ctx, C.c_void_p(gather_ptr)), "gossip_set_gather")
+
+    def round_begin(self, mode: int) -> int:
+        """Phase 1 of a partitioned round; returns the mode actually run (0 push, 1 pull)."""
+        got = C.c_int()
+        check(self._L.gossip_round_begin(self._ctx, mode, C.byref(got)), "gossip_round_begin")
+        return got.value
+
+    def round_compute(self) -> None:
+        check(self._L.gossip_round_compute(self._ctx), "gossip_round_compute")
+
     def round_push(self) -> None:
         check(self._L.gossip_round_push(self._ctx), "gossip_round_push")
 

@@ -172,6 +172,23 @@ class OraclePartition:
     def reset(self):
         self.L.oracle_part_reset(self.p)
 
+    def set_gather(self, gather_ptr):
+        self._gather = C.cast(C.c_void_p(gather_ptr), C.POINTER(C.c_uint64))
+
+    def round_begin(self, mode):
+        self._pull = bool(self.L.oracle_part_begin(self.p, C.c_int(1 if mode == 1 else 0)))
+        if self._pull:
+            self.L.oracle_part_publish(self.p, self._gather)
+        else:
+            C.memset(self._send, 0, self._send_words * 8)
+        return 1 if self._pull else 0
+
+    def round_compute(self):
+        if self._pull:
+            self.L.oracle_part_pull(self.p, self._gather)
+        else:
+            self.L.oracle_part_push_compute(self.p, self._send)
+
     def round_push(self):
         C.memset(self._send, 0, self._send_words * 8)
         self.L.oracle_part_push(self.p, self._send)

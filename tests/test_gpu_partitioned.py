@@ -13,9 +13,12 @@ from gossip_hip.workloads import config
 pytestmark = pytest.mark.gpu
 
 
-def run_partitioned(w, P):
+def run_partitioned(w, P, pull=True):
+    """Mirror of gossip_hip.distributed.PartitionedRun with the collectives done
+    by device copies: all-gather for pull rounds, all-to-all for push rounds."""
     import torch
     part = partition(w.n, P)
+    chunk = part[1]
     engines = [Engine(w.n, w.n_msgs, part=(part[p], part[p + 1]), device=0, **w.engine_kwargs()) for p in range(P)]
     stream = torch.cuda.current_stream().cuda_stream
     for e in engines:
@@ -29,21 +32,34 @@ def run_partitioned(w, P):
     nl = [part[p + 1] - part[p] for p in range(P)]
     sends = [torch.zeros(w.n * X, dtype=torch.int64, device="cuda") for _ in range(P)]
     recvs = [torch.zeros(P * nl[q] * X, dtype=torch.int64, device="cuda") for q in range(P)]
+    gathers = [torch.zeros(P * chunk * X, dtype=torch.int64, device="cuda") for _ in range(P)]
     for p, e in enumerate(engines):
         e.set_exchange(sends[p].data_ptr(), recvs[p].data_ptr(), part)
-    rounds, dig, cov = [], 0, 0
+        e.set_gather(gathers[p].data_ptr())
+    rounds, modes, dig, cov, prev_new = [], [], 0, 0, 0
     while True:
+        want = 1 if pull and prev_new * 1000 >= 50 * w.n else 0
+        got = {e.round_begin(want) for e in engines}
+        assert len(got) == 1
+        mode = got.pop()
+        modes.append(mode)
+        if mode == 1:   # all-gather of every block's new words
+            for q in range(P):
+                for p in range(P):
+                    gathers[q][p * chunk * X:(p + 1) * chunk * X].copy_(gathers[p][p * chunk * X:(p + 1) * chunk * X])
         for e in engines:
-            e.round_push()
-        for q in range(P):
-            for p in range(P):
-                recvs[q][p * nl[q] * X:(p + 1) * nl[q] * X].copy_(sends[p][part[q] * X:part[q + 1] * X])
+            e.round_compute()
+        if mode == 0:   # all-to-all of the remote masks
+            for q in range(P):
+                for p in range(P):
+                    recvs[q][p * nl[q] * X:(p + 1) * nl[q] * X].copy_(sends[p][part[q] * X:part[q + 1] * X])
         loc = [e.round_finish() for e in engines]
         g = {f: sum(l[f] for l in loc) for f in STAT_FIELDS}
         dig = (dig + g["digest"]) & MASK64
         cov += g["covered"]
         g.update(round=loc[0]["round"], flags=loc[0]["flags"], digest=dig, covered=cov,
                  duplicates=g["deliveries"] - g["new_receipts"])
+        prev_new = g["new_receipts"]
         fins = {e.round_commit(g["new_receipts"]) for e in engines}
         assert len(fins) == 1
         rounds.append(g)
@@ -60,16 +76,19 @@ def run_partitioned(w, P):
     csrs = [e.read_csr() for e in engines]
     for e in engines:
         e.close()
-    return rounds, seen, reps, csrs, part
+    return rounds, seen, reps, csrs, part, modes
 
 
+@pytest.mark.parametrize("pull", [True, False])
 @pytest.mark.parametrize("P", [2, 3, 4])
 @pytest.mark.parametrize("idx,n", [(2, 1 << 15), (3, 100_000), (5, 1 << 15)])
-def test_partitioned_gpu_equals_oracle(oracle, idx, n, P):
+def test_partitioned_gpu_equals_oracle(oracle, idx, n, P, pull):
     w = config(idx, n, pick=oracle.pick_origins)
     rp, col = oracle.gen_workload(w)
     ref = oracle.simulate_workload(w, rp, col)
-    rounds, seen, reps, csrs, part = run_partitioned(w, P)
+    rounds, seen, reps, csrs, part, modes = run_partitioned(w, P, pull)
+    if pull and idx != 5:
+        assert 1 in modes and 0 in modes
     for p, (lrp, lcol) in enumerate(csrs):   # partitioned generator = slices of the global overlay
         base = int(rp[part[p]])
         assert np.array_equal(lrp, rp[part[p]:part[p + 1] + 1] - np.uint64(base))
