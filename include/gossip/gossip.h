@@ -158,15 +158,26 @@ gossip_status gossip_run(gossip_ctx* ctx, gossip_round_stats* per_round, uint32_
  *   PULL: all-gather(gather)            every rank's new words, before compute
  *   gossip_round_compute                push (writes send) or pull (reads gather)
  *   PUSH: all-to-all(send -> recv)
+ *   PUSH_SPARSE: all-to-all(counts), all-to-all(records) -> gossip_round_finish_sparse
  *   gossip_round_finish                 applies recv (push); local stats, digest/covered as increments
  *   all-reduce of the stats; gossip_round_commit(global new_receipts)
  * The mode must be the same on every rank: choose it from global stats. */
 #define GOSSIP_MODE_AUTO (-1) /* single partition only: the engine decides */
 #define GOSSIP_MODE_PUSH 0
 #define GOSSIP_MODE_PULL 1
+#define GOSSIP_MODE_PUSH_SPARSE 2 /* push; only touched peers are exchanged (needs gossip_set_sparse) */
 gossip_status gossip_set_exchange(gossip_ctx* ctx, void* send_dev, void* recv_dev, uint32_t world,
                                   const uint64_t* part_begins /* world+1 */);
 gossip_status gossip_set_gather(gossip_ctx* ctx, void* gather_dev);
+/* Sparse push rounds: seg = device buffer of world*chunk*(1+X) u64; after
+ * gossip_round_compute, destination q's records {peer, words[X]} sit at
+ * seg + q*chunk*(1+X) and gossip_sparse_counts gives their numbers (the
+ * staging buffer is left cleared).  The caller exchanges counts, then the
+ * records, and finishes with gossip_round_finish_sparse(received records). */
+gossip_status gossip_set_sparse(gossip_ctx* ctx, void* seg_dev);
+gossip_status gossip_sparse_counts(gossip_ctx* ctx, uint64_t* counts /* world */);
+gossip_status gossip_round_finish_sparse(gossip_ctx* ctx, const void* records_dev, uint64_t n_records,
+                                         gossip_round_stats* local_out);
 gossip_status gossip_round_begin(gossip_ctx* ctx, int requested_mode, int* mode);
 gossip_status gossip_round_compute(gossip_ctx* ctx);
 /* begin(PUSH) + compute: push-only partitioned rounds */

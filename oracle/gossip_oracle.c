@@ -902,6 +902,41 @@ int oracle_part_push(oracle_part* p, uint64_t* send) {
 }
 
 
+/* sparse exchange: compact send (dense, global index) into per-destination
+ * records {peer, words[W]} at seg + q*chunk*(1+W); clears send; counts[q] */
+void oracle_part_compact(oracle_part* p, uint64_t* send, uint64_t chunk, uint32_t world, uint64_t* seg,
+                         uint64_t* counts) {
+    const uint32_t W = p->W;
+    memset(counts, 0, world * sizeof(uint64_t));
+    for (uint64_t v = 0; v < p->n; ++v) {
+        int any = 0;
+        for (uint32_t w = 0; w < W; ++w) any |= send[v * W + w] != 0;
+        if (!any) continue;
+        const uint64_t q = v / chunk;
+        uint64_t* rec = seg + (q * chunk + counts[q]++) * (1 + W);
+        rec[0] = v;
+        for (uint32_t w = 0; w < W; ++w) { rec[1 + w] = send[v * W + w]; send[v * W + w] = 0; }
+    }
+}
+
+/* sparse exchange, receiving side: test-and-set of the received records */
+int oracle_part_finish_records(oracle_part* p, const uint64_t* rec, uint64_t n_rec, oracle_stats* out) {
+    const uint32_t W = p->W;
+    for (uint64_t i = 0; i < n_rec; ++i) {
+        const uint64_t lv = rec[i * (1 + W)] - p->b;
+        for (uint32_t w = 0; w < W; ++w) {
+            const uint64_t fr = rec[i * (1 + W) + 1 + w] & ~p->seen[lv * W + w];
+            if (!fr) continue;
+            p->seen[lv * W + w] |= fr;
+            p->nx[lv * W + w] |= fr;
+            p->cur.new_receipts += (uint64_t)__builtin_popcountll(fr);
+        }
+    }
+    p->cur.duplicates = p->cur.deliveries - p->cur.new_receipts;
+    if (out) *out = p->cur;
+    return 0;
+}
+
 /* test-and-set of the masks received from every block (recv: world x nl x W) */
 int oracle_part_finish(oracle_part* p, const uint64_t* recv, uint32_t world, oracle_stats* out) {
     const uint32_t W = p->W;

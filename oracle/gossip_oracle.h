@@ -146,6 +146,9 @@ int oracle_part_begin(oracle_part* p, int requested_pull); /* returns 1 if this 
 void oracle_part_publish(oracle_part* p, uint64_t* gather);
 int oracle_part_pull(oracle_part* p, const uint64_t* gather);
 int oracle_part_push_compute(oracle_part* p, uint64_t* send);
+void oracle_part_compact(oracle_part* p, uint64_t* send, uint64_t chunk, uint32_t world, uint64_t* seg,
+                         uint64_t* counts);
+int oracle_part_finish_records(oracle_part* p, const uint64_t* rec, uint64_t n_rec, oracle_stats* out);
 int oracle_part_finish(oracle_part* p, const uint64_t* recv, uint32_t world, oracle_stats* out);
 int oracle_part_commit(oracle_part* p, uint64_t global_new_receipts);
 void oracle_part_reset(oracle_part* p);

@@ -104,6 +104,10 @@ struct gossip_ctx {
     bool cur_remote = false;
     RoundArgs cur{};
     uint64_t* gather = nullptr;  // partitioned pull: every rank's new words, indexed by global peer
+    uint64_t* seg = nullptr;     // sparse push: per-destination record segments (world x chunk records)
+    unsigned long long* d_counts = nullptr;  // records per destination rank
+    uint64_t* h_counts = nullptr;            // pinned copy
+    bool cur_sparse = false;
     int pull_unroll = 2;         // 64-edge batches in flight per wave in pull_light (GOSSIP_PULL_UNROLL)
     uint64_t frontier_est = 0;   // activated peers of the previous round
     std::vector<uint64_t> inj_prefix;  // per sorted injection: cumulative mask words
@@ -370,6 +374,7 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
     } else {
         pull = requested == GOSSIP_MODE_PULL && pull_ok;
     }
+    c->cur_sparse = !pull && remote && requested == GOSSIP_MODE_PUSH_SPARSE && c->seg != nullptr;
     c->last_pull = pull;
     c->last_front = false;
     if (pull) {
@@ -394,12 +399,14 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
             HIPCHK(hipMemsetAsync(c->nx, 0, c->n_local * c->Wp * sizeof(uint64_t), c->stream));
             c->nx_dirty = false;
         }
-        if (remote) HIPCHK(hipMemsetAsync(c->send, 0, c->n * c->Wp * sizeof(uint64_t), c->stream));
+        // dense exchange: clear the staging buffer; sparse: it is kept clear by the compaction pass
+        if (remote && !c->cur_sparse) HIPCHK(hipMemsetAsync(c->send, 0, c->n * c->Wp * sizeof(uint64_t), c->stream));
+        if (c->cur_sparse) HIPCHK(hipMemsetAsync(c->d_counts, 0, c->world * sizeof(unsigned long long), c->stream));
     }
     c->cur = a;
     c->cur_remote = remote;
     c->in_round = true;
-    if (mode) *mode = pull ? GOSSIP_MODE_PULL : GOSSIP_MODE_PUSH;
+    if (mode) *mode = pull ? GOSSIP_MODE_PULL : c->cur_sparse ? GOSSIP_MODE_PUSH_SPARSE : GOSSIP_MODE_PUSH;
     return GOSSIP_OK;
 }
 
@@ -420,6 +427,12 @@ gossip_status round_compute(gossip_ctx* c) {
     const bool remote = c->cur_remote;
     HIPCHK(timed(c, "push_heavy", [&] { return launch_push_heavy(a, pw, c->any_dead, remote, c->stream); }));
     HIPCHK(timed(c, "push_light", [&] { return launch_push_light(a, pw, c->any_dead, remote, c->stream); }));
+    if (c->cur_sparse) {
+        HIPCHK(timed(c, "compact_send", [&] {
+            return launch_compact_send(a, pw, c->part_begins[1], c->d_counts, c->seg, c->stream);
+        }));
+        HIPCHK(hipMemcpyAsync(c->h_counts, c->d_counts, c->world * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    }
     return GOSSIP_OK;
 }
 
@@ -572,6 +585,8 @@ void gossip_destroy(gossip_ctx* c) {
     hipFree(c->d_inj_origin);
     hipFree(c->d_inj_msg);
     hipFree(c->d_kill_peer);
+    hipFree(c->d_counts);
+    if (c->h_counts) hipHostFree(c->h_counts);
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
@@ -832,6 +847,39 @@ gossip_status gossip_set_gather(gossip_ctx* c, void* gather) {
     return GOSSIP_OK;
 }
 
+gossip_status gossip_set_sparse(gossip_ctx* c, void* seg) {
+    if (!c || !seg) return fail(GOSSIP_EINVAL, "null argument");
+    if (c->part_begins.size() < 2) return fail(GOSSIP_ESTATE, "call gossip_set_exchange first");
+    if (set_dev(c)) return GOSSIP_EHIP;
+    if (!c->d_counts) {
+        HIPCHK(hipMalloc((void**)&c->d_counts, (c->world + 1) * sizeof(unsigned long long)));
+        HIPCHK(hipHostMalloc((void**)&c->h_counts, (c->world + 1) * sizeof(uint64_t)));
+    }
+    c->seg = (uint64_t*)seg;
+    return GOSSIP_OK;
+}
+
+gossip_status gossip_sparse_counts(gossip_ctx* c, uint64_t* counts) {
+    if (!c || !counts) return fail(GOSSIP_EINVAL, "null argument");
+    if (!c->cur_sparse) return fail(GOSSIP_ESTATE, "not a sparse push round");
+    if (set_dev(c)) return GOSSIP_EHIP;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    std::memcpy(counts, c->h_counts, c->world * sizeof(uint64_t));
+    return GOSSIP_OK;
+}
+
+gossip_status gossip_round_finish_sparse(gossip_ctx* c, const void* records, uint64_t n_records,
+                                         gossip_round_stats* out) {
+    if (!c || (n_records && !records)) return fail(GOSSIP_EINVAL, "null argument");
+    if (!c->cur_sparse) return fail(GOSSIP_ESTATE, "not a sparse push round");
+    if (set_dev(c)) return GOSSIP_EHIP;
+    RoundArgs a = make_args(c);
+    HIPCHK(timed(c, "apply_remote", [&] {
+        return launch_apply_records(a, pack_w(c), (const uint64_t*)records, n_records, c->stream);
+    }));
+    return read_slot(c, out, false);
+}
+
 gossip_status gossip_round_begin(gossip_ctx* c, int requested_mode, int* mode) {
     if (!c) return fail(GOSSIP_EINVAL, "null ctx");
     if (c->world > 1 && !c->send) return fail(GOSSIP_ESTATE, "call gossip_set_exchange first");
@@ -859,6 +907,7 @@ gossip_status gossip_round_finish(gossip_ctx* c, gossip_round_stats* out) {
     if (!c) return fail(GOSSIP_EINVAL, "null ctx");
     if (!c->recv) return fail(GOSSIP_ESTATE, "call gossip_set_exchange first");
     if (c->in_round) return fail(GOSSIP_ESTATE, "gossip_round_compute first");
+    if (c->cur_sparse) return fail(GOSSIP_ESTATE, "sparse push round: use gossip_round_finish_sparse");
     if (set_dev(c)) return GOSSIP_EHIP;
     RoundArgs a = make_args(c);
     if (!c->last_pull)  // push round: OR in what the other blocks sent; pull rounds pulled it already

@@ -70,6 +70,9 @@ hipError_t launch_pull_light(const RoundArgs& a, uint32_t W, int unroll, hipStre
 hipError_t launch_pull_heavy(const RoundArgs& a, uint32_t W, hipStream_t s);
 hipError_t launch_apply_remote(const RoundArgs& a, uint32_t W, const uint64_t* recv, uint32_t world,
                                uint64_t part_stride, hipStream_t s);
+hipError_t launch_compact_send(const RoundArgs& a, uint32_t W, uint64_t chunk, unsigned long long* counts,
+                               uint64_t* seg, hipStream_t s);
+hipError_t launch_apply_records(const RoundArgs& a, uint32_t W, const uint64_t* rec, uint64_t n_rec, hipStream_t s);
 hipError_t launch_coverage(const uint64_t* words, uint64_t n_local, uint32_t W, unsigned long long* counts,
                            hipStream_t s);
 hipError_t launch_heavy_count(const uint64_t* rp, uint64_t n_local, unsigned long long* n_chunks, hipStream_t s);

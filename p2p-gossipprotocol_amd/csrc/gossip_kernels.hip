@@ -647,6 +647,76 @@ __global__ __launch_bounds__(kBlock) void k_apply_remote(RoundArgs a, const uint
     flush(acc, a.st);
 }
 
+// ---------------------------------------------------------------------------
+// Sparse exchange (push rounds of a partitioned run): the dense staging
+// buffer (send, one entry per global peer, OR of everything this rank pushed
+// to that peer) is compacted into per-destination-rank records
+// {peer, words[W]} and cleared in the same pass, so only the touched peers
+// cross xGMI.  Records of a destination stay <= its block size.
+// ---------------------------------------------------------------------------
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_compact_send(RoundArgs a, uint64_t chunk, unsigned long long* counts,
+                                                         uint64_t* seg) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t n_tiles = (a.n_global + 63) >> 6;
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); t < n_tiles; t += nwaves) {
+        const uint64_t v = (t << 6) + lane;
+        uint64_t m[W];
+        bool any = false;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            m[w] = v < a.n_global ? a.send[v * W + w] : 0ull;
+            any |= m[w] != 0;
+        }
+        const unsigned long long act = __ballot(any);
+        if (!act) continue;
+        const uint64_t q = v / chunk;
+        const int lead = __builtin_ctzll(act);
+        const uint64_t q0 = __shfl(q, lead);
+        const bool uniform = __ballot(any && q != q0) == 0ull;  // the tile's active peers share one block
+        unsigned long long idx = 0;
+        if (uniform) {
+            unsigned long long base = 0;
+            if (lane == lead) base = atomicAdd(&counts[q0], (unsigned long long)__popcll(act));
+            idx = __shfl(base, lead) + lane_rank(act);
+        } else if (any) {
+            idx = atomicAdd(&counts[q], 1ull);
+        }
+        if (any) {
+            uint64_t* rec = seg + (q * chunk + idx) * (1 + W);
+            rec[0] = v;
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                rec[1 + w] = m[w];
+                a.send[v * W + w] = 0ull;
+            }
+        }
+    }
+}
+
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_apply_records(RoundArgs a, const uint64_t* rec, uint64_t n_rec) {
+    Acc acc;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n_rec; i += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t* r = rec + i * (1 + W);
+        const uint64_t lv = r[0] - a.begin;
+        unsigned long long* sp = reinterpret_cast<unsigned long long*>(a.seen) + lv * W;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            const unsigned long long m = r[1 + w];
+            if (!m || !(m & ~sp[w])) continue;
+            const unsigned long long fr = m & ~atomicOr(sp + w, m);
+            if (fr) {
+                const unsigned long long onx = atomicOr(reinterpret_cast<unsigned long long*>(a.nx) + lv * W + w, fr);
+                acc.activated += onx == 0;
+                acc.fresh += (unsigned long long)__popcll(fr);
+            }
+        }
+    }
+    flush(acc, a.st);
+}
+
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_coverage(const uint64_t* words, uint64_t n, unsigned long long* counts) {
     __shared__ unsigned int cnt[64 * W];
@@ -815,6 +885,21 @@ hipError_t launch_apply_remote(const RoundArgs& a, uint32_t W_, const uint64_t* 
     const unsigned g = grid_for(a.n_local, kBlock);
     GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_apply_remote<W>, dim3(g), dim3(kBlock), 0, s, a, recv, world,
                                                    part_stride));
+    return hipGetLastError();
+}
+
+hipError_t launch_compact_send(const RoundArgs& a, uint32_t W_, uint64_t chunk, unsigned long long* counts,
+                               uint64_t* seg, hipStream_t s) {
+    const uint64_t tiles = (a.n_global + 63) / 64;
+    GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_compact_send<W>, dim3(grid_for(tiles, kWavesPerBlock)),
+                                                   dim3(kBlock), 0, s, a, chunk, counts, seg));
+    return hipGetLastError();
+}
+
+hipError_t launch_apply_records(const RoundArgs& a, uint32_t W_, const uint64_t* rec, uint64_t n_rec, hipStream_t s) {
+    if (!n_rec) return hipSuccess;
+    GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_apply_records<W>, dim3(grid_for(n_rec, kBlock)), dim3(kBlock),
+                                                   0, s, a, rec, n_rec));
     return hipGetLastError();
 }
 

@@ -30,6 +30,7 @@ FLAG_FORCE_PULL = 4
 MODE_AUTO = -1
 MODE_PUSH = 0
 MODE_PULL = 1
+MODE_PUSH_SPARSE = 2
 
 
 class GossipConfig(C.Structure):
@@ -111,6 +112,9 @@ def lib() -> C.CDLL:
         "gossip_set_gather": (i32, [P, P]),
         "gossip_round_begin": (i32, [P, i32, C.POINTER(C.c_int)]),
         "gossip_round_compute": (i32, [P]),
+        "gossip_set_sparse": (i32, [P, P]),
+        "gossip_sparse_counts": (i32, [P, pu64]),
+        "gossip_round_finish_sparse": (i32, [P, P, u64, C.POINTER(RoundStats)]),
         "gossip_round_finish": (i32, [P, C.POINTER(RoundStats)]),
         "gossip_round_commit": (i32, [P, u64, C.POINTER(C.c_int)]),
         "gossip_read_seen": (i32, [P, pu64]),

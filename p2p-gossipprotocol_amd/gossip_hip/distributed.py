@@ -16,9 +16,12 @@ Per round (the reference's hop broadcastMessage -> handleClient, peer.cpp:
   3. engine.round_compute()    each peer ORs its neighbours' words (no atomics)
   PUSH (sparse rounds):
   2. engine.round_compute()    local push; remote masks OR-ed into a dense
-                               send buffer indexed by global peer
-  3. all_to_all_single         rank p's slice of every send buffer -> rank p
-  4. engine.round_finish()     (push: test-and-set of the received masks)
+                               staging buffer indexed by global peer, then
+                               (PUSH_SPARSE) compacted into {peer, words}
+                               records per destination rank
+  3. all_to_all_single         PUSH: rank p's slice of every staging buffer;
+                               PUSH_SPARSE: record counts, then the records
+  4. engine.round_finish()     test-and-set of the received masks/records
   5. all_reduce(stats)         one int64 vector; drives the common termination
   6. engine.round_commit()
 
@@ -39,7 +42,7 @@ MASK32 = (1 << 32) - 1
 MASK64 = (1 << 64) - 1
 
 
-MODE_PUSH, MODE_PULL = 0, 1
+MODE_PUSH, MODE_PULL, MODE_PUSH_SPARSE = 0, 1, 2
 
 
 def partition(n: int, world: int) -> list[int]:
@@ -54,7 +57,7 @@ def partition(n: int, world: int) -> list[int]:
 
 class PartitionedRun:
     def __init__(self, engine, n: int, rank: int, world: int, device: torch.device, group=None,
-                 pull_permille: int = 50, pull: bool = True):
+                 pull_permille: int = 50, pull: bool = True, sparse: bool = True, sparse_permille: int = 250):
         self.engine = engine
         self.n, self.rank, self.world = n, rank, world
         self.device = device
@@ -78,6 +81,13 @@ class PartitionedRun:
             self.gather = torch.zeros(world * self.chunk * X, dtype=torch.int64, device=device)
             self.gather_mine = self.gather[rank * self.chunk * X:(rank + 1) * self.chunk * X]
             engine.set_gather(self.gather.data_ptr())
+        self.sparse = sparse
+        self.sparse_permille = sparse_permille
+        self.R = 1 + X  # words per sparse record {peer, words[X]}
+        if sparse:
+            self.seg = torch.zeros(world * self.chunk * self.R, dtype=torch.int64, device=device)
+            self.rec_in = torch.zeros(world * self.n_local * self.R, dtype=torch.int64, device=device)
+            engine.set_sparse(self.seg.data_ptr())
         self.prev_new = 0
         self.modes = []
         self.cum_digest = 0
@@ -100,16 +110,25 @@ class PartitionedRun:
 
     def step(self) -> tuple[dict, bool]:
         e = self.engine
-        want = MODE_PULL if self.pull and self.prev_new * 1000 >= self.pull_permille * self.n else MODE_PUSH
+        if self.pull and self.prev_new * 1000 >= self.pull_permille * self.n:
+            want = MODE_PULL
+        elif self.sparse and self.prev_new * 1000 < self.sparse_permille * self.n:
+            want = MODE_PUSH_SPARSE
+        else:
+            want = MODE_PUSH
         mode = e.round_begin(want)
+        self.modes.append(mode)
         if mode == MODE_PULL:
             dist.all_gather_into_tensor(self.gather, self.gather_mine, group=self.group)
             e.round_compute()
+            local = e.round_finish()
+        elif mode == MODE_PUSH_SPARSE:
+            e.round_compute()
+            local = self._sparse_exchange(e)
         else:
             e.round_compute()
             dist.all_to_all_single(self.recv, self.send, self.out_splits, self.in_splits, group=self.group)
-        self.modes.append(mode)
-        local = e.round_finish()
+            local = e.round_finish()
         g = self._allreduce(local)
         self.prev_new = g["new_receipts"]
         out = {"round": local["round"], "flags": local["flags"]}
@@ -119,6 +138,20 @@ class PartitionedRun:
         out["seed_removals"] = 0  # filled from the gathered reports (finalize)
         finished = e.round_commit(out["new_receipts"])
         return out, finished
+
+    def _sparse_exchange(self, e) -> dict:
+        """Counts first (P int64), then the packed records of every destination."""
+        R, chunk = self.R, self.chunk
+        counts = [int(c) for c in e.sparse_counts(self.world)]
+        c_out = torch.tensor(counts, dtype=torch.int64, device=self.device)
+        c_in = torch.zeros(self.world, dtype=torch.int64, device=self.device)
+        dist.all_to_all_single(c_in, c_out, group=self.group)
+        got = c_in.tolist()
+        send = torch.cat([self.seg[q * chunk * R:(q * chunk + counts[q]) * R] for q in range(self.world)])
+        total = sum(got)
+        recv = self.rec_in[:total * R]
+        dist.all_to_all_single(recv, send, [g * R for g in got], [c * R for c in counts], group=self.group)
+        return e.round_finish_sparse(recv.data_ptr(), total)
 
     def run(self, max_rounds: int = 4096) -> list[dict]:
         self.cum_digest = self.cum_covered = 0

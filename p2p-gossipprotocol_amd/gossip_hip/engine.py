@@ -163,6 +163,20 @@ class Engine:
     def round_compute(self) -> None:
         check(self._L.gossip_round_compute(self._ctx), "gossip_round_compute")
 
+    def set_sparse(self, seg_ptr: int) -> None:
+        check(self._L.gossip_set_sparse(self._ctx, C.c_void_p(seg_ptr)), "gossip_set_sparse")
+
+    def sparse_counts(self, world: int) -> np.ndarray:
+        out = np.zeros(world, dtype=np.uint64)
+        check(self._L.gossip_sparse_counts(self._ctx, _ptr(out, C.c_uint64)), "gossip_sparse_counts")
+        return out
+
+    def round_finish_sparse(self, records_ptr: int, n_records: int) -> dict:
+        st = RoundStats()
+        check(self._L.gossip_round_finish_sparse(self._ctx, C.c_void_p(records_ptr), n_records, C.byref(st)),
+              "gossip_round_finish_sparse")
+        return st.as_dict()
+
     def round_push(self) -> None:
         check(self._L.gossip_round_push(self._ctx), "gossip_round_push")
 

@@ -175,19 +175,37 @@ class OraclePartition:
     def set_gather(self, gather_ptr):
         self._gather = C.cast(C.c_void_p(gather_ptr), C.POINTER(C.c_uint64))
 
+    def set_sparse(self, seg_ptr):
+        self._seg = C.cast(C.c_void_p(seg_ptr), C.POINTER(C.c_uint64))
+        self._counts = np.zeros(self.world, dtype=np.uint64)
+
     def round_begin(self, mode):
         self._pull = bool(self.L.oracle_part_begin(self.p, C.c_int(1 if mode == 1 else 0)))
+        self._sparse = (not self._pull) and mode == 2 and getattr(self, "_seg", None) is not None
         if self._pull:
             self.L.oracle_part_publish(self.p, self._gather)
-        else:
+        elif not self._sparse:
             C.memset(self._send, 0, self._send_words * 8)
-        return 1 if self._pull else 0
+        return 1 if self._pull else (2 if self._sparse else 0)
 
     def round_compute(self):
         if self._pull:
             self.L.oracle_part_pull(self.p, self._gather)
         else:
             self.L.oracle_part_push_compute(self.p, self._send)
+            if self._sparse:
+                chunk = -(-self.w.n // self.world)
+                self.L.oracle_part_compact(self.p, self._send, C.c_uint64(chunk), C.c_uint32(self.world),
+                                           self._seg, _p(self._counts, C.c_uint64))
+
+    def sparse_counts(self, world):
+        return self._counts.copy()
+
+    def round_finish_sparse(self, records_ptr, n_records):
+        st = OStats()
+        self.L.oracle_part_finish_records(self.p, C.cast(C.c_void_p(records_ptr), C.POINTER(C.c_uint64)),
+                                          C.c_uint64(n_records), C.byref(st))
+        return st.as_dict()
 
     def round_push(self):
         C.memset(self._send, 0, self._send_words * 8)

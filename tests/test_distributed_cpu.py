@@ -23,7 +23,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, idx, n, out_dir, pull):
+def _worker(rank, world, port, idx, n, out_dir, pull, sparse):
     sys.path[:0] = [str(REPO / "p2p-gossipprotocol_amd"), str(REPO / "tests")]
     import torch
     import torch.distributed as dist
@@ -38,10 +38,12 @@ def _worker(rank, world, port, idx, n, out_dir, pull):
     rp, col = orc.gen_workload(w, threads=1)
     part = partition(w.n, world)
     eng = oracle_ref.OraclePartition(orc, w, rp, col, part[rank], part[rank + 1])
-    run = PartitionedRun(eng, w.n, rank, world, torch.device("cpu"), pull=pull)
+    run = PartitionedRun(eng, w.n, rank, world, torch.device("cpu"), pull=pull, sparse=sparse)
     stats = run.run()
     if pull and w.churn_threshold == 0:
-        assert 1 in run.modes and 0 in run.modes, run.modes   # both exchange patterns exercised
+        assert 1 in run.modes, run.modes
+    if sparse:
+        assert 2 in run.modes, run.modes
     reps = run.finalize(stats)
     seen = run.gather_seen()
     if rank == 0:
@@ -51,12 +53,12 @@ def _worker(rank, world, port, idx, n, out_dir, pull):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("pull", [True, False])
+@pytest.mark.parametrize("pull,sparse", [(True, True), (False, True), (False, False)])
 @pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("idx,n", [(2, 3000), (5, 4096), (3, 2048)])
-def test_partitioned_equals_single(oracle, tmp_path, world, idx, n, pull):
+def test_partitioned_equals_single(oracle, tmp_path, world, idx, n, pull, sparse):
     from gossip_hip.workloads import config
-    mp.spawn(_worker, args=(world, _free_port(), idx, n, str(tmp_path), pull), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), idx, n, str(tmp_path), pull, sparse), nprocs=world, join=True)
     out = json.loads((tmp_path / "out.json").read_text())
     seen = np.load(tmp_path / "seen.npy")
     w = config(idx, n, pick=oracle.pick_origins)

@@ -13,7 +13,7 @@ from gossip_hip.workloads import config
 pytestmark = pytest.mark.gpu
 
 
-def run_partitioned(w, P, pull=True):
+def run_partitioned(w, P, pull=True, sparse=False):
     """Mirror of gossip_hip.distributed.PartitionedRun with the collectives done
     by device copies: all-gather for pull rounds, all-to-all for push rounds."""
     import torch
@@ -33,12 +33,16 @@ def run_partitioned(w, P, pull=True):
     sends = [torch.zeros(w.n * X, dtype=torch.int64, device="cuda") for _ in range(P)]
     recvs = [torch.zeros(P * nl[q] * X, dtype=torch.int64, device="cuda") for q in range(P)]
     gathers = [torch.zeros(P * chunk * X, dtype=torch.int64, device="cuda") for _ in range(P)]
+    R = 1 + X
+    segs = [torch.zeros(P * chunk * R, dtype=torch.int64, device="cuda") for _ in range(P)]
+    rec_in = [torch.zeros(P * nl[q] * R, dtype=torch.int64, device="cuda") for q in range(P)]
     for p, e in enumerate(engines):
         e.set_exchange(sends[p].data_ptr(), recvs[p].data_ptr(), part)
         e.set_gather(gathers[p].data_ptr())
+        e.set_sparse(segs[p].data_ptr())
     rounds, modes, dig, cov, prev_new = [], [], 0, 0, 0
     while True:
-        want = 1 if pull and prev_new * 1000 >= 50 * w.n else 0
+        want = 1 if pull and prev_new * 1000 >= 50 * w.n else (2 if sparse else 0)
         got = {e.round_begin(want) for e in engines}
         assert len(got) == 1
         mode = got.pop()
@@ -53,7 +57,19 @@ def run_partitioned(w, P, pull=True):
             for q in range(P):
                 for p in range(P):
                     recvs[q][p * nl[q] * X:(p + 1) * nl[q] * X].copy_(sends[p][part[q] * X:part[q + 1] * X])
-        loc = [e.round_finish() for e in engines]
+        if mode == 2:   # counts, then the records of every sender, in sender order
+            counts = [e.sparse_counts(P) for e in engines]
+            loc = []
+            for q, e in enumerate(engines):
+                off = 0
+                for p in range(P):
+                    c = int(counts[p][q])
+                    rec_in[q][off * R:(off + c) * R].copy_(segs[p][q * chunk * R:(q * chunk + c) * R])
+                    off += c
+                loc.append(e.round_finish_sparse(rec_in[q].data_ptr(), off))
+            assert all(not torch.any(sd) for sd in sends)   # compaction left the staging buffers clear
+        else:
+            loc = [e.round_finish() for e in engines]
         g = {f: sum(l[f] for l in loc) for f in STAT_FIELDS}
         dig = (dig + g["digest"]) & MASK64
         cov += g["covered"]
@@ -79,16 +95,18 @@ def run_partitioned(w, P, pull=True):
     return rounds, seen, reps, csrs, part, modes
 
 
-@pytest.mark.parametrize("pull", [True, False])
+@pytest.mark.parametrize("pull,sparse", [(True, True), (True, False), (False, True)])
 @pytest.mark.parametrize("P", [2, 3, 4])
 @pytest.mark.parametrize("idx,n", [(2, 1 << 15), (3, 100_000), (5, 1 << 15)])
-def test_partitioned_gpu_equals_oracle(oracle, idx, n, P, pull):
+def test_partitioned_gpu_equals_oracle(oracle, idx, n, P, pull, sparse):
     w = config(idx, n, pick=oracle.pick_origins)
     rp, col = oracle.gen_workload(w)
     ref = oracle.simulate_workload(w, rp, col)
-    rounds, seen, reps, csrs, part, modes = run_partitioned(w, P, pull)
+    rounds, seen, reps, csrs, part, modes = run_partitioned(w, P, pull, sparse)
     if pull and idx != 5:
-        assert 1 in modes and 0 in modes
+        assert 1 in modes
+    if sparse:
+        assert 2 in modes
     for p, (lrp, lcol) in enumerate(csrs):   # partitioned generator = slices of the global overlay
         base = int(rp[part[p]])
         assert np.array_equal(lrp, rp[part[p]:part[p + 1] + 1] - np.uint64(base))
