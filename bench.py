@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--pull-permille", type=int, default=0, help="push/pull switch point (0 = engine default)")
     ap.add_argument("--front-permille", type=int, default=0, help="frontier-bitmap switch point (0 = default)")
     ap.add_argument("--mode", default="auto", choices=["auto", "push", "pull"])
+    ap.add_argument("--force-partitioned", action="store_true",
+                    help="use the multi-rank driver (RCCL collectives) even at WORLD_SIZE 1")
     return ap.parse_args()
 
 
@@ -116,7 +118,8 @@ def main():
 
     w = config(args.config, args.n or None)
     tune = dict(pull_permille=args.pull_permille, front_permille=args.front_permille, mode=args.mode)
-    if world > 1:
+    partitioned = world > 1 or args.force_partitioned
+    if partitioned:
         import torch.distributed as dist
 
         from gossip_hip.distributed import PartitionedRun, partition
@@ -153,6 +156,11 @@ def main():
             torch.cuda.synchronize()
 
     shape = eng.shape()
+    n_edges = shape["n_edges"]
+    if partitioned:
+        t = torch.tensor([n_edges], dtype=torch.int64, device=dev)
+        dist.all_reduce(t)
+        n_edges = int(t.item())
     for _ in range(args.warmup):
         one_step()
     if not args.no_timing:
@@ -164,7 +172,7 @@ def main():
         stats = one_step()
     barrier()
     dt = time.perf_counter() - t0
-    if world > 1:
+    if partitioned:
         import torch.distributed as dist
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -207,7 +215,7 @@ def main():
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic (Philox-generated power-law overlay and origins)",
-            "config": {"workload": w.name, "peers": w.n, "edges": shape["n_edges"] if world == 1 else None,
+            "config": {"workload": w.name, "peers": w.n, "edges": n_edges,
                        "messages": w.n_msgs, "rounds": len(stats),
                        "rounds_to_full_coverage": rounds_to_full(stats),
                        "deliveries_per_step": deliveries, "parallelism": f"vertex-partition x{world}"},
@@ -217,8 +225,11 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args, args.config)
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if partitioned:
         import torch.distributed as dist
+        reps = runner.finalize(stats)
+        if rank == 0 and args.force_partitioned:
+            print(json.dumps({"partitioned_check": {"modes": runner.modes, "reports": int(len(reps))}}), flush=True)
         dist.destroy_process_group()
 
 
