@@ -109,6 +109,7 @@ struct gossip_ctx {
     uint64_t* h_counts = nullptr;            // pinned copy
     bool cur_sparse = false;
     int pull_unroll = 2;         // 64-edge batches in flight per wave in pull_light (GOSSIP_PULL_UNROLL)
+    uint32_t heavy = kHeavyDegree;  // light/heavy row threshold (GOSSIP_HEAVY_DEGREE)
     uint64_t frontier_est = 0;   // activated peers of the previous round
     std::vector<uint64_t> inj_prefix;  // per sorted injection: cumulative mask words
     uint64_t cum_digest = 0, cum_covered = 0;
@@ -229,6 +230,7 @@ RoundArgs make_args(gossip_ctx* c) {
     a.report_cap = c->report_cap;
     a.round = c->round;
     a.max_missed = c->cfg.max_missed;
+    a.heavy = c->heavy;
     return a;
 }
 
@@ -241,14 +243,14 @@ gossip_status install_graph(gossip_ctx* c, uint64_t* d_rp, uint32_t* d_col, uint
     unsigned long long* d_cnt = nullptr;
     HIPCHK(hipMalloc((void**)&d_cnt, 2 * sizeof(unsigned long long)));
     HIPCHK(hipMemsetAsync(d_cnt, 0, 2 * sizeof(unsigned long long), c->stream));
-    HIPCHK(launch_heavy_count(c->rp, c->n_local, d_cnt, c->stream));
+    HIPCHK(launch_heavy_count(c->rp, c->n_local, c->heavy, d_cnt, c->stream));
     unsigned long long nch = 0;
     HIPCHK(hipMemcpyAsync(&nch, d_cnt, sizeof(nch), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     c->n_chunks = nch;
     if (nch) {
         HIPCHK(hipMalloc((void**)&c->chunks, nch * sizeof(HeavyChunk)));
-        HIPCHK(launch_heavy_fill(c->rp, c->n_local, c->chunks, d_cnt + 1, c->stream));
+        HIPCHK(launch_heavy_fill(c->rp, c->n_local, c->heavy, c->chunks, d_cnt + 1, c->stream));
     }
     HIPCHK(hipStreamSynchronize(c->stream));
     hipFree(d_cnt);
@@ -537,6 +539,7 @@ gossip_status gossip_create(const gossip_config* cfg, gossip_ctx** out) {
     if (!c->cfg.graph_model) c->cfg.graph_model = GOSSIP_GRAPH_POWERLAW;
     c->device = dev;
     if (const char* u = std::getenv("GOSSIP_PULL_UNROLL")) c->pull_unroll = std::atoi(u);
+    if (const char* h = std::getenv("GOSSIP_HEAVY_DEGREE")) c->heavy = (uint32_t)std::max(1, std::atoi(h));
     c->n = cfg->n_peers;
     c->begin = b;
     c->end = e;

@@ -8,8 +8,8 @@
 namespace gossip {
 
 constexpr uint32_t kMaskedEdge = 0x80000000u;  // col[e] bit 31: edge dropped by liveness (peer.cpp:388)
-constexpr uint32_t kHeavyDegree = 256;         // rows longer than this go to the edge-chunked kernel
-constexpr uint32_t kHeavyChunk = 2048;         // edges per heavy chunk (one workgroup)
+constexpr uint32_t kHeavyDegree = 256;         // default: rows longer than this go to the edge-chunked kernels
+constexpr uint32_t kHeavyChunk = 1024;         // edges per heavy chunk (one wave)
 constexpr int kBlock = 256;                    // 4 waves of 64
 constexpr int kMaxWords = 8;                   // M <= 512 concurrent messages
 
@@ -51,6 +51,8 @@ struct RoundArgs {
     uint64_t report_cap;
     uint32_t round;
     uint32_t max_missed;
+    uint32_t heavy;                // light/heavy row threshold (rows > heavy are chunked)
+    uint32_t pad0;
     uint64_t inj_mask[kMaxWords];  // messages injected so far (pull: bits a peer can still learn)
     uint64_t* front;               // pull rounds: 1 bit per source peer, set iff its new words are nonzero
     const uint64_t* nw_src;        // pull rounds: new words of every source, indexed by (global) peer id
@@ -75,9 +77,10 @@ hipError_t launch_compact_send(const RoundArgs& a, uint32_t W, uint64_t chunk, u
 hipError_t launch_apply_records(const RoundArgs& a, uint32_t W, const uint64_t* rec, uint64_t n_rec, hipStream_t s);
 hipError_t launch_coverage(const uint64_t* words, uint64_t n_local, uint32_t W, unsigned long long* counts,
                            hipStream_t s);
-hipError_t launch_heavy_count(const uint64_t* rp, uint64_t n_local, unsigned long long* n_chunks, hipStream_t s);
-hipError_t launch_heavy_fill(const uint64_t* rp, uint64_t n_local, HeavyChunk* chunks, unsigned long long* cursor,
-                             hipStream_t s);
+hipError_t launch_heavy_count(const uint64_t* rp, uint64_t n_local, uint32_t heavy, unsigned long long* n_chunks,
+                              hipStream_t s);
+hipError_t launch_heavy_fill(const uint64_t* rp, uint64_t n_local, uint32_t heavy, HeavyChunk* chunks,
+                             unsigned long long* cursor, hipStream_t s);
 
 // ---- overlay generator (gossip_graph.hip) ----
 // Builds the owned rows of the powerlaw overlay on the device.  On success

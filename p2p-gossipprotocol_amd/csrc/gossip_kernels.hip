@@ -11,8 +11,9 @@
 // bitsets.  Work mapping: one wave64 per tile of 64 consecutive peers with
 // an in-wave prefix sum over row lengths ("edge-space expansion"), so the
 // wave's lanes walk consecutive col entries of the tile -- one contiguous
-// span when the tile's rows are all active; rows longer than kHeavyDegree
-// are cut into kHeavyChunk-edge chunks, one workgroup each.
+// span when the tile's rows are all active; rows longer than the heavy
+// threshold (RoundArgs.heavy) are cut into kHeavyChunk-edge chunks, one wave
+// each, so no wave walks a long tail.
 #include <hip/hip_runtime.h>
 
 #include "gossip_internal.hpp"
@@ -181,7 +182,7 @@ __global__ __launch_bounds__(kBlock) void k_push_light(RoundArgs a, uint32_t wd)
             acc.covered += pc;
             rb = a.rp[v];
             const uint64_t d = a.rp[v + 1] - rb;
-            deg = d <= kHeavyDegree ? (uint32_t)d : 0u;
+            deg = d <= a.heavy ? (uint32_t)d : 0u;
         }
         tile_edges(deg, rb, [&](int s, bool valid, uint64_t e) {
             uint64_t ms[W];
@@ -199,12 +200,14 @@ __global__ __launch_bounds__(kBlock) void k_push_light(RoundArgs a, uint32_t wd)
     }
 }
 
-// push: heavy rows, one workgroup per kHeavyChunk-edge chunk; runs before
+// push: heavy rows, one wave per kHeavyChunk-edge chunk; runs before
 // k_push_light (which clears the new words).
 template <int W, bool CA, bool RM>
 __global__ __launch_bounds__(kBlock) void k_push_heavy(RoundArgs a) {
     Acc acc;
-    for (uint64_t ci = blockIdx.x; ci < a.n_chunks; ci += gridDim.x) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    for (uint64_t ci = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); ci < a.n_chunks; ci += nwaves) {
         const HeavyChunk ch = a.chunks[ci];
         uint64_t m[W];
         bool act = false;
@@ -215,13 +218,12 @@ __global__ __launch_bounds__(kBlock) void k_push_heavy(RoundArgs a) {
             act |= m[w] != 0;
             pc += (uint32_t)__popcll(m[w]);
         }
-        if (!act) continue;  // uniform over the workgroup
-        for (uint64_t e = ch.e0 + threadIdx.x; e < ch.e1; e += kBlock) deliver<W, CA, RM>(a, a.col[e], m, pc, acc);
+        if (!act) continue;  // uniform over the wave
+        for (uint64_t e = ch.e0 + lane; e < ch.e1; e += 64) deliver<W, CA, RM>(a, a.col[e], m, pc, acc);
     }
     acc.htrav = acc.trav;
     flush(acc, a.st);
 }
-
 
 // ---------------------------------------------------------------------------
 // pull (direction-optimised dense rounds): every peer that can still learn a
@@ -231,8 +233,9 @@ __global__ __launch_bounds__(kBlock) void k_push_heavy(RoundArgs a) {
 // no dead peers and no masked edges, edge u->v is traversed iff u is in the
 // frontier, so traversals/deliveries are summed on the source side
 // (deg(u), popcount(new[u]) * deg(u)) and new_receipts on the receiving side.
-// Rows longer than kHeavyDegree are pulled by k_pull_heavy (one workgroup per
-// chunk, one atomicOr per chunk).  P = 1 only (col ids index nw directly).
+// Heavy rows are pulled by k_pull_heavy (one wave per chunk, one atomicOr per
+// chunk).  Gathers read nw_src: the own new words (P = 1) or the all-gathered
+// words of every block, indexed by global peer (P > 1).
 // ---------------------------------------------------------------------------
 // Frontier bitmap for a pull round: one ballot per 64-peer tile, stored by
 // the tile's own wave (no atomics).  n/8 bytes -- cache-resident at 2^28 peers.
@@ -316,7 +319,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_light(RoundArgs a, uint32_t wd)
             acc.trav += d;
             acc.deliv += (unsigned long long)pc * d;
         }
-        const bool light = d <= kHeavyDegree;
+        const bool light = d <= a.heavy;
 #pragma unroll
         for (int w = 0; w < W; ++w) my[lane * W + w] = 0ull;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -401,55 +404,49 @@ __global__ __launch_bounds__(kBlock) void k_pull_light(RoundArgs a, uint32_t wd)
 
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_pull_heavy(RoundArgs a) {
-    __shared__ unsigned long long need_s[W];
-    __shared__ unsigned long long red[kWavesPerBlock][W];
     Acc acc;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (uint64_t ci = blockIdx.x; ci < a.n_chunks; ci += gridDim.x) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    for (uint64_t ci = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); ci < a.n_chunks; ci += nwaves) {
         const HeavyChunk ch = a.chunks[ci];
-        if (threadIdx.x < W) need_s[threadIdx.x] = a.inj_mask[threadIdx.x] & ~a.seen[(uint64_t)ch.v * W + threadIdx.x];
-        __syncthreads();
         uint64_t need[W], part[W];
         bool any = false;
 #pragma unroll
         for (int w = 0; w < W; ++w) {
-            need[w] = need_s[w];
+            // one lane reads, every lane uses the same value: the branch below stays wave-uniform
+            const uint64_t s0 = __shfl(a.seen[(uint64_t)ch.v * W + w], 0);
+            need[w] = a.inj_mask[w] & ~s0;
             part[w] = 0;
             any |= need[w] != 0;
         }
-        if (any) {  // uniform: every thread read the same need_s
-            for (uint64_t e = ch.e0 + threadIdx.x; e < ch.e1; e += kBlock) {
-                const uint32_t u = a.col[e];
-                acc.pulled++;
-                if (a.front && !((a.front[u >> 6] >> (u & 63)) & 1ull)) continue;
+        if (!any) continue;
+        for (uint64_t e = ch.e0 + lane; e < ch.e1; e += 64) {
+            const uint32_t u = a.col[e];
+            acc.pulled++;
+            if (a.front && !((a.front[u >> 6] >> (u & 63)) & 1ull)) continue;
 #pragma unroll
-                for (int w = 0; w < W; ++w)
-                    if (need[w]) part[w] |= a.nw_src[(uint64_t)u * W + w] & need[w];
-            }
+            for (int w = 0; w < W; ++w)
+                if (need[w]) part[w] |= a.nw_src[(uint64_t)u * W + w] & need[w];
+        }
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) part[w] |= __shfl_xor(part[w], off);
+        }
+        if (lane == 0) {
 #pragma unroll
             for (int w = 0; w < W; ++w) {
-#pragma unroll
-                for (int off = 32; off > 0; off >>= 1) part[w] |= __shfl_xor(part[w], off);
-                if (lane == 0) red[wid][w] = part[w];
-            }
-            __syncthreads();
-            if (threadIdx.x < W) {
-                const int w = threadIdx.x;
-                uint64_t tot = 0;
-                for (int k = 0; k < kWavesPerBlock; ++k) tot |= red[k][w];
-                if (tot) {
-                    unsigned long long* sp = reinterpret_cast<unsigned long long*>(a.seen) + (uint64_t)ch.v * W + w;
-                    const unsigned long long fr = tot & ~atomicOr(sp, (unsigned long long)tot);
-                    if (fr) {
-                        const unsigned long long onx =
-                            atomicOr(reinterpret_cast<unsigned long long*>(a.nx) + (uint64_t)ch.v * W + w, fr);
-                        acc.activated += onx == 0;
-                        acc.fresh += (unsigned long long)__popcll(fr);
-                    }
+                if (!part[w]) continue;
+                unsigned long long* sp = reinterpret_cast<unsigned long long*>(a.seen) + (uint64_t)ch.v * W + w;
+                const unsigned long long fr = part[w] & ~atomicOr(sp, (unsigned long long)part[w]);
+                if (fr) {
+                    const unsigned long long onx =
+                        atomicOr(reinterpret_cast<unsigned long long*>(a.nx) + (uint64_t)ch.v * W + w, fr);
+                    acc.activated += onx == 0;
+                    acc.fresh += (unsigned long long)__popcll(fr);
                 }
             }
         }
-        __syncthreads();
     }
     acc.htrav = acc.pulled;  // heavy-row edges scanned
     acc.pulled = 0;
@@ -516,7 +513,7 @@ __global__ __launch_bounds__(kBlock) void k_liveness_light(RoundArgs a) {
         if (act) {
             rb = a.rp[v];
             const uint64_t d = a.rp[v + 1] - rb;
-            deg = d <= kHeavyDegree ? (uint32_t)d : 0u;
+            deg = d <= a.heavy ? (uint32_t)d : 0u;
         }
         const uint32_t tile_base = (uint32_t)(a.begin + (t << 6));
         tile_edges(deg, rb, [&](int s, bool valid, uint64_t e) {
@@ -531,12 +528,14 @@ __global__ __launch_bounds__(kBlock) void k_liveness_light(RoundArgs a) {
 
 __global__ __launch_bounds__(kBlock) void k_liveness_heavy(RoundArgs a) {
     Acc acc;
-    for (uint64_t ci = blockIdx.x; ci < a.n_chunks; ci += gridDim.x) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    for (uint64_t ci = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); ci < a.n_chunks; ci += nwaves) {
         const HeavyChunk ch = a.chunks[ci];
         const uint32_t u = (uint32_t)(a.begin + ch.v);
         if (!bit_alive(a.alive, u)) continue;
-        for (uint64_t base = ch.e0; base < ch.e1; base += kBlock) {
-            const uint64_t e = base + threadIdx.x;
+        for (uint64_t base = ch.e0; base < ch.e1; base += 64) {
+            const uint64_t e = base + lane;
             bool emit;
             uint32_t dead;
             ping_edge(a, e < ch.e1, e, emit, dead, acc.checked);
@@ -732,20 +731,21 @@ __global__ __launch_bounds__(kBlock) void k_coverage(const uint64_t* words, uint
         if (cnt[i]) atomicAdd(&counts[i], (unsigned long long)cnt[i]);
 }
 
-__global__ void k_heavy_count(const uint64_t* rp, uint64_t n, unsigned long long* n_chunks) {
+__global__ void k_heavy_count(const uint64_t* rp, uint64_t n, uint32_t heavy, unsigned long long* n_chunks) {
     unsigned long long mine = 0;
     for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t d = rp[v + 1] - rp[v];
-        if (d > kHeavyDegree) mine += (d + kHeavyChunk - 1) / kHeavyChunk;
+        if (d > heavy) mine += (d + kHeavyChunk - 1) / kHeavyChunk;
     }
     mine = wave_sum(mine);
     if ((threadIdx.x & 63) == 0 && mine) atomicAdd(n_chunks, mine);
 }
 
-__global__ void k_heavy_fill(const uint64_t* rp, uint64_t n, HeavyChunk* chunks, unsigned long long* cursor) {
+__global__ void k_heavy_fill(const uint64_t* rp, uint64_t n, uint32_t heavy, HeavyChunk* chunks,
+                             unsigned long long* cursor) {
     for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t b = rp[v], e = rp[v + 1];
-        if (e - b <= kHeavyDegree) continue;
+        if (e - b <= heavy) continue;
         const uint64_t nc = (e - b + kHeavyChunk - 1) / kHeavyChunk;
         const unsigned long long at = atomicAdd(cursor, (unsigned long long)nc);
         for (uint64_t k = 0; k < nc; ++k) {
@@ -797,7 +797,7 @@ hipError_t launch_kills(const RoundArgs& a, uint32_t W_, const uint32_t* peers, 
 hipError_t launch_liveness(const RoundArgs& a, hipStream_t s, int heavy) {
     if (heavy) {
         if (!a.n_chunks) return hipSuccess;
-        hipLaunchKernelGGL(k_liveness_heavy, dim3(grid_for(a.n_chunks, 1)), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL(k_liveness_heavy, dim3(grid_for(a.n_chunks, kWavesPerBlock)), dim3(kBlock), 0, s, a);
     } else {
         const uint64_t tiles = (a.n_local + 63) / 64;
         hipLaunchKernelGGL(k_liveness_light, dim3(grid_for(tiles, kWavesPerBlock)), dim3(kBlock), 0, s, a);
@@ -815,7 +815,7 @@ hipError_t launch_inject(const RoundArgs& a, uint32_t W_, const uint32_t* origin
 
 hipError_t launch_push_heavy(const RoundArgs& a, uint32_t W_, bool check_alive, bool remote, hipStream_t s) {
     if (!a.n_chunks) return hipSuccess;
-    const unsigned g = grid_for(a.n_chunks, 1);
+    const unsigned g = grid_for(a.n_chunks, kWavesPerBlock);
 #define GOSSIP_HEAVY(CA, RM) hipLaunchKernelGGL((k_push_heavy<W, CA, RM>), dim3(g), dim3(kBlock), 0, s, a)
     GOSSIP_DISPATCH_W(wp_of(W_), {
         if (check_alive) {
@@ -875,8 +875,8 @@ hipError_t launch_pull_light(const RoundArgs& a, uint32_t W_, int unroll, hipStr
 
 hipError_t launch_pull_heavy(const RoundArgs& a, uint32_t W_, hipStream_t s) {
     if (!a.n_chunks) return hipSuccess;
-    GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_pull_heavy<W>, dim3(grid_for(a.n_chunks, 1)), dim3(kBlock), 0, s,
-                                                   a));
+    GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_pull_heavy<W>, dim3(grid_for(a.n_chunks, kWavesPerBlock)),
+                                                   dim3(kBlock), 0, s, a));
     return hipGetLastError();
 }
 
@@ -911,14 +911,16 @@ hipError_t launch_coverage(const uint64_t* words, uint64_t n_local, uint32_t W_,
     return hipGetLastError();
 }
 
-hipError_t launch_heavy_count(const uint64_t* rp, uint64_t n_local, unsigned long long* n_chunks, hipStream_t s) {
-    hipLaunchKernelGGL(k_heavy_count, dim3(grid_for(n_local, kBlock)), dim3(kBlock), 0, s, rp, n_local, n_chunks);
+hipError_t launch_heavy_count(const uint64_t* rp, uint64_t n_local, uint32_t heavy, unsigned long long* n_chunks,
+                              hipStream_t s) {
+    hipLaunchKernelGGL(k_heavy_count, dim3(grid_for(n_local, kBlock)), dim3(kBlock), 0, s, rp, n_local, heavy, n_chunks);
     return hipGetLastError();
 }
 
-hipError_t launch_heavy_fill(const uint64_t* rp, uint64_t n_local, HeavyChunk* chunks, unsigned long long* cursor,
-                             hipStream_t s) {
-    hipLaunchKernelGGL(k_heavy_fill, dim3(grid_for(n_local, kBlock)), dim3(kBlock), 0, s, rp, n_local, chunks, cursor);
+hipError_t launch_heavy_fill(const uint64_t* rp, uint64_t n_local, uint32_t heavy, HeavyChunk* chunks,
+                             unsigned long long* cursor, hipStream_t s) {
+    hipLaunchKernelGGL(k_heavy_fill, dim3(grid_for(n_local, kBlock)), dim3(kBlock), 0, s, rp, n_local, heavy, chunks,
+                       cursor);
     return hipGetLastError();
 }
 

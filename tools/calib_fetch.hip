@@ -33,6 +33,60 @@ __global__ void k_gather8(const uint64_t* t, uint64_t mask, uint64_t reads, unsi
     }
     if (acc == 0x12345ull) *sink = 1;
 }
+__global__ void k_gather8_nt(const uint64_t* t, uint64_t mask, uint64_t reads, unsigned* sink) {
+    uint64_t acc = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < reads; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t h = (i + 1) * 0x9E3779B97F4A7C15ull;
+        h ^= h >> 29;
+        acc ^= __builtin_nontemporal_load(t + (h & mask));
+    }
+    if (acc == 0x12345ull) *sink = 1;
+}
+__global__ void k_gather8_sc1(const uint64_t* t, uint64_t mask, uint64_t reads, unsigned* sink) {
+    uint64_t acc = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < reads; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t h = (i + 1) * 0x9E3779B97F4A7C15ull;
+        h ^= h >> 29;
+        acc ^= __hip_atomic_load(t + (h & mask), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (acc == 0x12345ull) *sink = 1;
+}
+// 4 independent gathers per thread per iteration (more memory-level parallelism)
+__global__ void k_gather8_x4(const uint64_t* t, uint64_t mask, uint64_t reads, unsigned* sink) {
+    uint64_t acc = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < reads / 4; i += stride) {
+        uint64_t v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            uint64_t h = (i * 4 + k + 1) * 0x9E3779B97F4A7C15ull;
+            h ^= h >> 29;
+            v[k] = t[h & mask];
+        }
+        acc ^= v[0] ^ v[1] ^ v[2] ^ v[3];
+    }
+    if (acc == 0x12345ull) *sink = 1;
+}
+// gathers confined to a 32 MiB window (Infinity-Cache resident)
+__global__ void k_gather8_mall(const uint64_t* t, uint64_t reads, unsigned* sink) {
+    uint64_t acc = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < reads; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t h = (i + 1) * 0x9E3779B97F4A7C15ull;
+        h ^= h >> 29;
+        acc ^= t[h & ((32ull << 20) / 8 - 1)];
+    }
+    if (acc == 0x12345ull) *sink = 1;
+}
+// gathers confined to a 2 MiB window (L2 resident on every XCD)
+__global__ void k_gather8_l2(const uint64_t* t, uint64_t reads, unsigned* sink) {
+    uint64_t acc = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < reads; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t h = (i + 1) * 0x9E3779B97F4A7C15ull;
+        h ^= h >> 29;
+        acc ^= t[h & ((2ull << 20) / 8 - 1)];
+    }
+    if (acc == 0x12345ull) *sink = 1;
+}
 __global__ void k_store8(uint64_t* p, uint64_t n) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
         p[i] = i;
@@ -62,6 +116,11 @@ int main() {
         run("stream4", [&] { hipLaunchKernelGGL(k_stream4, dim3(4096), dim3(256), 0, 0, (const unsigned*)buf, bytes / 4, sink); }, (double)bytes);
         run("gather8", [&] { hipLaunchKernelGGL(k_gather8, dim3(4096), dim3(256), 0, 0, (const uint64_t*)buf, bytes / 8 - 1, reads, sink); }, (double)reads * 8);
         run("store8", [&] { hipLaunchKernelGGL(k_store8, dim3(4096), dim3(256), 0, 0, (uint64_t*)buf, bytes / 8); }, (double)bytes);
+        run("gather8nt", [&] { hipLaunchKernelGGL(k_gather8_nt, dim3(4096), dim3(256), 0, 0, (const uint64_t*)buf, bytes / 8 - 1, reads, sink); }, (double)reads * 8);
+        run("gather8sc1", [&] { hipLaunchKernelGGL(k_gather8_sc1, dim3(4096), dim3(256), 0, 0, (const uint64_t*)buf, bytes / 8 - 1, reads, sink); }, (double)reads * 8);
+        run("gather8x4", [&] { hipLaunchKernelGGL(k_gather8_x4, dim3(4096), dim3(256), 0, 0, (const uint64_t*)buf, bytes / 8 - 1, reads, sink); }, (double)reads * 8);
+        run("gather8mall", [&] { hipLaunchKernelGGL(k_gather8_mall, dim3(4096), dim3(256), 0, 0, (const uint64_t*)buf, reads, sink); }, (double)reads * 8);
+        run("gather8l2", [&] { hipLaunchKernelGGL(k_gather8_l2, dim3(4096), dim3(256), 0, 0, (const uint64_t*)buf, reads, sink); }, (double)reads * 8);
     }
     hipDeviceSynchronize();
     printf("reads=%llu\n", (unsigned long long)reads);
