@@ -74,8 +74,10 @@ struct gossip_ctx {
     uint32_t* alive = nullptr;
     uint32_t* registered = nullptr;
     uint8_t* miss = nullptr;
-    DevStats* st = nullptr;
-    DevStats* h_st = nullptr;  // pinned
+    DevStats* st = nullptr;    // kStatLines striped lines of the current round (zeroed after each read)
+    DevStats* h_st = nullptr;  // pinned, kStatLines lines
+    DevStats last_st{};        // decoded sums of round last_st_round
+    uint32_t last_st_round = ~0u;
     unsigned long long* cov_hist = nullptr;
     DeadReport* reports = nullptr;
     unsigned long long* n_reports = nullptr;
@@ -217,7 +219,7 @@ RoundArgs make_args(gossip_ctx* c) {
     a.front = c->front;
     a.send = c->send;
     a.miss = c->miss;
-    a.st = c->st + c->round;
+    a.st = c->st;
     a.cov = c->cov_hist ? c->cov_hist + (uint64_t)c->round * 64 * c->Wp : nullptr;
     a.chunks = c->chunks;
     a.n_chunks = c->n_chunks;
@@ -439,9 +441,19 @@ gossip_status round_compute(gossip_ctx* c) {
 }
 
 gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative) {
-    HIPCHK(hipMemcpyAsync(c->h_st, c->st + c->round, sizeof(DevStats), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    const DevStats& d = *c->h_st;
+    if (c->last_st_round != c->round) {  // read once per round, then the lines are re-zeroed for the next
+        HIPCHK(hipMemcpyAsync(c->h_st, c->st, kStatLines * sizeof(DevStats), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(hipMemsetAsync(c->st, 0, kStatLines * sizeof(DevStats), c->stream));
+        DevStats sum{};
+        const unsigned long long* src = reinterpret_cast<const unsigned long long*>(c->h_st);
+        unsigned long long* dst = reinterpret_cast<unsigned long long*>(&sum);
+        for (int l = 0; l < kStatLines; ++l)
+            for (int f = 0; f < 16; ++f) dst[f] += src[l * 16 + f];
+        c->last_st = sum;
+        c->last_st_round = c->round;
+    }
+    const DevStats d = c->last_st;
     c->frontier_est = d.activated;
     if (c->timing) {
         if (c->last_pull) {
@@ -566,9 +578,9 @@ gossip_status gossip_create(const gossip_config* cfg, gossip_ctx** out) {
     if ((err = hipMalloc((void**)&c->front, ((c->n_local + 63) / 64 + 1) * 8)) != hipSuccess) return bail("front", err);
     if ((err = hipMalloc((void**)&c->alive, bitwords * 4)) != hipSuccess) return bail("alive", err);
     if ((err = hipMalloc((void**)&c->registered, bitwords * 4)) != hipSuccess) return bail("registry", err);
-    if ((err = hipMalloc((void**)&c->st, (uint64_t)c->cfg.max_rounds * sizeof(DevStats))) != hipSuccess)
+    if ((err = hipMalloc((void**)&c->st, kStatLines * sizeof(DevStats))) != hipSuccess)
         return bail("stats", err);
-    if ((err = hipHostMalloc((void**)&c->h_st, sizeof(DevStats))) != hipSuccess) return bail("pinned stats", err);
+    if ((err = hipHostMalloc((void**)&c->h_st, kStatLines * sizeof(DevStats))) != hipSuccess) return bail("pinned stats", err);
     if ((err = hipMalloc((void**)&c->n_reports, sizeof(unsigned long long))) != hipSuccess) return bail("nrep", err);
     if (c->cfg.flags & GOSSIP_FLAG_COVERAGE_HISTORY) {
         if ((err = hipMalloc((void**)&c->cov_hist, (uint64_t)c->cfg.max_rounds * 64 * c->Wp * 8)) != hipSuccess)
@@ -772,7 +784,8 @@ gossip_status gossip_reset(gossip_ctx* c) {
         HIPCHK(hipMemcpyAsync(c->registered + bitwords - 1, &tail, 4, hipMemcpyHostToDevice, s));
         HIPCHK(hipStreamSynchronize(s));
     }
-    HIPCHK(hipMemsetAsync(c->st, 0, (uint64_t)c->cfg.max_rounds * sizeof(DevStats), s));
+    HIPCHK(hipMemsetAsync(c->st, 0, kStatLines * sizeof(DevStats), s));
+    c->last_st_round = ~0u;
     HIPCHK(hipMemsetAsync(c->n_reports, 0, sizeof(unsigned long long), s));
     if (c->cov_hist) HIPCHK(hipMemsetAsync(c->cov_hist, 0, (uint64_t)c->cfg.max_rounds * 64 * c->Wp * 8, s));
     if (c->miss) HIPCHK(hipMemsetAsync(c->miss, 0, c->n_edges + 1, s));

@@ -12,6 +12,7 @@ constexpr uint32_t kHeavyDegree = 256;         // default: rows longer than this
 constexpr uint32_t kHeavyChunk = 1024;         // edges per heavy chunk (one wave)
 constexpr int kBlock = 256;                    // 4 waves of 64
 constexpr int kMaxWords = 8;                   // M <= 512 concurrent messages
+constexpr int kStatLines = 64;                 // striped DevStats lines per round (summed at read)
 
 // Per-round device counters (all integer; order-independent sums).
 struct DevStats {
@@ -41,7 +42,7 @@ struct RoundArgs {
     uint64_t* nx;           // next round's new words (fresh)
     uint64_t* send;         // dense remote staging (n_global * W) or null
     uint8_t* miss;          // per-edge miss counters
-    DevStats* st;           // this round's slot
+    DevStats* st;           // this round's kStatLines striped lines
     unsigned long long* cov;  // per-message coverage increments of this round (history) or null
     const HeavyChunk* chunks;
     uint64_t n_chunks;
