@@ -43,6 +43,8 @@ typedef int gossip_status;
 #define GOSSIP_FLAG_COVERAGE_HISTORY 1u /* keep per-message coverage for every round */
 #define GOSSIP_FLAG_FORCE_PUSH 2u       /* never use pull rounds */
 #define GOSSIP_FLAG_FORCE_PULL 4u       /* pull every eligible round (symmetric overlay, nobody dead, P = 1) */
+#define GOSSIP_FLAG_NO_BIN 8u           /* do not lay out the binned edge slots (saves ~(4 + 2 + 8W) B per edge) */
+#define GOSSIP_FLAG_FORCE_BIN 16u       /* every pull-eligible round runs binned (needs the slot layout) */
 
 /*
  * Replaces: NetworkConfig's parsed values (config.cpp:31-42,93-96) plus the
@@ -67,6 +69,9 @@ typedef struct gossip_config {
     uint64_t report_capacity; /* dead-node report buffer entries (0 = default) */
     uint32_t pull_permille;   /* pull when the frontier estimate >= this per-mille of the owned peers (0 = 50) */
     uint32_t front_permille;  /* pull rounds probe a frontier bitmap below this per-mille (0 = 400; 1000 = always) */
+    uint32_t bin_permille;    /* a dense round runs binned while the (peer, message) pairs still missing are
+                                 >= this per-mille of the owned peers (0 = default) */
+    uint32_t reserved0;
 } gossip_config;
 
 /*

@@ -1,0 +1,332 @@
+// gossip_bins.hip -- bootstrap-time bin layout for binned dense rounds.
+//
+// A dense round of the round contract is, per peer v,
+//   next[v] = (OR over u in N(v) of new[u]) & ~seen[v]
+// -- handleClient's dedup (peer.cpp:277-285) applied to every copy that
+// broadcastMessage (peer.cpp:310-316) sends.  Gathering new[u] per edge costs
+// one random HBM line per edge.  The overlay is static, so instead each edge
+// u->v with a light destination v gets a fixed "slot" in a destination-bin-
+// major array: slots of bin b hold exactly the edges into b's peers, in
+// source order.  A binned round then
+//   (1) scatter: per source chunk (kBinChunkWords words of new[], one XCD's
+//       L2), walk the chunk's edges in bin order ("cb" lists) and write new[u]
+//       into their slots.  Within a (chunk, bin) pair the slots are
+//       consecutive, so the writes are runs of ~E/(chunks*bins) slots, and the
+//       new[u] reads hit the L2 (random 8-B stores beyond the caches run at
+//       ~22 G/s, L2-resident loads at ~230 G/s: tools/calib_l2.hip);
+//   (2) apply: each bin's slots are folded into an LDS accumulator (streamed).
+// Rows longer than the heavy threshold are not binned as destinations:
+// k_pull_heavy gathers them (they are satisfied after a few edges).
+//
+// Layout (built here, once per overlay):
+//   bins    : whole 64-peer tiles, <= kBinWords/Wp peers and <= kBinSlotCap slots
+//   bdst    : u16 per slot -> destination - bin.v0 (padding slots: 0, val 0)
+//   val     : Wp u64 per slot (rewritten whole by every binned round)
+//   cb_slot, cb_src : u32 per binned edge in (source chunk, bin, CSR) order
+//   chunk_begin     : offsets of each source chunk's cb entries
+// Construction: key = bin of the destination (heavy -> n_bins), stable radix
+// sort of (key, edge) -> slot of edge = b.s0 + (position - b.u0); then key =
+// chunk * n_bins + bin, stable sort -> cb order.  Stability keeps CSR order
+// inside every bin and every (chunk, bin) pair.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "gossip_internal.hpp"
+
+namespace gossip {
+
+namespace {
+
+unsigned gridn(uint64_t items) {
+    uint64_t g = (items + 255) / 256;
+    if (g < 1) g = 1;
+    if (g > 65536) g = 65536;
+    return (unsigned)g;
+}
+
+// Per 64-peer tile: number of binned slots (sum of light row lengths; on a
+// symmetric overlay a row's length is also its in-degree) + light bitmap.
+__global__ void k_tile_slots(const uint64_t* rp, uint64_t n, uint32_t heavy, uint32_t* tile_slots,
+                             unsigned long long* light_bits) {
+    const uint64_t n_tiles = (n + 63) / 64;
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n_tiles * 64;
+         v += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t d = 0;
+        bool light = false;
+        if (v < n) {
+            d = rp[v + 1] - rp[v];
+            light = d <= heavy;
+        }
+        const unsigned long long bits = __ballot(light);
+        uint64_t sl = light ? d : 0;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) sl += __shfl_xor(sl, off);
+        if ((threadIdx.x & 63) == 0) {  // blockDim is a multiple of 64: a wave is one tile
+            tile_slots[v >> 6] = (uint32_t)sl;
+            light_bits[v >> 6] = bits;
+        }
+    }
+}
+
+__global__ void k_bin_keys(const uint32_t* col, uint64_t m, const unsigned long long* light_bits,
+                           const uint32_t* bin_of_tile, uint32_t n_bins, uint32_t* keys, uint32_t* vals) {
+    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t v = col[e] & ~kMaskedEdge;
+        const bool light = (light_bits[v >> 6] >> (v & 63)) & 1ull;
+        keys[e] = light ? bin_of_tile[v >> 6] : n_bins;
+        vals[e] = (uint32_t)e;
+    }
+}
+
+__global__ void k_bin_assign(const uint32_t* skeys, const uint32_t* svals, uint64_t m, const Bin* bins,
+                             uint32_t n_bins, const uint32_t* col, uint32_t* slot, uint16_t* bdst) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t b = skeys[i];
+        const uint32_t e = svals[i];
+        if (b >= n_bins) {
+            slot[e] = kNoSlot;
+            continue;
+        }
+        const Bin bn = bins[b];
+        const uint64_t pos = bn.s0 + (i - bn.u0);
+        slot[e] = (uint32_t)pos;
+        bdst[pos] = (uint16_t)((col[e] & ~kMaskedEdge) - bn.v0);
+    }
+}
+
+__global__ void k_edge_rows(const uint64_t* rp, uint64_t n, uint32_t* src) {
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x)
+        for (uint64_t e = rp[v]; e < rp[v + 1]; ++e) src[e] = (uint32_t)v;
+}
+
+__global__ void k_cb_keys(const uint32_t* slot, const uint32_t* src, const uint32_t* col, uint64_t m,
+                          const uint32_t* bin_of_tile, uint32_t n_bins, uint32_t chunk, uint32_t* keys,
+                          uint32_t* vals) {
+    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t v = col[e] & ~kMaskedEdge;
+        keys[e] = slot[e] == kNoSlot ? kNoSlot : (src[e] / chunk) * n_bins + bin_of_tile[v >> 6];
+        vals[e] = (uint32_t)e;
+    }
+}
+
+__global__ void k_cb_fill(const uint32_t* svals, uint64_t n_binned, const uint32_t* slot, const uint32_t* src,
+                          uint32_t* cb_slot, uint32_t* cb_src) {
+    for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n_binned;
+         p += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t e = svals[p];
+        cb_slot[p] = slot[e];
+        cb_src[p] = src[e];
+    }
+}
+
+// chunk_begin[c] = first cb position whose key >= c * n_bins (keys sorted).
+__global__ void k_chunk_bounds(const uint32_t* skeys, uint64_t n_binned, uint32_t n_bins, uint64_t n_chunks,
+                               uint64_t* chunk_begin) {
+    const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c > n_chunks) return;
+    if (c == n_chunks) {
+        chunk_begin[c] = n_binned;
+        return;
+    }
+    const uint64_t want = c * n_bins;
+    uint64_t lo = 0, hi = n_binned;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) / 2;
+        if (skeys[mid] < want) lo = mid + 1;
+        else hi = mid;
+    }
+    chunk_begin[c] = lo;
+}
+
+#define BCHECK(x)                                                         \
+    do {                                                                  \
+        hipError_t e_ = (x);                                              \
+        if (e_ != hipSuccess) {                                           \
+            if (err) *err = std::string(#x ": ") + hipGetErrorString(e_); \
+            rc = e_;                                                      \
+            goto done;                                                    \
+        }                                                                 \
+    } while (0)
+
+}  // namespace
+
+void free_bins(BinState* b) {
+    hipFree(b->bins);
+    hipFree(b->cb_slot);
+    hipFree(b->cb_src);
+    hipFree(b->chunk_begin);
+    hipFree(b->bdst);
+    hipFree(b->val);
+    *b = BinState{};
+}
+
+hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n, uint64_t m, uint32_t heavy, uint32_t Wp,
+                      hipStream_t s, BinState* out, std::string* err) {
+    hipError_t rc = hipSuccess;
+    const uint64_t n_tiles = (n + 63) / 64;
+    const uint32_t max_peers = kBinWords / Wp;  // a multiple of 64 for Wp <= 8
+    uint32_t* tile_slots = nullptr;
+    unsigned long long* light_bits = nullptr;
+    uint32_t* bin_of_tile = nullptr;
+    uint32_t *keys_in = nullptr, *vals_in = nullptr, *keys_out = nullptr, *vals_out = nullptr;
+    uint32_t *slot = nullptr, *src = nullptr;
+    uint64_t chunk_words = kBinChunkWords;
+    if (const char* c = std::getenv("GOSSIP_BIN_CHUNK")) chunk_words = std::max<uint64_t>(64, std::strtoull(c, nullptr, 0));
+    const uint64_t chunk = std::max<uint64_t>(1, chunk_words / Wp);
+    const uint64_t n_chunks = (n + chunk - 1) / chunk;
+    int end_bit2 = 1;
+    void* temp = nullptr;
+    size_t temp_bytes = 0;
+    BinState st;
+    std::vector<uint32_t> h_tile(n_tiles), h_bot(n_tiles);
+    std::vector<Bin> h_bins;
+    uint64_t slots = 0, upos = 0;
+    int end_bit = 1;
+    size_t free_b = 0, total_b = 0;
+
+    if (m >= kNoSlot) {
+        if (err) *err = "too many edges for 32-bit slots";
+        return hipErrorInvalidValue;
+    }
+    BCHECK(hipMalloc((void**)&tile_slots, n_tiles * sizeof(uint32_t)));
+    BCHECK(hipMalloc((void**)&light_bits, n_tiles * sizeof(unsigned long long)));
+    hipLaunchKernelGGL(k_tile_slots, dim3(gridn(n_tiles * 64)), dim3(256), 0, s, rp, n, heavy, tile_slots, light_bits);
+    BCHECK(hipGetLastError());
+    BCHECK(hipMemcpyAsync(h_tile.data(), tile_slots, n_tiles * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    BCHECK(hipStreamSynchronize(s));
+
+    // bins: greedy runs of whole tiles
+    for (uint64_t t = 0; t < n_tiles;) {
+        Bin b{};
+        b.v0 = (uint32_t)(t * 64);
+        b.s0 = slots;
+        b.u0 = upos;
+        uint64_t cnt = 0, peers = 0;
+        while (t < n_tiles && (peers == 0 || (peers + 64 <= max_peers && cnt + h_tile[t] <= kBinSlotCap))) {
+            h_bot[t] = (uint32_t)h_bins.size();
+            cnt += h_tile[t];
+            peers += 64;
+            ++t;
+        }
+        b.v1 = (uint32_t)std::min<uint64_t>(b.v0 + peers, n);
+        upos += cnt;
+        slots += (cnt + kBinSlotPad - 1) / kBinSlotPad * kBinSlotPad;
+        b.s1 = b.s0 + cnt;
+        h_bins.push_back(b);
+    }
+    while ((1ull << end_bit) <= h_bins.size()) ++end_bit;  // keys in [0, n_bins]
+    if (n_chunks * h_bins.size() >= kNoSlot) {
+        if (err) *err = "too many (chunk, bin) pairs for 32-bit keys";
+        rc = hipErrorInvalidValue;
+        goto done;
+    }
+    while ((1ull << end_bit2) <= n_chunks * h_bins.size()) ++end_bit2;
+    // (the kNoSlot sentinel's low end_bit2 bits are all ones: it still sorts last)
+
+    // memory: peak while the cb lists are sorted (slot, src, 2 x keys, 2 x vals,
+    // temp ~ 4 B per edge) next to bdst/val
+    BCHECK(hipMemGetInfo(&free_b, &total_b));
+    {
+        const uint64_t persist = slots * 2 + slots * Wp * 8 + h_bins.size() * sizeof(Bin);
+        const uint64_t peak = m * 28 + persist + (1ull << 30);
+        if (peak > free_b) {
+            if (err) *err = "bin layout does not fit in free device memory";
+            rc = hipErrorOutOfMemory;
+            goto done;
+        }
+    }
+    BCHECK(hipMalloc((void**)&st.bins, h_bins.size() * sizeof(Bin)));
+    BCHECK(hipMemcpyAsync(st.bins, h_bins.data(), h_bins.size() * sizeof(Bin), hipMemcpyHostToDevice, s));
+    BCHECK(hipMalloc((void**)&bin_of_tile, n_tiles * sizeof(uint32_t)));
+    BCHECK(hipMemcpyAsync(bin_of_tile, h_bot.data(), n_tiles * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    BCHECK(hipMalloc((void**)&keys_in, (m + 1) * sizeof(uint32_t)));
+    BCHECK(hipMalloc((void**)&vals_in, (m + 1) * sizeof(uint32_t)));
+    BCHECK(hipMalloc((void**)&keys_out, (m + 1) * sizeof(uint32_t)));
+    BCHECK(hipMalloc((void**)&vals_out, (m + 1) * sizeof(uint32_t)));
+    hipLaunchKernelGGL(k_bin_keys, dim3(gridn(m)), dim3(256), 0, s, col, m, light_bits, bin_of_tile,
+                       (uint32_t)h_bins.size(), keys_in, vals_in);
+    BCHECK(hipGetLastError());
+    BCHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, keys_in, keys_out, vals_in, vals_out, (size_t)m, 0,
+                                              end_bit, s));
+    BCHECK(hipMalloc(&temp, temp_bytes + 16));
+    BCHECK(hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys_in, keys_out, vals_in, vals_out, (size_t)m, 0,
+                                              end_bit, s));
+    BCHECK(hipStreamSynchronize(s));
+    hipFree(keys_in);
+    hipFree(vals_in);
+    hipFree(temp);
+    keys_in = vals_in = nullptr;
+    temp = nullptr;
+
+    st.n_bins = h_bins.size();
+    st.n_slots = slots;
+    st.n_binned = upos;
+    st.n_chunks = n_chunks;
+    st.chunk = chunk;
+    BCHECK(hipMalloc((void**)&slot, (m + 1) * sizeof(uint32_t)));
+    BCHECK(hipMalloc((void**)&st.bdst, (slots + kBinSlotPad) * sizeof(uint16_t)));
+    BCHECK(hipMalloc((void**)&st.val, (slots + kBinSlotPad) * Wp * sizeof(uint64_t)));
+    BCHECK(hipMemsetAsync(st.bdst, 0, (slots + kBinSlotPad) * sizeof(uint16_t), s));
+    BCHECK(hipMemsetAsync(st.val, 0, (slots + kBinSlotPad) * Wp * sizeof(uint64_t), s));
+    hipLaunchKernelGGL(k_bin_assign, dim3(gridn(m)), dim3(256), 0, s, keys_out, vals_out, m, st.bins,
+                       (uint32_t)st.n_bins, col, slot, st.bdst);
+    BCHECK(hipGetLastError());
+
+    // cb order: (source chunk, bin, CSR)
+    BCHECK(hipMalloc((void**)&src, (m + 1) * sizeof(uint32_t)));
+    hipLaunchKernelGGL(k_edge_rows, dim3(gridn(n)), dim3(256), 0, s, rp, n, src);
+    BCHECK(hipGetLastError());
+    BCHECK(hipMalloc((void**)&keys_in, (m + 1) * sizeof(uint32_t)));
+    BCHECK(hipMalloc((void**)&vals_in, (m + 1) * sizeof(uint32_t)));
+    hipLaunchKernelGGL(k_cb_keys, dim3(gridn(m)), dim3(256), 0, s, slot, src, col, m, bin_of_tile,
+                       (uint32_t)st.n_bins, (uint32_t)chunk, keys_in, vals_in);
+    BCHECK(hipGetLastError());
+    temp_bytes = 0;
+    BCHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, keys_in, keys_out, vals_in, vals_out, (size_t)m, 0,
+                                              end_bit2, s));
+    BCHECK(hipMalloc(&temp, temp_bytes + 16));
+    BCHECK(hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys_in, keys_out, vals_in, vals_out, (size_t)m, 0,
+                                              end_bit2, s));
+    BCHECK(hipStreamSynchronize(s));
+    hipFree(keys_in);
+    hipFree(vals_in);
+    hipFree(temp);
+    keys_in = vals_in = nullptr;
+    temp = nullptr;
+    BCHECK(hipMalloc((void**)&st.cb_slot, (upos + 1) * sizeof(uint32_t)));
+    BCHECK(hipMalloc((void**)&st.cb_src, (upos + 1) * sizeof(uint32_t)));
+    BCHECK(hipMalloc((void**)&st.chunk_begin, (n_chunks + 1) * sizeof(uint64_t)));
+    hipLaunchKernelGGL(k_cb_fill, dim3(gridn(upos)), dim3(256), 0, s, vals_out, upos, slot, src, st.cb_slot,
+                       st.cb_src);
+    BCHECK(hipGetLastError());
+    hipLaunchKernelGGL(k_chunk_bounds, dim3(gridn(n_chunks + 1)), dim3(256), 0, s, keys_out, upos,
+                       (uint32_t)st.n_bins, n_chunks, st.chunk_begin);
+    BCHECK(hipGetLastError());
+    BCHECK(hipStreamSynchronize(s));
+
+done:
+    hipFree(tile_slots);
+    hipFree(light_bits);
+    hipFree(bin_of_tile);
+    hipFree(keys_in);
+    hipFree(vals_in);
+    hipFree(keys_out);
+    hipFree(vals_out);
+    hipFree(temp);
+    hipFree(slot);
+    hipFree(src);
+    if (rc != hipSuccess) {
+        hipGetLastError();  // clear a sticky allocation error
+        free_bins(&st);
+        return rc;
+    }
+    *out = st;
+    return hipSuccess;
+}
+
+}  // namespace gossip

@@ -106,6 +106,12 @@ struct gossip_ctx {
     bool cur_remote = false;
     RoundArgs cur{};
     uint64_t* gather = nullptr;  // partitioned pull: every rank's new words, indexed by global peer
+    BinState bins;               // binned dense rounds: slot layout (gossip_bins.hip)
+    bool bins_ready = false;
+    bool last_bin = false;       // the pull round in flight runs binned
+    uint32_t bin_variant = 0;    // measurement only (GOSSIP_BIN_VARIANT)
+    int bin_grid = 0;            // k_bin_scatter workgroups (0 = full chip; GOSSIP_BIN_GRID)
+    uint64_t last_fresh = 0;     // new receipts of the previous round
     uint64_t* seg = nullptr;     // sparse push: per-destination record segments (world x chunk records)
     unsigned long long* d_counts = nullptr;  // records per destination rank
     uint64_t* h_counts = nullptr;            // pinned copy
@@ -195,6 +201,8 @@ void free_state(gossip_ctx* c) {
 }
 
 void free_graph(gossip_ctx* c) {
+    free_bins(&c->bins);
+    c->bins_ready = false;
     hipFree(c->rp);
     hipFree(c->col);
     hipFree(c->chunks);
@@ -315,6 +323,20 @@ gossip_status upload_csr(gossip_ctx* c, const uint64_t* rp, const uint32_t* col,
     return install_graph(c, d_rp, d_col, m);
 }
 
+// Slot layout for binned dense rounds: only for a full, symmetric overlay
+// (pull-eligible); skipped, not failed, when it does not fit in HBM.
+gossip_status prepare_bins(gossip_ctx* c) {
+    free_bins(&c->bins);
+    c->bins_ready = false;
+    if (!c->symmetric || c->n_local != c->n || (c->cfg.flags & GOSSIP_FLAG_NO_BIN) || !c->n_edges) return GOSSIP_OK;
+    std::string err;
+    const hipError_t e = build_bins(c->rp, c->col, c->n, c->n_edges, c->heavy, c->Wp, c->stream, &c->bins, &err);
+    if (e == hipErrorOutOfMemory || e == hipErrorInvalidValue) return GOSSIP_OK;  // dense rounds gather instead
+    if (e != hipSuccess) return fail(GOSSIP_EHIP, "bin layout: " + err);
+    c->bins_ready = true;
+    return GOSSIP_OK;
+}
+
 uint32_t kills_in_round(const gossip_ctx* c, uint32_t r, uint32_t* first) {
     auto lo = std::lower_bound(c->kill_round_sorted.begin(), c->kill_round_sorted.end(), r);
     auto hi = std::upper_bound(c->kill_round_sorted.begin(), c->kill_round_sorted.end(), r);
@@ -378,8 +400,26 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
     } else {
         pull = requested == GOSSIP_MODE_PULL && pull_ok;
     }
+    // binned (single partition): every pull-eligible round when forced; in auto
+    // mode while many (peer, message) pairs are still missing -- then nearly
+    // every edge has to be looked at and streaming beats gathering.
+    bool bin = false;
+    if (!remote && pull_ok && c->bins_ready && requested == GOSSIP_MODE_AUTO) {
+        if (c->cfg.flags & GOSSIP_FLAG_FORCE_BIN) {
+            pull = bin = true;
+        } else if (pull && !(c->cfg.flags & GOSSIP_FLAG_FORCE_PULL)) {
+            uint64_t injected = 0;
+            for (int w = 0; w < kMaxWords; ++w) injected += (uint64_t)__builtin_popcountll(a.inj_mask[w]);
+            const uint64_t have = c->cum_covered + c->last_fresh + cnt;
+            const uint64_t total = injected * c->n_local;
+            const uint64_t missing = total > have ? total - have : 0;
+            const uint32_t bpm = c->cfg.bin_permille ? c->cfg.bin_permille : 4000;
+            bin = missing * 1000 >= c->n_local * (uint64_t)bpm;
+        }
+    }
     c->cur_sparse = !pull && remote && requested == GOSSIP_MODE_PUSH_SPARSE && c->seg != nullptr;
     c->last_pull = pull;
+    c->last_bin = bin;
     c->last_front = false;
     if (pull) {
         a.nw_src = c->nw;
@@ -392,7 +432,7 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
         }
         // frontier bitmap only when enough neighbours are outside the frontier to pay for the probe
         const uint32_t fpm = c->cfg.front_permille ? c->cfg.front_permille : 400;
-        if (requested == GOSSIP_MODE_AUTO && (c->frontier_est + cnt) * 1000 < c->n_local * (uint64_t)fpm) {
+        if (!bin && requested == GOSSIP_MODE_AUTO && (c->frontier_est + cnt) * 1000 < c->n_local * (uint64_t)fpm) {
             a.front = c->front;
             c->last_front = true;
         } else {
@@ -421,6 +461,14 @@ gossip_status round_compute(gossip_ctx* c) {
     RoundArgs a = c->cur;
     const uint32_t pw = pack_w(c);
     c->in_round = false;
+    if (c->last_bin) {
+        BinArgs b{c->bins.bins,        c->bins.n_bins,   c->bins.cb_slot, c->bins.cb_src, c->bins.chunk_begin,
+                  c->bins.n_chunks,    c->bins.chunk,    c->bins.bdst,    c->bins.val,     c->bin_variant};
+        HIPCHK(timed(c, "bin_scatter", [&] { return launch_bin_scatter(a, b, pw, c->bin_grid, c->stream); }));
+        HIPCHK(timed(c, "bin_apply", [&] { return launch_bin_apply(a, b, pw, c->stream); }));
+        HIPCHK(timed(c, "pull_heavy", [&] { return launch_pull_heavy(a, pw, c->stream); }));
+        return GOSSIP_OK;
+    }
     if (c->last_pull) {
         if (a.front) HIPCHK(timed(c, "frontier_bits", [&] { return launch_frontier_bits(a, pw, c->stream); }));
         // nx is written whole by pull_light; heavy rows are OR-ed in afterwards
@@ -455,8 +503,14 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
     }
     const DevStats d = c->last_st;
     c->frontier_est = d.activated;
+    c->last_fresh = d.new_receipts;
     if (c->timing) {
-        if (c->last_pull) {
+        if (c->last_bin) {
+            const double wb = 8.0 * c->Wp;
+            c->kbytes["bin_scatter"] += (16.0 + wb) * c->n_local + (8.0 + wb) * c->bins.n_binned;
+            c->kbytes["bin_apply"] += (2.0 + wb) * (double)d.pull_edges + 2.0 * wb * c->n_local;
+            c->kbytes["pull_heavy"] += 12.0 * (double)d.heavy_traversals;
+        } else if (c->last_pull) {
             if (c->last_front) c->kbytes["frontier_bits"] += 8.125 * (c->gather ? c->n : c->n_local);
             c->kbytes["pull_light"] += 40.0 * c->n_local + 4.0 * (double)d.pull_edges + 8.0 * (double)d.pull_gathers;
             c->kbytes["pull_heavy"] += 12.0 * (double)d.heavy_traversals;
@@ -551,7 +605,13 @@ gossip_status gossip_create(const gossip_config* cfg, gossip_ctx** out) {
     if (!c->cfg.graph_model) c->cfg.graph_model = GOSSIP_GRAPH_POWERLAW;
     c->device = dev;
     if (const char* u = std::getenv("GOSSIP_PULL_UNROLL")) c->pull_unroll = std::atoi(u);
+    if (const char* u = std::getenv("GOSSIP_PULL_NT"); u && std::atoi(u)) c->pull_unroll |= kPullNT;
     if (const char* h = std::getenv("GOSSIP_HEAVY_DEGREE")) c->heavy = (uint32_t)std::max(1, std::atoi(h));
+    if (const char* g = std::getenv("GOSSIP_BIN_GRID")) c->bin_grid = std::atoi(g);
+    if (const char* u = std::getenv("GOSSIP_BIN_NT"); u && std::atoi(u)) c->bin_grid |= kPullNT;
+    if (const char* u = std::getenv("GOSSIP_BIN_U8"); u && std::atoi(u)) c->bin_grid |= kBinU8;
+    if (const char* u = std::getenv("GOSSIP_BIN_VARIANT")) c->bin_variant = (uint32_t)std::atoi(u);
+    if (const char* b = std::getenv("GOSSIP_BIN_PERMILLE"); b && !cfg->bin_permille) c->cfg.bin_permille = (uint32_t)std::atoi(b);
     c->n = cfg->n_peers;
     c->begin = b;
     c->end = e;
@@ -650,7 +710,7 @@ gossip_status gossip_build_graph(gossip_ctx* c) {
         return fail(GOSSIP_EHIP, "overlay generator: " + err);
     gossip_status st = install_graph(c, rp, col, m);
     c->symmetric = true;  // powerlaw overlay is symmetrised by construction
-    return st;
+    return st ? st : prepare_bins(c);
 }
 
 gossip_status gossip_load_csr(gossip_ctx* c, const uint64_t* rp, const uint32_t* col, uint64_t n_rows,
@@ -677,7 +737,7 @@ gossip_status gossip_load_csr(gossip_ctx* c, const uint64_t* rp, const uint32_t*
     if (set_dev(c)) return GOSSIP_EHIP;
     gossip_status st = upload_csr(c, rp, col, n_edges);
     c->symmetric = sym;
-    return st;
+    return st ? st : prepare_bins(c);
 }
 
 gossip_status gossip_read_csr(gossip_ctx* c, uint64_t* rp, uint32_t* col) {
@@ -796,6 +856,8 @@ gossip_status gossip_reset(gossip_ctx* c) {
     c->any_masked = false;
     c->nx_dirty = false;
     c->last_pull = false;
+    c->last_bin = false;
+    c->last_fresh = 0;
     c->frontier_est = 0;
     c->round = 0;
     c->finished = false;

@@ -13,6 +13,8 @@ constexpr uint32_t kHeavyChunk = 1024;         // edges per heavy chunk (one wav
 constexpr int kBlock = 256;                    // 4 waves of 64
 constexpr int kMaxWords = 8;                   // M <= 512 concurrent messages
 constexpr int kStatLines = 64;                 // striped DevStats lines per round (summed at read)
+constexpr int kPullNT = 0x100;                 // launch_pull_light unroll flag: non-temporal streamed accesses
+constexpr int kBinU8 = 0x200;                  // launch_bin_scatter grid flag: 8 entries in flight per lane
 
 // Per-round device counters (all integer; order-independent sums).
 struct DevStats {
@@ -25,6 +27,44 @@ struct HeavyChunk {
     uint32_t v;    // local row
     uint32_t pad;
     uint64_t e0, e1;
+};
+
+// Binned dense rounds (layout in gossip_bins.hip).
+constexpr uint32_t kBinWords = 8192;        // LDS accumulator words per bin (64 KB)
+constexpr uint32_t kBinSlotPad = 8;         // bin slot ranges padded to 8 slots (16-B loads)
+constexpr uint64_t kBinSlotCap = 1u << 17;  // slots per bin (load balance between bins)
+constexpr uint32_t kBinChunkWords = 1u << 18;  // source chunk: its new words (2 MB) stay in one XCD's L2
+constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
+
+struct Bin {
+    uint32_t v0, v1;  // destination peers [v0, v1) (local ids, whole 64-peer tiles)
+    uint64_t s0, s1;  // padded slot range
+    uint64_t u0;      // first position of this bin in the unpadded (sorted) order
+};
+
+struct BinArgs {
+    const Bin* bins;
+    uint64_t n_bins;
+    const uint32_t* cb_slot;      // per binned edge, chunk-major order: its slot
+    const uint32_t* cb_src;       // per binned edge, chunk-major order: its source peer (local)
+    const uint64_t* chunk_begin;  // n_chunks + 1 offsets into cb_*
+    uint64_t n_chunks, chunk;     // source chunks of `chunk` peers
+    const uint16_t* bdst;         // per slot: destination - bin.v0
+    uint64_t* val;                // per slot: Wp words, the source's new words of this round
+    uint32_t variant;             // measurement only (GOSSIP_BIN_VARIANT): 1 = skip stores, 2 = skip gathers
+};
+
+struct BinState {
+    Bin* bins = nullptr;
+    uint64_t n_bins = 0;
+    uint32_t* cb_slot = nullptr;
+    uint32_t* cb_src = nullptr;
+    uint64_t* chunk_begin = nullptr;
+    uint64_t n_chunks = 0, chunk = 0;
+    uint16_t* bdst = nullptr;
+    uint64_t* val = nullptr;
+    uint64_t n_slots = 0;   // padded
+    uint64_t n_binned = 0;  // edges with a slot (light destinations)
 };
 
 struct DeadReport {
@@ -76,6 +116,8 @@ hipError_t launch_apply_remote(const RoundArgs& a, uint32_t W, const uint64_t* r
 hipError_t launch_compact_send(const RoundArgs& a, uint32_t W, uint64_t chunk, unsigned long long* counts,
                                uint64_t* seg, hipStream_t s);
 hipError_t launch_apply_records(const RoundArgs& a, uint32_t W, const uint64_t* rec, uint64_t n_rec, hipStream_t s);
+hipError_t launch_bin_scatter(const RoundArgs& a, const BinArgs& b, uint32_t W, int grid, hipStream_t s);
+hipError_t launch_bin_apply(const RoundArgs& a, const BinArgs& b, uint32_t W, hipStream_t s);
 hipError_t launch_coverage(const uint64_t* words, uint64_t n_local, uint32_t W, unsigned long long* counts,
                            hipStream_t s);
 hipError_t launch_heavy_count(const uint64_t* rp, uint64_t n_local, uint32_t heavy, unsigned long long* n_chunks,
@@ -88,6 +130,14 @@ hipError_t launch_heavy_fill(const uint64_t* rp, uint64_t n_local, uint32_t heav
 // *rp (n_local+1) and *col (n_edges) are device allocations owned by the caller.
 hipError_t build_powerlaw_device(uint64_t n_global, uint64_t begin, uint64_t end, uint32_t list_len, uint32_t seed,
                                  uint64_t** rp, uint32_t** col, uint64_t* n_edges, hipStream_t s, std::string* err);
+
+// ---- bin layout (gossip_bins.hip) ----
+// Lays out the light-destination edges of a full (n_local == n) symmetric
+// overlay bin-major.  Returns hipErrorOutOfMemory (state untouched) when the
+// layout does not fit next to what is already resident.
+hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n, uint64_t n_edges, uint32_t heavy,
+                      uint32_t Wp, hipStream_t s, BinState* out, std::string* err);
+void free_bins(BinState* b);
 
 // Exact integer threshold ceil(2^32 (j/L)^2.5) (host only).
 uint64_t pick_threshold(uint32_t j, uint32_t L);

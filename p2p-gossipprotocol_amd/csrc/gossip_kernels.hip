@@ -269,7 +269,20 @@ __device__ __forceinline__ int src_lane(uint32_t incl, uint32_t p) {
     return s;
 }
 
-template <int W, bool COV, bool FRONT, int kPullUnroll>  // kPullUnroll: 64-edge batches in flight per wave
+// Streamed (touched-once) loads/stores of a pull round; NT marks them
+// non-temporal so they do not push the gathered new words out of L2/MALL.
+template <bool NT, class T>
+__device__ __forceinline__ T ld_s(const T* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <bool NT, class T>
+__device__ __forceinline__ void st_s(T* p, T v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+template <int W, bool COV, bool FRONT, int kPullUnroll, bool NT>  // kPullUnroll: 64-edge batches in flight per wave
 __global__ __launch_bounds__(kBlock) void k_pull_light(RoundArgs a, uint32_t wd) {
     __shared__ unsigned int cov_s[COV ? 64 * W : 1];
     __shared__ unsigned long long acc_s[kWavesPerBlock][64 * W];
@@ -289,8 +302,8 @@ __global__ __launch_bounds__(kBlock) void k_pull_light(RoundArgs a, uint32_t wd)
         bool act = false, needy = false;
 #pragma unroll
         for (int w = 0; w < W; ++w) {
-            m[w] = vv ? a.nw[v * W + w] : 0ull;
-            sv[w] = vv ? a.seen[v * W + w] : ~0ull;
+            m[w] = vv ? ld_s<NT>(a.nw + v * W + w) : 0ull;
+            sv[w] = vv ? ld_s<NT>(a.seen + v * W + w) : ~0ull;
             need[w] = a.inj_mask[w] & ~sv[w];
             act |= m[w] != 0;
             needy |= need[w] != 0;
@@ -298,13 +311,13 @@ __global__ __launch_bounds__(kBlock) void k_pull_light(RoundArgs a, uint32_t wd)
         if (!__any(act || needy)) {
             if (vv)
 #pragma unroll
-                for (int w = 0; w < W; ++w) a.nx[v * W + w] = 0ull;  // nx is written whole in a pull round
+                for (int w = 0; w < W; ++w) st_s<NT>(a.nx + v * W + w, (uint64_t)0);  // nx is written whole in a pull round
             continue;
         }
         uint64_t rb = 0, d = 0;
         if (vv) {
-            rb = a.rp[v];
-            d = a.rp[v + 1] - rb;
+            rb = ld_s<NT>(a.rp + v);
+            d = ld_s<NT>(a.rp + v + 1) - rb;
         }
         if (act) {  // source side of this peer's pushes (broadcastMessage, peer.cpp:310-316)
             uint32_t pc = 0;
@@ -354,7 +367,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_light(RoundArgs a, uint32_t wd)
             // phase 2..4: independent loads, kPullUnroll deep
             uint32_t u[kPullUnroll];
 #pragma unroll
-            for (int j = 0; j < kPullUnroll; ++j) u[j] = (ok >> j) & 1 ? a.col[e[j]] : 0u;
+            for (int j = 0; j < kPullUnroll; ++j) u[j] = (ok >> j) & 1 ? ld_s<NT>(a.col + e[j]) : 0u;
             acc.pulled += (unsigned)__builtin_popcount(ok);
             if (FRONT) {
                 uint64_t fb[kPullUnroll];
@@ -387,11 +400,11 @@ __global__ __launch_bounds__(kBlock) void k_pull_light(RoundArgs a, uint32_t wd)
             for (int w = 0; w < W; ++w) {
                 const uint64_t fr = light ? (my[lane * W + w] & need[w]) : 0ull;
                 if (fr) {  // handleClient: new -> Message-List insert (peer.cpp:281-282)
-                    a.seen[v * W + w] = sv[w] | fr;
+                    st_s<NT>(a.seen + v * W + w, sv[w] | fr);
                     acc.fresh += (unsigned long long)__popcll(fr);
                     acc.activated++;
                 }
-                a.nx[v * W + w] = fr;  // heavy rows: 0 here, OR-ed by k_pull_heavy afterwards
+                st_s<NT>(a.nx + v * W + w, fr);  // heavy rows: 0 here, OR-ed by k_pull_heavy afterwards
             }
         }
     }
@@ -451,6 +464,148 @@ __global__ __launch_bounds__(kBlock) void k_pull_heavy(RoundArgs a) {
     }
     acc.htrav = acc.pulled;  // heavy-row edges scanned
     acc.pulled = 0;
+    flush(acc, a.st);
+}
+
+// ---------------------------------------------------------------------------
+// binned dense rounds (layout: gossip_bins.hip).  Same round contract and the
+// same source-side accounting as pull: every peer v ends with
+// next[v] = (OR of new[u] over u in N(v)) & ~seen[v]; heavy destinations are
+// left to k_pull_heavy.
+// ---------------------------------------------------------------------------
+// Phase 1: every binned edge's slot receives its source's new words (frontier
+// or not -- the slots are rewritten whole, so no state survives between binned
+// rounds).  XCD-aware: workgroups are dispatched round-robin over the 8 XCDs
+// (blockIdx % 8); XCD x sweeps the contiguous eighth [x N/8, (x+1) N/8) of the
+// cb entries (balanced by edges, not peers: the hub chunks hold most edges)
+// with all its workgroups abreast, so at any time it gathers from one or two
+// source chunks (2 MB of new words each) held in its L2, while the cb order
+// turns the slot writes into runs.  The same pass books the source-side stats
+// of the XCD's eighth of the peers.
+template <int W, bool COV, bool NT, int kU>  // kU: cb entries in flight per lane
+__global__ __launch_bounds__(kBlock) void k_bin_scatter(RoundArgs a, BinArgs b, uint32_t wd) {
+    __shared__ unsigned int cov_s[COV ? 64 * W : 1];
+    if (COV) {
+        for (int i = threadIdx.x; i < 64 * W; i += kBlock) cov_s[i] = 0;
+        __syncthreads();
+    }
+    Acc acc;
+    const uint32_t xcd = blockIdx.x & 7, part = blockIdx.x >> 3, parts = gridDim.x >> 3;
+    // source side of the pushes (broadcastMessage, peer.cpp:310-316)
+    {
+        const uint64_t v0 = a.n_local * xcd / 8, v1 = a.n_local * (xcd + 1) / 8;
+        for (uint64_t v = v0 + (uint64_t)part * kBlock + threadIdx.x; v < v1; v += (uint64_t)parts * kBlock) {
+            uint32_t pc = 0;
+            bool act = false;
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                const uint64_t m = a.nw[v * W + w];
+                if (!m) continue;
+                act = true;
+                pc += (uint32_t)__popcll(m);
+                if (w < (int)wd) acc.digest += digest_weight((a.begin + v) * wd + w) * m;
+                if (COV)
+                    for (uint64_t x = m; x; x &= x - 1) atomicAdd(&cov_s[w * 64 + __builtin_ctzll(x)], 1u);
+            }
+            if (act) {
+                const uint64_t d = a.rp[v + 1] - a.rp[v];
+                acc.frontier++;
+                acc.covered += pc;
+                acc.trav += d;
+                acc.deliv += (unsigned long long)pc * d;
+            }
+        }
+    }
+    const uint64_t N = b.chunk_begin[b.n_chunks];
+    const uint64_t x0 = N * xcd / 8, x1 = N * (xcd + 1) / 8;
+    for (uint64_t p = x0 + (uint64_t)part * kBlock * kU + threadIdx.x; p < x1; p += (uint64_t)parts * kBlock * kU) {
+        uint32_t sl[kU], u[kU];
+#pragma unroll
+        for (int j = 0; j < kU; ++j) {
+            const uint64_t q = p + (uint64_t)j * kBlock;
+            sl[j] = q < x1 ? ld_s<NT>(b.cb_slot + q) : kNoSlot;
+            u[j] = q < x1 ? ld_s<NT>(b.cb_src + q) : 0u;
+        }
+        uint64_t x[kU][W];
+#pragma unroll
+        for (int j = 0; j < kU; ++j)
+#pragma unroll
+            for (int w = 0; w < W; ++w)
+                x[j][w] = sl[j] != kNoSlot ? (b.variant == 2 ? (uint64_t)u[j] : a.nw[(uint64_t)u[j] * W + w]) : 0ull;
+        if (b.variant == 1) {
+            uint64_t z = 0;
+#pragma unroll
+            for (int j = 0; j < kU; ++j) z |= x[j][0];
+            if (z == 0x123456789ull) b.val[0] = z;
+            continue;
+        }
+#pragma unroll
+        for (int j = 0; j < kU; ++j)
+            if (sl[j] != kNoSlot)
+#pragma unroll
+                for (int w = 0; w < W; ++w) st_s<NT>(b.val + (uint64_t)sl[j] * W + w, x[j][w]);
+    }
+    flush(acc, a.st);
+    if (COV) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < 64 * W; i += kBlock)
+            if (cov_s[i]) atomicAdd(&a.cov[i], (unsigned long long)cov_s[i]);
+    }
+}
+
+// Phase 2: one workgroup per bin folds the bin's slots into an LDS
+// accumulator (ds_or_b64), then applies handleClient's test-and-set to the
+// bin's peers with plain stores.  A bin none of whose peers can still learn
+// anything skips its slots.
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_bin_apply(RoundArgs a, BinArgs b) {
+    __shared__ unsigned long long acc_s[kBinWords];
+    Acc acc;
+    const Bin bn = b.bins[blockIdx.x];
+    const uint32_t nv = bn.v1 - bn.v0;
+    const uint64_t v0 = bn.v0;
+    bool needy = false;
+    for (uint32_t i = threadIdx.x; i < nv * W; i += kBlock) {
+        acc_s[i] = 0ull;
+        needy |= (a.inj_mask[i % W] & ~a.seen[v0 * W + i]) != 0;
+    }
+    if (!__syncthreads_or(needy)) {
+        for (uint32_t i = threadIdx.x; i < nv * W; i += kBlock) a.nx[v0 * W + i] = 0ull;
+        flush(acc, a.st);
+        return;
+    }
+    if (threadIdx.x == 0) acc.pulled = bn.s1 - bn.s0;  // slots scanned (byte accounting)
+    // 8 slots per lane per step: 16 B of bdst, 64*W B of val
+    for (uint64_t i = bn.s0 + (uint64_t)threadIdx.x * 8; i < bn.s1; i += (uint64_t)kBlock * 8) {
+        const uint4 dd = *reinterpret_cast<const uint4*>(b.bdst + i);
+        uint64_t x[8 * W];
+        const uint4* vp = reinterpret_cast<const uint4*>(b.val + i * W);
+#pragma unroll
+        for (int q = 0; q < 4 * W; ++q) {
+            const uint4 y = vp[q];
+            x[2 * q] = ((uint64_t)y.y << 32) | y.x;
+            x[2 * q + 1] = ((uint64_t)y.w << 32) | y.z;
+        }
+        const uint32_t dw[4] = {dd.x, dd.y, dd.z, dd.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t dl = (dw[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
+#pragma unroll
+            for (int w = 0; w < W; ++w)
+                if (x[k * W + w]) atomicOr(&acc_s[dl * W + w], (unsigned long long)x[k * W + w]);
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nv * W; i += kBlock) {
+        const uint64_t sv = a.seen[v0 * W + i];
+        const uint64_t fr = acc_s[i] & a.inj_mask[i % W] & ~sv;
+        if (fr) {  // handleClient: new -> Message-List insert (peer.cpp:281-282)
+            a.seen[v0 * W + i] = sv | fr;
+            acc.fresh += (unsigned long long)__popcll(fr);
+            acc.activated++;
+        }
+        a.nx[v0 * W + i] = fr;  // heavy rows: 0 here, OR-ed by k_pull_heavy afterwards
+    }
     flush(acc, a.st);
 }
 
@@ -860,17 +1015,25 @@ hipError_t launch_pull_light(const RoundArgs& a, uint32_t W_, int unroll, hipStr
     const uint64_t tiles = (a.n_local + 63) / 64;
     const unsigned g = grid_for(tiles, kWavesPerBlock);
     const uint32_t wd = wd_of(W_);
-#define GOSSIP_PULL(COV, FR)                                                                                 \
-    do {                                                                                                     \
-        if (unroll >= 4) hipLaunchKernelGGL((k_pull_light<W, COV, FR, 4>), dim3(g), dim3(kBlock), 0, s, a, wd); \
-        else if (unroll == 2) hipLaunchKernelGGL((k_pull_light<W, COV, FR, 2>), dim3(g), dim3(kBlock), 0, s, a, wd); \
-        else hipLaunchKernelGGL((k_pull_light<W, COV, FR, 1>), dim3(g), dim3(kBlock), 0, s, a, wd);          \
+    const bool nt = (unroll & kPullNT) != 0;
+    unroll &= ~kPullNT;
+#define GOSSIP_PULL_U(COV, FR, U)                                                                               \
+    do {                                                                                                        \
+        if (nt) hipLaunchKernelGGL((k_pull_light<W, COV, FR, U, true>), dim3(g), dim3(kBlock), 0, s, a, wd);    \
+        else hipLaunchKernelGGL((k_pull_light<W, COV, FR, U, false>), dim3(g), dim3(kBlock), 0, s, a, wd);      \
+    } while (0)
+#define GOSSIP_PULL(COV, FR)                                  \
+    do {                                                      \
+        if (unroll >= 4) GOSSIP_PULL_U(COV, FR, 4);           \
+        else if (unroll == 2) GOSSIP_PULL_U(COV, FR, 2);      \
+        else GOSSIP_PULL_U(COV, FR, 1);                       \
     } while (0)
     GOSSIP_DISPATCH_W(wp_of(W_), {
         if (a.cov) { if (a.front) GOSSIP_PULL(true, true); else GOSSIP_PULL(true, false); }
         else { if (a.front) GOSSIP_PULL(false, true); else GOSSIP_PULL(false, false); }
     });
 #undef GOSSIP_PULL
+#undef GOSSIP_PULL_U
     return hipGetLastError();
 }
 
@@ -901,6 +1064,29 @@ hipError_t launch_apply_records(const RoundArgs& a, uint32_t W_, const uint64_t*
     if (!n_rec) return hipSuccess;
     GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_apply_records<W>, dim3(grid_for(n_rec, kBlock)), dim3(kBlock),
                                                    0, s, a, rec, n_rec));
+    return hipGetLastError();
+}
+
+hipError_t launch_bin_scatter(const RoundArgs& a, const BinArgs& b, uint32_t W_, int grid, hipStream_t s) {
+    const int gg = grid & ~(kPullNT | kBinU8);
+    unsigned g = gg > 0 ? (unsigned)gg : 512u;  // 2 workgroups per CU: fewer abreast = fewer L2 slices in use
+    g = (g + 7) / 8 * 8;  // the XCD-aware walk needs a multiple of 8 workgroups
+    const uint32_t wd = wd_of(W_);
+    const bool nt = (grid & kPullNT) != 0;
+    const bool u8 = (grid & kBinU8) != 0;
+    GOSSIP_DISPATCH_W(wp_of(W_), {
+        if (a.cov) hipLaunchKernelGGL((k_bin_scatter<W, true, false, 4>), dim3(g), dim3(kBlock), 0, s, a, b, wd);
+        else if (nt) hipLaunchKernelGGL((k_bin_scatter<W, false, true, 4>), dim3(g), dim3(kBlock), 0, s, a, b, wd);
+        else if (u8) hipLaunchKernelGGL((k_bin_scatter<W, false, false, 8>), dim3(g), dim3(kBlock), 0, s, a, b, wd);
+        else hipLaunchKernelGGL((k_bin_scatter<W, false, false, 4>), dim3(g), dim3(kBlock), 0, s, a, b, wd);
+    });
+    return hipGetLastError();
+}
+
+hipError_t launch_bin_apply(const RoundArgs& a, const BinArgs& b, uint32_t W_, hipStream_t s) {
+    if (!b.n_bins) return hipSuccess;
+    GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_bin_apply<W>, dim3((unsigned)b.n_bins), dim3(kBlock), 0, s, a,
+                                                   b));
     return hipGetLastError();
 }
 

@@ -27,6 +27,8 @@ GRAPH_REF_BOOTSTRAP = 2
 FLAG_COVERAGE_HISTORY = 1
 FLAG_FORCE_PUSH = 2
 FLAG_FORCE_PULL = 4
+FLAG_NO_BIN = 8
+FLAG_FORCE_BIN = 16
 MODE_AUTO = -1
 MODE_PUSH = 0
 MODE_PULL = 1
@@ -53,6 +55,8 @@ class GossipConfig(C.Structure):
         ("report_capacity", C.c_uint64),
         ("pull_permille", C.c_uint32),
         ("front_permille", C.c_uint32),
+        ("bin_permille", C.c_uint32),
+        ("reserved0", C.c_uint32),
     ]
 
 

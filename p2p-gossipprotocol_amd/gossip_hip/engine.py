@@ -16,7 +16,8 @@ from . import _abi
 from ._abi import DeadReport, GossipConfig, RoundStats, check
 
 _GRAPHS = {"powerlaw": _abi.GRAPH_POWERLAW, "ref_bootstrap": _abi.GRAPH_REF_BOOTSTRAP}
-KERNELS = ("push_light", "push_heavy", "frontier_bits", "pull_light", "pull_heavy", "liveness", "churn", "kills",
+KERNELS = ("push_light", "push_heavy", "frontier_bits", "pull_light", "pull_heavy", "bin_scatter", "bin_apply",
+           "liveness", "churn", "kills",
            "inject", "apply_remote")
 
 
@@ -39,7 +40,7 @@ class Engine:
                  n_seeds: int = 20, churn_threshold: int = 0, ping_every: int = 0, max_missed: int = 3,
                  max_rounds: int = 4096, min_rounds: int = 0, device: int = -1, coverage_history: bool = False,
                  part: tuple[int, int] = (0, 0), report_capacity: int = 0, mode: str = "auto",
-                 pull_permille: int = 0, front_permille: int = 0):
+                 pull_permille: int = 0, front_permille: int = 0, bin_permille: int = 0, bins: bool = True):
         self._L = _abi.lib()
         cfg = GossipConfig()
         cfg.n_peers = n_peers
@@ -55,11 +56,12 @@ class Engine:
         cfg.max_rounds = max_rounds
         cfg.min_rounds = min_rounds
         cfg.device = device
-        cfg.flags = (_abi.FLAG_COVERAGE_HISTORY if coverage_history else 0) | {
-            "auto": 0, "push": _abi.FLAG_FORCE_PUSH, "pull": _abi.FLAG_FORCE_PULL}[mode]
+        cfg.flags = (_abi.FLAG_COVERAGE_HISTORY if coverage_history else 0) | (0 if bins else _abi.FLAG_NO_BIN) | {
+            "auto": 0, "push": _abi.FLAG_FORCE_PUSH, "pull": _abi.FLAG_FORCE_PULL, "bin": _abi.FLAG_FORCE_BIN}[mode]
         cfg.report_capacity = report_capacity
         cfg.pull_permille = pull_permille
         cfg.front_permille = front_permille
+        cfg.bin_permille = bin_permille
         self.cfg = cfg
         ctx = C.c_void_p()
         check(self._L.gossip_create(C.byref(cfg), C.byref(ctx)), "gossip_create")

@@ -25,7 +25,7 @@ def _hand_csr(case):
     return rp, np.array([c for r in rows for c in r], dtype=np.uint32)
 
 
-@pytest.mark.parametrize("mode", ["push", "pull"])
+@pytest.mark.parametrize("mode", ["push", "pull", "bin"])
 @pytest.mark.parametrize("case", json.loads((GOLDEN / "hand_graphs.json").read_text())["cases"],
                          ids=lambda c: c["name"])
 def test_hand_graphs(case, mode):
@@ -70,7 +70,7 @@ def _compare(e, ref, w):
     return got
 
 
-@pytest.mark.parametrize("mode", ["auto", "push", "pull"])
+@pytest.mark.parametrize("mode", ["auto", "push", "pull", "bin"])
 @pytest.mark.parametrize("idx,n", [(1, None), (2, 1 << 16), (3, 1 << 18), (5, 1 << 16), (5, 50_000)])
 def test_workload_parity(oracle, idx, n, mode):
     w = config(idx, n, pick=oracle.pick_origins)
@@ -87,7 +87,7 @@ def test_workload_parity(oracle, idx, n, mode):
         assert e.run() == first
 
 
-@pytest.mark.parametrize("mode", ["push", "pull"])
+@pytest.mark.parametrize("mode", ["push", "pull", "bin"])
 @pytest.mark.parametrize("M", [65, 130, 300, 512])
 def test_multiword_messages(oracle, M, mode):
     n = 1 << 14
@@ -95,7 +95,7 @@ def test_multiword_messages(oracle, M, mode):
     origins = rng.integers(0, n, M).astype(np.uint32)
     rounds = rng.integers(0, 4, M).astype(np.uint32)
     rp, col = oracle.gen("powerlaw", n, 6, 77)
-    churn = 42949673 * 2 if mode == "push" else 0   # pull rounds need a churn-free run
+    churn = 42949673 * 2 if mode == "push" else 0   # pull/binned rounds need a churn-free run
     ref = oracle.simulate(rp, col, n, M, origins, rounds, seed=77, churn_threshold=churn, ping_every=2,
                           max_missed=2)
     with Engine(n, M, rng_seed=77, churn_threshold=churn, ping_every=2, max_missed=2, mode=mode) as e:
@@ -105,9 +105,10 @@ def test_multiword_messages(oracle, M, mode):
         _compare(e, ref, None)
 
 
-def test_coverage_history_last_row_is_final(oracle):
+@pytest.mark.parametrize("mode", ["auto", "bin"])
+def test_coverage_history_last_row_is_final(oracle, mode):
     w = config(3, 1 << 14, pick=oracle.pick_origins)
-    with _engine(w, coverage_history=True) as e:
+    with _engine(w, coverage_history=True, mode=mode) as e:
         stats = run_engine(e, w)
         hist = e.coverage_history()
         assert hist.shape[0] == len(stats)
@@ -155,12 +156,14 @@ def test_full_size_properties(idx, mode):
 
 
 def test_push_equals_pull_at_full_size():
-    """config 3 at its full 2^24 peers: the direction-optimised schedule and the
-    push-only schedule produce identical rounds and seen sets."""
+    """config 3 at its full 2^24 peers: the direction-optimised schedule, the
+    gather-pull and binned schedules and the push-only schedule produce
+    identical rounds and seen sets."""
     w = config(3)
     out = {}
-    for mode in ("push", "auto"):
+    for mode in ("push", "auto", "pull", "bin"):
         with _engine(w, mode=mode) as e:
             out[mode] = (run_engine(e, w), e.read_seen())
-    assert out["push"][0] == out["auto"][0]
-    assert np.array_equal(out["push"][1], out["auto"][1])
+    for mode in ("auto", "pull", "bin"):
+        assert out["push"][0] == out[mode][0], mode
+        assert np.array_equal(out["push"][1], out[mode][1]), mode
