@@ -160,6 +160,10 @@ void free_bins(BinState* b) {
     hipFree(b->cb_slot);
     hipFree(b->cb_src);
     hipFree(b->chunk_begin);
+    hipFree(b->units);
+    hipFree(b->xcd_units);
+    hipFree(b->nz[0]);
+    hipFree(b->nz[1]);
     hipFree(b->bdst);
     hipFree(b->val);
     *b = BinState{};
@@ -308,6 +312,39 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n, uint6
                        (uint32_t)st.n_bins, n_chunks, st.chunk_begin);
     BCHECK(hipGetLastError());
     BCHECK(hipStreamSynchronize(s));
+
+    // scatter work units: chunks split into <= kBinUnitCap entries; the unit
+    // list is cut into 8 contiguous ranges of equal entry counts (one per XCD)
+    {
+        std::vector<uint64_t> cbeg(n_chunks + 1);
+        BCHECK(hipMemcpy(cbeg.data(), st.chunk_begin, (n_chunks + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost));
+        std::vector<BinUnit> units;
+        uint64_t cap = kBinUnitCap;
+        if (const char* e = std::getenv("GOSSIP_BIN_UNIT")) cap = std::max<uint64_t>(1024, std::strtoull(e, nullptr, 0));
+        for (uint64_t c = 0; c < n_chunks; ++c) {
+            const uint64_t len = cbeg[c + 1] - cbeg[c];
+            const uint64_t k = std::max<uint64_t>(1, (len + cap - 1) / cap);
+            for (uint64_t j = 0; j < k; ++j)
+                units.push_back(BinUnit{(uint32_t)c, j == 0 ? 1u : 0u, cbeg[c] + len * j / k, cbeg[c] + len * (j + 1) / k});
+        }
+        std::vector<uint64_t> xu(9, units.size());
+        xu[0] = 0;
+        uint64_t acc = 0;
+        int x = 1;
+        for (uint64_t i = 0; i < units.size() && x < 8; ++i) {
+            acc += units[i].p1 - units[i].p0;
+            while (x < 8 && acc * 8 >= upos * (uint64_t)x) xu[x++] = i + 1;
+        }
+        st.n_units = units.size();
+        BCHECK(hipMalloc((void**)&st.units, units.size() * sizeof(BinUnit)));
+        BCHECK(hipMemcpy(st.units, units.data(), units.size() * sizeof(BinUnit), hipMemcpyHostToDevice));
+        BCHECK(hipMalloc((void**)&st.xcd_units, 9 * sizeof(uint64_t)));
+        BCHECK(hipMemcpy(st.xcd_units, xu.data(), 9 * sizeof(uint64_t), hipMemcpyHostToDevice));
+        for (int k = 0; k < 2; ++k) {  // val starts zeroed: no slot holds anything yet
+            BCHECK(hipMalloc((void**)&st.nz[k], (n / 64 + 2) * sizeof(uint64_t)));
+            BCHECK(hipMemset(st.nz[k], 0, (n / 64 + 2) * sizeof(uint64_t)));
+        }
+    }
 
 done:
     hipFree(tile_slots);

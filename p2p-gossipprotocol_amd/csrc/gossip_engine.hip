@@ -109,9 +109,8 @@ struct gossip_ctx {
     BinState bins;               // binned dense rounds: slot layout (gossip_bins.hip)
     bool bins_ready = false;
     bool last_bin = false;       // the pull round in flight runs binned
-    uint32_t bin_variant = 0;    // measurement only (GOSSIP_BIN_VARIANT)
-    int bin_grid = 0;            // k_bin_scatter workgroups (0 = full chip; GOSSIP_BIN_GRID)
     uint64_t last_fresh = 0;     // new receipts of the previous round
+    bool bin_noskip = false;     // GOSSIP_BIN_NOSKIP: rewrite every slot each binned round (A/B measurement)
     uint64_t* seg = nullptr;     // sparse push: per-destination record segments (world x chunk records)
     unsigned long long* d_counts = nullptr;  // records per destination rank
     uint64_t* h_counts = nullptr;            // pinned copy
@@ -333,6 +332,8 @@ gossip_status prepare_bins(gossip_ctx* c) {
     const hipError_t e = build_bins(c->rp, c->col, c->n, c->n_edges, c->heavy, c->Wp, c->stream, &c->bins, &err);
     if (e == hipErrorOutOfMemory || e == hipErrorInvalidValue) return GOSSIP_OK;  // dense rounds gather instead
     if (e != hipSuccess) return fail(GOSSIP_EHIP, "bin layout: " + err);
+    if (c->bin_noskip)  // nz[0] stays "every slot may hold something": every slot is rewritten each round
+        HIPCHK(hipMemset(c->bins.nz[0], 0xFF, (c->n / 64 + 2) * sizeof(uint64_t)));
     c->bins_ready = true;
     return GOSSIP_OK;
 }
@@ -463,9 +464,11 @@ gossip_status round_compute(gossip_ctx* c) {
     c->in_round = false;
     if (c->last_bin) {
         BinArgs b{c->bins.bins,        c->bins.n_bins,   c->bins.cb_slot, c->bins.cb_src, c->bins.chunk_begin,
-                  c->bins.n_chunks,    c->bins.chunk,    c->bins.bdst,    c->bins.val,     c->bin_variant};
-        HIPCHK(timed(c, "bin_scatter", [&] { return launch_bin_scatter(a, b, pw, c->bin_grid, c->stream); }));
+                  c->bins.n_chunks,    c->bins.chunk,    c->bins.units,   c->bins.xcd_units, c->bins.bdst,
+                  c->bins.val,         c->bins.nz[c->bins.nz_cur], c->bins.nz[c->bins.nz_cur ^ 1]};
+        HIPCHK(timed(c, "bin_scatter", [&] { return launch_bin_scatter(a, b, pw, c->stream); }));
         HIPCHK(timed(c, "bin_apply", [&] { return launch_bin_apply(a, b, pw, c->stream); }));
+        if (!c->bin_noskip) c->bins.nz_cur ^= 1;
         HIPCHK(timed(c, "pull_heavy", [&] { return launch_pull_heavy(a, pw, c->stream); }));
         return GOSSIP_OK;
     }
@@ -507,7 +510,7 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
     if (c->timing) {
         if (c->last_bin) {
             const double wb = 8.0 * c->Wp;
-            c->kbytes["bin_scatter"] += (16.0 + wb) * c->n_local + (8.0 + wb) * c->bins.n_binned;
+            c->kbytes["bin_scatter"] += (16.0 + wb) * c->n_local + 8.0 * c->bins.n_binned + wb * (double)d.pull_gathers;
             c->kbytes["bin_apply"] += (2.0 + wb) * (double)d.pull_edges + 2.0 * wb * c->n_local;
             c->kbytes["pull_heavy"] += 12.0 * (double)d.heavy_traversals;
         } else if (c->last_pull) {
@@ -607,10 +610,7 @@ gossip_status gossip_create(const gossip_config* cfg, gossip_ctx** out) {
     if (const char* u = std::getenv("GOSSIP_PULL_UNROLL")) c->pull_unroll = std::atoi(u);
     if (const char* u = std::getenv("GOSSIP_PULL_NT"); u && std::atoi(u)) c->pull_unroll |= kPullNT;
     if (const char* h = std::getenv("GOSSIP_HEAVY_DEGREE")) c->heavy = (uint32_t)std::max(1, std::atoi(h));
-    if (const char* g = std::getenv("GOSSIP_BIN_GRID")) c->bin_grid = std::atoi(g);
-    if (const char* u = std::getenv("GOSSIP_BIN_NT"); u && std::atoi(u)) c->bin_grid |= kPullNT;
-    if (const char* u = std::getenv("GOSSIP_BIN_U8"); u && std::atoi(u)) c->bin_grid |= kBinU8;
-    if (const char* u = std::getenv("GOSSIP_BIN_VARIANT")) c->bin_variant = (uint32_t)std::atoi(u);
+    if (const char* u = std::getenv("GOSSIP_BIN_NOSKIP"); u && std::atoi(u)) c->bin_noskip = true;
     if (const char* b = std::getenv("GOSSIP_BIN_PERMILLE"); b && !cfg->bin_permille) c->cfg.bin_permille = (uint32_t)std::atoi(b);
     c->n = cfg->n_peers;
     c->begin = b;
@@ -849,6 +849,7 @@ gossip_status gossip_reset(gossip_ctx* c) {
     HIPCHK(hipMemsetAsync(c->n_reports, 0, sizeof(unsigned long long), s));
     if (c->cov_hist) HIPCHK(hipMemsetAsync(c->cov_hist, 0, (uint64_t)c->cfg.max_rounds * 64 * c->Wp * 8, s));
     if (c->miss) HIPCHK(hipMemsetAsync(c->miss, 0, c->n_edges + 1, s));
+    // the slot words survive a reset; nz[nz_cur] still says which of them are nonzero
     if (c->any_masked && c->col && c->n_edges) {
         hipLaunchKernelGGL(k_unmask, dim3(2048), dim3(256), 0, s, c->col, c->n_edges);
         HIPCHK(hipGetLastError());

@@ -14,7 +14,6 @@ constexpr int kBlock = 256;                    // 4 waves of 64
 constexpr int kMaxWords = 8;                   // M <= 512 concurrent messages
 constexpr int kStatLines = 64;                 // striped DevStats lines per round (summed at read)
 constexpr int kPullNT = 0x100;                 // launch_pull_light unroll flag: non-temporal streamed accesses
-constexpr int kBinU8 = 0x200;                  // launch_bin_scatter grid flag: 8 entries in flight per lane
 
 // Per-round device counters (all integer; order-independent sums).
 struct DevStats {
@@ -33,13 +32,20 @@ struct HeavyChunk {
 constexpr uint32_t kBinWords = 8192;        // LDS accumulator words per bin (64 KB)
 constexpr uint32_t kBinSlotPad = 8;         // bin slot ranges padded to 8 slots (16-B loads)
 constexpr uint64_t kBinSlotCap = 1u << 17;  // slots per bin (load balance between bins)
-constexpr uint32_t kBinChunkWords = 1u << 18;  // source chunk: its new words (2 MB) stay in one XCD's L2
+constexpr uint32_t kBinChunkWords = 1u << 14;  // source chunk: its new words (128 KB) are staged in LDS
+constexpr uint64_t kBinUnitCap = 1u << 16;     // cb entries per scatter work unit (hub chunks are split)
+constexpr int kScatterBlock = 1024;            // k_bin_scatter_lds: one 16-wave workgroup per CU
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 
 struct Bin {
     uint32_t v0, v1;  // destination peers [v0, v1) (local ids, whole 64-peer tiles)
     uint64_t s0, s1;  // padded slot range
     uint64_t u0;      // first position of this bin in the unpadded (sorted) order
+};
+
+struct BinUnit {        // one scatter work unit: cb entries [p0, p1) of source chunk c
+    uint32_t c, first;  // first: this unit books the chunk's source-side stats
+    uint64_t p0, p1;
 };
 
 struct BinArgs {
@@ -49,9 +55,12 @@ struct BinArgs {
     const uint32_t* cb_src;       // per binned edge, chunk-major order: its source peer (local)
     const uint64_t* chunk_begin;  // n_chunks + 1 offsets into cb_*
     uint64_t n_chunks, chunk;     // source chunks of `chunk` peers
+    const BinUnit* units;         // scatter work units, in chunk order
+    const uint64_t* xcd_units;    // 9 offsets: XCD x sweeps units [xcd_units[x], xcd_units[x+1])
     const uint16_t* bdst;         // per slot: destination - bin.v0
     uint64_t* val;                // per slot: Wp words, the source's new words of this round
-    uint32_t variant;             // measurement only (GOSSIP_BIN_VARIANT): 1 = skip stores, 2 = skip gathers
+    const uint64_t* nz_prev;      // per source bit: its slots hold nonzero words (previous binned round)
+    uint64_t* nz_next;            // the same bits for this round's words
 };
 
 struct BinState {
@@ -61,8 +70,13 @@ struct BinState {
     uint32_t* cb_src = nullptr;
     uint64_t* chunk_begin = nullptr;
     uint64_t n_chunks = 0, chunk = 0;
+    BinUnit* units = nullptr;
+    uint64_t* xcd_units = nullptr;
+    uint64_t n_units = 0;
     uint16_t* bdst = nullptr;
     uint64_t* val = nullptr;
+    uint64_t* nz[2] = {nullptr, nullptr};  // per-source "slots hold nonzero" bits; nz[nz_cur] = previous round
+    int nz_cur = 0;
     uint64_t n_slots = 0;   // padded
     uint64_t n_binned = 0;  // edges with a slot (light destinations)
 };
@@ -116,7 +130,7 @@ hipError_t launch_apply_remote(const RoundArgs& a, uint32_t W, const uint64_t* r
 hipError_t launch_compact_send(const RoundArgs& a, uint32_t W, uint64_t chunk, unsigned long long* counts,
                                uint64_t* seg, hipStream_t s);
 hipError_t launch_apply_records(const RoundArgs& a, uint32_t W, const uint64_t* rec, uint64_t n_rec, hipStream_t s);
-hipError_t launch_bin_scatter(const RoundArgs& a, const BinArgs& b, uint32_t W, int grid, hipStream_t s);
+hipError_t launch_bin_scatter(const RoundArgs& a, const BinArgs& b, uint32_t W, hipStream_t s);
 hipError_t launch_bin_apply(const RoundArgs& a, const BinArgs& b, uint32_t W, hipStream_t s);
 hipError_t launch_coverage(const uint64_t* words, uint64_t n_local, uint32_t W, unsigned long long* counts,
                            hipStream_t s);

@@ -49,10 +49,11 @@ struct Acc {
 // atomics serialise (~9 ns each measured); one line per round hit by every
 // wave cost ~0.65 ms per pull round at 2^20 peers.  Must be reached by every
 // wave of the block (it holds a barrier).
+template <int kWaves = kWavesPerBlock>
 __device__ __forceinline__ void flush(Acc& acc, DevStats* st) {
     constexpr int kF = 16;
     static_assert(sizeof(DevStats) == kF * 8, "one u64 per stat field");
-    __shared__ unsigned long long red[kWavesPerBlock][kF];
+    __shared__ unsigned long long red[kWaves][kF];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     // DevStats field order
     const unsigned long long v[kF] = {acc.frontier, acc.trav,     acc.deliv,   acc.undeliv, acc.fresh,  acc.injected,
@@ -67,7 +68,7 @@ __device__ __forceinline__ void flush(Acc& acc, DevStats* st) {
     if (threadIdx.x < kF) {
         unsigned long long s_ = 0;
 #pragma unroll
-        for (int w = 0; w < kWavesPerBlock; ++w) s_ += red[w][threadIdx.x];
+        for (int w = 0; w < kWaves; ++w) s_ += red[w][threadIdx.x];
         if (s_) atomicAdd(reinterpret_cast<unsigned long long*>(st + blockIdx.x % kStatLines) + threadIdx.x, s_);
     }
 }
@@ -473,82 +474,87 @@ __global__ __launch_bounds__(kBlock) void k_pull_heavy(RoundArgs a) {
 // next[v] = (OR of new[u] over u in N(v)) & ~seen[v]; heavy destinations are
 // left to k_pull_heavy.
 // ---------------------------------------------------------------------------
-// Phase 1: every binned edge's slot receives its source's new words (frontier
-// or not -- the slots are rewritten whole, so no state survives between binned
-// rounds).  XCD-aware: workgroups are dispatched round-robin over the 8 XCDs
-// (blockIdx % 8); XCD x sweeps the contiguous eighth [x N/8, (x+1) N/8) of the
-// cb entries (balanced by edges, not peers: the hub chunks hold most edges)
-// with all its workgroups abreast, so at any time it gathers from one or two
-// source chunks (2 MB of new words each) held in its L2, while the cb order
-// turns the slot writes into runs.  The same pass books the source-side stats
-// of the XCD's eighth of the peers.
-template <int W, bool COV, bool NT, int kU>  // kU: cb entries in flight per lane
-__global__ __launch_bounds__(kBlock) void k_bin_scatter(RoundArgs a, BinArgs b, uint32_t wd) {
+// Phase 1 (scatter): one 16-wave workgroup per CU stages a
+// source chunk's new words (kBinChunkWords words, 128 KB) in LDS and writes
+// them into the slots of the chunk's binned edges, walked in bin order (the cb
+// list).  The units of XCD x are a contiguous range of the chunk order, dealt
+// round-robin to its workgroups: the ~32 chunks in flight on an XCD are
+// consecutive, and their slot runs inside each bin are adjacent, so the lines
+// of a bin fill up in that XCD's L2 from several workgroups before they are
+// written back.
+template <int W, bool COV>
+__global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_lds(RoundArgs a, BinArgs b, uint32_t wd) {
+    constexpr int kWaves = kScatterBlock / 64;
+    __shared__ unsigned long long slice[kBinChunkWords];
+    // which of the chunk's sources have anything to write: nonzero new words
+    // now, or nonzero in the previous binned round (their slots still hold
+    // it).  A source with neither finds zeros in its slots and skips them.
+    __shared__ unsigned long long live_s[kBinChunkWords / 64];
     __shared__ unsigned int cov_s[COV ? 64 * W : 1];
     if (COV) {
-        for (int i = threadIdx.x; i < 64 * W; i += kBlock) cov_s[i] = 0;
-        __syncthreads();
+        for (int i = threadIdx.x; i < 64 * W; i += kScatterBlock) cov_s[i] = 0;
     }
     Acc acc;
-    const uint32_t xcd = blockIdx.x & 7, part = blockIdx.x >> 3, parts = gridDim.x >> 3;
-    // source side of the pushes (broadcastMessage, peer.cpp:310-316)
-    {
-        const uint64_t v0 = a.n_local * xcd / 8, v1 = a.n_local * (xcd + 1) / 8;
-        for (uint64_t v = v0 + (uint64_t)part * kBlock + threadIdx.x; v < v1; v += (uint64_t)parts * kBlock) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t xcd = blockIdx.x & 7, member = blockIdx.x >> 3, members = gridDim.x >> 3;
+    const uint64_t u1 = b.xcd_units[xcd + 1];
+    for (uint64_t ui = b.xcd_units[xcd] + member; ui < u1; ui += members) {
+        const BinUnit un = b.units[ui];
+        const uint64_t vb = (uint64_t)un.c * b.chunk, ve = min(vb + b.chunk, a.n_local);  // vb % 64 == 0
+        __syncthreads();  // previous unit's readers are done with the slice
+        for (uint64_t v = vb + threadIdx.x; v < ((ve + 63) & ~63ull); v += kScatterBlock) {
+            const bool vv = v < ve;
             uint32_t pc = 0;
-            bool act = false;
+            bool nz = false;
 #pragma unroll
             for (int w = 0; w < W; ++w) {
-                const uint64_t m = a.nw[v * W + w];
+                const uint64_t m = vv ? a.nw[v * W + w] : 0ull;
+                if (vv) slice[(v - vb) * W + w] = m;
                 if (!m) continue;
-                act = true;
+                nz = true;
+                if (!un.first) continue;
                 pc += (uint32_t)__popcll(m);
                 if (w < (int)wd) acc.digest += digest_weight((a.begin + v) * wd + w) * m;
                 if (COV)
                     for (uint64_t x = m; x; x &= x - 1) atomicAdd(&cov_s[w * 64 + __builtin_ctzll(x)], 1u);
             }
-            if (act) {
+            if (pc) {  // source side of this peer's pushes (broadcastMessage, peer.cpp:310-316)
                 const uint64_t d = a.rp[v + 1] - a.rp[v];
                 acc.frontier++;
                 acc.covered += pc;
                 acc.trav += d;
                 acc.deliv += (unsigned long long)pc * d;
             }
+            const unsigned long long bits = __ballot(nz);
+            if (lane == 0) {
+                const uint64_t word = v >> 6;
+                live_s[(v - vb) >> 6] = bits | b.nz_prev[word];
+                if (un.first) b.nz_next[word] = bits;
+            }
+        }
+        __syncthreads();
+        constexpr int kU = 4;
+        for (uint64_t p = un.p0 + threadIdx.x; p < un.p1; p += (uint64_t)kScatterBlock * kU) {
+            uint32_t sl[kU], u[kU];
+#pragma unroll
+            for (int j = 0; j < kU; ++j) {
+                const uint64_t q = p + (uint64_t)j * kScatterBlock;
+                sl[j] = q < un.p1 ? b.cb_slot[q] : kNoSlot;
+                u[j] = q < un.p1 ? b.cb_src[q] - (uint32_t)vb : 0u;
+            }
+#pragma unroll
+            for (int j = 0; j < kU; ++j)
+                if (sl[j] != kNoSlot && ((live_s[u[j] >> 6] >> (u[j] & 63)) & 1ull)) {
+#pragma unroll
+                    for (int w = 0; w < W; ++w) b.val[(uint64_t)sl[j] * W + w] = slice[(uint64_t)u[j] * W + w];
+                    acc.gathered++;  // slots written (byte accounting)
+                }
         }
     }
-    const uint64_t N = b.chunk_begin[b.n_chunks];
-    const uint64_t x0 = N * xcd / 8, x1 = N * (xcd + 1) / 8;
-    for (uint64_t p = x0 + (uint64_t)part * kBlock * kU + threadIdx.x; p < x1; p += (uint64_t)parts * kBlock * kU) {
-        uint32_t sl[kU], u[kU];
-#pragma unroll
-        for (int j = 0; j < kU; ++j) {
-            const uint64_t q = p + (uint64_t)j * kBlock;
-            sl[j] = q < x1 ? ld_s<NT>(b.cb_slot + q) : kNoSlot;
-            u[j] = q < x1 ? ld_s<NT>(b.cb_src + q) : 0u;
-        }
-        uint64_t x[kU][W];
-#pragma unroll
-        for (int j = 0; j < kU; ++j)
-#pragma unroll
-            for (int w = 0; w < W; ++w)
-                x[j][w] = sl[j] != kNoSlot ? (b.variant == 2 ? (uint64_t)u[j] : a.nw[(uint64_t)u[j] * W + w]) : 0ull;
-        if (b.variant == 1) {
-            uint64_t z = 0;
-#pragma unroll
-            for (int j = 0; j < kU; ++j) z |= x[j][0];
-            if (z == 0x123456789ull) b.val[0] = z;
-            continue;
-        }
-#pragma unroll
-        for (int j = 0; j < kU; ++j)
-            if (sl[j] != kNoSlot)
-#pragma unroll
-                for (int w = 0; w < W; ++w) st_s<NT>(b.val + (uint64_t)sl[j] * W + w, x[j][w]);
-    }
-    flush(acc, a.st);
+    flush<kWaves>(acc, a.st);
     if (COV) {
         __syncthreads();
-        for (int i = threadIdx.x; i < 64 * W; i += kBlock)
+        for (int i = threadIdx.x; i < 64 * W; i += kScatterBlock)
             if (cov_s[i]) atomicAdd(&a.cov[i], (unsigned long long)cov_s[i]);
     }
 }
@@ -1067,18 +1073,11 @@ hipError_t launch_apply_records(const RoundArgs& a, uint32_t W_, const uint64_t*
     return hipGetLastError();
 }
 
-hipError_t launch_bin_scatter(const RoundArgs& a, const BinArgs& b, uint32_t W_, int grid, hipStream_t s) {
-    const int gg = grid & ~(kPullNT | kBinU8);
-    unsigned g = gg > 0 ? (unsigned)gg : 512u;  // 2 workgroups per CU: fewer abreast = fewer L2 slices in use
-    g = (g + 7) / 8 * 8;  // the XCD-aware walk needs a multiple of 8 workgroups
+hipError_t launch_bin_scatter(const RoundArgs& a, const BinArgs& b, uint32_t W_, hipStream_t s) {
     const uint32_t wd = wd_of(W_);
-    const bool nt = (grid & kPullNT) != 0;
-    const bool u8 = (grid & kBinU8) != 0;
-    GOSSIP_DISPATCH_W(wp_of(W_), {
-        if (a.cov) hipLaunchKernelGGL((k_bin_scatter<W, true, false, 4>), dim3(g), dim3(kBlock), 0, s, a, b, wd);
-        else if (nt) hipLaunchKernelGGL((k_bin_scatter<W, false, true, 4>), dim3(g), dim3(kBlock), 0, s, a, b, wd);
-        else if (u8) hipLaunchKernelGGL((k_bin_scatter<W, false, false, 8>), dim3(g), dim3(kBlock), 0, s, a, b, wd);
-        else hipLaunchKernelGGL((k_bin_scatter<W, false, false, 4>), dim3(g), dim3(kBlock), 0, s, a, b, wd);
+    GOSSIP_DISPATCH_W(wp_of(W_), {  // one workgroup per CU (128 KB of LDS each)
+        if (a.cov) hipLaunchKernelGGL((k_bin_scatter_lds<W, true>), dim3(256), dim3(kScatterBlock), 0, s, a, b, wd);
+        else hipLaunchKernelGGL((k_bin_scatter_lds<W, false>), dim3(256), dim3(kScatterBlock), 0, s, a, b, wd);
     });
     return hipGetLastError();
 }

@@ -1,6 +1,7 @@
 #!/bin/bash
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-for s in "GOSSIP_BIN_GRID=512" "GOSSIP_BIN_GRID=512 GOSSIP_BIN_U8=1" "GOSSIP_BIN_GRID=512 GOSSIP_BIN_CHUNK=131072" "GOSSIP_BIN_GRID=512 GOSSIP_BIN_CHUNK=65536" "GOSSIP_BIN_GRID=1024 GOSSIP_BIN_CHUNK=65536" "GOSSIP_BIN_GRID=512 GOSSIP_BIN_CHUNK=131072 GOSSIP_BIN_VARIANT=1" "GOSSIP_BIN_GRID=512 GOSSIP_BIN_CHUNK=65536 GOSSIP_BIN_VARIANT=1" "GOSSIP_BIN_GRID=512 GOSSIP_BIN_CHUNK=65536 GOSSIP_BIN_VARIANT=2" "GOSSIP_BIN_GRID=512 GOSSIP_BIN_CHUNK=524288"; do
-  env $s timeout -k 10 120 python -u tools/bin_probe.py 4 || exit 1
-done
+mkdir -p gpurun_out/bin
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 120 --timeout-method thread -k "bin or full_size" > gpurun_out/bin/pytest.log 2>&1 || { tail -40 gpurun_out/bin/pytest.log; exit 1; }
+tail -3 gpurun_out/bin/pytest.log
+bash tools/sweep_env.sh - GOSSIP_BIN_NOSKIP=1 - GOSSIP_BIN_NOSKIP=1
