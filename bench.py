@@ -48,27 +48,42 @@ def parse():
     return ap.parse_args()
 
 
+# kernel timer name -> rocprofv3 kernel-name prefix in the PMC summary
+PMC_KERNELS = {"bin_scatter": "k_bin_scatter_lds", "bin_apply": "k_bin_apply", "pull_light": "k_pull_light",
+               "push_light": "k_push_light", "push_heavy": "k_push_heavy", "pull_heavy": "k_pull_heavy"}
+
+
 def pmc_traffic(workload: str, kernel: str, alg_bytes_per_launch: float, n_local: int):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
     (FETCH_SIZE and WRITE_SIZE, separate runs of this same command) with the
-    gfx950 corrections measured by tools/calib_fetch.hip: FETCH_SIZE counts
-    1/2 of coalesced streamed bytes and one 64-B line per random 8-B gather,
-    so traffic = fetch_counted + streamed_reads / 2 + write_counted."""
+    gfx950 corrections measured by tools/calib_fetch.hip (profiles/r01/
+    calib_fetch_timing.log): FETCH_SIZE counts 1/2 of coalesced streamed bytes
+    and one 64-B line per random 8-B gather; WRITE_SIZE counts stores 1:1.
+    bin_scatter / bin_apply read only coalesced streams (traffic = 2 x fetch +
+    write); pull_light mixes streams with random gathers (only its streamed
+    reads are doubled)."""
     path = REPO / "profiles" / "r01" / "config4_pmc_summary.json"
-    if not workload.startswith("config4") or not path.exists():
+    if not workload.startswith("config4") or not path.exists() or kernel not in PMC_KERNELS:
         return None, None
     prof = json.loads(path.read_text())
-    key = next((k for k in prof["kernels"] if k.startswith("k_" + kernel)), None)
-    if key is None or "fetch_bytes_per_launch_counted" not in prof["kernels"][key]:
+    keys = [k for k in prof["kernels"] if k.startswith(PMC_KERNELS[kernel] + "<") or k == PMC_KERNELS[kernel]]
+    keys = [k for k in keys if "fetch_bytes_per_launch_counted" in prof["kernels"][k]]
+    if not keys:
         return None, None
-    k = prof["kernels"][key]
-    if kernel == "pull_light":
+    launches = sum(prof["kernels"][k]["launches"] for k in keys)
+    fetch = sum(prof["kernels"][k]["fetch_bytes_per_launch_counted"] * prof["kernels"][k]["launches"] for k in keys)
+    write = sum(prof["kernels"][k].get("write_bytes_per_launch_counted", 0.0) * prof["kernels"][k]["launches"]
+                for k in keys)
+    fetch, write = fetch / launches, write / launches
+    if kernel in ("bin_scatter", "bin_apply"):
+        t = 2 * fetch + write
+    elif kernel == "pull_light":
         scanned = max(alg_bytes_per_launch - 40.0 * n_local, 0.0) / 12.0
-        streamed = 24.0 * n_local + 4.0 * scanned
+        t = fetch + (24.0 * n_local + 4.0 * scanned) / 2 + write
     else:
-        streamed = 0.0
-    t = k["fetch_bytes_per_launch_counted"] + streamed / 2 + k.get("write_bytes_per_launch_counted", 0.0)
-    return round(t), f"{path.relative_to(REPO)} ({key}: {k['launches']} launches, avg {k['avg_ms']:.3f} ms)"
+        t = fetch + write
+    avg = sum(prof["kernels"][k]["avg_ms"] * prof["kernels"][k]["launches"] for k in keys) / launches
+    return round(t), f"{path.relative_to(REPO)} ({', '.join(keys)}: {launches} launches, avg {avg:.3f} ms)"
 
 
 def rounds_to_full(stats: list[dict]) -> int:

@@ -415,7 +415,8 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
             const uint64_t total = injected * c->n_local;
             const uint64_t missing = total > have ? total - have : 0;
             const uint32_t bpm = c->cfg.bin_permille ? c->cfg.bin_permille : 4000;
-            bin = missing * 1000 >= c->n_local * (uint64_t)bpm;
+            // and only on a wide frontier: a narrow one is cheaper to gather from (frontier bitmap)
+            bin = missing * 1000 >= c->n_local * (uint64_t)bpm && (c->frontier_est + cnt) * 10 >= c->n_local;
         }
     }
     c->cur_sparse = !pull && remote && requested == GOSSIP_MODE_PUSH_SPARSE && c->seg != nullptr;

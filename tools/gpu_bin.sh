@@ -1,7 +1,8 @@
 #!/bin/bash
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-mkdir -p gpurun_out/bin
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 120 --timeout-method thread -k "bin or full_size" > gpurun_out/bin/pytest.log 2>&1 || { tail -40 gpurun_out/bin/pytest.log; exit 1; }
-tail -3 gpurun_out/bin/pytest.log
-bash tools/sweep_env.sh - GOSSIP_BIN_NOSKIP=1 - GOSSIP_BIN_NOSKIP=1
+bash tools/sweep_env.sh -
+BENCH_ARGS="--pull-permille 10" bash tools/sweep_env.sh - 
+BENCH_ARGS="--pull-permille 5" bash tools/sweep_env.sh - 
+BENCH_ARGS="--pull-permille 20" bash tools/sweep_env.sh - 
+BENCH_ARGS="--pull-permille 10 --front-permille 1000" bash tools/sweep_env.sh - 

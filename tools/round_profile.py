@@ -24,7 +24,9 @@ while True:
     cb = {k: e.kernel_bytes(k) for k in KERNELS}
     d = {k: round(cur[k] - prev[k], 3) for k in KERNELS if cur[k] - prev[k] > 0.001}
     gb = {k: round((cb[k] - pb[k]) / 1e9, 3) for k in KERNELS if cb[k] - pb[k] > 0}
-    print(st["round"], "F=%.3f" % (st["frontier"] / w.n), "T/E=%.3f" % (st["traversals"] / E), d, gb, flush=True)
+    print(st["round"], "F=%.3f" % (st["frontier"] / w.n), "T/E=%.3f" % (st["traversals"] / E),
+          "fresh/n=%.3f" % (st["new_receipts"] / w.n), "cov/(n*M)=%.4f" % (st["covered"] / (w.n * w.n_msgs)), d, gb,
+          flush=True)
     prev, pb = cur, cb
     if fin:
         break
