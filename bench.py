@@ -139,6 +139,8 @@ def main():
 
         from gossip_hip.distributed import PartitionedRun, partition
 
+        for k, v in (("RANK", "0"), ("WORLD_SIZE", "1"), ("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29511")):
+            os.environ.setdefault(k, v)  # --force-partitioned run without a launcher
         dist.init_process_group("nccl", device_id=dev)
         part = partition(w.n, world)
         eng = Engine(w.n, w.n_msgs, device=local, part=(part[rank], part[rank + 1]), **tune, **w.engine_kwargs())

@@ -160,7 +160,7 @@ gossip_status gossip_run(gossip_ctx* ctx, gossip_round_stats* per_round, uint32_
  *          needs blocks begins[p] = min(p*chunk, n_peers); rank p's new words at p*chunk*X
  * Per round:
  *   gossip_round_begin(mode)            churn, liveness, injection; returns the mode run
- *   PULL: all-gather(gather)            every rank's new words, before compute
+ *   PULL/BIN: all-gather(gather)        every rank's new words, before compute
  *   gossip_round_compute                push (writes send) or pull (reads gather)
  *   PUSH: all-to-all(send -> recv)
  *   PUSH_SPARSE: all-to-all(counts), all-to-all(records) -> gossip_round_finish_sparse
@@ -171,6 +171,7 @@ gossip_status gossip_run(gossip_ctx* ctx, gossip_round_stats* per_round, uint32_
 #define GOSSIP_MODE_PUSH 0
 #define GOSSIP_MODE_PULL 1
 #define GOSSIP_MODE_PUSH_SPARSE 2 /* push; only touched peers are exchanged (needs gossip_set_sparse) */
+#define GOSSIP_MODE_BIN 3         /* pull semantics (same all-gather), run binned when the slot layout exists */
 gossip_status gossip_set_exchange(gossip_ctx* ctx, void* send_dev, void* recv_dev, uint32_t world,
                                   const uint64_t* part_begins /* world+1 */);
 gossip_status gossip_set_gather(gossip_ctx* ctx, void* gather_dev);

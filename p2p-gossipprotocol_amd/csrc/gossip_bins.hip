@@ -1,33 +1,36 @@
 // gossip_bins.hip -- bootstrap-time bin layout for binned dense rounds.
 //
-// A dense round of the round contract is, per peer v,
+// A dense round of the round contract is, per owned peer v,
 //   next[v] = (OR over u in N(v) of new[u]) & ~seen[v]
 // -- handleClient's dedup (peer.cpp:277-285) applied to every copy that
 // broadcastMessage (peer.cpp:310-316) sends.  Gathering new[u] per edge costs
-// one random HBM line per edge.  The overlay is static, so instead each edge
-// u->v with a light destination v gets a fixed "slot" in a destination-bin-
-// major array: slots of bin b hold exactly the edges into b's peers, in
-// source order.  A binned round then
-//   (1) scatter: per source chunk (kBinChunkWords words of new[], one XCD's
-//       L2), walk the chunk's edges in bin order ("cb" lists) and write new[u]
-//       into their slots.  Within a (chunk, bin) pair the slots are
-//       consecutive, so the writes are runs of ~E/(chunks*bins) slots, and the
-//       new[u] reads hit the L2 (random 8-B stores beyond the caches run at
-//       ~22 G/s, L2-resident loads at ~230 G/s: tools/calib_l2.hip);
-//   (2) apply: each bin's slots are folded into an LDS accumulator (streamed).
-// Rows longer than the heavy threshold are not binned as destinations:
-// k_pull_heavy gathers them (they are satisfied after a few edges).
+// one random HBM line per edge.  The overlay is static, so instead every edge
+// into a light owned peer v gets a fixed "slot" in a destination-bin-major
+// array.  On a symmetric overlay the in-edges of v are v's own row, so the
+// layout is built from the owned rows alone: destination = the row (local),
+// source = the column (global).  That holds for one partition (P = 1) and for
+// a vertex block of a partitioned run, where the sources' words come from the
+// all-gathered buffer.  A binned round then
+//   (1) scatter (k_bin_scatter_lds): per source chunk (kBinChunkWords words,
+//       staged in LDS), walk the chunk's edges in bin order (the cb lists) and
+//       store new[src] into their slots.  Within a (chunk, bin) pair the slots
+//       are consecutive, so the stores form short runs; the runs of the chunks
+//       an XCD works on together are adjacent and merge in its L2;
+//   (2) apply (k_bin_apply): fold each bin's slots into an LDS accumulator.
+// Rows longer than the heavy threshold are not binned: k_pull_heavy gathers
+// them (they are satisfied after a few edges).
 //
 // Layout (built here, once per overlay):
 //   bins    : whole 64-peer tiles, <= kBinWords/Wp peers and <= kBinSlotCap slots
 //   bdst    : u16 per slot -> destination - bin.v0 (padding slots: 0, val 0)
-//   val     : Wp u64 per slot (rewritten whole by every binned round)
-//   cb_slot, cb_src : u32 per binned edge in (source chunk, bin, CSR) order
-//   chunk_begin     : offsets of each source chunk's cb entries
-// Construction: key = bin of the destination (heavy -> n_bins), stable radix
-// sort of (key, edge) -> slot of edge = b.s0 + (position - b.u0); then key =
-// chunk * n_bins + bin, stable sort -> cb order.  Stability keeps CSR order
-// inside every bin and every (chunk, bin) pair.
+//   val     : Wp u64 per slot (the source's words of the last binned round)
+//   cb_slot, cb_src : u32 per binned edge in (source chunk, bin) order
+//   chunk_begin     : offsets of each (global) source chunk's cb entries
+//   units, xcd_units: scatter work units and their split over the 8 XCDs
+// Construction: (a) 64-bit key (bin << 32 | source) per edge of a light row,
+// radix sort -> slot of an edge = b.s0 + (position - b.u0), so a bin's slots are
+// in source order; (b) key = chunk(source) * n_bins + bin, sort -> cb order.
+// The (chunk, bin) slots are contiguous because chunks are source ranges.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -73,20 +76,26 @@ __global__ void k_tile_slots(const uint64_t* rp, uint64_t n, uint32_t heavy, uin
     }
 }
 
-__global__ void k_bin_keys(const uint32_t* col, uint64_t m, const unsigned long long* light_bits,
-                           const uint32_t* bin_of_tile, uint32_t n_bins, uint32_t* keys, uint32_t* vals) {
+__global__ void k_edge_rows(const uint64_t* rp, uint64_t n, uint32_t* row) {
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x)
+        for (uint64_t e = rp[v]; e < rp[v + 1]; ++e) row[e] = (uint32_t)v;
+}
+
+// (a) key = bin of the (light) destination row << 32 | source; heavy rows last.
+__global__ void k_bin_keys(const uint32_t* row, const uint32_t* col, uint64_t m, const unsigned long long* light_bits,
+                           const uint32_t* bin_of_tile, unsigned long long* keys, uint32_t* vals) {
     for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t v = col[e] & ~kMaskedEdge;
+        const uint32_t v = row[e];
         const bool light = (light_bits[v >> 6] >> (v & 63)) & 1ull;
-        keys[e] = light ? bin_of_tile[v >> 6] : n_bins;
+        keys[e] = light ? ((unsigned long long)bin_of_tile[v >> 6] << 32) | (col[e] & ~kMaskedEdge) : ~0ull;
         vals[e] = (uint32_t)e;
     }
 }
 
-__global__ void k_bin_assign(const uint32_t* skeys, const uint32_t* svals, uint64_t m, const Bin* bins,
-                             uint32_t n_bins, const uint32_t* col, uint32_t* slot, uint16_t* bdst) {
+__global__ void k_bin_assign(const unsigned long long* skeys, const uint32_t* svals, uint64_t m, const Bin* bins,
+                             uint32_t n_bins, const uint32_t* row, uint32_t* slot, uint16_t* bdst) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t b = skeys[i];
+        const uint64_t b = skeys[i] >> 32;
         const uint32_t e = svals[i];
         if (b >= n_bins) {
             slot[e] = kNoSlot;
@@ -95,32 +104,28 @@ __global__ void k_bin_assign(const uint32_t* skeys, const uint32_t* svals, uint6
         const Bin bn = bins[b];
         const uint64_t pos = bn.s0 + (i - bn.u0);
         slot[e] = (uint32_t)pos;
-        bdst[pos] = (uint16_t)((col[e] & ~kMaskedEdge) - bn.v0);
+        bdst[pos] = (uint16_t)(row[e] - bn.v0);
     }
 }
 
-__global__ void k_edge_rows(const uint64_t* rp, uint64_t n, uint32_t* src) {
-    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x)
-        for (uint64_t e = rp[v]; e < rp[v + 1]; ++e) src[e] = (uint32_t)v;
-}
-
-__global__ void k_cb_keys(const uint32_t* slot, const uint32_t* src, const uint32_t* col, uint64_t m,
+// (b) key = chunk(source) * n_bins + bin(destination row); unbinned edges last.
+__global__ void k_cb_keys(const uint32_t* slot, const uint32_t* row, const uint32_t* col, uint64_t m,
                           const uint32_t* bin_of_tile, uint32_t n_bins, uint32_t chunk, uint32_t* keys,
                           uint32_t* vals) {
     for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t v = col[e] & ~kMaskedEdge;
-        keys[e] = slot[e] == kNoSlot ? kNoSlot : (src[e] / chunk) * n_bins + bin_of_tile[v >> 6];
+        const uint32_t u = col[e] & ~kMaskedEdge;
+        keys[e] = slot[e] == kNoSlot ? kNoSlot : (u / chunk) * n_bins + bin_of_tile[row[e] >> 6];
         vals[e] = (uint32_t)e;
     }
 }
 
-__global__ void k_cb_fill(const uint32_t* svals, uint64_t n_binned, const uint32_t* slot, const uint32_t* src,
+__global__ void k_cb_fill(const uint32_t* svals, uint64_t n_binned, const uint32_t* slot, const uint32_t* col,
                           uint32_t* cb_slot, uint32_t* cb_src) {
     for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n_binned;
          p += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t e = svals[p];
         cb_slot[p] = slot[e];
-        cb_src[p] = src[e];
+        cb_src[p] = col[e] & ~kMaskedEdge;
     }
 }
 
@@ -169,37 +174,38 @@ void free_bins(BinState* b) {
     *b = BinState{};
 }
 
-hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n, uint64_t m, uint32_t heavy, uint32_t Wp,
-                      hipStream_t s, BinState* out, std::string* err) {
+hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local, uint64_t n_global, uint64_t m,
+                      uint32_t heavy, uint32_t Wp, hipStream_t s, BinState* out, std::string* err) {
     hipError_t rc = hipSuccess;
-    const uint64_t n_tiles = (n + 63) / 64;
+    const uint64_t n_tiles = (n_local + 63) / 64;
     const uint32_t max_peers = kBinWords / Wp;  // a multiple of 64 for Wp <= 8
     uint32_t* tile_slots = nullptr;
     unsigned long long* light_bits = nullptr;
     uint32_t* bin_of_tile = nullptr;
+    unsigned long long *keys64_in = nullptr, *keys64_out = nullptr;
     uint32_t *keys_in = nullptr, *vals_in = nullptr, *keys_out = nullptr, *vals_out = nullptr;
-    uint32_t *slot = nullptr, *src = nullptr;
+    uint32_t *slot = nullptr, *row = nullptr;
     uint64_t chunk_words = kBinChunkWords;
     if (const char* c = std::getenv("GOSSIP_BIN_CHUNK")) chunk_words = std::max<uint64_t>(64, std::strtoull(c, nullptr, 0));
-    const uint64_t chunk = std::max<uint64_t>(1, chunk_words / Wp);
-    const uint64_t n_chunks = (n + chunk - 1) / chunk;
-    int end_bit2 = 1;
+    const uint64_t chunk = std::max<uint64_t>(64, chunk_words / Wp);
+    const uint64_t n_chunks = (n_global + chunk - 1) / chunk;
     void* temp = nullptr;
     size_t temp_bytes = 0;
     BinState st;
     std::vector<uint32_t> h_tile(n_tiles), h_bot(n_tiles);
     std::vector<Bin> h_bins;
     uint64_t slots = 0, upos = 0;
-    int end_bit = 1;
+    int end_bit = 33, end_bit2 = 1;
     size_t free_b = 0, total_b = 0;
 
-    if (m >= kNoSlot) {
+    if (m >= kNoSlot || n_global >= (1ull << 32)) {
         if (err) *err = "too many edges for 32-bit slots";
         return hipErrorInvalidValue;
     }
     BCHECK(hipMalloc((void**)&tile_slots, n_tiles * sizeof(uint32_t)));
     BCHECK(hipMalloc((void**)&light_bits, n_tiles * sizeof(unsigned long long)));
-    hipLaunchKernelGGL(k_tile_slots, dim3(gridn(n_tiles * 64)), dim3(256), 0, s, rp, n, heavy, tile_slots, light_bits);
+    hipLaunchKernelGGL(k_tile_slots, dim3(gridn(n_tiles * 64)), dim3(256), 0, s, rp, n_local, heavy, tile_slots,
+                       light_bits);
     BCHECK(hipGetLastError());
     BCHECK(hipMemcpyAsync(h_tile.data(), tile_slots, n_tiles * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     BCHECK(hipStreamSynchronize(s));
@@ -217,27 +223,26 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n, uint6
             peers += 64;
             ++t;
         }
-        b.v1 = (uint32_t)std::min<uint64_t>(b.v0 + peers, n);
+        b.v1 = (uint32_t)std::min<uint64_t>(b.v0 + peers, n_local);
         upos += cnt;
         slots += (cnt + kBinSlotPad - 1) / kBinSlotPad * kBinSlotPad;
         b.s1 = b.s0 + cnt;
         h_bins.push_back(b);
     }
-    while ((1ull << end_bit) <= h_bins.size()) ++end_bit;  // keys in [0, n_bins]
+    while ((1ull << (end_bit - 32)) <= h_bins.size()) ++end_bit;
     if (n_chunks * h_bins.size() >= kNoSlot) {
         if (err) *err = "too many (chunk, bin) pairs for 32-bit keys";
         rc = hipErrorInvalidValue;
         goto done;
     }
+    // (the kNoSlot sentinel's low end_bit2 bits are all ones: it sorts last)
     while ((1ull << end_bit2) <= n_chunks * h_bins.size()) ++end_bit2;
-    // (the kNoSlot sentinel's low end_bit2 bits are all ones: it still sorts last)
 
-    // memory: peak while the cb lists are sorted (slot, src, 2 x keys, 2 x vals,
-    // temp ~ 4 B per edge) next to bdst/val
+    // memory peak: row + slot + 64-bit keys in/out + vals in/out (+ temp) next to bdst/val
     BCHECK(hipMemGetInfo(&free_b, &total_b));
     {
-        const uint64_t persist = slots * 2 + slots * Wp * 8 + h_bins.size() * sizeof(Bin);
-        const uint64_t peak = m * 28 + persist + (1ull << 30);
+        const uint64_t persist = slots * 2 + slots * Wp * 8 + upos * 8 + h_bins.size() * sizeof(Bin);
+        const uint64_t peak = m * 36 + persist + (1ull << 30);
         if (peak > free_b) {
             if (err) *err = "bin layout does not fit in free device memory";
             rc = hipErrorOutOfMemory;
@@ -248,23 +253,27 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n, uint6
     BCHECK(hipMemcpyAsync(st.bins, h_bins.data(), h_bins.size() * sizeof(Bin), hipMemcpyHostToDevice, s));
     BCHECK(hipMalloc((void**)&bin_of_tile, n_tiles * sizeof(uint32_t)));
     BCHECK(hipMemcpyAsync(bin_of_tile, h_bot.data(), n_tiles * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-    BCHECK(hipMalloc((void**)&keys_in, (m + 1) * sizeof(uint32_t)));
-    BCHECK(hipMalloc((void**)&vals_in, (m + 1) * sizeof(uint32_t)));
-    BCHECK(hipMalloc((void**)&keys_out, (m + 1) * sizeof(uint32_t)));
-    BCHECK(hipMalloc((void**)&vals_out, (m + 1) * sizeof(uint32_t)));
-    hipLaunchKernelGGL(k_bin_keys, dim3(gridn(m)), dim3(256), 0, s, col, m, light_bits, bin_of_tile,
-                       (uint32_t)h_bins.size(), keys_in, vals_in);
+    BCHECK(hipMalloc((void**)&row, (m + 1) * sizeof(uint32_t)));
+    hipLaunchKernelGGL(k_edge_rows, dim3(gridn(n_local)), dim3(256), 0, s, rp, n_local, row);
     BCHECK(hipGetLastError());
-    BCHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, keys_in, keys_out, vals_in, vals_out, (size_t)m, 0,
-                                              end_bit, s));
+
+    // (a) slots
+    BCHECK(hipMalloc((void**)&keys64_in, (m + 1) * sizeof(unsigned long long)));
+    BCHECK(hipMalloc((void**)&keys64_out, (m + 1) * sizeof(unsigned long long)));
+    BCHECK(hipMalloc((void**)&vals_in, (m + 1) * sizeof(uint32_t)));
+    BCHECK(hipMalloc((void**)&vals_out, (m + 1) * sizeof(uint32_t)));
+    hipLaunchKernelGGL(k_bin_keys, dim3(gridn(m)), dim3(256), 0, s, row, col, m, light_bits, bin_of_tile, keys64_in,
+                       vals_in);
+    BCHECK(hipGetLastError());
+    BCHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, keys64_in, keys64_out, vals_in, vals_out, (size_t)m,
+                                              0, end_bit, s));
     BCHECK(hipMalloc(&temp, temp_bytes + 16));
-    BCHECK(hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys_in, keys_out, vals_in, vals_out, (size_t)m, 0,
+    BCHECK(hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys64_in, keys64_out, vals_in, vals_out, (size_t)m, 0,
                                               end_bit, s));
     BCHECK(hipStreamSynchronize(s));
-    hipFree(keys_in);
-    hipFree(vals_in);
+    hipFree(keys64_in);
     hipFree(temp);
-    keys_in = vals_in = nullptr;
+    keys64_in = nullptr;
     temp = nullptr;
 
     st.n_bins = h_bins.size();
@@ -277,17 +286,17 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n, uint6
     BCHECK(hipMalloc((void**)&st.val, (slots + kBinSlotPad) * Wp * sizeof(uint64_t)));
     BCHECK(hipMemsetAsync(st.bdst, 0, (slots + kBinSlotPad) * sizeof(uint16_t), s));
     BCHECK(hipMemsetAsync(st.val, 0, (slots + kBinSlotPad) * Wp * sizeof(uint64_t), s));
-    hipLaunchKernelGGL(k_bin_assign, dim3(gridn(m)), dim3(256), 0, s, keys_out, vals_out, m, st.bins,
-                       (uint32_t)st.n_bins, col, slot, st.bdst);
+    hipLaunchKernelGGL(k_bin_assign, dim3(gridn(m)), dim3(256), 0, s, keys64_out, vals_out, m, st.bins,
+                       (uint32_t)st.n_bins, row, slot, st.bdst);
     BCHECK(hipGetLastError());
+    BCHECK(hipStreamSynchronize(s));
+    hipFree(keys64_out);
+    keys64_out = nullptr;
 
-    // cb order: (source chunk, bin, CSR)
-    BCHECK(hipMalloc((void**)&src, (m + 1) * sizeof(uint32_t)));
-    hipLaunchKernelGGL(k_edge_rows, dim3(gridn(n)), dim3(256), 0, s, rp, n, src);
-    BCHECK(hipGetLastError());
+    // (b) cb order: (source chunk, bin)
     BCHECK(hipMalloc((void**)&keys_in, (m + 1) * sizeof(uint32_t)));
-    BCHECK(hipMalloc((void**)&vals_in, (m + 1) * sizeof(uint32_t)));
-    hipLaunchKernelGGL(k_cb_keys, dim3(gridn(m)), dim3(256), 0, s, slot, src, col, m, bin_of_tile,
+    BCHECK(hipMalloc((void**)&keys_out, (m + 1) * sizeof(uint32_t)));
+    hipLaunchKernelGGL(k_cb_keys, dim3(gridn(m)), dim3(256), 0, s, slot, row, col, m, bin_of_tile,
                        (uint32_t)st.n_bins, (uint32_t)chunk, keys_in, vals_in);
     BCHECK(hipGetLastError());
     temp_bytes = 0;
@@ -305,7 +314,7 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n, uint6
     BCHECK(hipMalloc((void**)&st.cb_slot, (upos + 1) * sizeof(uint32_t)));
     BCHECK(hipMalloc((void**)&st.cb_src, (upos + 1) * sizeof(uint32_t)));
     BCHECK(hipMalloc((void**)&st.chunk_begin, (n_chunks + 1) * sizeof(uint64_t)));
-    hipLaunchKernelGGL(k_cb_fill, dim3(gridn(upos)), dim3(256), 0, s, vals_out, upos, slot, src, st.cb_slot,
+    hipLaunchKernelGGL(k_cb_fill, dim3(gridn(upos)), dim3(256), 0, s, vals_out, upos, slot, col, st.cb_slot,
                        st.cb_src);
     BCHECK(hipGetLastError());
     hipLaunchKernelGGL(k_chunk_bounds, dim3(gridn(n_chunks + 1)), dim3(256), 0, s, keys_out, upos,
@@ -313,8 +322,9 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n, uint6
     BCHECK(hipGetLastError());
     BCHECK(hipStreamSynchronize(s));
 
-    // scatter work units: chunks split into <= kBinUnitCap entries; the unit
-    // list is cut into 8 contiguous ranges of equal entry counts (one per XCD)
+    // scatter work units: chunks split into <= kBinUnitCap entries (every chunk
+    // has at least one: its first unit books the chunk's source-side stats);
+    // the unit list is cut into 8 contiguous ranges of equal entry counts (one per XCD)
     {
         std::vector<uint64_t> cbeg(n_chunks + 1);
         BCHECK(hipMemcpy(cbeg.data(), st.chunk_begin, (n_chunks + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost));
@@ -341,8 +351,8 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n, uint6
         BCHECK(hipMalloc((void**)&st.xcd_units, 9 * sizeof(uint64_t)));
         BCHECK(hipMemcpy(st.xcd_units, xu.data(), 9 * sizeof(uint64_t), hipMemcpyHostToDevice));
         for (int k = 0; k < 2; ++k) {  // val starts zeroed: no slot holds anything yet
-            BCHECK(hipMalloc((void**)&st.nz[k], (n / 64 + 2) * sizeof(uint64_t)));
-            BCHECK(hipMemset(st.nz[k], 0, (n / 64 + 2) * sizeof(uint64_t)));
+            BCHECK(hipMalloc((void**)&st.nz[k], (n_global / 64 + 2) * sizeof(uint64_t)));
+            BCHECK(hipMemset(st.nz[k], 0, (n_global / 64 + 2) * sizeof(uint64_t)));
         }
     }
 
@@ -350,13 +360,15 @@ done:
     hipFree(tile_slots);
     hipFree(light_bits);
     hipFree(bin_of_tile);
+    hipFree(keys64_in);
+    hipFree(keys64_out);
     hipFree(keys_in);
     hipFree(vals_in);
     hipFree(keys_out);
     hipFree(vals_out);
     hipFree(temp);
     hipFree(slot);
-    hipFree(src);
+    hipFree(row);
     if (rc != hipSuccess) {
         hipGetLastError();  // clear a sticky allocation error
         free_bins(&st);

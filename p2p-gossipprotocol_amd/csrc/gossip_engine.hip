@@ -327,9 +327,10 @@ gossip_status upload_csr(gossip_ctx* c, const uint64_t* rp, const uint32_t* col,
 gossip_status prepare_bins(gossip_ctx* c) {
     free_bins(&c->bins);
     c->bins_ready = false;
-    if (!c->symmetric || c->n_local != c->n || (c->cfg.flags & GOSSIP_FLAG_NO_BIN) || !c->n_edges) return GOSSIP_OK;
+    if (!c->symmetric || (c->cfg.flags & GOSSIP_FLAG_NO_BIN) || !c->n_edges) return GOSSIP_OK;
     std::string err;
-    const hipError_t e = build_bins(c->rp, c->col, c->n, c->n_edges, c->heavy, c->Wp, c->stream, &c->bins, &err);
+    const hipError_t e =
+        build_bins(c->rp, c->col, c->n_local, c->n, c->n_edges, c->heavy, c->Wp, c->stream, &c->bins, &err);
     if (e == hipErrorOutOfMemory || e == hipErrorInvalidValue) return GOSSIP_OK;  // dense rounds gather instead
     if (e != hipSuccess) return fail(GOSSIP_EHIP, "bin layout: " + err);
     if (c->bin_noskip)  // nz[0] stays "every slot may hold something": every slot is rewritten each round
@@ -399,12 +400,12 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
         pull = !remote && pull_ok &&
                ((c->cfg.flags & GOSSIP_FLAG_FORCE_PULL) || (c->frontier_est + cnt) * 1000 >= c->n_local * (uint64_t)permille);
     } else {
-        pull = requested == GOSSIP_MODE_PULL && pull_ok;
+        pull = (requested == GOSSIP_MODE_PULL || requested == GOSSIP_MODE_BIN) && pull_ok;
     }
     // binned (single partition): every pull-eligible round when forced; in auto
     // mode while many (peer, message) pairs are still missing -- then nearly
     // every edge has to be looked at and streaming beats gathering.
-    bool bin = false;
+    bool bin = pull && c->bins_ready && requested == GOSSIP_MODE_BIN;  // driver-chosen (partitioned runs)
     if (!remote && pull_ok && c->bins_ready && requested == GOSSIP_MODE_AUTO) {
         if (c->cfg.flags & GOSSIP_FLAG_FORCE_BIN) {
             pull = bin = true;
@@ -452,7 +453,7 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
     c->cur = a;
     c->cur_remote = remote;
     c->in_round = true;
-    if (mode) *mode = pull ? GOSSIP_MODE_PULL : c->cur_sparse ? GOSSIP_MODE_PUSH_SPARSE : GOSSIP_MODE_PUSH;
+    if (mode) *mode = bin ? GOSSIP_MODE_BIN : pull ? GOSSIP_MODE_PULL : c->cur_sparse ? GOSSIP_MODE_PUSH_SPARSE : GOSSIP_MODE_PUSH;
     return GOSSIP_OK;
 }
 

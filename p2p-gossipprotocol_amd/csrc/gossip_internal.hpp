@@ -146,11 +146,12 @@ hipError_t build_powerlaw_device(uint64_t n_global, uint64_t begin, uint64_t end
                                  uint64_t** rp, uint32_t** col, uint64_t* n_edges, hipStream_t s, std::string* err);
 
 // ---- bin layout (gossip_bins.hip) ----
-// Lays out the light-destination edges of a full (n_local == n) symmetric
-// overlay bin-major.  Returns hipErrorOutOfMemory (state untouched) when the
-// layout does not fit next to what is already resident.
-hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n, uint64_t n_edges, uint32_t heavy,
-                      uint32_t Wp, hipStream_t s, BinState* out, std::string* err);
+// Lays out the edges into the light owned rows of a symmetric overlay
+// bin-major (P = 1, or one vertex block of a partitioned run).  Returns
+// hipErrorOutOfMemory (state untouched) when the layout does not fit next to
+// what is already resident.
+hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local, uint64_t n_global, uint64_t n_edges,
+                      uint32_t heavy, uint32_t Wp, hipStream_t s, BinState* out, std::string* err);
 void free_bins(BinState* b);
 
 // Exact integer threshold ceil(2^32 (j/L)^2.5) (host only).

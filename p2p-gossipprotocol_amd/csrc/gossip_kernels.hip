@@ -500,26 +500,29 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_lds(RoundArgs a, 
     const uint64_t u1 = b.xcd_units[xcd + 1];
     for (uint64_t ui = b.xcd_units[xcd] + member; ui < u1; ui += members) {
         const BinUnit un = b.units[ui];
-        const uint64_t vb = (uint64_t)un.c * b.chunk, ve = min(vb + b.chunk, a.n_local);  // vb % 64 == 0
+        // global source chunk; words from nw_src (own words at P = 1, the all-gathered ones at P > 1)
+        const uint64_t vb = (uint64_t)un.c * b.chunk, ve = min(vb + b.chunk, a.n_src);  // vb % 64 == 0
         __syncthreads();  // previous unit's readers are done with the slice
         for (uint64_t v = vb + threadIdx.x; v < ((ve + 63) & ~63ull); v += kScatterBlock) {
             const bool vv = v < ve;
+            const bool own = un.first && v >= a.begin && v < a.end;  // stats: owned sources, once
             uint32_t pc = 0;
             bool nz = false;
 #pragma unroll
             for (int w = 0; w < W; ++w) {
-                const uint64_t m = vv ? a.nw[v * W + w] : 0ull;
+                const uint64_t m = vv ? a.nw_src[v * W + w] : 0ull;
                 if (vv) slice[(v - vb) * W + w] = m;
                 if (!m) continue;
                 nz = true;
-                if (!un.first) continue;
+                if (!own) continue;
                 pc += (uint32_t)__popcll(m);
-                if (w < (int)wd) acc.digest += digest_weight((a.begin + v) * wd + w) * m;
+                if (w < (int)wd) acc.digest += digest_weight(v * wd + w) * m;
                 if (COV)
                     for (uint64_t x = m; x; x &= x - 1) atomicAdd(&cov_s[w * 64 + __builtin_ctzll(x)], 1u);
             }
             if (pc) {  // source side of this peer's pushes (broadcastMessage, peer.cpp:310-316)
-                const uint64_t d = a.rp[v + 1] - a.rp[v];
+                const uint64_t lv = v - a.begin;
+                const uint64_t d = a.rp[lv + 1] - a.rp[lv];
                 acc.frontier++;
                 acc.covered += pc;
                 acc.trav += d;

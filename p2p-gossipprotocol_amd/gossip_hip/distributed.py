@@ -10,10 +10,13 @@ Per round (the reference's hop broadcastMessage -> handleClient, peer.cpp:
   1. engine.round_begin(mode)  churn, liveness, injection.  The mode is chosen
                                here from the previous round's GLOBAL new-receipt
                                count, so every rank runs the same one.
-  PULL (dense rounds):
+  PULL / BIN (dense rounds):
   2. all_gather_into_tensor    every rank's new words -> one buffer indexed by
                                global peer (blocks are ceil(n/P) peers)
-  3. engine.round_compute()    each peer ORs its neighbours' words (no atomics)
+  3. engine.round_compute()    each peer ORs its neighbours' words (no atomics):
+                               BIN streams them through the rank's slot layout
+                               (wide frontier, many pairs still missing), PULL
+                               gathers them (late rounds: few needy peers)
   PUSH (sparse rounds):
   2. engine.round_compute()    local push; remote masks OR-ed into a dense
                                staging buffer indexed by global peer, then
@@ -42,7 +45,7 @@ MASK32 = (1 << 32) - 1
 MASK64 = (1 << 64) - 1
 
 
-MODE_PUSH, MODE_PULL, MODE_PUSH_SPARSE = 0, 1, 2
+MODE_PUSH, MODE_PULL, MODE_PUSH_SPARSE, MODE_BIN = 0, 1, 2, 3
 
 
 def partition(n: int, world: int) -> list[int]:
@@ -57,7 +60,8 @@ def partition(n: int, world: int) -> list[int]:
 
 class PartitionedRun:
     def __init__(self, engine, n: int, rank: int, world: int, device: torch.device, group=None,
-                 pull_permille: int = 50, pull: bool = True, sparse: bool = True, sparse_permille: int = 250):
+                 pull_permille: int = 50, pull: bool = True, sparse: bool = True, sparse_permille: int = 250,
+                 bin_permille: int = 4000, bin_front_permille: int = 100):
         self.engine = engine
         self.n, self.rank, self.world = n, rank, world
         self.device = device
@@ -88,7 +92,10 @@ class PartitionedRun:
             self.seg = torch.zeros(world * self.chunk * self.R, dtype=torch.int64, device=device)
             self.rec_in = torch.zeros(world * self.n_local * self.R, dtype=torch.int64, device=device)
             engine.set_sparse(self.seg.data_ptr())
+        self.bin_permille = bin_permille
+        self.bin_front_permille = bin_front_permille
         self.prev_new = 0
+        self.injected = 0
         self.modes = []
         self.cum_digest = 0
         self.cum_covered = 0
@@ -111,14 +118,18 @@ class PartitionedRun:
     def step(self) -> tuple[dict, bool]:
         e = self.engine
         if self.pull and self.prev_new * 1000 >= self.pull_permille * self.n:
-            want = MODE_PULL
+            # binned while the last round's receipts are wide and many (peer, message)
+            # pairs are still missing (the same rule as the single-partition engine)
+            missing = self.injected * self.n - (self.cum_covered + self.prev_new)
+            wide = self.prev_new * 1000 >= self.bin_front_permille * self.n
+            want = MODE_BIN if wide and missing * 1000 >= self.bin_permille * self.n else MODE_PULL
         elif self.sparse and self.prev_new * 1000 < self.sparse_permille * self.n:
             want = MODE_PUSH_SPARSE
         else:
             want = MODE_PUSH
         mode = e.round_begin(want)
         self.modes.append(mode)
-        if mode == MODE_PULL:
+        if mode in (MODE_PULL, MODE_BIN):
             dist.all_gather_into_tensor(self.gather, self.gather_mine, group=self.group)
             e.round_compute()
             local = e.round_finish()
@@ -131,6 +142,7 @@ class PartitionedRun:
             local = e.round_finish()
         g = self._allreduce(local)
         self.prev_new = g["new_receipts"]
+        self.injected += g["injected"]
         out = {"round": local["round"], "flags": local["flags"]}
         for f in STAT_FIELDS:
             out[f] = g.get(f, 0)
@@ -156,6 +168,7 @@ class PartitionedRun:
     def run(self, max_rounds: int = 4096) -> list[dict]:
         self.cum_digest = self.cum_covered = 0
         self.prev_new = 0
+        self.injected = 0
         self.modes = []
         rounds = []
         for _ in range(max_rounds):

@@ -157,7 +157,7 @@ class Engine:
         check(self._L.gossip_set_gather(self._ctx, C.c_void_p(gather_ptr)), "gossip_set_gather")
 
     def round_begin(self, mode: int) -> int:
-        """Phase 1 of a partitioned round; returns the mode actually run (0 push, 1 pull)."""
+        """Phase 1 of a partitioned round; returns the mode actually run (0 push, 1 pull, 2 sparse push, 3 binned)."""
         got = C.c_int()
         check(self._L.gossip_round_begin(self._ctx, mode, C.byref(got)), "gossip_round_begin")
         return got.value

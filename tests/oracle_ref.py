@@ -180,13 +180,13 @@ class OraclePartition:
         self._counts = np.zeros(self.world, dtype=np.uint64)
 
     def round_begin(self, mode):
-        self._pull = bool(self.L.oracle_part_begin(self.p, C.c_int(1 if mode == 1 else 0)))
+        self._pull = bool(self.L.oracle_part_begin(self.p, C.c_int(1 if mode in (1, 3) else 0)))
         self._sparse = (not self._pull) and mode == 2 and getattr(self, "_seg", None) is not None
         if self._pull:
             self.L.oracle_part_publish(self.p, self._gather)
         elif not self._sparse:
             C.memset(self._send, 0, self._send_words * 8)
-        return 1 if self._pull else (2 if self._sparse else 0)
+        return (3 if mode == 3 else 1) if self._pull else (2 if self._sparse else 0)
 
     def round_compute(self):
         if self._pull:

@@ -13,7 +13,7 @@ from gossip_hip.workloads import config
 pytestmark = pytest.mark.gpu
 
 
-def run_partitioned(w, P, pull=True, sparse=False):
+def run_partitioned(w, P, pull=True, sparse=False, binned=False):
     """Mirror of gossip_hip.distributed.PartitionedRun with the collectives done
     by device copies: all-gather for pull rounds, all-to-all for push rounds."""
     import torch
@@ -42,12 +42,12 @@ def run_partitioned(w, P, pull=True, sparse=False):
         e.set_sparse(segs[p].data_ptr())
     rounds, modes, dig, cov, prev_new = [], [], 0, 0, 0
     while True:
-        want = 1 if pull and prev_new * 1000 >= 50 * w.n else (2 if sparse else 0)
+        want = (3 if binned else 1) if pull and prev_new * 1000 >= 50 * w.n else (2 if sparse else 0)
         got = {e.round_begin(want) for e in engines}
         assert len(got) == 1
         mode = got.pop()
         modes.append(mode)
-        if mode == 1:   # all-gather of every block's new words
+        if mode in (1, 3):   # all-gather of every block's new words
             for q in range(P):
                 for p in range(P):
                     gathers[q][p * chunk * X:(p + 1) * chunk * X].copy_(gathers[p][p * chunk * X:(p + 1) * chunk * X])
@@ -95,16 +95,17 @@ def run_partitioned(w, P, pull=True, sparse=False):
     return rounds, seen, reps, csrs, part, modes
 
 
-@pytest.mark.parametrize("pull,sparse", [(True, True), (True, False), (False, True)])
+@pytest.mark.parametrize("pull,sparse,binned", [(True, True, False), (True, False, False), (False, True, False),
+                                               (True, True, True)])
 @pytest.mark.parametrize("P", [2, 3, 4])
 @pytest.mark.parametrize("idx,n", [(2, 1 << 15), (3, 100_000), (5, 1 << 15)])
-def test_partitioned_gpu_equals_oracle(oracle, idx, n, P, pull, sparse):
+def test_partitioned_gpu_equals_oracle(oracle, idx, n, P, pull, sparse, binned):
     w = config(idx, n, pick=oracle.pick_origins)
     rp, col = oracle.gen_workload(w)
     ref = oracle.simulate_workload(w, rp, col)
-    rounds, seen, reps, csrs, part, modes = run_partitioned(w, P, pull, sparse)
+    rounds, seen, reps, csrs, part, modes = run_partitioned(w, P, pull, sparse, binned)
     if pull and idx != 5:
-        assert 1 in modes
+        assert (3 if binned else 1) in modes
     if sparse:
         assert 2 in modes
     for p, (lrp, lcol) in enumerate(csrs):   # partitioned generator = slices of the global overlay
