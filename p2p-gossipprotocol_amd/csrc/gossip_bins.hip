@@ -24,7 +24,7 @@
 //   bins    : whole 64-peer tiles, <= kBinWords/Wp peers and <= kBinSlotCap slots
 //   bdst    : u16 per slot -> destination - bin.v0 (padding slots: 0, val 0)
 //   val     : Wp u64 per slot (the source's words of the last binned round)
-//   cb_slot, cb_src : u32 per binned edge in (source chunk, bin) order
+//   cb_slot, cb_src : u32 slot / u16 chunk-local source per binned edge, (source chunk, bin) order
 //   chunk_begin     : offsets of each (global) source chunk's cb entries
 //   units, xcd_units: scatter work units and their split over the 8 XCDs
 // Construction: (a) 64-bit key (bin << 32 | source) per edge of a light row,
@@ -120,12 +120,12 @@ __global__ void k_cb_keys(const uint32_t* slot, const uint32_t* row, const uint3
 }
 
 __global__ void k_cb_fill(const uint32_t* svals, uint64_t n_binned, const uint32_t* slot, const uint32_t* col,
-                          uint32_t* cb_slot, uint32_t* cb_src) {
+                          uint32_t chunk, uint32_t* cb_slot, uint16_t* cb_src) {
     for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n_binned;
          p += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t e = svals[p];
         cb_slot[p] = slot[e];
-        cb_src[p] = col[e] & ~kMaskedEdge;
+        cb_src[p] = (uint16_t)((col[e] & ~kMaskedEdge) % chunk);  // source, local to its chunk
     }
 }
 
@@ -178,7 +178,12 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
                       uint32_t heavy, uint32_t Wp, hipStream_t s, BinState* out, std::string* err) {
     hipError_t rc = hipSuccess;
     const uint64_t n_tiles = (n_local + 63) / 64;
-    const uint32_t max_peers = kBinWords / Wp;  // a multiple of 64 for Wp <= 8
+    // bigger bins -> longer slot runs per (source chunk, bin) in the scatter
+    // (measured: 16 K-word bins 86 ms/step at config 4, 8 K-word bins 101 ms)
+    uint32_t bin_words = kBinWords;
+    if (const char* bw = std::getenv("GOSSIP_BIN_WORDS"); bw && std::atoi(bw) < (int)kBinWords) bin_words = kBinWords / 2;
+    const uint32_t max_peers = bin_words / Wp;  // a multiple of 64 for Wp <= 8
+    const uint64_t slot_cap = kBinSlotCap * bin_words / kBinWords;
     uint32_t* tile_slots = nullptr;
     unsigned long long* light_bits = nullptr;
     uint32_t* bin_of_tile = nullptr;
@@ -217,7 +222,7 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
         b.s0 = slots;
         b.u0 = upos;
         uint64_t cnt = 0, peers = 0;
-        while (t < n_tiles && (peers == 0 || (peers + 64 <= max_peers && cnt + h_tile[t] <= kBinSlotCap))) {
+        while (t < n_tiles && (peers == 0 || (peers + 64 <= max_peers && cnt + h_tile[t] <= slot_cap))) {
             h_bot[t] = (uint32_t)h_bins.size();
             cnt += h_tile[t];
             peers += 64;
@@ -277,6 +282,7 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
     temp = nullptr;
 
     st.n_bins = h_bins.size();
+    st.bin_words = bin_words;
     st.n_slots = slots;
     st.n_binned = upos;
     st.n_chunks = n_chunks;
@@ -312,10 +318,10 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
     keys_in = vals_in = nullptr;
     temp = nullptr;
     BCHECK(hipMalloc((void**)&st.cb_slot, (upos + 1) * sizeof(uint32_t)));
-    BCHECK(hipMalloc((void**)&st.cb_src, (upos + 1) * sizeof(uint32_t)));
+    BCHECK(hipMalloc((void**)&st.cb_src, (upos + 1) * sizeof(uint16_t)));
     BCHECK(hipMalloc((void**)&st.chunk_begin, (n_chunks + 1) * sizeof(uint64_t)));
-    hipLaunchKernelGGL(k_cb_fill, dim3(gridn(upos)), dim3(256), 0, s, vals_out, upos, slot, col, st.cb_slot,
-                       st.cb_src);
+    hipLaunchKernelGGL(k_cb_fill, dim3(gridn(upos)), dim3(256), 0, s, vals_out, upos, slot, col, (uint32_t)chunk,
+                       st.cb_slot, st.cb_src);
     BCHECK(hipGetLastError());
     hipLaunchKernelGGL(k_chunk_bounds, dim3(gridn(n_chunks + 1)), dim3(256), 0, s, keys_out, upos,
                        (uint32_t)st.n_bins, n_chunks, st.chunk_begin);

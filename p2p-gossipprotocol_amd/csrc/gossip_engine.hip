@@ -467,7 +467,7 @@ gossip_status round_compute(gossip_ctx* c) {
     if (c->last_bin) {
         BinArgs b{c->bins.bins,        c->bins.n_bins,   c->bins.cb_slot, c->bins.cb_src, c->bins.chunk_begin,
                   c->bins.n_chunks,    c->bins.chunk,    c->bins.units,   c->bins.xcd_units, c->bins.bdst,
-                  c->bins.val,         c->bins.nz[c->bins.nz_cur], c->bins.nz[c->bins.nz_cur ^ 1]};
+                  c->bins.val,         c->bins.bin_words, c->bins.nz[c->bins.nz_cur], c->bins.nz[c->bins.nz_cur ^ 1]};
         HIPCHK(timed(c, "bin_scatter", [&] { return launch_bin_scatter(a, b, pw, c->stream); }));
         HIPCHK(timed(c, "bin_apply", [&] { return launch_bin_apply(a, b, pw, c->stream); }));
         if (!c->bin_noskip) c->bins.nz_cur ^= 1;

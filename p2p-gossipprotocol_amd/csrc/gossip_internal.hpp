@@ -29,9 +29,9 @@ struct HeavyChunk {
 };
 
 // Binned dense rounds (layout in gossip_bins.hip).
-constexpr uint32_t kBinWords = 8192;        // LDS accumulator words per bin (64 KB)
+constexpr uint32_t kBinWords = 16384;       // LDS accumulator words per bin (128 KB; GOSSIP_BIN_WORDS=8192: 64 KB)
 constexpr uint32_t kBinSlotPad = 8;         // bin slot ranges padded to 8 slots (16-B loads)
-constexpr uint64_t kBinSlotCap = 1u << 17;  // slots per bin (load balance between bins)
+constexpr uint64_t kBinSlotCap = 1u << 18;  // slots per bin (load balance between bins)
 constexpr uint32_t kBinChunkWords = 1u << 14;  // source chunk: its new words (128 KB) are staged in LDS
 constexpr uint64_t kBinUnitCap = 1u << 16;     // cb entries per scatter work unit (hub chunks are split)
 constexpr int kScatterBlock = 1024;            // k_bin_scatter_lds: one 16-wave workgroup per CU
@@ -52,13 +52,14 @@ struct BinArgs {
     const Bin* bins;
     uint64_t n_bins;
     const uint32_t* cb_slot;      // per binned edge, chunk-major order: its slot
-    const uint32_t* cb_src;       // per binned edge, chunk-major order: its source peer (local)
+    const uint16_t* cb_src;       // per binned edge, chunk-major order: its source peer, local to the chunk
     const uint64_t* chunk_begin;  // n_chunks + 1 offsets into cb_*
     uint64_t n_chunks, chunk;     // source chunks of `chunk` peers
     const BinUnit* units;         // scatter work units, in chunk order
     const uint64_t* xcd_units;    // 9 offsets: XCD x sweeps units [xcd_units[x], xcd_units[x+1])
     const uint16_t* bdst;         // per slot: destination - bin.v0
     uint64_t* val;                // per slot: Wp words, the source's new words of this round
+    uint32_t bin_words;           // LDS accumulator words of a bin (kBinWords or kBinWords / 2)
     const uint64_t* nz_prev;      // per source bit: its slots hold nonzero words (previous binned round)
     uint64_t* nz_next;            // the same bits for this round's words
 };
@@ -67,7 +68,7 @@ struct BinState {
     Bin* bins = nullptr;
     uint64_t n_bins = 0;
     uint32_t* cb_slot = nullptr;
-    uint32_t* cb_src = nullptr;
+    uint16_t* cb_src = nullptr;
     uint64_t* chunk_begin = nullptr;
     uint64_t n_chunks = 0, chunk = 0;
     BinUnit* units = nullptr;
@@ -77,6 +78,7 @@ struct BinState {
     uint64_t* val = nullptr;
     uint64_t* nz[2] = {nullptr, nullptr};  // per-source "slots hold nonzero" bits; nz[nz_cur] = previous round
     int nz_cur = 0;
+    uint32_t bin_words = kBinWords;
     uint64_t n_slots = 0;   // padded
     uint64_t n_binned = 0;  // edges with a slot (light destinations)
 };

@@ -536,6 +536,17 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_lds(RoundArgs a, 
             }
         }
         __syncthreads();
+        // one cb entry: store the source's words into the slot (if it has anything to write)
+        auto put = [&](uint32_t sl, uint32_t u) {
+            if (sl == kNoSlot || !((live_s[u >> 6] >> (u & 63)) & 1ull)) return;
+#pragma unroll
+            for (int w = 0; w < W; ++w) b.val[(uint64_t)sl * W + w] = slice[(uint64_t)u * W + w];
+            acc.gathered++;  // slots written (byte accounting)
+        };
+        // consecutive lanes take consecutive entries: the stores of one
+        // instruction fall into a few slot runs (measured at config 4: 37 ms
+        // per step against 57 ms with 8 consecutive entries per lane; u16
+        // chunk-local sources 36-41 ms against 43-47 ms with u32 global ids)
         constexpr int kU = 4;
         for (uint64_t p = un.p0 + threadIdx.x; p < un.p1; p += (uint64_t)kScatterBlock * kU) {
             uint32_t sl[kU], u[kU];
@@ -543,15 +554,10 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_lds(RoundArgs a, 
             for (int j = 0; j < kU; ++j) {
                 const uint64_t q = p + (uint64_t)j * kScatterBlock;
                 sl[j] = q < un.p1 ? b.cb_slot[q] : kNoSlot;
-                u[j] = q < un.p1 ? b.cb_src[q] - (uint32_t)vb : 0u;
+                u[j] = q < un.p1 ? (uint32_t)b.cb_src[q] : 0u;
             }
 #pragma unroll
-            for (int j = 0; j < kU; ++j)
-                if (sl[j] != kNoSlot && ((live_s[u[j] >> 6] >> (u[j] & 63)) & 1ull)) {
-#pragma unroll
-                    for (int w = 0; w < W; ++w) b.val[(uint64_t)sl[j] * W + w] = slice[(uint64_t)u[j] * W + w];
-                    acc.gathered++;  // slots written (byte accounting)
-                }
+            for (int j = 0; j < kU; ++j) put(sl[j], u[j]);
         }
     }
     flush<kWaves>(acc, a.st);
@@ -566,26 +572,26 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_lds(RoundArgs a, 
 // accumulator (ds_or_b64), then applies handleClient's test-and-set to the
 // bin's peers with plain stores.  A bin none of whose peers can still learn
 // anything skips its slots.
-template <int W>
-__global__ __launch_bounds__(kBlock) void k_bin_apply(RoundArgs a, BinArgs b) {
-    __shared__ unsigned long long acc_s[kBinWords];
+template <int W, int kWords, int kB>  // kWords: LDS accumulator words; kB: threads
+__global__ __launch_bounds__(kB) void k_bin_apply(RoundArgs a, BinArgs b) {
+    __shared__ unsigned long long acc_s[kWords];
     Acc acc;
     const Bin bn = b.bins[blockIdx.x];
     const uint32_t nv = bn.v1 - bn.v0;
     const uint64_t v0 = bn.v0;
     bool needy = false;
-    for (uint32_t i = threadIdx.x; i < nv * W; i += kBlock) {
+    for (uint32_t i = threadIdx.x; i < nv * W; i += kB) {
         acc_s[i] = 0ull;
         needy |= (a.inj_mask[i % W] & ~a.seen[v0 * W + i]) != 0;
     }
     if (!__syncthreads_or(needy)) {
-        for (uint32_t i = threadIdx.x; i < nv * W; i += kBlock) a.nx[v0 * W + i] = 0ull;
-        flush(acc, a.st);
+        for (uint32_t i = threadIdx.x; i < nv * W; i += kB) a.nx[v0 * W + i] = 0ull;
+        flush<kB / 64>(acc, a.st);
         return;
     }
     if (threadIdx.x == 0) acc.pulled = bn.s1 - bn.s0;  // slots scanned (byte accounting)
     // 8 slots per lane per step: 16 B of bdst, 64*W B of val
-    for (uint64_t i = bn.s0 + (uint64_t)threadIdx.x * 8; i < bn.s1; i += (uint64_t)kBlock * 8) {
+    for (uint64_t i = bn.s0 + (uint64_t)threadIdx.x * 8; i < bn.s1; i += (uint64_t)kB * 8) {
         const uint4 dd = *reinterpret_cast<const uint4*>(b.bdst + i);
         uint64_t x[8 * W];
         const uint4* vp = reinterpret_cast<const uint4*>(b.val + i * W);
@@ -605,7 +611,7 @@ __global__ __launch_bounds__(kBlock) void k_bin_apply(RoundArgs a, BinArgs b) {
         }
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < nv * W; i += kBlock) {
+    for (uint32_t i = threadIdx.x; i < nv * W; i += kB) {
         const uint64_t sv = a.seen[v0 * W + i];
         const uint64_t fr = acc_s[i] & a.inj_mask[i % W] & ~sv;
         if (fr) {  // handleClient: new -> Message-List insert (peer.cpp:281-282)
@@ -615,7 +621,7 @@ __global__ __launch_bounds__(kBlock) void k_bin_apply(RoundArgs a, BinArgs b) {
         }
         a.nx[v0 * W + i] = fr;  // heavy rows: 0 here, OR-ed by k_pull_heavy afterwards
     }
-    flush(acc, a.st);
+    flush<kB / 64>(acc, a.st);
 }
 
 // ---------------------------------------------------------------------------
@@ -1087,8 +1093,13 @@ hipError_t launch_bin_scatter(const RoundArgs& a, const BinArgs& b, uint32_t W_,
 
 hipError_t launch_bin_apply(const RoundArgs& a, const BinArgs& b, uint32_t W_, hipStream_t s) {
     if (!b.n_bins) return hipSuccess;
-    GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_bin_apply<W>, dim3((unsigned)b.n_bins), dim3(kBlock), 0, s, a,
-                                                   b));
+    if (b.bin_words == kBinWords) {  // 128 KB accumulators: one 16-wave workgroup per CU
+        GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_apply<W, kBinWords, 1024>), dim3((unsigned)b.n_bins),
+                                                       dim3(1024), 0, s, a, b));
+    } else {  // 64 KB accumulators: two 4-wave workgroups per CU
+        GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_apply<W, kBinWords / 2, kBlock>), dim3((unsigned)b.n_bins),
+                                                       dim3(kBlock), 0, s, a, b));
+    }
     return hipGetLastError();
 }
 

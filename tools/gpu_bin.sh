@@ -2,8 +2,6 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/bin
-true
-true
-timeout -k 10 300 python -u bench.py --force-partitioned --no-cpu-baseline > gpurun_out/bin/part.json 2> gpurun_out/bin/part.err || { tail -20 gpurun_out/bin/part.err; exit 1; }
-cat gpurun_out/bin/part.json
-bash tools/sweep_env.sh -
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "bin" > gpurun_out/bin/pytest.log 2>&1 || { tail -40 gpurun_out/bin/pytest.log; exit 1; }
+tail -2 gpurun_out/bin/pytest.log
+bash tools/sweep_env.sh - GOSSIP_BIN_SRC32=1 - GOSSIP_BIN_SRC32=1
