@@ -181,7 +181,8 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
     // bigger bins -> longer slot runs per (source chunk, bin) in the scatter
     // (measured: 16 K-word bins 86 ms/step at config 4, 8 K-word bins 101 ms)
     uint32_t bin_words = kBinWords;
-    if (const char* bw = std::getenv("GOSSIP_BIN_WORDS"); bw && std::atoi(bw) < (int)kBinWords) bin_words = kBinWords / 2;
+    if (const char* bw = std::getenv("GOSSIP_BIN_WORDS"))
+        bin_words = std::max<uint32_t>(512, std::min<uint32_t>(kBinWords, (uint32_t)std::atoi(bw) / 512 * 512));
     const uint32_t max_peers = bin_words / Wp;  // a multiple of 64 for Wp <= 8
     const uint64_t slot_cap = kBinSlotCap * bin_words / kBinWords;
     uint32_t* tile_slots = nullptr;
@@ -191,7 +192,8 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
     uint32_t *keys_in = nullptr, *vals_in = nullptr, *keys_out = nullptr, *vals_out = nullptr;
     uint32_t *slot = nullptr, *row = nullptr;
     uint64_t chunk_words = kBinChunkWords;
-    if (const char* c = std::getenv("GOSSIP_BIN_CHUNK")) chunk_words = std::max<uint64_t>(64, std::strtoull(c, nullptr, 0));
+    if (const char* c = std::getenv("GOSSIP_BIN_CHUNK"))
+        chunk_words = std::max<uint64_t>(512, std::min<uint64_t>(kBinChunkWords, std::strtoull(c, nullptr, 0) / 512 * 512));
     const uint64_t chunk = std::max<uint64_t>(64, chunk_words / Wp);
     const uint64_t n_chunks = (n_global + chunk - 1) / chunk;
     void* temp = nullptr;

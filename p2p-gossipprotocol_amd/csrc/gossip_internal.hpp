@@ -29,10 +29,10 @@ struct HeavyChunk {
 };
 
 // Binned dense rounds (layout in gossip_bins.hip).
-constexpr uint32_t kBinWords = 16384;       // LDS accumulator words per bin (128 KB; GOSSIP_BIN_WORDS=8192: 64 KB)
+constexpr uint32_t kBinWords = 18432;       // LDS accumulator words per bin (144 KB; GOSSIP_BIN_WORDS: fewer)
 constexpr uint32_t kBinSlotPad = 8;         // bin slot ranges padded to 8 slots (16-B loads)
 constexpr uint64_t kBinSlotCap = 1u << 18;  // slots per bin (load balance between bins)
-constexpr uint32_t kBinChunkWords = 1u << 14;  // source chunk: its new words (128 KB) are staged in LDS
+constexpr uint32_t kBinChunkWords = 18432;     // source chunk: its new words (144 KB) are staged in LDS
 constexpr uint64_t kBinUnitCap = 1u << 16;     // cb entries per scatter work unit (hub chunks are split)
 constexpr int kScatterBlock = 1024;            // k_bin_scatter_lds: one 16-wave workgroup per CU
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;

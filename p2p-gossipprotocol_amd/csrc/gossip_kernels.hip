@@ -475,16 +475,18 @@ __global__ __launch_bounds__(kBlock) void k_pull_heavy(RoundArgs a) {
 // left to k_pull_heavy.
 // ---------------------------------------------------------------------------
 // Phase 1 (scatter): one 16-wave workgroup per CU stages a
-// source chunk's new words (kBinChunkWords words, 128 KB) in LDS and writes
+// source chunk's new words (kBinChunkWords words, 144 KB) in LDS and writes
 // them into the slots of the chunk's binned edges, walked in bin order (the cb
 // list).  The units of XCD x are a contiguous range of the chunk order, dealt
 // round-robin to its workgroups: the ~32 chunks in flight on an XCD are
 // consecutive, and their slot runs inside each bin are adjacent, so the lines
 // of a bin fill up in that XCD's L2 from several workgroups before they are
 // written back.
-template <int W, bool COV>
+template <int W, bool COV, int kU>  // kU: cb entries in flight per lane
 __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_lds(RoundArgs a, BinArgs b, uint32_t wd) {
     constexpr int kWaves = kScatterBlock / 64;
+    constexpr int kSliceIt = kBinChunkWords / kScatterBlock;  // slice words per lane
+    static_assert(kBinChunkWords % kScatterBlock == 0, "slice split");
     __shared__ unsigned long long slice[kBinChunkWords];
     // which of the chunk's sources have anything to write: nonzero new words
     // now, or nonzero in the previous binned round (their slots still hold
@@ -502,52 +504,76 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_lds(RoundArgs a, 
         const BinUnit un = b.units[ui];
         // global source chunk; words from nw_src (own words at P = 1, the all-gathered ones at P > 1)
         const uint64_t vb = (uint64_t)un.c * b.chunk, ve = min(vb + b.chunk, a.n_src);  // vb % 64 == 0
-        __syncthreads();  // previous unit's readers are done with the slice
-        for (uint64_t v = vb + threadIdx.x; v < ((ve + 63) & ~63ull); v += kScatterBlock) {
-            const bool vv = v < ve;
-            const bool own = un.first && v >= a.begin && v < a.end;  // stats: owned sources, once
-            uint32_t pc = 0;
-            bool nz = false;
+        const uint64_t nwords = (ve - vb) * W;
+        // stage the slice (and the previous round's live bits): every load of
+        // the lane in flight at once
+        const uint64_t n_src = ve - vb;
+        uint64_t r[kSliceIt];
 #pragma unroll
-            for (int w = 0; w < W; ++w) {
-                const uint64_t m = vv ? a.nw_src[v * W + w] : 0ull;
-                if (vv) slice[(v - vb) * W + w] = m;
-                if (!m) continue;
-                nz = true;
-                if (!own) continue;
-                pc += (uint32_t)__popcll(m);
-                if (w < (int)wd) acc.digest += digest_weight(v * wd + w) * m;
-                if (COV)
-                    for (uint64_t x = m; x; x &= x - 1) atomicAdd(&cov_s[w * 64 + __builtin_ctzll(x)], 1u);
+        for (int k = 0; k < kSliceIt; ++k) {
+            const uint64_t i = threadIdx.x + (uint64_t)k * kScatterBlock;
+            r[k] = i < nwords ? a.nw_src[vb * W + i] : 0ull;
+        }
+        const uint64_t prev = threadIdx.x < (n_src + 63) / 64 ? b.nz_prev[(vb >> 6) + threadIdx.x] : 0ull;
+        __syncthreads();  // previous unit's readers are done with the slice
+#pragma unroll
+        for (int k = 0; k < kSliceIt; ++k) slice[threadIdx.x + k * kScatterBlock] = r[k];
+        if (threadIdx.x < kBinChunkWords / 64) live_s[threadIdx.x] = prev;
+        __syncthreads();
+        // per source (a wave covers 64 consecutive ones): live bits and, in the
+        // chunk's first unit, the source side of its pushes (broadcastMessage,
+        // peer.cpp:310-316) for the owned sources; row lengths loaded together
+        constexpr int kSrcIt = (kBinChunkWords / W + kScatterBlock - 1) / kScatterBlock;
+        constexpr int kB = 6;  // sources whose row lengths are loaded together (register budget)
+#pragma unroll
+        for (int k0 = 0; k0 < kSrcIt; k0 += kB) {
+            uint32_t pcs[kB];
+#pragma unroll
+            for (int kk = 0; kk < kB; ++kk) {
+                const uint64_t j = threadIdx.x + (uint64_t)(k0 + kk) * kScatterBlock;
+                pcs[kk] = 0;
+                if (k0 + kk >= kSrcIt || j >= ((n_src + 63) & ~63ull)) continue;  // wave-uniform
+                const uint64_t v = vb + j;
+                const bool vv = j < n_src;
+                const bool own = vv && un.first && v >= a.begin && v < a.end;
+                bool nz = false;
+#pragma unroll
+                for (int w = 0; w < W; ++w) {
+                    const uint64_t m = vv ? slice[j * W + w] : 0ull;
+                    nz |= m != 0;
+                    if (!own || !m) continue;
+                    pcs[kk] += (uint32_t)__popcll(m);
+                    if (w < (int)wd) acc.digest += digest_weight(v * wd + w) * m;
+                    if (COV)
+                        for (uint64_t x = m; x; x &= x - 1) atomicAdd(&cov_s[w * 64 + __builtin_ctzll(x)], 1u);
+                }
+                const unsigned long long bits = __ballot(nz);
+                if (lane == 0) {
+                    live_s[j >> 6] |= bits;
+                    if (un.first) b.nz_next[v >> 6] = bits;
+                }
             }
-            if (pc) {  // source side of this peer's pushes (broadcastMessage, peer.cpp:310-316)
-                const uint64_t lv = v - a.begin;
-                const uint64_t d = a.rp[lv + 1] - a.rp[lv];
+            uint64_t d0[kB], d1[kB];
+#pragma unroll
+            for (int kk = 0; kk < kB; ++kk) {
+                const uint64_t lv = vb + threadIdx.x + (uint64_t)(k0 + kk) * kScatterBlock - a.begin;
+                d0[kk] = pcs[kk] ? a.rp[lv] : 0ull;
+                d1[kk] = pcs[kk] ? a.rp[lv + 1] : 0ull;
+            }
+#pragma unroll
+            for (int kk = 0; kk < kB; ++kk) {
+                if (!pcs[kk]) continue;
                 acc.frontier++;
-                acc.covered += pc;
-                acc.trav += d;
-                acc.deliv += (unsigned long long)pc * d;
-            }
-            const unsigned long long bits = __ballot(nz);
-            if (lane == 0) {
-                const uint64_t word = v >> 6;
-                live_s[(v - vb) >> 6] = bits | b.nz_prev[word];
-                if (un.first) b.nz_next[word] = bits;
+                acc.covered += pcs[kk];
+                acc.trav += d1[kk] - d0[kk];
+                acc.deliv += (unsigned long long)pcs[kk] * (d1[kk] - d0[kk]);
             }
         }
         __syncthreads();
-        // one cb entry: store the source's words into the slot (if it has anything to write)
-        auto put = [&](uint32_t sl, uint32_t u) {
-            if (sl == kNoSlot || !((live_s[u >> 6] >> (u & 63)) & 1ull)) return;
-#pragma unroll
-            for (int w = 0; w < W; ++w) b.val[(uint64_t)sl * W + w] = slice[(uint64_t)u * W + w];
-            acc.gathered++;  // slots written (byte accounting)
-        };
         // consecutive lanes take consecutive entries: the stores of one
         // instruction fall into a few slot runs (measured at config 4: 37 ms
         // per step against 57 ms with 8 consecutive entries per lane; u16
         // chunk-local sources 36-41 ms against 43-47 ms with u32 global ids)
-        constexpr int kU = 4;
         for (uint64_t p = un.p0 + threadIdx.x; p < un.p1; p += (uint64_t)kScatterBlock * kU) {
             uint32_t sl[kU], u[kU];
 #pragma unroll
@@ -557,7 +583,12 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_lds(RoundArgs a, 
                 u[j] = q < un.p1 ? (uint32_t)b.cb_src[q] : 0u;
             }
 #pragma unroll
-            for (int j = 0; j < kU; ++j) put(sl[j], u[j]);
+            for (int j = 0; j < kU; ++j) {
+                if (sl[j] == kNoSlot || !((live_s[u[j] >> 6] >> (u[j] & 63)) & 1ull)) continue;
+#pragma unroll
+                for (int w = 0; w < W; ++w) b.val[(uint64_t)sl[j] * W + w] = slice[(uint64_t)u[j] * W + w];
+                acc.gathered++;  // slots written (byte accounting)
+            }
         }
     }
     flush<kWaves>(acc, a.st);
@@ -1085,15 +1116,15 @@ hipError_t launch_apply_records(const RoundArgs& a, uint32_t W_, const uint64_t*
 hipError_t launch_bin_scatter(const RoundArgs& a, const BinArgs& b, uint32_t W_, hipStream_t s) {
     const uint32_t wd = wd_of(W_);
     GOSSIP_DISPATCH_W(wp_of(W_), {  // one workgroup per CU (128 KB of LDS each)
-        if (a.cov) hipLaunchKernelGGL((k_bin_scatter_lds<W, true>), dim3(256), dim3(kScatterBlock), 0, s, a, b, wd);
-        else hipLaunchKernelGGL((k_bin_scatter_lds<W, false>), dim3(256), dim3(kScatterBlock), 0, s, a, b, wd);
+        if (a.cov) hipLaunchKernelGGL((k_bin_scatter_lds<W, true, 4>), dim3(256), dim3(kScatterBlock), 0, s, a, b, wd);
+        else hipLaunchKernelGGL((k_bin_scatter_lds<W, false, 4>), dim3(256), dim3(kScatterBlock), 0, s, a, b, wd);
     });
     return hipGetLastError();
 }
 
 hipError_t launch_bin_apply(const RoundArgs& a, const BinArgs& b, uint32_t W_, hipStream_t s) {
     if (!b.n_bins) return hipSuccess;
-    if (b.bin_words == kBinWords) {  // 128 KB accumulators: one 16-wave workgroup per CU
+    if (b.bin_words > kBinWords / 2) {  // up to 144 KB accumulators: one 16-wave workgroup per CU
         GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_apply<W, kBinWords, 1024>), dim3((unsigned)b.n_bins),
                                                        dim3(1024), 0, s, a, b));
     } else {  // 64 KB accumulators: two 4-wave workgroups per CU
