@@ -208,7 +208,8 @@ gossip_status gossip_read_registered(gossip_ctx* ctx, uint8_t* out);
 
 /* ---- measurement ----------------------------------------------------------- */
 /* Per-kernel device time (ms) accumulated since timing was last enabled, by kernel name
- * ("push_light", "push_heavy", "liveness", "churn", "inject", "apply_remote"),
+ * ("push_light", "push_heavy", "pull_light", "pull_heavy", "frontier_bits", "bin_scatter", "bin_apply",
+ * "liveness", "churn", "kills", "inject", "apply_remote"),
  * measured with HIP events on the ctx stream.  enable != 0 turns timing on. */
 gossip_status gossip_enable_timing(gossip_ctx* ctx, int enable);
 gossip_status gossip_kernel_time(gossip_ctx* ctx, const char* kernel, double* ms, uint64_t* launches);
@@ -217,7 +218,10 @@ gossip_status gossip_kernel_time(gossip_ctx* ctx, const char* kernel, double* ms
  * rows to "push_light", heavy rows to "push_heavy"); liveness = 6.125 B per
  * live edge checked; pull = 40 B per owned peer + 4 B per edge scanned + 8 B
  * per neighbour word gathered ("pull_light"), 12 B per heavy-row edge scanned
- * ("pull_heavy"), 8.125 B per owned peer ("frontier_bits"). */
+ * ("pull_heavy"), 8.125 B per owned peer ("frontier_bits"); binned rounds:
+ * 8·Wp B per source word staged + 16 B per frontier peer + 6 B per binned edge
+ * + 8·Wp B per slot written ("bin_scatter"), (2 + 8·Wp) B per slot scanned +
+ * 16·Wp B per owned peer ("bin_apply"). */
 gossip_status gossip_kernel_bytes(gossip_ctx* ctx, const char* kernel, double* bytes);
 
 #ifdef __cplusplus

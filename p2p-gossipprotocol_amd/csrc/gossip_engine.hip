@@ -512,7 +512,9 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
     if (c->timing) {
         if (c->last_bin) {
             const double wb = 8.0 * c->Wp;
-            c->kbytes["bin_scatter"] += (16.0 + wb) * c->n_local + 8.0 * c->bins.n_binned + wb * (double)d.pull_gathers;
+            // slices of every source chunk + row bounds of the frontier + 6 B cb entry per binned edge + slot writes
+            const double n_src = c->gather ? (double)c->n : (double)c->n_local;
+            c->kbytes["bin_scatter"] += wb * n_src + 16.0 * d.frontier + 6.0 * c->bins.n_binned + wb * (double)d.pull_gathers;
             c->kbytes["bin_apply"] += (2.0 + wb) * (double)d.pull_edges + 2.0 * wb * c->n_local;
             c->kbytes["pull_heavy"] += 12.0 * (double)d.heavy_traversals;
         } else if (c->last_pull) {
