@@ -574,20 +574,34 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_lds(RoundArgs a, 
         // instruction fall into a few slot runs (measured at config 4: 37 ms
         // per step against 57 ms with 8 consecutive entries per lane; u16
         // chunk-local sources 36-41 ms against 43-47 ms with u32 global ids)
-        for (uint64_t p = un.p0 + threadIdx.x; p < un.p1; p += (uint64_t)kScatterBlock * kU) {
-            uint32_t sl[kU], u[kU];
+        // software-pipelined: the next kU entries are loaded before this
+        // batch's LDS reads and stores, so every wave keeps two batches of
+        // loads in flight
+        const uint64_t step = (uint64_t)kScatterBlock * kU;
+        uint32_t sl[kU], u[kU];
+        auto load = [&](uint64_t p, uint32_t (&s_)[kU], uint32_t (&u_)[kU]) {
 #pragma unroll
             for (int j = 0; j < kU; ++j) {
                 const uint64_t q = p + (uint64_t)j * kScatterBlock;
-                sl[j] = q < un.p1 ? b.cb_slot[q] : kNoSlot;
-                u[j] = q < un.p1 ? (uint32_t)b.cb_src[q] : 0u;
+                s_[j] = q < un.p1 ? __builtin_nontemporal_load(b.cb_slot + q) : kNoSlot;
+                u_[j] = q < un.p1 ? (uint32_t)__builtin_nontemporal_load(b.cb_src + q) : 0u;
             }
+        };
+        load(un.p0 + threadIdx.x, sl, u);
+        for (uint64_t p = un.p0 + threadIdx.x; p < un.p1; p += step) {
+            uint32_t sn[kU], un_[kU];
+            load(p + step, sn, un_);
 #pragma unroll
             for (int j = 0; j < kU; ++j) {
                 if (sl[j] == kNoSlot || !((live_s[u[j] >> 6] >> (u[j] & 63)) & 1ull)) continue;
 #pragma unroll
                 for (int w = 0; w < W; ++w) b.val[(uint64_t)sl[j] * W + w] = slice[(uint64_t)u[j] * W + w];
                 acc.gathered++;  // slots written (byte accounting)
+            }
+#pragma unroll
+            for (int j = 0; j < kU; ++j) {
+                sl[j] = sn[j];
+                u[j] = un_[j];
             }
         }
     }

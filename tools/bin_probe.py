@@ -1,5 +1,6 @@
-"""Times the first binned round of config 4 (per-kernel ms); run once per
-GOSSIP_BIN_* setting (measurement variants change later rounds)."""
+"""Times the first binned round of config 4 (per-kernel ms): once on a fresh
+layout (clean slots) and once after a full run (slots hold the last run's
+words).  Run once per GOSSIP_BIN_* setting."""
 import os
 import sys
 from pathlib import Path
@@ -12,7 +13,11 @@ w = config(int(sys.argv[1]) if len(sys.argv) > 1 else 4)
 e = Engine(w.n, w.n_msgs, device=0, **w.engine_kwargs())
 e.build_graph()
 e.inject(w.origins, w.inject_rounds)
-for rep in range(2):
+tag = " ".join(f"{k}={v}" for k, v in os.environ.items() if k.startswith("GOSSIP_"))
+for label in ("clean", "after-run"):
+    if label == "after-run":
+        e.reset()
+        e.run()
     e.reset()
     e.enable_timing(True)
     while True:
@@ -20,7 +25,5 @@ for rep in range(2):
         t = e.kernel_time("bin_scatter")
         if t[1] or fin:
             break
-    if rep:
-        tag = " ".join(f"{k}={v}" for k, v in os.environ.items() if k.startswith("GOSSIP_"))
-        print(f"[{tag}] round {st['round']} scatter {t[0]:.3f} ms apply {e.kernel_time('bin_apply')[0]:.3f} ms",
-              flush=True)
+    print(f"[{tag}] {label} round {st['round']} scatter {t[0]:.3f} ms apply {e.kernel_time('bin_apply')[0]:.3f} ms",
+          flush=True)
