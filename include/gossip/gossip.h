@@ -71,7 +71,9 @@ typedef struct gossip_config {
     uint32_t front_permille;  /* pull rounds probe a frontier bitmap below this per-mille (0 = 400; 1000 = always) */
     uint32_t bin_permille;    /* a dense round runs binned while the (peer, message) pairs still missing are
                                  >= this per-mille of the owned peers (0 = default) */
-    uint32_t reserved0;
+    uint32_t extra_cap;       /* re-bootstrap after a death (handleDeadPeer peer.cpp:398-404): a reporter
+                                 re-selects from a seed response and keeps up to this many extra out-edges
+                                 (0 = off, the reference's literal drop-only behaviour; <= 64) */
 } gossip_config;
 
 /*
@@ -95,6 +97,7 @@ typedef struct gossip_round_stats {
     uint64_t seed_removals; /* seed-registry entries removed (first report of a peer) */
     uint64_t digest;        /* sum_v,w g(v*W+w) * seen[v][w] mod 2^64 at push start */
     uint64_t covered;       /* sum popcount(seen) at push start */
+    uint64_t reconnects;    /* out-edges added by re-bootstrap this round (extra_cap > 0) */
 } gossip_round_stats;
 
 /* A dead-node report: reporter u detected dead peer v in round r
@@ -130,6 +133,11 @@ gossip_status gossip_load_csr(gossip_ctx* ctx, const uint64_t* row_ptr, const ui
                               uint64_t n_edges);
 /* Copies the owned CSR back (row_ptr: n_local+1, col: n_edges; masked edges have bit 31 set). */
 gossip_status gossip_read_csr(gossip_ctx* ctx, uint64_t* row_ptr, uint32_t* col);
+/* Re-bootstrap edges of the owned peers (connectedPeers entries added by
+ * selectAndConnectPeers after a death, peer.cpp:398-404 -> :214-253):
+ * counts[n_local], cols[n_local * extra_cap] (row u's first counts[u] entries,
+ * global ids, bit 31 = dropped again by liveness). */
+gossip_status gossip_read_extra(gossip_ctx* ctx, uint32_t* counts, uint32_t* cols);
 
 /* ---- schedule ------------------------------------------------------------ */
 /* Replaces messageGenerationLoop (peer.cpp:357-379): message m (msgNumber of

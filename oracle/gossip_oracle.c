@@ -296,6 +296,13 @@ struct oracle_sim {
     /* reports */
     oracle_report* rep;
     uint64_t n_rep, cap_rep;
+    /* re-bootstrap overflow rows: extra out-edges, K per peer */
+    uint32_t K;
+    uint32_t* ex_col;
+    uint32_t* ex_cnt;
+    uint8_t* ex_masked;
+    uint8_t* ex_miss;
+    uint64_t thr[65];
     /* fast variant */
     uint64_t *seen, *nw, *nx;
     /* literal variant */
@@ -358,6 +365,16 @@ oracle_sim* oracle_sim_create(const oracle_sim_cfg* cfg, const uint64_t* row_ptr
     memset(s->registered, 1, s->n);
     s->masked = (uint8_t*)calloc(s->e + 1, 1);
     s->miss = (uint8_t*)calloc(s->e + 1, 1);
+    s->K = cfg->extra_cap;
+    if (s->K) {
+        if (cfg->list_len < 2 || cfg->list_len > 64) { free(s->alive); free(s->registered); free(s->masked);
+                                                        free(s->miss); free(s); return NULL; }
+        s->ex_col = (uint32_t*)calloc(s->n * s->K, sizeof(uint32_t));
+        s->ex_cnt = (uint32_t*)calloc(s->n, sizeof(uint32_t));
+        s->ex_masked = (uint8_t*)calloc(s->n * s->K, 1);
+        s->ex_miss = (uint8_t*)calloc(s->n * s->K, 1);
+        for (uint32_t j = 1; j < cfg->list_len; ++j) s->thr[j] = oracle_threshold(j, cfg->list_len);
+    }
     s->origin = (uint32_t*)calloc(s->M, sizeof(uint32_t));
     s->inject_round = (uint32_t*)malloc(s->M * sizeof(uint32_t));
     for (uint32_t m = 0; m < s->M; ++m) s->inject_round[m] = 0xFFFFFFFFu; /* unscheduled */
@@ -384,6 +401,7 @@ void oracle_sim_destroy(oracle_sim* s) {
     free(s->alive); free(s->registered); free(s->masked); free(s->miss);
     free(s->origin); free(s->inject_round); free(s->kill_peer); free(s->kill_round);
     free(s->rep); free(s->seen); free(s->nw); free(s->nx);
+    free(s->ex_col); free(s->ex_cnt); free(s->ex_masked); free(s->ex_miss);
     if (s->lists) {
         for (uint64_t v = 0; v < s->n; ++v) {
             free(s->lists[v].key); free(s->lists[v].sent_to);
@@ -410,6 +428,15 @@ int oracle_sim_schedule(oracle_sim* s, const uint32_t* origin, const uint32_t* i
         s->kill_peer[i] = kill_peer[i];
         s->kill_round[i] = kill_round[i];
     }
+    return 0;
+}
+
+static int cmp_rep(const void* a, const void* b) {
+    const oracle_report* x = (const oracle_report*)a;
+    const oracle_report* y = (const oracle_report*)b;
+    if (x->round != y->round) return x->round < y->round ? -1 : 1;
+    if (x->reporter != y->reporter) return x->reporter < y->reporter ? -1 : 1;
+    if (x->dead != y->dead) return x->dead < y->dead ? -1 : 1;
     return 0;
 }
 
@@ -455,23 +482,70 @@ static uint64_t do_churn(oracle_sim* s, uint32_t r) {
     return died;
 }
 
+/* one ping of an out-edge (pingLoop peer.cpp:328-346); returns 1 when the
+ * edge is dropped (handleDeadPeer :383-397) and reported to the seeds (:158-167) */
+static int ping_one(oracle_sim* s, uint32_t r, uint32_t u, uint32_t v, uint8_t* masked, uint8_t* miss,
+                    oracle_stats* st) {
+    if (*masked) return 0;
+    if (s->alive[v]) { *miss = 0; return 0; }               /* ping ok -> reset (:340-341) */
+    if (*miss < 255) (*miss)++;                             /* failedAttempts++ (:336) */
+    if (*miss < s->cfg.max_missed) return 0;                /* >= 3 -> dead (:337-338) */
+    *masked = 1;                                            /* connectedPeers.erase (:388) */
+    push_report(s, r, u, v);
+    st->reports++;
+    if (s->registered[v]) { s->registered[v] = 0; st->seed_removals++; } /* seed.cpp:162 */
+    return 1;
+}
+
+static int has_out_edge(const oracle_sim* s, uint32_t u, uint32_t c) {
+    uint64_t lo = s->rp[u], hi = s->rp[u + 1];            /* rows are sorted */
+    while (lo < hi) {
+        uint64_t mid = (lo + hi) / 2;
+        if (s->col[mid] < c) lo = mid + 1; else hi = mid;
+    }
+    if (lo < s->rp[u + 1] && s->col[lo] == c) return 1;
+    for (uint32_t k = 0; k < s->ex_cnt[u]; ++k)
+        if (s->ex_col[(uint64_t)u * s->K + k] == c) return 1;
+    return 0;
+}
+
+/* Re-bootstrap (handleDeadPeer :398-404 -> connectToSeed -> selectAndConnectPeers
+ * :214-253): reporter u draws one seed response of L candidates keyed by
+ * (round, dead peer) and connects to the first k (the power-law pick); a
+ * candidate that is u, dead (connect() fails), already connected (the
+ * connectedPeers map) or beyond the overflow row's capacity is skipped. */
+static void rebootstrap(oracle_sim* s, uint32_t r, uint32_t u, uint32_t dead, oracle_stats* st) {
+    const uint32_t L = s->cfg.list_len;
+    const uint32_t k = pick_count(philox_x(s->cfg.seed, u, ORACLE_P_REBOOT, r, dead, 0, 0), L, s->thr);
+    for (uint32_t i = 0; i < k; ++i) {
+        const uint32_t x = philox_x(s->cfg.seed, u, ORACLE_P_REBOOT, r, dead, 1 + (i >> 2), i & 3);
+        const uint32_t c = oracle_skew_pick(x, s->n);
+        if (c == u || !s->alive[c] || has_out_edge(s, u, c)) continue;
+        if (s->ex_cnt[u] >= s->K) continue;
+        const uint64_t slot = (uint64_t)u * s->K + s->ex_cnt[u]++;
+        s->ex_col[slot] = c;
+        s->ex_masked[slot] = 0;
+        s->ex_miss[slot] = 0;
+        st->reconnects++;
+    }
+}
+
 /* step 2: liveness (pingLoop peer.cpp:328-346 + handleDeadPeer :383-397 + seed :158-167) */
 static void do_liveness(oracle_sim* s, uint32_t r, oracle_stats* st) {
+    const uint64_t first = s->n_rep;
     for (uint64_t u = 0; u < s->n; ++u) {
         if (!s->alive[u]) continue;
-        for (uint64_t e = s->rp[u]; e < s->rp[u + 1]; ++e) {
-            if (s->masked[e]) continue;
-            uint32_t v = s->col[e];
-            if (s->alive[v]) { s->miss[e] = 0; continue; }      /* ping ok -> reset (:340-341) */
-            if (s->miss[e] < 255) s->miss[e]++;                  /* failedAttempts++ (:336) */
-            if (s->miss[e] >= s->cfg.max_missed) {               /* >= 3 -> dead (:337-338) */
-                s->masked[e] = 1;                                /* connectedPeers.erase (:388) */
-                push_report(s, r, (uint32_t)u, v);
-                st->reports++;
-                if (s->registered[v]) { s->registered[v] = 0; st->seed_removals++; } /* seed.cpp:162 */
-            }
+        for (uint64_t e = s->rp[u]; e < s->rp[u + 1]; ++e)
+            ping_one(s, r, (uint32_t)u, s->col[e], &s->masked[e], &s->miss[e], st);
+        for (uint32_t k = 0; s->K && k < s->ex_cnt[u]; ++k) {
+            const uint64_t x = u * s->K + k;
+            ping_one(s, r, (uint32_t)u, s->ex_col[x], &s->ex_masked[x], &s->ex_miss[x], st);
         }
     }
+    if (!s->K) return;
+    /* this round's reports in (reporter, dead) order */
+    qsort(s->rep + first, s->n_rep - first, sizeof(oracle_report), cmp_rep);
+    for (uint64_t i = first; i < s->n_rep; ++i) rebootstrap(s, r, s->rep[i].reporter, s->rep[i].dead, st);
 }
 
 static void stats_start_fast(oracle_sim* s, oracle_stats* st) {
@@ -519,10 +593,14 @@ static int step_fast(oracle_sim* s, oracle_stats* st) {
         uint64_t pc = 0;
         for (uint32_t w = 0; w < W; ++w) { act |= mk[w] != 0; pc += (uint64_t)__builtin_popcountll(mk[w]); }
         if (!act) continue;
-        for (uint64_t e = s->rp[u]; e < s->rp[u + 1]; ++e) {
-            if (s->masked[e]) continue;
+        const uint64_t n_out = s->rp[u + 1] - s->rp[u] + (s->K ? s->ex_cnt[u] : 0);
+        for (uint64_t i = 0; i < n_out; ++i) {   /* the row, then the re-bootstrap edges */
+            const uint64_t e = s->rp[u] + i;
+            const int base = e < s->rp[u + 1];
+            const uint64_t x = base ? 0 : (uint64_t)u * s->K + (e - s->rp[u + 1]);
+            if (base ? s->masked[e] : s->ex_masked[x]) continue;
             ++trav;
-            uint32_t v = s->col[e];
+            uint32_t v = base ? s->col[e] : s->ex_col[x];
             if (!s->alive[v]) { undeliv += pc; continue; }
             deliv += pc;
             for (uint32_t w = 0; w < W; ++w) {
@@ -572,10 +650,14 @@ static int step_literal(oracle_sim* s, oracle_stats* st) {
     /* push: every sender broadcasts every outbox message to every live out-edge */
     for (uint64_t u = 0; u < s->n; ++u) {
         if (!s->outbox_n[u]) continue;
-        for (uint64_t e = s->rp[u]; e < s->rp[u + 1]; ++e) {
-            if (s->masked[e]) continue;
+        const uint64_t n_out = s->rp[u + 1] - s->rp[u] + (s->K ? s->ex_cnt[u] : 0);
+        for (uint64_t i = 0; i < n_out; ++i) {   /* connectedPeers: the row, then the re-bootstrap edges */
+            const uint64_t e = s->rp[u] + i;
+            const int base = e < s->rp[u + 1];
+            const uint64_t x = base ? 0 : (uint64_t)u * s->K + (e - s->rp[u + 1]);
+            if (base ? s->masked[e] : s->ex_masked[x]) continue;
             st->traversals++;
-            uint32_t v = s->col[e];
+            uint32_t v = base ? s->col[e] : s->ex_col[x];
             for (uint32_t i = 0; i < s->outbox_n[u]; ++i) {
                 uint32_t m = s->outbox[u][i];
                 if (!s->alive[v]) { st->undelivered++; continue; } /* send() fails: not in sentTo */
@@ -660,20 +742,23 @@ void oracle_sim_coverage(const oracle_sim* s, uint64_t* out) {
     }
 }
 
-static int cmp_rep(const void* a, const void* b) {
-    const oracle_report* x = (const oracle_report*)a;
-    const oracle_report* y = (const oracle_report*)b;
-    if (x->round != y->round) return x->round < y->round ? -1 : 1;
-    if (x->reporter != y->reporter) return x->reporter < y->reporter ? -1 : 1;
-    if (x->dead != y->dead) return x->dead < y->dead ? -1 : 1;
-    return 0;
-}
 
 uint64_t oracle_sim_reports(const oracle_sim* s, oracle_report* buf, uint64_t cap) {
     qsort(s->rep, s->n_rep, sizeof(oracle_report), cmp_rep);
     uint64_t k = s->n_rep < cap ? s->n_rep : cap;
     if (buf && k) memcpy(buf, s->rep, k * sizeof(oracle_report));
     return s->n_rep;
+}
+
+/* re-bootstrap edges: counts[n], cols[n * extra_cap] (bit 31 = dropped by liveness) */
+void oracle_sim_extra(const oracle_sim* s, uint32_t* counts, uint32_t* cols) {
+    for (uint64_t u = 0; u < s->n; ++u) {
+        counts[u] = s->K ? s->ex_cnt[u] : 0;
+        for (uint32_t k = 0; k < s->K; ++k) {
+            const uint64_t x = u * s->K + k;
+            cols[x] = k < s->ex_cnt[u] ? (s->ex_col[x] | (s->ex_masked[x] ? 0x80000000u : 0u)) : 0u;
+        }
+    }
 }
 
 void oracle_sim_alive(const oracle_sim* s, uint8_t* out) { memcpy(out, s->alive, s->n); }
@@ -714,7 +799,7 @@ struct oracle_part {
 
 oracle_part* oracle_part_create(const oracle_sim_cfg* cfg, uint64_t b, uint64_t e, const uint64_t* row_ptr,
                                 const uint32_t* col) {
-    if (!cfg || b >= e || e > cfg->n) return NULL;
+    if (!cfg || b >= e || e > cfg->n || cfg->extra_cap) return NULL;  /* no re-bootstrap in the emulation */
     oracle_part* p = (oracle_part*)calloc(1, sizeof(oracle_part));
     p->cfg = *cfg;
     if (p->cfg.max_rounds == 0) p->cfg.max_rounds = 1u << 20;

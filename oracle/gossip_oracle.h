@@ -41,7 +41,8 @@ enum {
     ORACLE_P_TARGET = 2,  /* ctr {2, response, i>>2, 0}[i&3] -> candidate i (powerlaw) */
     ORACLE_P_SHUFFLE = 3, /* ctr {3, response, d>>2, 0}[d&3] -> Fisher-Yates draw d (peer.cpp:224-225) */
     ORACLE_P_CHURN = 4,   /* ctr {4, round, 0, 0}.x -> peer dies if < churn_threshold */
-    ORACLE_P_ORIGIN = 5   /* key {seed, 0xFFFFFFFF}, ctr {5, k, attempt, 0}.x -> origin k */
+    ORACLE_P_ORIGIN = 5,  /* key {seed, 0xFFFFFFFF}, ctr {5, k, attempt, 0}.x -> origin k */
+    ORACLE_P_REBOOT = 6   /* ctr {6, round, dead, 0}.x -> k draw; ctr {6, round, dead, 1+(i>>2)}[i&3] -> candidate i */
 };
 
 /* Integer threshold for the reference's power-law pick
@@ -93,6 +94,7 @@ typedef struct oracle_stats {
     uint64_t seed_removals; /* registry entries removed this round */
     uint64_t digest;        /* sum g(v*W+w) * seen[v][w] mod 2^64 at push start */
     uint64_t covered;       /* sum popcount(seen) at push start */
+    uint64_t reconnects;    /* out-edges added by re-bootstrap this round (extra_cap > 0) */
 } oracle_stats;
 
 typedef struct oracle_report {
@@ -110,6 +112,8 @@ typedef struct oracle_sim_cfg {
     uint32_t min_rounds;
     int threads;               /* fast driver OpenMP threads */
     int variant;               /* 0 fast (mask), 1 literal (message lists) */
+    uint32_t extra_cap;        /* re-bootstrap after a death: up to this many extra out-edges per peer (0 = off) */
+    uint32_t list_len;         /* re-bootstrap: candidates per seed response (powerlaw list_len) */
 } oracle_sim_cfg;
 
 typedef struct oracle_sim oracle_sim;
@@ -127,6 +131,7 @@ void oracle_sim_seen(const oracle_sim* s, uint64_t* out);          /* n*W words 
 void oracle_sim_coverage(const oracle_sim* s, uint64_t* out);      /* M counts (current) */
 uint64_t oracle_sim_reports(const oracle_sim* s, oracle_report* buf, uint64_t cap); /* sorted (round,u,v) */
 void oracle_sim_alive(const oracle_sim* s, uint8_t* out);          /* n bytes */
+void oracle_sim_extra(const oracle_sim* s, uint32_t* counts, uint32_t* cols); /* n, n*extra_cap */
 void oracle_sim_registered(const oracle_sim* s, uint8_t* out);     /* n bytes */
 uint64_t oracle_sim_sent_to_total(const oracle_sim* s);             /* literal variant: sum sentTo */
 

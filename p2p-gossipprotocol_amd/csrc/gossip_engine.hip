@@ -6,6 +6,7 @@
 // light) followed by one 128-byte stats read-back that decides termination.
 // No exception crosses the ABI; all errors become gossip_status codes.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <chrono>
@@ -106,6 +107,17 @@ struct gossip_ctx {
     bool cur_remote = false;
     RoundArgs cur{};
     uint64_t* gather = nullptr;  // partitioned pull: every rank's new words, indexed by global peer
+    // re-bootstrap overflow rows (cfg.extra_cap > 0)
+    uint32_t* ex_col = nullptr;
+    uint32_t* ex_cnt = nullptr;
+    uint8_t* ex_miss = nullptr;
+    uint64_t n_rep_seen = 0;                  // reports already re-bootstrapped
+    unsigned long long* rb_keys = nullptr;    // this round's report keys (sorted in place via rb_keys2)
+    unsigned long long* rb_keys2 = nullptr;
+    uint64_t rb_cap = 0;
+    void* rb_temp = nullptr;
+    size_t rb_temp_bytes = 0;
+    RebootArgs reboot{};
     BinState bins;               // binned dense rounds: slot layout (gossip_bins.hip)
     bool bins_ready = false;
     bool last_bin = false;       // the pull round in flight runs binned
@@ -190,6 +202,18 @@ void free_state(gossip_ctx* c) {
     hipFree(c->cov_hist);
     hipFree(c->reports);
     hipFree(c->n_reports);
+    hipFree(c->ex_col);
+    hipFree(c->ex_cnt);
+    hipFree(c->ex_miss);
+    hipFree(c->rb_keys);
+    hipFree(c->rb_keys2);
+    hipFree(c->rb_temp);
+    c->ex_col = c->ex_cnt = nullptr;
+    c->ex_miss = nullptr;
+    c->rb_keys = c->rb_keys2 = nullptr;
+    c->rb_temp = nullptr;
+    c->rb_cap = 0;
+    c->rb_temp_bytes = 0;
     c->seen = c->nw = c->nx = nullptr;
     c->alive = c->registered = nullptr;
     c->miss = nullptr;
@@ -240,6 +264,10 @@ RoundArgs make_args(gossip_ctx* c) {
     a.round = c->round;
     a.max_missed = c->cfg.max_missed;
     a.heavy = c->heavy;
+    a.ex_col = c->ex_col;
+    a.ex_cnt = c->ex_cnt;
+    a.ex_miss = c->ex_miss;
+    a.ex_cap = c->cfg.extra_cap;
     return a;
 }
 
@@ -353,6 +381,37 @@ uint32_t injections_in_round(const gossip_ctx* c, uint32_t r, uint32_t* first) {
     return (uint32_t)(hi - lo);
 }
 
+// Re-bootstrap (handleDeadPeer peer.cpp:398-404): this round's reports, sorted
+// by (reporter, dead), each make the reporter re-select from a seed response.
+gossip_status rebootstrap_round(gossip_ctx* c, const RoundArgs& a) {
+    unsigned long long total = 0;
+    HIPCHK(hipMemcpyAsync(&total, c->n_reports, sizeof(total), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const uint64_t upto = std::min<uint64_t>(total, c->report_cap);
+    const uint64_t n = upto > c->n_rep_seen ? upto - c->n_rep_seen : 0;
+    if (!n) return GOSSIP_OK;
+    if (n > c->rb_cap) {
+        hipFree(c->rb_keys);
+        hipFree(c->rb_keys2);
+        hipFree(c->rb_temp);
+        c->rb_keys = c->rb_keys2 = nullptr;
+        c->rb_temp = nullptr;
+        c->rb_cap = std::max<uint64_t>(n, 1u << 16);
+        HIPCHK(hipMalloc((void**)&c->rb_keys, c->rb_cap * sizeof(unsigned long long)));
+        HIPCHK(hipMalloc((void**)&c->rb_keys2, c->rb_cap * sizeof(unsigned long long)));
+        c->rb_temp_bytes = 0;
+        HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, c->rb_temp_bytes, c->rb_keys, c->rb_keys2, (size_t)c->rb_cap,
+                                                 0, 64, c->stream));
+        HIPCHK(hipMalloc(&c->rb_temp, c->rb_temp_bytes + 16));
+    }
+    HIPCHK(launch_reboot_keys(a, c->n_rep_seen, n, c->rb_keys, c->stream));
+    size_t tb = c->rb_temp_bytes;
+    HIPCHK(hipcub::DeviceRadixSort::SortKeys(c->rb_temp, tb, c->rb_keys, c->rb_keys2, (size_t)n, 0, 64, c->stream));
+    HIPCHK(launch_rebootstrap(a, c->reboot, c->rb_keys2, n, c->stream));
+    c->n_rep_seen = upto;
+    return GOSSIP_OK;
+}
+
 // Round phase 1: churn, kills, liveness, injection; choose push or pull.
 // requested: GOSSIP_MODE_AUTO (P = 1: the engine's frontier estimate decides),
 // GOSSIP_MODE_PUSH or GOSSIP_MODE_PULL (partitioned runs: the driver decides
@@ -377,9 +436,15 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
     if (c->cfg.ping_every && c->round % c->cfg.ping_every == 0) {
         HIPCHK(timed(c, "liveness", [&] {
             hipError_t e = launch_liveness(a, c->stream, 1);
-            return e != hipSuccess ? e : launch_liveness(a, c->stream, 0);
+            if (e == hipSuccess) e = launch_liveness(a, c->stream, 0);
+            if (e == hipSuccess && c->cfg.extra_cap) e = launch_liveness_extra(a, c->stream);
+            return e;
         }));
         c->any_masked = true;
+        if (c->cfg.extra_cap) {
+            gossip_status rs = rebootstrap_round(c, a);
+            if (rs) return rs;
+        }
     }
     cnt = injections_in_round(c, c->round, &first);
     if (cnt)
@@ -482,6 +547,8 @@ gossip_status round_compute(gossip_ctx* c) {
         return GOSSIP_OK;
     }
     const bool remote = c->cur_remote;
+    if (c->cfg.extra_cap)
+        HIPCHK(timed(c, "push_extra", [&] { return launch_push_extra(a, pw, c->any_dead, remote, c->stream); }));
     HIPCHK(timed(c, "push_heavy", [&] { return launch_push_heavy(a, pw, c->any_dead, remote, c->stream); }));
     HIPCHK(timed(c, "push_light", [&] { return launch_push_light(a, pw, c->any_dead, remote, c->stream); }));
     if (c->cur_sparse) {
@@ -502,7 +569,7 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
         const unsigned long long* src = reinterpret_cast<const unsigned long long*>(c->h_st);
         unsigned long long* dst = reinterpret_cast<unsigned long long*>(&sum);
         for (int l = 0; l < kStatLines; ++l)
-            for (int f = 0; f < 16; ++f) dst[f] += src[l * 16 + f];
+            for (int f = 0; f < kStatFields; ++f) dst[f] += src[l * kStatFields + f];
         c->last_st = sum;
         c->last_st_round = c->round;
     }
@@ -540,6 +607,7 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
     s.died = d.died;
     s.reports = d.reports;
     s.seed_removals = d.seed_removals;
+    s.reconnects = d.reconnects;
     if (cumulative) {
         c->cum_digest += d.digest;
         c->cum_covered += d.covered;
@@ -646,6 +714,21 @@ gossip_status gossip_create(const gossip_config* cfg, gossip_ctx** out) {
         return bail("stats", err);
     if ((err = hipHostMalloc((void**)&c->h_st, kStatLines * sizeof(DevStats))) != hipSuccess) return bail("pinned stats", err);
     if ((err = hipMalloc((void**)&c->n_reports, sizeof(unsigned long long))) != hipSuccess) return bail("nrep", err);
+    if (c->cfg.extra_cap) {
+        if (c->cfg.extra_cap > 64) {
+            free_state(c);
+            if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
+            delete c;
+            return fail(GOSSIP_EINVAL, "extra_cap must be <= 64");
+        }
+        const uint64_t slots = c->n_local * c->cfg.extra_cap;
+        if ((err = hipMalloc((void**)&c->ex_col, slots * 4 + 4)) != hipSuccess) return bail("extra edges", err);
+        if ((err = hipMalloc((void**)&c->ex_cnt, c->n_local * 4 + 4)) != hipSuccess) return bail("extra counts", err);
+        if ((err = hipMalloc((void**)&c->ex_miss, slots + 1)) != hipSuccess) return bail("extra misses", err);
+        c->reboot.L = c->cfg.list_len;
+        c->reboot.seed = c->cfg.rng_seed;
+        for (uint32_t j = 1; j < c->cfg.list_len && j < 64; ++j) c->reboot.thr[j] = (uint32_t)pick_threshold(j, c->cfg.list_len);
+    }
     if (c->cfg.flags & GOSSIP_FLAG_COVERAGE_HISTORY) {
         if ((err = hipMalloc((void**)&c->cov_hist, (uint64_t)c->cfg.max_rounds * 64 * c->Wp * 8)) != hipSuccess)
             return bail("coverage history", err);
@@ -754,6 +837,22 @@ gossip_status gossip_read_csr(gossip_ctx* c, uint64_t* rp, uint32_t* col) {
     return GOSSIP_OK;
 }
 
+gossip_status gossip_read_extra(gossip_ctx* c, uint32_t* counts, uint32_t* cols) {
+    if (!c || !counts || !cols) return fail(GOSSIP_EINVAL, "null argument");
+    if (set_dev(c)) return GOSSIP_EHIP;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const uint32_t K = c->cfg.extra_cap;
+    if (!K) {
+        std::memset(counts, 0, c->n_local * 4);
+        return GOSSIP_OK;
+    }
+    HIPCHK(hipMemcpy(counts, c->ex_cnt, c->n_local * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(cols, c->ex_col, c->n_local * K * 4, hipMemcpyDeviceToHost));
+    for (uint64_t u = 0; u < c->n_local; ++u)  // entries past the count are stale: report zeros
+        for (uint32_t k = counts[u]; k < K; ++k) cols[u * K + k] = 0;
+    return GOSSIP_OK;
+}
+
 gossip_status gossip_inject(gossip_ctx* c, const uint32_t* origin, const uint32_t* inject_round, uint32_t n_msgs) {
     if (!c || !origin || !inject_round) return fail(GOSSIP_EINVAL, "null argument");
     if (n_msgs != c->M) return fail(GOSSIP_EINVAL, "n_msgs must equal cfg.n_msgs");
@@ -858,6 +957,11 @@ gossip_status gossip_reset(gossip_ctx* c) {
         hipLaunchKernelGGL(k_unmask, dim3(2048), dim3(256), 0, s, c->col, c->n_edges);
         HIPCHK(hipGetLastError());
     }
+    if (c->cfg.extra_cap) {
+        HIPCHK(hipMemsetAsync(c->ex_cnt, 0, c->n_local * 4 + 4, s));
+        HIPCHK(hipMemsetAsync(c->ex_miss, 0, c->n_local * c->cfg.extra_cap + 1, s));
+    }
+    c->n_rep_seen = 0;
     c->any_masked = false;
     c->nx_dirty = false;
     c->last_pull = false;

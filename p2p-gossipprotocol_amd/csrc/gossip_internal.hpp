@@ -18,9 +18,11 @@ constexpr int kPullNT = 0x100;                 // launch_pull_light unroll flag:
 // Per-round device counters (all integer; order-independent sums).
 struct DevStats {
     unsigned long long frontier, traversals, deliveries, undelivered, new_receipts, injected, died, reports,
-        seed_removals, digest, covered, heavy_traversals, live_checked, activated, pull_edges, pull_gathers;
+        seed_removals, digest, covered, heavy_traversals, live_checked, activated, pull_edges, pull_gathers,
+        reconnects;
 };
-static_assert(sizeof(DevStats) == 128, "DevStats layout");
+constexpr int kStatFields = 17;
+static_assert(sizeof(DevStats) == kStatFields * 8, "DevStats layout");
 
 struct HeavyChunk {
     uint32_t v;    // local row
@@ -114,6 +116,20 @@ struct RoundArgs {
     uint64_t* front;               // pull rounds: 1 bit per source peer, set iff its new words are nonzero
     const uint64_t* nw_src;        // pull rounds: new words of every source, indexed by (global) peer id
     uint64_t n_src;                // peers covered by nw_src / front
+    // re-bootstrap overflow rows (extra_cap > 0): extra out-edges of the owned peers
+    uint32_t* ex_col;              // n_local * ex_cap, global ids, bit 31 = masked by liveness
+    uint32_t* ex_cnt;              // n_local
+    uint8_t* ex_miss;              // n_local * ex_cap
+    uint32_t ex_cap;
+    uint32_t pad1;
+};
+
+// Re-bootstrap draw (handleDeadPeer peer.cpp:398-404 -> selectAndConnectPeers
+// :214-253): one seed response of L candidates, keyed by (round, dead peer).
+struct RebootArgs {
+    uint32_t thr[64];  // power-law thresholds t[j], 1 <= j < L
+    uint32_t L;
+    uint32_t seed;
 };
 
 // ---- launchers (gossip_kernels.hip) ----
@@ -134,6 +150,13 @@ hipError_t launch_compact_send(const RoundArgs& a, uint32_t W, uint64_t chunk, u
 hipError_t launch_apply_records(const RoundArgs& a, uint32_t W, const uint64_t* rec, uint64_t n_rec, hipStream_t s);
 hipError_t launch_bin_scatter(const RoundArgs& a, const BinArgs& b, uint32_t W, hipStream_t s);
 hipError_t launch_bin_apply(const RoundArgs& a, const BinArgs& b, uint32_t W, hipStream_t s);
+hipError_t launch_liveness_extra(const RoundArgs& a, hipStream_t s);
+hipError_t launch_push_extra(const RoundArgs& a, uint32_t W, bool check_alive, bool remote, hipStream_t s);
+// this round's reports [first, first + n) -> keys (local reporter << 32 | dead), unsorted
+hipError_t launch_reboot_keys(const RoundArgs& a, uint64_t first, uint64_t n, unsigned long long* keys, hipStream_t s);
+// keys sorted: every reporter re-selects once per report, in dead order
+hipError_t launch_rebootstrap(const RoundArgs& a, const RebootArgs& r, const unsigned long long* keys, uint64_t n,
+                              hipStream_t s);
 hipError_t launch_coverage(const uint64_t* words, uint64_t n_local, uint32_t W, unsigned long long* counts,
                            hipStream_t s);
 hipError_t launch_heavy_count(const uint64_t* rp, uint64_t n_local, uint32_t heavy, unsigned long long* n_chunks,

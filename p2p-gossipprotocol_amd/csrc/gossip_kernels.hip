@@ -41,7 +41,7 @@ __device__ __forceinline__ uint32_t lane_rank(unsigned long long mask) {
 struct Acc {
     unsigned long long frontier = 0, trav = 0, deliv = 0, undeliv = 0, fresh = 0, digest = 0, covered = 0, died = 0,
                        reports = 0, removals = 0, injected = 0, htrav = 0, checked = 0,
-                       activated = 0, pulled = 0, gathered = 0;
+                       activated = 0, pulled = 0, gathered = 0, reconnects = 0;
 };
 
 // Block-level flush: wave sums -> LDS -> one atomic per nonzero field per
@@ -51,14 +51,14 @@ struct Acc {
 // wave of the block (it holds a barrier).
 template <int kWaves = kWavesPerBlock>
 __device__ __forceinline__ void flush(Acc& acc, DevStats* st) {
-    constexpr int kF = 16;
+    constexpr int kF = kStatFields;
     static_assert(sizeof(DevStats) == kF * 8, "one u64 per stat field");
     __shared__ unsigned long long red[kWaves][kF];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     // DevStats field order
     const unsigned long long v[kF] = {acc.frontier, acc.trav,     acc.deliv,   acc.undeliv, acc.fresh,  acc.injected,
                                       acc.died,     acc.reports,  acc.removals, acc.digest, acc.covered, acc.htrav,
-                                      acc.checked,  acc.activated, acc.pulled,  acc.gathered};
+                                      acc.checked,  acc.activated, acc.pulled,  acc.gathered, acc.reconnects};
 #pragma unroll
     for (int f = 0; f < kF; ++f) {
         const unsigned long long s_ = wave_sum(v[f]);
@@ -762,6 +762,126 @@ __global__ __launch_bounds__(kBlock) void k_liveness_heavy(RoundArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// re-bootstrap after a death: handleDeadPeer
+// (peer.cpp:398-404) re-registers with the seeds and runs
+// selectAndConnectPeers (:214-253) on their lists; the new connectedPeers
+// entries live in per-peer overflow rows (ex_col, up to ex_cap each).
+// ---------------------------------------------------------------------------
+// one thread per owned peer; the wave runs max(ex_cnt) iterations so that the
+// report ballot is wave-uniform
+__global__ __launch_bounds__(kBlock) void k_liveness_extra(RoundArgs a) {
+    Acc acc;
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    const uint64_t n_pad = (a.n_local + 63) & ~63ull;
+    for (uint64_t u = (uint64_t)blockIdx.x * kBlock + threadIdx.x; u < n_pad; u += stride) {
+        const bool vu = u < a.n_local && bit_alive(a.alive, (uint32_t)(a.begin + u));
+        const uint32_t cnt = vu ? a.ex_cnt[u] : 0u;
+        uint32_t kmax = cnt;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, off));
+        for (uint32_t k = 0; k < kmax; ++k) {
+            bool emit = false;
+            uint32_t dead = 0;
+            if (k < cnt) {
+                const uint64_t x = u * a.ex_cap + k;
+                const uint32_t c = a.ex_col[x];
+                if (!(c & kMaskedEdge)) {
+                    acc.checked++;
+                    if (bit_alive(a.alive, c)) {  // ping ok (peer.cpp:340-341)
+                        if (a.ex_miss[x]) a.ex_miss[x] = 0;
+                    } else {
+                        uint32_t mm = a.ex_miss[x];
+                        if (mm < 255) ++mm;  // failedAttempts++ (:336)
+                        a.ex_miss[x] = (uint8_t)mm;
+                        if (mm >= a.max_missed) {  // >= 3 -> dead (:337)
+                            a.ex_col[x] = c | kMaskedEdge;
+                            emit = true;
+                            dead = c;
+                        }
+                    }
+                }
+            }
+            emit_reports(a, emit, (uint32_t)(a.begin + u), dead, acc);
+        }
+    }
+    flush(acc, a.st);
+}
+
+// push over the overflow rows; runs before k_push_light (which consumes new[])
+template <int W, bool CA, bool RM>
+__global__ __launch_bounds__(kBlock) void k_push_extra(RoundArgs a) {
+    Acc acc;
+    for (uint64_t u = (uint64_t)blockIdx.x * kBlock + threadIdx.x; u < a.n_local; u += (uint64_t)gridDim.x * kBlock) {
+        const uint32_t cnt = a.ex_cnt[u];
+        if (!cnt) continue;
+        uint64_t m[W];
+        uint32_t pc = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            m[w] = a.nw[u * W + w];
+            pc += (uint32_t)__popcll(m[w]);
+        }
+        if (!pc) continue;
+        for (uint32_t k = 0; k < cnt; ++k) deliver<W, CA, RM>(a, a.ex_col[u * a.ex_cap + k], m, pc, acc);
+    }
+    flush(acc, a.st);
+}
+
+__global__ void k_reboot_keys(DeadReport* rep, uint64_t first, uint64_t n, uint64_t begin, unsigned long long* keys) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const DeadReport r = rep[first + i];
+        keys[i] = ((unsigned long long)(r.reporter - begin) << 32) | r.dead;
+    }
+}
+
+// u already has an out-edge to c (its sorted row, masked or not, or an extra)
+__device__ __forceinline__ bool has_out_edge(const RoundArgs& a, uint64_t u, uint32_t c) {
+    uint64_t lo = a.rp[u], hi = a.rp[u + 1];
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if ((a.col[mid] & ~kMaskedEdge) < c) lo = mid + 1;
+        else hi = mid;
+    }
+    if (lo < a.rp[u + 1] && (a.col[lo] & ~kMaskedEdge) == c) return true;
+    const uint32_t cnt = a.ex_cnt[u];
+    for (uint32_t k = 0; k < cnt; ++k)
+        if ((a.ex_col[u * a.ex_cap + k] & ~kMaskedEdge) == c) return true;
+    return false;
+}
+
+// one thread per reporter (the first of its run of sorted keys): its reports
+// in dead order, each a seed response of L candidates, the first k kept
+// (the power-law pick) unless self, dead (connect() fails), already connected
+// (connectedPeers is a map) or the overflow row is full
+__global__ __launch_bounds__(kBlock) void k_rebootstrap(RoundArgs a, RebootArgs rb, const unsigned long long* keys,
+                                                        uint64_t n) {
+    Acc acc;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t u = keys[i] >> 32;
+        if (i > 0 && (keys[i - 1] >> 32) == u) continue;  // not the first report of u
+        const uint32_t ug = (uint32_t)(a.begin + u);
+        for (uint64_t j = i; j < n && (keys[j] >> 32) == u; ++j) {
+            const uint32_t dead = (uint32_t)keys[j];
+            const uint32_t x0 = philox4x32_10(P_REBOOT, a.round, dead, 0, rb.seed, ug).x;
+            uint32_t k = 0;
+            for (uint32_t t = 1; t < rb.L; ++t) k += x0 >= rb.thr[t];
+            for (uint32_t c_i = 0; c_i < k; ++c_i) {
+                const u32x4 r = philox4x32_10(P_REBOOT, a.round, dead, 1 + (c_i >> 2), rb.seed, ug);
+                const uint32_t c = skew_pick(lane_of(r, c_i & 3), a.n_global);
+                if (c == ug || !bit_alive(a.alive, c) || has_out_edge(a, u, c)) continue;
+                const uint32_t cnt = a.ex_cnt[u];
+                if (cnt >= a.ex_cap) continue;
+                a.ex_col[u * a.ex_cap + cnt] = c;
+                a.ex_miss[u * a.ex_cap + cnt] = 0;
+                a.ex_cnt[u] = cnt + 1;
+                acc.reconnects++;
+            }
+        }
+    }
+    flush(acc, a.st);
+}
+
+// ---------------------------------------------------------------------------
 // churn / kills: a dead peer stops receiving, forwarding and pinging.  Its
 // pending new words are dropped, but they are already in seen, so their
 // digest/coverage contribution is booked here.
@@ -1145,6 +1265,40 @@ hipError_t launch_bin_apply(const RoundArgs& a, const BinArgs& b, uint32_t W_, h
         GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_apply<W, kBinWords / 2, kBlock>), dim3((unsigned)b.n_bins),
                                                        dim3(kBlock), 0, s, a, b));
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_liveness_extra(const RoundArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_liveness_extra, dim3(grid_for((a.n_local + 63) & ~63ull, kBlock)), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_push_extra(const RoundArgs& a, uint32_t W_, bool check_alive, bool remote, hipStream_t s) {
+    const unsigned g = grid_for(a.n_local, kBlock);
+#define GOSSIP_EXTRA(CA, RM) hipLaunchKernelGGL((k_push_extra<W, CA, RM>), dim3(g), dim3(kBlock), 0, s, a)
+    GOSSIP_DISPATCH_W(wp_of(W_), {
+        if (check_alive) {
+            if (remote) GOSSIP_EXTRA(true, true); else GOSSIP_EXTRA(true, false);
+        } else {
+            if (remote) GOSSIP_EXTRA(false, true); else GOSSIP_EXTRA(false, false);
+        }
+    });
+#undef GOSSIP_EXTRA
+    return hipGetLastError();
+}
+
+hipError_t launch_reboot_keys(const RoundArgs& a, uint64_t first, uint64_t n, unsigned long long* keys,
+                              hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_reboot_keys, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, a.reports, first, n, a.begin,
+                       keys);
+    return hipGetLastError();
+}
+
+hipError_t launch_rebootstrap(const RoundArgs& a, const RebootArgs& r, const unsigned long long* keys, uint64_t n,
+                              hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_rebootstrap, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, a, r, keys, n);
     return hipGetLastError();
 }
 

@@ -17,6 +17,7 @@ enum : uint32_t {
     P_SHUFFLE = 3,  // {3, response, d>>2, 0}[d&3]  Fisher-Yates draw (peer.cpp:224-225)
     P_CHURN = 4,    // {4, round, 0, 0}.x           death test
     P_ORIGIN = 5,   // key {seed, ~0u}, {5, k, attempt, 0}.x  origin pick
+    P_REBOOT = 6,   // {6, round, dead, 0}.x k draw; {6, round, dead, 1+(i>>2)}[i&3] candidate i (re-bootstrap)
 };
 
 struct u32x4 {

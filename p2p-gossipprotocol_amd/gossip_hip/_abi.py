@@ -56,12 +56,12 @@ class GossipConfig(C.Structure):
         ("pull_permille", C.c_uint32),
         ("front_permille", C.c_uint32),
         ("bin_permille", C.c_uint32),
-        ("reserved0", C.c_uint32),
+        ("extra_cap", C.c_uint32),
     ]
 
 
 STAT_FIELDS = ("frontier", "traversals", "deliveries", "undelivered", "new_receipts", "duplicates", "injected",
-               "died", "reports", "seed_removals", "digest", "covered")
+               "died", "reports", "seed_removals", "digest", "covered", "reconnects")
 
 
 class RoundStats(C.Structure):
@@ -105,6 +105,7 @@ def lib() -> C.CDLL:
         "gossip_build_graph": (i32, [P]),
         "gossip_load_csr": (i32, [P, pu64, pu32, u64, u64]),
         "gossip_read_csr": (i32, [P, pu64, pu32]),
+        "gossip_read_extra": (i32, [P, pu32, pu32]),
         "gossip_inject": (i32, [P, pu32, pu32, u32]),
         "gossip_schedule_kills": (i32, [P, pu32, pu32, u32]),
         "gossip_pick_origins": (i32, [u64, u32, u32, pu32]),

@@ -16,9 +16,8 @@ from . import _abi
 from ._abi import DeadReport, GossipConfig, RoundStats, check
 
 _GRAPHS = {"powerlaw": _abi.GRAPH_POWERLAW, "ref_bootstrap": _abi.GRAPH_REF_BOOTSTRAP}
-KERNELS = ("push_light", "push_heavy", "frontier_bits", "pull_light", "pull_heavy", "bin_scatter", "bin_apply",
-           "liveness", "churn", "kills",
-           "inject", "apply_remote")
+KERNELS = ("push_light", "push_heavy", "push_extra", "frontier_bits", "pull_light", "pull_heavy", "bin_scatter",
+           "bin_apply", "liveness", "churn", "kills", "inject", "apply_remote")
 
 
 def _u32(a) -> np.ndarray:
@@ -40,7 +39,8 @@ class Engine:
                  n_seeds: int = 20, churn_threshold: int = 0, ping_every: int = 0, max_missed: int = 3,
                  max_rounds: int = 4096, min_rounds: int = 0, device: int = -1, coverage_history: bool = False,
                  part: tuple[int, int] = (0, 0), report_capacity: int = 0, mode: str = "auto",
-                 pull_permille: int = 0, front_permille: int = 0, bin_permille: int = 0, bins: bool = True):
+                 pull_permille: int = 0, front_permille: int = 0, bin_permille: int = 0, bins: bool = True,
+                 extra_cap: int = 0):
         self._L = _abi.lib()
         cfg = GossipConfig()
         cfg.n_peers = n_peers
@@ -62,6 +62,7 @@ class Engine:
         cfg.pull_permille = pull_permille
         cfg.front_permille = front_permille
         cfg.bin_permille = bin_permille
+        cfg.extra_cap = extra_cap
         self.cfg = cfg
         ctx = C.c_void_p()
         check(self._L.gossip_create(C.byref(cfg), C.byref(ctx)), "gossip_create")
@@ -118,6 +119,14 @@ class Engine:
         col = np.zeros(max(s["n_edges"], 1), dtype=np.uint32)
         check(self._L.gossip_read_csr(self._ctx, _ptr(rp, C.c_uint64), _ptr(col, C.c_uint32)), "gossip_read_csr")
         return rp, col[: s["n_edges"]]
+
+    def read_extra(self) -> tuple[np.ndarray, np.ndarray]:
+        """Re-bootstrap edges: counts[n_local], cols[n_local, extra_cap] (bit 31 = dropped again)."""
+        nl, K = self.shape()["n_local"], self.cfg.extra_cap
+        cnt = np.zeros(nl, dtype=np.uint32)
+        cols = np.zeros(max(nl * K, 1), dtype=np.uint32)
+        check(self._L.gossip_read_extra(self._ctx, _ptr(cnt, C.c_uint32), _ptr(cols, C.c_uint32)), "gossip_read_extra")
+        return cnt, cols[: nl * K].reshape(nl, K)
 
     # -- schedule ---------------------------------------------------------------
     def inject(self, origin, inject_round) -> None:

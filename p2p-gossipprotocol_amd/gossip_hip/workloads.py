@@ -36,11 +36,12 @@ class Workload:
     ping_every: int = 0
     max_missed: int = 3
     min_rounds: int = 0
+    extra_cap: int = 0   # re-bootstrap after a death; 0 = drop-only (the literal reference)
 
     def engine_kwargs(self) -> dict:
         return dict(rng_seed=self.rng_seed, graph=self.graph, list_len=self.list_len, n_seeds=self.n_seeds,
                     churn_threshold=self.churn_threshold, ping_every=self.ping_every, max_missed=self.max_missed,
-                    min_rounds=self.min_rounds)
+                    min_rounds=self.min_rounds, extra_cap=self.extra_cap)
 
 
 def _batches(origins: np.ndarray, per_origin: int, every: int) -> tuple[np.ndarray, np.ndarray]:
@@ -50,9 +51,16 @@ def _batches(origins: np.ndarray, per_origin: int, every: int) -> tuple[np.ndarr
     return o, r
 
 
-def config(idx: int, n: int | None = None, pick=None) -> Workload:
+def config(idx: int, n: int | None = None, pick=None, rebootstrap: int = 0) -> Workload:
     """BASELINE.json configs[idx-1]; n overrides the peer count (parity runs).
-    pick(n, seed, count) -> origins (defaults to the engine's Philox pick)."""
+    pick(n, seed, count) -> origins (defaults to the engine's Philox pick).
+    rebootstrap > 0 turns on re-bootstrap after a death with that many extra
+    out-edges per peer (configs 1 and 5, the ones with deaths)."""
+    w = _config(idx, n, pick)
+    return replace(w, extra_cap=rebootstrap, name=w.name + f"_reboot{rebootstrap}") if rebootstrap else w
+
+
+def _config(idx: int, n: int | None, pick) -> Workload:
     if pick is None:
         from .engine import pick_origins as pick
     if idx == 1:

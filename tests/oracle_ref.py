@@ -11,7 +11,7 @@ from pathlib import Path
 import numpy as np
 
 STAT_FIELDS = ("frontier", "traversals", "deliveries", "undelivered", "new_receipts", "duplicates", "injected",
-               "died", "reports", "seed_removals", "digest", "covered")
+               "died", "reports", "seed_removals", "digest", "covered", "reconnects")
 
 
 class OStats(C.Structure):
@@ -24,7 +24,8 @@ class OStats(C.Structure):
 class OCfg(C.Structure):
     _fields_ = [("n", C.c_uint64), ("n_msgs", C.c_uint32), ("seed", C.c_uint32), ("churn_threshold", C.c_uint32),
                 ("ping_every", C.c_uint32), ("max_missed", C.c_uint32), ("max_rounds", C.c_uint32),
-                ("min_rounds", C.c_uint32), ("threads", C.c_int), ("variant", C.c_int)]
+                ("min_rounds", C.c_uint32), ("threads", C.c_int), ("variant", C.c_int), ("extra_cap", C.c_uint32),
+                ("list_len", C.c_uint32)]
 
 
 class OReport(C.Structure):
@@ -85,10 +86,12 @@ class Oracle:
         return self.gen(w.graph, w.n, arg, w.rng_seed, threads)
 
     def simulate(self, rp, col, n, n_msgs, origins, inject_rounds, *, seed=0, churn_threshold=0, ping_every=0,
-                 max_missed=3, max_rounds=4096, min_rounds=0, kills=(), variant=0, threads=8):
+                 max_missed=3, max_rounds=4096, min_rounds=0, kills=(), variant=0, threads=8, extra_cap=0,
+                 list_len=6):
         rp = np.ascontiguousarray(rp, dtype=np.uint64)
         col = np.ascontiguousarray(col if len(col) else np.zeros(1), dtype=np.uint32)
-        cfg = OCfg(n, n_msgs, seed, churn_threshold, ping_every, max_missed, max_rounds, min_rounds, threads, variant)
+        cfg = OCfg(n, n_msgs, seed, churn_threshold, ping_every, max_missed, max_rounds, min_rounds, threads, variant,
+                   extra_cap, list_len)
         s = self.L.oracle_sim_create(C.byref(cfg), _p(rp, C.c_uint64), _p(col, C.c_uint32))
         assert s, "oracle_sim_create failed"
         s = C.c_void_p(s)
@@ -117,8 +120,11 @@ class Oracle:
             reg = np.zeros(n, dtype=np.uint8)
             self.L.oracle_sim_registered(s, _p(reg, C.c_uint8))
             sent = int(self.L.oracle_sim_sent_to_total(s))
+            ex_cnt = np.zeros(n, dtype=np.uint32)
+            ex_col = np.zeros(max(n * extra_cap, 1), dtype=np.uint32)
+            self.L.oracle_sim_extra(s, _p(ex_cnt, C.c_uint32), _p(ex_col, C.c_uint32))
             return dict(stats=stats, seen=seen, coverage=cov, reports=reps, alive=alive, registered=reg,
-                        sent_to_total=sent)
+                        sent_to_total=sent, extra_counts=ex_cnt, extra_cols=ex_col[:n * extra_cap].reshape(n, extra_cap))
         finally:
             self.L.oracle_sim_destroy(s)
 
@@ -126,7 +132,7 @@ class Oracle:
         return self.simulate(rp, col, w.n, w.n_msgs, w.origins, w.inject_rounds, seed=w.rng_seed,
                              churn_threshold=w.churn_threshold, ping_every=w.ping_every, max_missed=w.max_missed,
                              min_rounds=w.min_rounds, kills=w.kills, variant=variant, threads=threads,
-                             max_rounds=max_rounds)
+                             max_rounds=max_rounds, extra_cap=w.extra_cap, list_len=w.list_len)
 
 
 class OraclePartition:

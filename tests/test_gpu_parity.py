@@ -167,3 +167,25 @@ def test_push_equals_pull_at_full_size():
     for mode in ("auto", "pull", "bin"):
         assert out["push"][0] == out[mode][0], mode
         assert np.array_equal(out["push"][1], out[mode][1]), mode
+
+
+@pytest.mark.parametrize("idx,n,cap", [(5, 1 << 14, 4), (5, 50_000, 16), (1, None, 8), (1, 40, 3)])
+def test_rebootstrap_parity(oracle, idx, n, cap):
+    """Re-bootstrap after a death (handleDeadPeer
+    peer.cpp:398-404): extra out-edges, their liveness and the pushes over
+    them, bit-exact against the oracle."""
+    w = config(idx, n, pick=oracle.pick_origins, rebootstrap=cap)
+    rp, col = oracle.gen_workload(w)
+    ref = oracle.simulate_workload(w, rp, col)
+    with _engine(w) as e:
+        e.build_graph()
+        e.inject(w.origins, w.inject_rounds)
+        if w.kills:
+            e.schedule_kills([k[0] for k in w.kills], [k[1] for k in w.kills])
+        e.reset()
+        first = _compare(e, ref, w)
+        cnt, ex = e.read_extra()
+        assert np.array_equal(cnt, ref["extra_counts"])
+        assert np.array_equal(ex, ref["extra_cols"])
+        e.reset()
+        assert e.run() == first

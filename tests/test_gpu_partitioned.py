@@ -115,3 +115,17 @@ def test_partitioned_gpu_equals_oracle(oracle, idx, n, P, pull, sparse, binned):
     assert rounds == ref["stats"]
     assert np.array_equal(seen, ref["seen"])
     assert np.array_equal(reps, ref["reports"])
+
+
+@pytest.mark.parametrize("P", [2, 3])
+def test_partitioned_rebootstrap_equals_oracle(oracle, P):
+    """Re-bootstrap is per reporter, so a vertex-partitioned run adds the same
+    edges as the single-partition oracle."""
+    w = config(5, 1 << 15, pick=oracle.pick_origins, rebootstrap=8)
+    rp, col = oracle.gen_workload(w)
+    ref = oracle.simulate_workload(w, rp, col)
+    rounds, seen, reps, csrs, part, modes = run_partitioned(w, P, True, True)
+    assert rounds == ref["stats"]
+    assert np.array_equal(seen, ref["seen"])
+    assert np.array_equal(reps, ref["reports"])
+    assert sum(r["reconnects"] for r in rounds) > 0

@@ -4,6 +4,8 @@ import hashlib
 import json
 from pathlib import Path
 
+from dataclasses import replace
+
 import numpy as np
 import pytest
 
@@ -143,3 +145,37 @@ def test_config1_literal_reference_run(oracle):
 def test_pick_origins_distinct(oracle):
     o = oracle.pick_origins(1 << 20, 0x5EED0003, 64)
     assert len(set(o.tolist())) == 64 and o.max() < (1 << 20)
+
+
+@pytest.mark.parametrize("idx,n,cap", [(5, 1 << 12, 4), (5, 3000, 16), (1, None, 8), (1, 40, 3)])
+def test_rebootstrap_literal_equals_fast(oracle, idx, n, cap):
+    """Re-bootstrap after a death (handleDeadPeer peer.cpp:398-404): both
+    round drivers add the same out-edges and deliver over them identically."""
+    w = config(idx, n, pick=oracle.pick_origins, rebootstrap=cap)
+    rp, col = oracle.gen_workload(w)
+    fast = oracle.simulate_workload(w, rp, col, variant=0)
+    lit = oracle.simulate_workload(w, rp, col, variant=1)
+    assert fast["stats"] == lit["stats"]
+    assert np.array_equal(fast["seen"], lit["seen"])
+    assert np.array_equal(fast["extra_counts"], lit["extra_counts"])
+    assert np.array_equal(fast["extra_cols"], lit["extra_cols"])
+    assert sum(s["reconnects"] for s in fast["stats"]) == int(fast["extra_counts"].sum())
+    if idx == 5:   # at n = 8 the literal DAG already links every candidate: nothing new to add
+        assert fast["extra_counts"].sum() > 0
+
+
+def test_rebootstrap_edges_are_new_live_and_bounded(oracle):
+    w = config(5, 1 << 12, pick=oracle.pick_origins, rebootstrap=6)
+    rp, col = oracle.gen_workload(w)
+    out = oracle.simulate_workload(w, rp, col)
+    cnt, ex = out["extra_counts"], out["extra_cols"]
+    assert int(cnt.max()) <= 6
+    reporters = set(out["reports"][:, 1].tolist())
+    for u in np.nonzero(cnt)[0].tolist():
+        assert u in reporters                                  # only peers that detected a death re-select
+        targets = (ex[u, :cnt[u]] & np.uint32(0x7FFFFFFF)).tolist()
+        assert len(set(targets)) == len(targets)               # connectedPeers is a map
+        assert u not in targets
+        assert not set(targets) & set(col[rp[u]:rp[u + 1]].tolist())
+    off = oracle.simulate_workload(replace(w, extra_cap=0), rp, col)
+    assert all(s["reconnects"] == 0 for s in off["stats"])

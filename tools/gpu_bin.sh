@@ -1,9 +1,7 @@
 #!/bin/bash
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-mkdir -p gpurun_out/bin
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "bin" > gpurun_out/bin/pytest.log 2>&1 || { tail -40 gpurun_out/bin/pytest.log; exit 1; }
-tail -2 gpurun_out/bin/pytest.log
-timeout -k 10 120 python -u tools/bin_probe.py 4 || exit 1
-timeout -k 10 120 python -u tools/bin_probe.py 4 || exit 1
-bash tools/sweep_env.sh - -
+mkdir -p gpurun_out/rb
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/rb/pytest.log 2>&1 || { grep -E "PASS|FAIL|Error|error" gpurun_out/rb/pytest.log | tail -30; exit 1; }
+tail -3 gpurun_out/rb/pytest.log
+bash tools/sweep_env.sh -
