@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--pull-permille", type=int, default=0, help="push/pull switch point (0 = engine default)")
     ap.add_argument("--front-permille", type=int, default=0, help="frontier-bitmap switch point (0 = default)")
     ap.add_argument("--mode", default="auto", choices=["auto", "push", "pull"])
+    ap.add_argument("--rebootstrap", type=int, default=0,
+                    help="re-bootstrap after a death with this many extra out-edges per peer (configs 1, 5)")
     ap.add_argument("--force-partitioned", action="store_true",
                     help="use the multi-rank driver (RCCL collectives) even at WORLD_SIZE 1")
     return ap.parse_args()
@@ -131,7 +133,7 @@ def main():
     from gossip_hip import Engine
     from gossip_hip.workloads import config
 
-    w = config(args.config, args.n or None)
+    w = config(args.config, args.n or None, rebootstrap=args.rebootstrap)
     tune = dict(pull_permille=args.pull_permille, front_permille=args.front_permille, mode=args.mode)
     partitioned = world > 1 or args.force_partitioned
     if partitioned:

@@ -404,10 +404,13 @@ gossip_status rebootstrap_round(gossip_ctx* c, const RoundArgs& a) {
                                                  0, 64, c->stream));
         HIPCHK(hipMalloc(&c->rb_temp, c->rb_temp_bytes + 16));
     }
-    HIPCHK(launch_reboot_keys(a, c->n_rep_seen, n, c->rb_keys, c->stream));
-    size_t tb = c->rb_temp_bytes;
-    HIPCHK(hipcub::DeviceRadixSort::SortKeys(c->rb_temp, tb, c->rb_keys, c->rb_keys2, (size_t)n, 0, 64, c->stream));
-    HIPCHK(launch_rebootstrap(a, c->reboot, c->rb_keys2, n, c->stream));
+    HIPCHK(timed(c, "rebootstrap", [&] {
+        hipError_t e = launch_reboot_keys(a, c->n_rep_seen, n, c->rb_keys, c->stream);
+        size_t tb = c->rb_temp_bytes;
+        if (e == hipSuccess)
+            e = hipcub::DeviceRadixSort::SortKeys(c->rb_temp, tb, c->rb_keys, c->rb_keys2, (size_t)n, 0, 64, c->stream);
+        return e != hipSuccess ? e : launch_rebootstrap(a, c->reboot, c->rb_keys2, n, c->stream);
+    }));
     c->n_rep_seen = upto;
     return GOSSIP_OK;
 }
