@@ -460,8 +460,12 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
                                  c->inj_round_sorted.begin());
         for (int w = 0; w < kMaxWords; ++w) a.inj_mask[w] = hi ? c->inj_prefix[(uint64_t)(hi - 1) * kMaxWords + w] : 0;
     }
-    const bool pull_ok = c->symmetric && !c->any_dead && !(c->cfg.flags & GOSSIP_FLAG_FORCE_PUSH) &&
-                         (!remote || c->gather != nullptr);
+    // dead peers are fine for pull / binned rounds (a live peer's in-edges from
+    // live peers are never masked: only edges to dead peers are); re-bootstrap
+    // edges are not (they break the symmetry the pull relies on)
+    const bool pull_ok = c->symmetric && (!c->any_dead || !c->cfg.extra_cap) &&
+                         !(c->cfg.flags & GOSSIP_FLAG_FORCE_PUSH) && (!remote || c->gather != nullptr);
+    a.dead_mode = c->any_dead ? 1u : 0u;
     bool pull;
     if (requested == GOSSIP_MODE_AUTO) {
         const uint32_t permille = c->cfg.pull_permille ? c->cfg.pull_permille : 50;
@@ -532,6 +536,8 @@ gossip_status round_compute(gossip_ctx* c) {
     RoundArgs a = c->cur;
     const uint32_t pw = pack_w(c);
     c->in_round = false;
+    if (c->last_pull && a.dead_mode)
+        HIPCHK(timed(c, "src_count", [&] { return launch_src_count(a, pw, c->stream); }));
     if (c->last_bin) {
         BinArgs b{c->bins.bins,        c->bins.n_bins,   c->bins.cb_slot, c->bins.cb_src, c->bins.chunk_begin,
                   c->bins.n_chunks,    c->bins.chunk,    c->bins.units,   c->bins.xcd_units, c->bins.bdst,
@@ -587,6 +593,10 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
             c->kbytes["bin_scatter"] += wb * n_src + 16.0 * d.frontier + 6.0 * c->bins.n_binned + wb * (double)d.pull_gathers;
             c->kbytes["bin_apply"] += (2.0 + wb) * (double)d.pull_edges + 2.0 * wb * c->n_local;
             c->kbytes["pull_heavy"] += 12.0 * (double)d.heavy_traversals;
+        }
+        if (c->last_pull && c->cur.dead_mode) c->kbytes["src_count"] += 32.0 * d.frontier + 4.125 * (double)d.traversals;
+        if (c->last_bin) {
+            // booked above
         } else if (c->last_pull) {
             if (c->last_front) c->kbytes["frontier_bits"] += 8.125 * (c->gather ? c->n : c->n_local);
             c->kbytes["pull_light"] += 40.0 * c->n_local + 4.0 * (double)d.pull_edges + 8.0 * (double)d.pull_gathers;

@@ -111,7 +111,8 @@ struct RoundArgs {
     uint32_t round;
     uint32_t max_missed;
     uint32_t heavy;                // light/heavy row threshold (rows > heavy are chunked)
-    uint32_t pad0;
+    uint32_t dead_mode;            // some peers are dead: dense rounds skip dead destinations and the
+                                   // traversal stats come from k_src_count (per-edge alive test)
     uint64_t inj_mask[kMaxWords];  // messages injected so far (pull: bits a peer can still learn)
     uint64_t* front;               // pull rounds: 1 bit per source peer, set iff its new words are nonzero
     const uint64_t* nw_src;        // pull rounds: new words of every source, indexed by (global) peer id
@@ -157,6 +158,7 @@ hipError_t launch_reboot_keys(const RoundArgs& a, uint64_t first, uint64_t n, un
 // keys sorted: every reporter re-selects once per report, in dead order
 hipError_t launch_rebootstrap(const RoundArgs& a, const RebootArgs& r, const unsigned long long* keys, uint64_t n,
                               hipStream_t s);
+hipError_t launch_src_count(const RoundArgs& a, uint32_t W, hipStream_t s);
 hipError_t launch_coverage(const uint64_t* words, uint64_t n_local, uint32_t W, unsigned long long* counts,
                            hipStream_t s);
 hipError_t launch_heavy_count(const uint64_t* rp, uint64_t n_local, uint32_t heavy, unsigned long long* n_chunks,

@@ -301,11 +301,12 @@ __global__ __launch_bounds__(kBlock) void k_pull_light(RoundArgs a, uint32_t wd)
         const bool vv = v < a.n_local;
         uint64_t m[W], need[W], sv[W];
         bool act = false, needy = false;
+        const bool va = vv && (!a.dead_mode || bit_alive(a.alive, (uint32_t)(a.begin + v)));  // dead: no receive
 #pragma unroll
         for (int w = 0; w < W; ++w) {
             m[w] = vv ? ld_s<NT>(a.nw + v * W + w) : 0ull;
             sv[w] = vv ? ld_s<NT>(a.seen + v * W + w) : ~0ull;
-            need[w] = a.inj_mask[w] & ~sv[w];
+            need[w] = va ? a.inj_mask[w] & ~sv[w] : 0ull;
             act |= m[w] != 0;
             needy |= need[w] != 0;
         }
@@ -331,8 +332,10 @@ __global__ __launch_bounds__(kBlock) void k_pull_light(RoundArgs a, uint32_t wd)
             }
             acc.frontier++;
             acc.covered += pc;
-            acc.trav += d;
-            acc.deliv += (unsigned long long)pc * d;
+            if (!a.dead_mode) {  // every edge alive and unmasked; else k_src_count books them
+                acc.trav += d;
+                acc.deliv += (unsigned long long)pc * d;
+            }
         }
         const bool light = d <= a.heavy;
 #pragma unroll
@@ -370,6 +373,9 @@ __global__ __launch_bounds__(kBlock) void k_pull_light(RoundArgs a, uint32_t wd)
 #pragma unroll
             for (int j = 0; j < kPullUnroll; ++j) u[j] = (ok >> j) & 1 ? ld_s<NT>(a.col + e[j]) : 0u;
             acc.pulled += (unsigned)__builtin_popcount(ok);
+#pragma unroll
+            for (int j = 0; j < kPullUnroll; ++j)  // masked: the neighbour is dead, its words are zero
+                if (u[j] & kMaskedEdge) ok &= ~(1u << j);
             if (FRONT) {
                 uint64_t fb[kPullUnroll];
 #pragma unroll
@@ -431,6 +437,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_heavy(RoundArgs a) {
             // one lane reads, every lane uses the same value: the branch below stays wave-uniform
             const uint64_t s0 = __shfl(a.seen[(uint64_t)ch.v * W + w], 0);
             need[w] = a.inj_mask[w] & ~s0;
+            if (a.dead_mode && !bit_alive(a.alive, (uint32_t)(a.begin + ch.v))) need[w] = 0;  // dead: no receive
             part[w] = 0;
             any |= need[w] != 0;
         }
@@ -438,6 +445,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_heavy(RoundArgs a) {
         for (uint64_t e = ch.e0 + lane; e < ch.e1; e += 64) {
             const uint32_t u = a.col[e];
             acc.pulled++;
+            if (u & kMaskedEdge) continue;  // the neighbour is dead, its words are zero
             if (a.front && !((a.front[u >> 6] >> (u & 63)) & 1ull)) continue;
 #pragma unroll
             for (int w = 0; w < W; ++w)
@@ -565,8 +573,10 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_lds(RoundArgs a, 
                 if (!pcs[kk]) continue;
                 acc.frontier++;
                 acc.covered += pcs[kk];
-                acc.trav += d1[kk] - d0[kk];
-                acc.deliv += (unsigned long long)pcs[kk] * (d1[kk] - d0[kk]);
+                if (!a.dead_mode) {  // else k_src_count books them
+                    acc.trav += d1[kk] - d0[kk];
+                    acc.deliv += (unsigned long long)pcs[kk] * (d1[kk] - d0[kk]);
+                }
             }
         }
         __syncthreads();
@@ -627,7 +637,8 @@ __global__ __launch_bounds__(kB) void k_bin_apply(RoundArgs a, BinArgs b) {
     bool needy = false;
     for (uint32_t i = threadIdx.x; i < nv * W; i += kB) {
         acc_s[i] = 0ull;
-        needy |= (a.inj_mask[i % W] & ~a.seen[v0 * W + i]) != 0;
+        const bool va = !a.dead_mode || bit_alive(a.alive, (uint32_t)(a.begin + v0 + i / W));
+        needy |= va && (a.inj_mask[i % W] & ~a.seen[v0 * W + i]) != 0;
     }
     if (!__syncthreads_or(needy)) {
         for (uint32_t i = threadIdx.x; i < nv * W; i += kB) a.nx[v0 * W + i] = 0ull;
@@ -658,7 +669,8 @@ __global__ __launch_bounds__(kB) void k_bin_apply(RoundArgs a, BinArgs b) {
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < nv * W; i += kB) {
         const uint64_t sv = a.seen[v0 * W + i];
-        const uint64_t fr = acc_s[i] & a.inj_mask[i % W] & ~sv;
+        const bool va = !a.dead_mode || bit_alive(a.alive, (uint32_t)(a.begin + v0 + i / W));  // dead: no receive
+        const uint64_t fr = va ? acc_s[i] & a.inj_mask[i % W] & ~sv : 0ull;
         if (fr) {  // handleClient: new -> Message-List insert (peer.cpp:281-282)
             a.seen[v0 * W + i] = sv | fr;
             acc.fresh += (unsigned long long)__popcll(fr);
@@ -667,6 +679,59 @@ __global__ __launch_bounds__(kB) void k_bin_apply(RoundArgs a, BinArgs b) {
         a.nx[v0 * W + i] = fr;  // heavy rows: 0 here, OR-ed by k_pull_heavy afterwards
     }
     flush<kB / 64>(acc, a.st);
+}
+
+// ---------------------------------------------------------------------------
+// Source side of a dense round with dead peers (broadcastMessage,
+// peer.cpp:310-316): every unmasked out-edge of a frontier peer is a
+// traversal, a delivery to a live target and an undelivered send to a dead
+// one.  Reads only; the receive side is the pull / binned kernels'.
+// ---------------------------------------------------------------------------
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_src_count(RoundArgs a) {
+    Acc acc;
+    const int lane = threadIdx.x & 63;
+    const uint64_t n_tiles = (a.n_local + 63) >> 6;
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); t < n_tiles; t += nwaves) {
+        const uint64_t v = (t << 6) + lane;
+        uint32_t pc = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) pc += v < a.n_local ? (uint32_t)__popcll(a.nw[v * W + w]) : 0u;
+        if (!__any(pc != 0)) continue;
+        uint32_t deg = 0;
+        uint64_t rb = 0;
+        if (pc) {
+            rb = a.rp[v];
+            const uint64_t d = a.rp[v + 1] - rb;
+            deg = d <= a.heavy ? (uint32_t)d : 0u;
+        }
+        tile_edges(deg, rb, [&](int s, bool valid, uint64_t e) {
+            const uint32_t pcs = __shfl(pc, s);
+            if (!valid) return;
+            const uint32_t c = a.col[e];
+            if (c & kMaskedEdge) return;
+            acc.trav++;
+            if (bit_alive(a.alive, c)) acc.deliv += pcs;
+            else acc.undeliv += pcs;
+        });
+    }
+    // heavy rows: one wave per chunk
+    for (uint64_t ci = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); ci < a.n_chunks; ci += nwaves) {
+        const HeavyChunk ch = a.chunks[ci];
+        uint32_t pc = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) pc += (uint32_t)__popcll(a.nw[(uint64_t)ch.v * W + w]);
+        if (!pc) continue;
+        for (uint64_t e = ch.e0 + lane; e < ch.e1; e += 64) {
+            const uint32_t c = a.col[e];
+            if (c & kMaskedEdge) continue;
+            acc.trav++;
+            if (bit_alive(a.alive, c)) acc.deliv += pc;
+            else acc.undeliv += pc;
+        }
+    }
+    flush(acc, a.st);
 }
 
 // ---------------------------------------------------------------------------
@@ -1339,6 +1404,13 @@ hipError_t launch_rebootstrap(const RoundArgs& a, const RebootArgs& r, const uns
                               hipStream_t s) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_rebootstrap, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, a, r, keys, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_src_count(const RoundArgs& a, uint32_t W_, hipStream_t s) {
+    const uint64_t tiles = (a.n_local + 63) / 64;
+    GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_src_count<W>, dim3(grid_for(tiles, kWavesPerBlock)), dim3(kBlock),
+                                                   0, s, a));
     return hipGetLastError();
 }
 

@@ -95,7 +95,7 @@ def test_multiword_messages(oracle, M, mode):
     origins = rng.integers(0, n, M).astype(np.uint32)
     rounds = rng.integers(0, 4, M).astype(np.uint32)
     rp, col = oracle.gen("powerlaw", n, 6, 77)
-    churn = 42949673 * 2 if mode == "push" else 0   # pull/binned rounds need a churn-free run
+    churn = 42949673 * 2   # dead peers: pull and binned rounds skip them as destinations
     ref = oracle.simulate(rp, col, n, M, origins, rounds, seed=77, churn_threshold=churn, ping_every=2,
                           max_missed=2)
     with Engine(n, M, rng_seed=77, churn_threshold=churn, ping_every=2, max_missed=2, mode=mode) as e:
