@@ -29,8 +29,10 @@
 //   units, xcd_units: scatter work units and their split over the 8 XCDs
 // Construction: (a) 64-bit key (bin << 32 | source) per edge of a light row,
 // radix sort -> slot of an edge = b.s0 + (position - b.u0), so a bin's slots are
-// in source order; (b) key = chunk(source) * n_bins + bin, sort -> cb order.
-// The (chunk, bin) slots are contiguous because chunks are source ranges.
+// in source order; (b) key = chunk(source) * n_bins + bin per slot-order
+// position, stable sort -> cb order.  The (chunk, bin) slots are contiguous
+// because chunks are source ranges, and the cb entries of a pair are in slot
+// order, so a run of consecutive entries stores to consecutive slots.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -93,39 +95,37 @@ __global__ void k_bin_keys(const uint32_t* row, const uint32_t* col, uint64_t m,
 }
 
 __global__ void k_bin_assign(const unsigned long long* skeys, const uint32_t* svals, uint64_t m, const Bin* bins,
-                             uint32_t n_bins, const uint32_t* row, uint32_t* slot, uint16_t* bdst) {
+                             uint32_t n_bins, const uint32_t* row, uint16_t* bdst) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t b = skeys[i] >> 32;
-        const uint32_t e = svals[i];
-        if (b >= n_bins) {
-            slot[e] = kNoSlot;
-            continue;
-        }
+        if (b >= n_bins) continue;
         const Bin bn = bins[b];
-        const uint64_t pos = bn.s0 + (i - bn.u0);
-        slot[e] = (uint32_t)pos;
-        bdst[pos] = (uint16_t)(row[e] - bn.v0);
+        bdst[bn.s0 + (i - bn.u0)] = (uint16_t)(row[svals[i]] - bn.v0);
     }
 }
 
-// (b) key = chunk(source) * n_bins + bin(destination row); unbinned edges last.
-__global__ void k_cb_keys(const uint32_t* slot, const uint32_t* row, const uint32_t* col, uint64_t m,
-                          const uint32_t* bin_of_tile, uint32_t n_bins, uint32_t chunk, uint32_t* keys,
-                          uint32_t* vals) {
-    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t u = col[e] & ~kMaskedEdge;
-        keys[e] = slot[e] == kNoSlot ? kNoSlot : (u / chunk) * n_bins + bin_of_tile[row[e] >> 6];
-        vals[e] = (uint32_t)e;
+// (b) per position i of the slot order (sorted keys of (a)): key = chunk(source)
+// * n_bins + bin.  Sorted stably, so the entries of a (chunk, bin) pair stay
+// in slot order: consecutive cb entries of a pair have consecutive slots.
+__global__ void k_cb_keys(const unsigned long long* skeys, uint64_t n_binned, uint32_t n_bins, uint32_t chunk,
+                          uint32_t* keys, uint32_t* vals) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_binned;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = skeys[i];
+        keys[i] = (uint32_t)(k & 0xFFFFFFFFu) / chunk * n_bins + (uint32_t)(k >> 32);
+        vals[i] = (uint32_t)i;
     }
 }
 
-__global__ void k_cb_fill(const uint32_t* svals, uint64_t n_binned, const uint32_t* slot, const uint32_t* col,
+__global__ void k_cb_fill(const uint32_t* svals, uint64_t n_binned, const unsigned long long* skeys, const Bin* bins,
                           uint32_t chunk, uint32_t* cb_slot, uint16_t* cb_src) {
     for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n_binned;
          p += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t e = svals[p];
-        cb_slot[p] = slot[e];
-        cb_src[p] = (uint16_t)((col[e] & ~kMaskedEdge) % chunk);  // source, local to its chunk
+        const uint32_t i = svals[p];
+        const uint64_t k = skeys[i];
+        const Bin bn = bins[k >> 32];
+        cb_slot[p] = (uint32_t)(bn.s0 + (i - bn.u0));
+        cb_src[p] = (uint16_t)((uint32_t)(k & 0xFFFFFFFFu) % chunk);  // source, local to its chunk
     }
 }
 
@@ -190,7 +190,7 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
     uint32_t* bin_of_tile = nullptr;
     unsigned long long *keys64_in = nullptr, *keys64_out = nullptr;
     uint32_t *keys_in = nullptr, *vals_in = nullptr, *keys_out = nullptr, *vals_out = nullptr;
-    uint32_t *slot = nullptr, *row = nullptr;
+    uint32_t* row = nullptr;
     uint64_t chunk_words = kBinChunkWords;
     if (const char* c = std::getenv("GOSSIP_BIN_CHUNK"))
         chunk_words = std::max<uint64_t>(512, std::min<uint64_t>(kBinChunkWords, std::strtoull(c, nullptr, 0) / 512 * 512));
@@ -245,7 +245,7 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
     // (the kNoSlot sentinel's low end_bit2 bits are all ones: it sorts last)
     while ((1ull << end_bit2) <= n_chunks * h_bins.size()) ++end_bit2;
 
-    // memory peak: row + slot + 64-bit keys in/out + vals in/out (+ temp) next to bdst/val
+    // memory peak: row + 64-bit keys in/out + vals in/out (+ temp) next to bdst/val
     BCHECK(hipMemGetInfo(&free_b, &total_b));
     {
         const uint64_t persist = slots * 2 + slots * Wp * 8 + upos * 8 + h_bins.size() * sizeof(Bin);
@@ -289,29 +289,28 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
     st.n_binned = upos;
     st.n_chunks = n_chunks;
     st.chunk = chunk;
-    BCHECK(hipMalloc((void**)&slot, (m + 1) * sizeof(uint32_t)));
     BCHECK(hipMalloc((void**)&st.bdst, (slots + kBinSlotPad) * sizeof(uint16_t)));
     BCHECK(hipMalloc((void**)&st.val, (slots + kBinSlotPad) * Wp * sizeof(uint64_t)));
     BCHECK(hipMemsetAsync(st.bdst, 0, (slots + kBinSlotPad) * sizeof(uint16_t), s));
     BCHECK(hipMemsetAsync(st.val, 0, (slots + kBinSlotPad) * Wp * sizeof(uint64_t), s));
     hipLaunchKernelGGL(k_bin_assign, dim3(gridn(m)), dim3(256), 0, s, keys64_out, vals_out, m, st.bins,
-                       (uint32_t)st.n_bins, row, slot, st.bdst);
+                       (uint32_t)st.n_bins, row, st.bdst);
     BCHECK(hipGetLastError());
     BCHECK(hipStreamSynchronize(s));
-    hipFree(keys64_out);
-    keys64_out = nullptr;
+    hipFree(row);
+    row = nullptr;
 
-    // (b) cb order: (source chunk, bin)
-    BCHECK(hipMalloc((void**)&keys_in, (m + 1) * sizeof(uint32_t)));
-    BCHECK(hipMalloc((void**)&keys_out, (m + 1) * sizeof(uint32_t)));
-    hipLaunchKernelGGL(k_cb_keys, dim3(gridn(m)), dim3(256), 0, s, slot, row, col, m, bin_of_tile,
-                       (uint32_t)st.n_bins, (uint32_t)chunk, keys_in, vals_in);
+    // (b) cb order: (source chunk, bin), slot order inside a pair
+    BCHECK(hipMalloc((void**)&keys_in, (upos + 1) * sizeof(uint32_t)));
+    BCHECK(hipMalloc((void**)&keys_out, (upos + 1) * sizeof(uint32_t)));
+    hipLaunchKernelGGL(k_cb_keys, dim3(gridn(upos)), dim3(256), 0, s, keys64_out, upos, (uint32_t)st.n_bins,
+                       (uint32_t)chunk, keys_in, vals_in);
     BCHECK(hipGetLastError());
     temp_bytes = 0;
-    BCHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, keys_in, keys_out, vals_in, vals_out, (size_t)m, 0,
-                                              end_bit2, s));
+    BCHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, keys_in, keys_out, vals_in, vals_out, (size_t)upos,
+                                              0, end_bit2, s));
     BCHECK(hipMalloc(&temp, temp_bytes + 16));
-    BCHECK(hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys_in, keys_out, vals_in, vals_out, (size_t)m, 0,
+    BCHECK(hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys_in, keys_out, vals_in, vals_out, (size_t)upos, 0,
                                               end_bit2, s));
     BCHECK(hipStreamSynchronize(s));
     hipFree(keys_in);
@@ -322,13 +321,15 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
     BCHECK(hipMalloc((void**)&st.cb_slot, (upos + 1) * sizeof(uint32_t)));
     BCHECK(hipMalloc((void**)&st.cb_src, (upos + 1) * sizeof(uint16_t)));
     BCHECK(hipMalloc((void**)&st.chunk_begin, (n_chunks + 1) * sizeof(uint64_t)));
-    hipLaunchKernelGGL(k_cb_fill, dim3(gridn(upos)), dim3(256), 0, s, vals_out, upos, slot, col, (uint32_t)chunk,
-                       st.cb_slot, st.cb_src);
+    hipLaunchKernelGGL(k_cb_fill, dim3(gridn(upos)), dim3(256), 0, s, vals_out, upos, keys64_out, st.bins,
+                       (uint32_t)chunk, st.cb_slot, st.cb_src);
     BCHECK(hipGetLastError());
     hipLaunchKernelGGL(k_chunk_bounds, dim3(gridn(n_chunks + 1)), dim3(256), 0, s, keys_out, upos,
                        (uint32_t)st.n_bins, n_chunks, st.chunk_begin);
     BCHECK(hipGetLastError());
     BCHECK(hipStreamSynchronize(s));
+    hipFree(keys64_out);
+    keys64_out = nullptr;
 
     // scatter work units: chunks split into <= kBinUnitCap entries (every chunk
     // has at least one: its first unit books the chunk's source-side stats);
@@ -375,7 +376,6 @@ done:
     hipFree(keys_out);
     hipFree(vals_out);
     hipFree(temp);
-    hipFree(slot);
     hipFree(row);
     if (rc != hipSuccess) {
         hipGetLastError();  // clear a sticky allocation error

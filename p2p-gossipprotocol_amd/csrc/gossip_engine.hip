@@ -123,6 +123,7 @@ struct gossip_ctx {
     bool last_bin = false;       // the pull round in flight runs binned
     uint64_t last_fresh = 0;     // new receipts of the previous round
     bool bin_noskip = false;     // GOSSIP_BIN_NOSKIP: rewrite every slot each binned round (A/B measurement)
+    uint32_t scatter_probe = 0;  // GOSSIP_SCATTER_PROBE: partial scatter for timing breakdowns (wrong results)
     uint64_t* seg = nullptr;     // sparse push: per-destination record segments (world x chunk records)
     unsigned long long* d_counts = nullptr;  // records per destination rank
     uint64_t* h_counts = nullptr;            // pinned copy
@@ -541,7 +542,7 @@ gossip_status round_compute(gossip_ctx* c) {
     if (c->last_bin) {
         BinArgs b{c->bins.bins,        c->bins.n_bins,   c->bins.cb_slot, c->bins.cb_src, c->bins.chunk_begin,
                   c->bins.n_chunks,    c->bins.chunk,    c->bins.units,   c->bins.xcd_units, c->bins.bdst,
-                  c->bins.val,         c->bins.bin_words, c->bins.nz[c->bins.nz_cur], c->bins.nz[c->bins.nz_cur ^ 1]};
+                  c->bins.val,         c->bins.bin_words, c->bins.nz[c->bins.nz_cur], c->bins.nz[c->bins.nz_cur ^ 1], c->scatter_probe};
         HIPCHK(timed(c, "bin_scatter", [&] { return launch_bin_scatter(a, b, pw, c->stream); }));
         HIPCHK(timed(c, "bin_apply", [&] { return launch_bin_apply(a, b, pw, c->stream); }));
         if (!c->bin_noskip) c->bins.nz_cur ^= 1;
@@ -696,6 +697,7 @@ gossip_status gossip_create(const gossip_config* cfg, gossip_ctx** out) {
     if (const char* u = std::getenv("GOSSIP_PULL_NT"); u && std::atoi(u)) c->pull_unroll |= kPullNT;
     if (const char* h = std::getenv("GOSSIP_HEAVY_DEGREE")) c->heavy = (uint32_t)std::max(1, std::atoi(h));
     if (const char* u = std::getenv("GOSSIP_BIN_NOSKIP"); u && std::atoi(u)) c->bin_noskip = true;
+    if (const char* u = std::getenv("GOSSIP_SCATTER_PROBE")) c->scatter_probe = (uint32_t)std::atoi(u);
     if (const char* b = std::getenv("GOSSIP_BIN_PERMILLE"); b && !cfg->bin_permille) c->cfg.bin_permille = (uint32_t)std::atoi(b);
     c->n = cfg->n_peers;
     c->begin = b;

@@ -35,7 +35,7 @@ constexpr uint32_t kBinWords = 18432;       // LDS accumulator words per bin (14
 constexpr uint32_t kBinSlotPad = 8;         // bin slot ranges padded to 8 slots (16-B loads)
 constexpr uint64_t kBinSlotCap = 1u << 18;  // slots per bin (load balance between bins)
 constexpr uint32_t kBinChunkWords = 18432;     // source chunk: its new words (144 KB) are staged in LDS
-constexpr uint64_t kBinUnitCap = 1u << 16;     // cb entries per scatter work unit (hub chunks are split)
+constexpr uint64_t kBinUnitCap = 1u << 17;     // cb entries per scatter work unit (hub chunks are split)
 constexpr int kScatterBlock = 1024;            // k_bin_scatter_lds: one 16-wave workgroup per CU
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 
@@ -64,6 +64,8 @@ struct BinArgs {
     uint32_t bin_words;           // LDS accumulator words of a bin (kBinWords or kBinWords / 2)
     const uint64_t* nz_prev;      // per source bit: its slots hold nonzero words (previous binned round)
     uint64_t* nz_next;            // the same bits for this round's words
+    uint32_t probe;               // measurement only (GOSSIP_SCATTER_PROBE): 1 staging only, 2 + entry loads,
+                                  // 3 + LDS reads; results are then wrong
 };
 
 struct BinState {

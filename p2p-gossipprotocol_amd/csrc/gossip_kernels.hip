@@ -15,6 +15,7 @@
 // threshold (RoundArgs.heavy) are cut into kHeavyChunk-edge chunks, one wave
 // each, so no wave walks a long tail.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "gossip_internal.hpp"
 #include "philox.hpp"
@@ -580,6 +581,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_lds(RoundArgs a, 
             }
         }
         __syncthreads();
+        if (b.probe == 1) continue;
         // consecutive lanes take consecutive entries: the stores of one
         // instruction fall into a few slot runs (measured at config 4: 37 ms
         // per step against 57 ms with 8 consecutive entries per lane; u16
@@ -601,6 +603,15 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_lds(RoundArgs a, 
         for (uint64_t p = un.p0 + threadIdx.x; p < un.p1; p += step) {
             uint32_t sn[kU], un_[kU];
             load(p + step, sn, un_);
+            if (b.probe == 2) {
+#pragma unroll
+                for (int j = 0; j < kU; ++j) acc.gathered += sl[j] != kNoSlot && u[j] != 0xFFFFu;
+            } else if (b.probe == 3) {
+#pragma unroll
+                for (int j = 0; j < kU; ++j)
+                    if (sl[j] != kNoSlot && ((live_s[u[j] >> 6] >> (u[j] & 63)) & 1ull))
+                        acc.gathered += slice[(uint64_t)u[j] * W] & 1;
+            } else
 #pragma unroll
             for (int j = 0; j < kU; ++j) {
                 if (sl[j] == kNoSlot || !((live_s[u[j] >> 6] >> (u[j] & 63)) & 1ull)) continue;
@@ -1352,10 +1363,21 @@ hipError_t launch_apply_records(const RoundArgs& a, uint32_t W_, const uint64_t*
     return hipGetLastError();
 }
 
+// cb entries in flight per lane in k_bin_scatter_lds (GOSSIP_SCATTER_U: 4 or 8)
+static int scatter_u() {
+    static const int u = [] {
+        const char* e = getenv("GOSSIP_SCATTER_U");
+        return e && atoi(e) == 8 ? 8 : 4;
+    }();
+    return u;
+}
+
 hipError_t launch_bin_scatter(const RoundArgs& a, const BinArgs& b, uint32_t W_, hipStream_t s) {
     const uint32_t wd = wd_of(W_);
     GOSSIP_DISPATCH_W(wp_of(W_), {  // one workgroup per CU (128 KB of LDS each)
         if (a.cov) hipLaunchKernelGGL((k_bin_scatter_lds<W, true, 4>), dim3(256), dim3(kScatterBlock), 0, s, a, b, wd);
+        else if (scatter_u() == 8)
+            hipLaunchKernelGGL((k_bin_scatter_lds<W, false, 8>), dim3(256), dim3(kScatterBlock), 0, s, a, b, wd);
         else hipLaunchKernelGGL((k_bin_scatter_lds<W, false, 4>), dim3(256), dim3(kScatterBlock), 0, s, a, b, wd);
     });
     return hipGetLastError();
