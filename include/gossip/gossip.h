@@ -74,6 +74,10 @@ typedef struct gossip_config {
     uint32_t extra_cap;       /* re-bootstrap after a death (handleDeadPeer peer.cpp:398-404): a reporter
                                  re-selects from a seed response and keeps up to this many extra out-edges
                                  (0 = off, the reference's literal drop-only behaviour; <= 64) */
+    uint32_t list_cap;        /* ref_bootstrap: bytes of a seed's peer_list a peer reads -- the reference's 4 KB
+                                 recv (peer.cpp:188-190; 4095 = faithful).  A peer whose list is
+                                 longer fails registration and never starts (registered, not alive).  0 = no cap */
+    uint32_t reserved1;       /* must be 0 */
 } gossip_config;
 
 /*

@@ -16,6 +16,7 @@
 
 #include <math.h>
 #include <stdlib.h>
+#include <stdio.h>
 #include <string.h>
 #ifdef _OPENMP
 #include <omp.h>
@@ -264,6 +265,36 @@ void oracle_pick_origins(uint64_t n, uint32_t seed, uint32_t count, uint32_t* ou
     }
 }
 
+/* F10: PeerNode::connectToSeed reads one 4 KB recv (peer.cpp:186-190) and
+ * json::parse fails on a truncated peer_list (:193-207); start() needs q
+ * answers (:62-78).  Peer i's list at seeds 0..q-1 is the registry {0..i} in
+ * registration order -- the compact sorted-key JSON the seed sends
+ * (seed.cpp:117-125) -- built here entry by entry, with the build's address
+ * mapping (127.0.0.1:5000+id up to 60000 peers, else 10.a.b.c:5000+(id>>24))
+ * and a 10-digit lastSeen.  The first peer whose list exceeds list_cap bytes
+ * fails at every one of those seeds; seeds q..S-1 cannot make up the quorum,
+ * and every later list is longer still. */
+uint64_t oracle_started_under_cap(uint64_t n, uint32_t list_cap) {
+    if (!list_cap) return n;
+    uint64_t bytes = strlen("{\"peers\":[") + strlen("],\"type\":\"peer_list\"}");
+    char e[128];
+    for (uint64_t i = 0; i < n; ++i) {
+        char ip[32];
+        unsigned port;
+        if (n <= 60000) { snprintf(ip, sizeof ip, "127.0.0.1"); port = 5000u + (unsigned)i; }
+        else {
+            snprintf(ip, sizeof ip, "10.%u.%u.%u", (unsigned)((i >> 16) & 255), (unsigned)((i >> 8) & 255),
+                     (unsigned)(i & 255));
+            port = 5000u + (unsigned)(i >> 24);
+        }
+        const int len = snprintf(e, sizeof e, "%s{\"ip\":\"%s\",\"lastSeen\":%lld,\"port\":%u}", i ? "," : "", ip,
+                                 1740441600LL, port);
+        bytes += (uint64_t)len;
+        if (bytes > list_cap) return i;
+    }
+    return n;
+}
+
 /* ------------------------------------------------------------------------ */
 /* Round driver                                                             */
 /* ------------------------------------------------------------------------ */
@@ -363,6 +394,8 @@ oracle_sim* oracle_sim_create(const oracle_sim_cfg* cfg, const uint64_t* row_ptr
     s->registered = (uint8_t*)malloc(s->n);
     memset(s->alive, 1, s->n);
     memset(s->registered, 1, s->n);
+    if (cfg->n_started && cfg->n_started < s->n)  /* failed registration: registered, never alive */
+        memset(s->alive + cfg->n_started, 0, s->n - cfg->n_started);
     s->masked = (uint8_t*)calloc(s->e + 1, 1);
     s->miss = (uint8_t*)calloc(s->e + 1, 1);
     s->K = cfg->extra_cap;

@@ -73,6 +73,9 @@ int oracle_gen_powerlaw(uint64_t n, uint32_t list_len, uint32_t seed, int thread
                         uint64_t** row_ptr, uint32_t** col, uint64_t* n_edges);
 /* Philox-chosen distinct origins (used by configs 2-5). */
 void oracle_pick_origins(uint64_t n, uint32_t seed, uint32_t count, uint32_t* out);
+/* F10 (peer.cpp:186-210,62-78): peers of the literal bootstrap that start when
+ * a peer reads at most list_cap bytes of a seed's peer_list (0 = no cap) */
+uint64_t oracle_started_under_cap(uint64_t n, uint32_t list_cap);
 void oracle_free(void* p);
 
 /* ---- digest weight g(i) ------------------------- */
@@ -114,6 +117,7 @@ typedef struct oracle_sim_cfg {
     int variant;               /* 0 fast (mask), 1 literal (message lists) */
     uint32_t extra_cap;        /* re-bootstrap after a death: up to this many extra out-edges per peer (0 = off) */
     uint32_t list_len;         /* re-bootstrap: candidates per seed response (powerlaw list_len) */
+    uint64_t n_started;        /* peers >= n_started never start (failed registration, F10); 0 = all start */
 } oracle_sim_cfg;
 
 typedef struct oracle_sim oracle_sim;

@@ -100,6 +100,7 @@ struct gossip_ctx {
     bool finished = false;
     bool any_dead = false;
     bool symmetric = false;      // overlay is symmetric (pull rounds allowed)
+    uint64_t n_started = 0;      // peers 0..n_started-1 start; the rest failed registration (list_cap, F10)
     bool nx_dirty = false;       // nx holds stale words (after a pull round)
     bool last_pull = false;      // mode of the round in flight
     bool last_front = false;     // pull round used the frontier bitmap
@@ -278,6 +279,7 @@ gossip_status install_graph(gossip_ctx* c, uint64_t* d_rp, uint32_t* d_col, uint
     c->rp = d_rp;
     c->col = d_col;
     c->n_edges = m;
+    c->n_started = c->n;
     unsigned long long* d_cnt = nullptr;
     HIPCHK(hipMalloc((void**)&d_cnt, 2 * sizeof(unsigned long long)));
     HIPCHK(hipMemsetAsync(d_cnt, 0, 2 * sizeof(unsigned long long), c->stream));
@@ -339,6 +341,36 @@ void host_ref_bootstrap(uint32_t n, uint32_t n_seeds, uint32_t seed, std::vector
             if (chosen[c]) col.push_back(c);
     }
     rp[n] = col.size();
+}
+
+// Bytes of one peer_list entry (surface/formats.cpp peer_list_json with
+// peer_address(id, n) and a 10-digit lastSeen):
+// {"ip":"<ip>","lastSeen":<10 digits>,"port":<port>}
+uint64_t peer_entry_bytes(uint64_t id, uint64_t n) {
+    uint64_t ip = 9, port = 5000 + id;  // "127.0.0.1":5000+id up to 60000 peers
+    if (n > 60000) {                     // "10.a.b.c":5000+(id>>24)
+        ip = 3;
+        for (int sh = 16; sh >= 0; sh -= 8) ip += std::to_string((id >> sh) & 255).size();
+        port = 5000 + (id >> 24);
+    }
+    return 39 + ip + std::to_string(port).size();
+}
+
+// Peers that start under the 4 KB peer-list read (peer.cpp:186-210,62-78; F10):
+// peer i registers with seeds 0, 1, ... in file order; seeds 0..q-1 all hold
+// the registry {0..i} (every peer, started or not, registers there first), so
+// either all q answers fit in list_cap bytes or none does, and the seeds
+// q..S-1 alone cannot reach the quorum.  The first peer whose list
+// {"peers":[...],"type":"peer_list"} does not fit, and every later one (the
+// lists only grow), never starts.
+uint64_t started_under_cap(uint64_t n, uint32_t list_cap) {
+    if (!list_cap) return n;
+    uint64_t bytes = 31;  // {"peers":[ + ],"type":"peer_list"}
+    for (uint64_t i = 0; i < n; ++i) {
+        bytes += (i ? 1 : 0) + peer_entry_bytes(i, n);
+        if (bytes > list_cap) return i;
+    }
+    return n;
 }
 
 gossip_status upload_csr(gossip_ctx* c, const uint64_t* rp, const uint32_t* col, uint64_t m) {
@@ -672,6 +704,7 @@ gossip_status gossip_create(const gossip_config* cfg, gossip_ctx** out) {
     uint64_t b = cfg->part_begin, e = cfg->part_end;
     if (b == 0 && e == 0) e = cfg->n_peers;
     if (b >= e || e > cfg->n_peers) return fail(GOSSIP_EINVAL, "bad partition range");
+    if (cfg->reserved1) return fail(GOSSIP_EINVAL, "reserved1 must be 0");
     if (cfg->graph_model == GOSSIP_GRAPH_REF_BOOTSTRAP && cfg->n_peers > 4096)
         return fail(GOSSIP_EINVAL, "ref_bootstrap supports n_peers <= 4096");
     int ndev = 0;
@@ -798,6 +831,7 @@ gossip_status gossip_build_graph(gossip_ctx* c) {
         host_ref_bootstrap((uint32_t)c->n, c->cfg.n_seeds, c->cfg.rng_seed, rp, col);
         gossip_status st = upload_csr(c, rp.data(), col.data(), col.size());
         c->symmetric = false;  // the literal bootstrap overlay is a DAG (F8)
+        c->n_started = started_under_cap(c->n, c->cfg.list_cap);
         return st;
     }
     if (c->cfg.graph_model != GOSSIP_GRAPH_POWERLAW) return fail(GOSSIP_EINVAL, "unknown graph_model");
@@ -962,6 +996,12 @@ gossip_status gossip_reset(gossip_ctx* c) {
         HIPCHK(hipMemcpyAsync(c->registered + bitwords - 1, &tail, 4, hipMemcpyHostToDevice, s));
         HIPCHK(hipStreamSynchronize(s));
     }
+    if (c->n_started < c->n) {  // failed registration (list_cap): registered, never alive
+        std::vector<uint32_t> bits(bitwords, 0u);
+        for (uint64_t v = 0; v < c->n_started; ++v) bits[v >> 5] |= 1u << (v & 31);
+        HIPCHK(hipMemcpyAsync(c->alive, bits.data(), bitwords * 4, hipMemcpyHostToDevice, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
     HIPCHK(hipMemsetAsync(c->st, 0, kStatLines * sizeof(DevStats), s));
     c->last_st_round = ~0u;
     HIPCHK(hipMemsetAsync(c->n_reports, 0, sizeof(unsigned long long), s));
@@ -985,7 +1025,7 @@ gossip_status gossip_reset(gossip_ctx* c) {
     c->frontier_est = 0;
     c->round = 0;
     c->finished = false;
-    c->any_dead = false;
+    c->any_dead = c->n_started < c->n;
     c->cum_digest = c->cum_covered = 0;
     HIPCHK(hipStreamSynchronize(s));
     return GOSSIP_OK;

@@ -57,6 +57,8 @@ class GossipConfig(C.Structure):
         ("front_permille", C.c_uint32),
         ("bin_permille", C.c_uint32),
         ("extra_cap", C.c_uint32),
+        ("list_cap", C.c_uint32),
+        ("reserved1", C.c_uint32),
     ]
 
 

@@ -40,7 +40,7 @@ class Engine:
                  max_rounds: int = 4096, min_rounds: int = 0, device: int = -1, coverage_history: bool = False,
                  part: tuple[int, int] = (0, 0), report_capacity: int = 0, mode: str = "auto",
                  pull_permille: int = 0, front_permille: int = 0, bin_permille: int = 0, bins: bool = True,
-                 extra_cap: int = 0):
+                 extra_cap: int = 0, list_cap: int = 0):
         self._L = _abi.lib()
         cfg = GossipConfig()
         cfg.n_peers = n_peers
@@ -63,6 +63,7 @@ class Engine:
         cfg.front_permille = front_permille
         cfg.bin_permille = bin_permille
         cfg.extra_cap = extra_cap
+        cfg.list_cap = list_cap
         self.cfg = cfg
         ctx = C.c_void_p()
         check(self._L.gossip_create(C.byref(cfg), C.byref(ctx)), "gossip_create")

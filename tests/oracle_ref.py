@@ -25,7 +25,7 @@ class OCfg(C.Structure):
     _fields_ = [("n", C.c_uint64), ("n_msgs", C.c_uint32), ("seed", C.c_uint32), ("churn_threshold", C.c_uint32),
                 ("ping_every", C.c_uint32), ("max_missed", C.c_uint32), ("max_rounds", C.c_uint32),
                 ("min_rounds", C.c_uint32), ("threads", C.c_int), ("variant", C.c_int), ("extra_cap", C.c_uint32),
-                ("list_len", C.c_uint32)]
+                ("list_len", C.c_uint32), ("n_started", C.c_uint64)]
 
 
 class OReport(C.Structure):
@@ -41,6 +41,7 @@ class Oracle:
         L = C.CDLL(str(so))
         L.oracle_threshold.restype = C.c_uint64
         L.oracle_skew_pick.restype = C.c_uint32
+        L.oracle_started_under_cap.restype = C.c_uint64
         L.oracle_skew_pick.argtypes = [C.c_uint32, C.c_uint64]
         L.oracle_digest_weight.restype = C.c_uint64
         L.oracle_digest_weight.argtypes = [C.c_uint64]
@@ -87,11 +88,11 @@ class Oracle:
 
     def simulate(self, rp, col, n, n_msgs, origins, inject_rounds, *, seed=0, churn_threshold=0, ping_every=0,
                  max_missed=3, max_rounds=4096, min_rounds=0, kills=(), variant=0, threads=8, extra_cap=0,
-                 list_len=6):
+                 list_len=6, n_started=0):
         rp = np.ascontiguousarray(rp, dtype=np.uint64)
         col = np.ascontiguousarray(col if len(col) else np.zeros(1), dtype=np.uint32)
         cfg = OCfg(n, n_msgs, seed, churn_threshold, ping_every, max_missed, max_rounds, min_rounds, threads, variant,
-                   extra_cap, list_len)
+                   extra_cap, list_len, n_started)
         s = self.L.oracle_sim_create(C.byref(cfg), _p(rp, C.c_uint64), _p(col, C.c_uint32))
         assert s, "oracle_sim_create failed"
         s = C.c_void_p(s)
@@ -132,7 +133,11 @@ class Oracle:
         return self.simulate(rp, col, w.n, w.n_msgs, w.origins, w.inject_rounds, seed=w.rng_seed,
                              churn_threshold=w.churn_threshold, ping_every=w.ping_every, max_missed=w.max_missed,
                              min_rounds=w.min_rounds, kills=w.kills, variant=variant, threads=threads,
-                             max_rounds=max_rounds, extra_cap=w.extra_cap, list_len=w.list_len)
+                             max_rounds=max_rounds, extra_cap=w.extra_cap, list_len=w.list_len,
+                             n_started=self.started_under_cap(w.n, w.list_cap) if w.graph == "ref_bootstrap" else 0)
+
+    def started_under_cap(self, n, list_cap):
+        return int(self.L.oracle_started_under_cap(C.c_uint64(n), C.c_uint32(list_cap)))
 
 
 class OraclePartition:

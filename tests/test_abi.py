@@ -65,3 +65,26 @@ def test_engine_fails_loudly_without_gpu():
     with pytest.raises(GossipError) as ei:
         Engine(1024, 64)
     assert ei.value.status == _abi.GOSSIP_ENODEV
+
+
+def test_ctypes_layouts_match_header(tmp_path):
+    """The ctypes mirrors of gossip_config / gossip_round_stats have the C header's size and field offsets."""
+    import subprocess
+
+    structs = {"gossip_config": _abi.GossipConfig, "gossip_round_stats": _abi.RoundStats}
+    lines = []
+    for cname, py in structs.items():
+        lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
+        for fname, _ in py._fields_:
+            lines.append(f'printf("{cname} {fname} %zu\\n", offsetof({cname}, {fname}));')
+    src = tmp_path / "layout.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "gossip/gossip.h"\nint main(void) {\n'
+                   + "\n".join(lines) + "\nreturn 0;\n}\n")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", str(_abi.REPO_ROOT / "include"), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    for row in filter(None, out):
+        cname, field, value = row.split()
+        py = structs[cname]
+        got = C.sizeof(py) if field == "size" else getattr(py, field).offset
+        assert got == int(value), (cname, field)

@@ -1,6 +1,7 @@
 """GPU parity: libgossip_hip (through its C-ABI) vs the CPU oracle on the
 same seeded inputs -- bit-exact stats, seen sets, reports, alive/registry --
 plus size-independent properties at BASELINE.json's full sizes."""
+import dataclasses
 import json
 from pathlib import Path
 
@@ -8,7 +9,7 @@ import numpy as np
 import pytest
 
 from gossip_hip import Engine
-from gossip_hip.workloads import config, run_engine
+from gossip_hip.workloads import _batches, config, run_engine
 
 pytestmark = pytest.mark.gpu
 GOLDEN = Path(__file__).resolve().parent / "golden"
@@ -167,6 +168,29 @@ def test_push_equals_pull_at_full_size():
     for mode in ("auto", "pull", "bin"):
         assert out["push"][0] == out[mode][0], mode
         assert np.array_equal(out["push"][1], out[mode][1]), mode
+
+
+@pytest.mark.parametrize("n,cap", [(120, 4095), (300, 4095), (60, 1500), (50, 0)])
+def test_f10_list_cap_parity(oracle, n, cap):
+    """The F10 knob (list_cap): under the reference's 4 KB
+    peer_list read, peers from the 77th on never start (registered, not
+    alive); messages they would generate are never sent.  Engine == oracle on
+    every round, with the config-1 kill and liveness schedule."""
+    base = config(1)
+    peers = np.array(sorted({0, 5, n // 3, 75 % n, 76 % n, n - 1}), dtype=np.uint32)
+    o, r = _batches(peers, 10, 5)
+    w = dataclasses.replace(base, n=n, n_msgs=int(o.size), origins=o, inject_rounds=r, list_cap=cap)
+    rp, col = oracle.gen_workload(w)
+    ref = oracle.simulate_workload(w, rp, col)
+    started = oracle.started_under_cap(n, cap)
+    assert int(ref["alive"][:started].sum()) >= started - 1 and not ref["alive"][started:].any()
+    with _engine(w) as e:
+        e.build_graph()
+        e.inject(w.origins, w.inject_rounds)
+        e.schedule_kills([k[0] for k in w.kills], [k[1] for k in w.kills])
+        e.reset()
+        assert e.alive()[:started].all() and not e.alive()[started:].any()
+        _compare(e, ref, w)
 
 
 @pytest.mark.parametrize("idx,n,cap", [(5, 1 << 14, 4), (5, 50_000, 16), (1, None, 8), (1, 40, 3)])

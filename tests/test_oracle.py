@@ -179,3 +179,29 @@ def test_rebootstrap_edges_are_new_live_and_bounded(oracle):
         assert not set(targets) & set(col[rp[u]:rp[u + 1]].tolist())
     off = oracle.simulate_workload(replace(w, extra_cap=0), rp, col)
     assert all(s["reconnects"] == 0 for s in off["stats"])
+
+
+@pytest.mark.parametrize("n,cap", [(120, 4095), (64, 1200)])
+def test_f10_literal_equals_fast(oracle, n, cap):
+    """F10 knob (list_cap): both drivers start the same peers and agree on every round."""
+    from gossip_hip.workloads import _batches
+    o, r = _batches(np.array([0, 7, n // 2, n - 1], dtype=np.uint32), 10, 5)
+    w = replace(config(1), n=n, n_msgs=int(o.size), origins=o, inject_rounds=r, list_cap=cap)
+    rp, col = oracle.gen_workload(w)
+    fast = oracle.simulate_workload(w, rp, col, variant=0)
+    lit = oracle.simulate_workload(w, rp, col, variant=1)
+    assert fast["stats"] == lit["stats"]
+    assert np.array_equal(fast["seen"], lit["seen"])
+    started = oracle.started_under_cap(n, cap)
+    assert started < n and not fast["alive"][started:].any() and fast["registered"][started:].all()
+    assert not fast["seen"][started:].any()  # never started: never received nor generated
+
+
+def test_f10_started_count(oracle):
+    """peer_list of k 127.0.0.1 peers = 30 + 53 k bytes: 76 fit in 4095 (77 fail)."""
+    assert oracle.started_under_cap(4096, 4095) == 76
+    assert oracle.started_under_cap(76, 4095) == 76
+    assert oracle.started_under_cap(10, 0) == 10
+    for k in (1, 2, 50):
+        assert oracle.started_under_cap(4096, 30 + 53 * k) == k
+        assert oracle.started_under_cap(4096, 30 + 53 * k - 1) == k - 1
