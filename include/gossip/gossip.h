@@ -77,7 +77,10 @@ typedef struct gossip_config {
     uint32_t list_cap;        /* ref_bootstrap: bytes of a seed's peer_list a peer reads -- the reference's 4 KB
                                  recv (peer.cpp:188-190; 4095 = faithful).  A peer whose list is
                                  longer fails registration and never starts (registered, not alive).  0 = no cap */
-    uint32_t reserved1;       /* must be 0 */
+    uint32_t rejoin_threshold; /* join churn (the reference has no rejoin path): a peer dead at the start of round
+                                  r restarts in r iff philox({seed,v},{7,r,0,0}).x < threshold -- re-registered,
+                                  empty Message-List, old connections gone, fresh out-edges from one seed response
+                                  into its overflow row (extra_cap > 0).  0 = never.  Single partition only */
 } gossip_config;
 
 /*
@@ -101,7 +104,8 @@ typedef struct gossip_round_stats {
     uint64_t seed_removals; /* seed-registry entries removed (first report of a peer) */
     uint64_t digest;        /* sum_v,w g(v*W+w) * seen[v][w] mod 2^64 at push start */
     uint64_t covered;       /* sum popcount(seen) at push start */
-    uint64_t reconnects;    /* out-edges added by re-bootstrap this round (extra_cap > 0) */
+    uint64_t reconnects;    /* out-edges added by re-bootstrap or a restart this round (extra_cap > 0) */
+    uint64_t rejoined;      /* dead peers restarted this round (rejoin_threshold > 0) */
 } gossip_round_stats;
 
 /* A dead-node report: reporter u detected dead peer v in round r

@@ -334,6 +334,7 @@ struct oracle_sim {
     uint8_t* ex_masked;
     uint8_t* ex_miss;
     uint64_t thr[65];
+    uint64_t sent_lost;  /* literal variant: sentTo counts of Message-Lists dropped by a restart */
     /* fast variant */
     uint64_t *seen, *nw, *nx;
     /* literal variant */
@@ -488,6 +489,66 @@ static int has_bit_fast(const oracle_sim* s, uint64_t v, uint32_t m) {
     return (int)((s->seen[v * s->W + (m >> 6)] >> (m & 63)) & 1u);
 }
 
+/* Join churn (the reference has no rejoin path): a peer
+ * dead at the start of round r restarts at the same address -- PeerNode::start
+ * again (peer.cpp:28-101): it re-registers with the seeds (seed.cpp:153-156),
+ * its Message-List is empty and its old connections are gone (its row is
+ * dropped), and it selects fresh out-edges from one seed response into its
+ * overflow row (extra_cap > 0; none otherwise).  Edges other peers still hold
+ * to its address deliver again; edges they already dropped stay dropped. */
+static int has_out_edge(const oracle_sim* s, uint32_t u, uint32_t c);
+
+static uint32_t* do_rejoin(oracle_sim* s, uint32_t r, uint64_t* n_rj) {
+    *n_rj = 0;
+    if (!s->cfg.rejoin_threshold) return NULL;
+    const uint64_t n_boot = s->cfg.n_started && s->cfg.n_started < s->n ? s->cfg.n_started : s->n;
+    uint32_t* list = NULL;
+    uint64_t cap = 0;
+    for (uint64_t v = 0; v < n_boot; ++v) {
+        if (s->alive[v]) continue;
+        if (philox_x(s->cfg.seed, (uint32_t)v, ORACLE_P_REJOIN, r, 0, 0, 0) >= s->cfg.rejoin_threshold) continue;
+        if (*n_rj == cap) { cap = cap ? 2 * cap : 256; list = (uint32_t*)realloc(list, cap * sizeof(uint32_t)); }
+        list[(*n_rj)++] = (uint32_t)v;
+        s->alive[v] = 1;
+        s->registered[v] = 1;
+        if (s->cfg.variant == 0) {
+            memset(s->seen + v * s->W, 0, s->W * sizeof(uint64_t));
+            memset(s->nw + v * s->W, 0, s->W * sizeof(uint64_t));
+        } else {
+            msg_list* l = &s->lists[v];
+            for (uint32_t i = 0; i < l->cap; ++i)
+                if (l->key[i] != 0xFFFFFFFFu) { s->sent_lost += l->sent_to[i]; l->key[i] = 0xFFFFFFFFu; }
+            l->size = 0;
+            s->outbox_n[v] = 0;
+        }
+        for (uint64_t e = s->rp[v]; e < s->rp[v + 1]; ++e) s->masked[e] = 1;
+        if (s->K) s->ex_cnt[v] = 0;
+    }
+    return list;
+}
+
+/* the restarted peers' selectAndConnectPeers (peer.cpp:214-253), after the
+ * round's deaths: one response of L candidates keyed by the round; self, dead
+ * and repeated candidates are skipped, at most K kept */
+static void rejoin_select(oracle_sim* s, uint32_t r, const uint32_t* list, uint64_t n_rj, oracle_stats* st) {
+    if (!s->K) return;
+    const uint32_t L = s->cfg.list_len;
+    for (uint64_t j = 0; j < n_rj; ++j) {
+        const uint32_t v = list[j];
+        if (!s->alive[v]) continue;  /* died again in the same round */
+        const uint32_t k = pick_count(philox_x(s->cfg.seed, v, ORACLE_P_REJOIN, r, 0, 0, 1), L, s->thr);
+        for (uint32_t i = 0; i < k; ++i) {
+            const uint32_t c = oracle_skew_pick(philox_x(s->cfg.seed, v, ORACLE_P_REJOIN, r, 1 + (i >> 2), 0, i & 3), s->n);
+            if (c == v || !s->alive[c] || has_out_edge(s, v, c) || s->ex_cnt[v] >= s->K) continue;
+            const uint64_t slot = (uint64_t)v * s->K + s->ex_cnt[v]++;
+            s->ex_col[slot] = c;
+            s->ex_masked[slot] = 0;
+            s->ex_miss[slot] = 0;
+            st->reconnects++;
+        }
+    }
+}
+
 /* step 1: churn (A11) + kill list -- a dead peer stops receiving, forwarding, pinging */
 static uint64_t do_churn(oracle_sim* s, uint32_t r) {
     uint64_t died = 0;
@@ -530,15 +591,17 @@ static int ping_one(oracle_sim* s, uint32_t r, uint32_t u, uint32_t v, uint8_t* 
     return 1;
 }
 
+/* u holds a connection to c: an unmasked entry of its sorted row or of its
+ * overflow row (a dropped edge is erased from connectedPeers, peer.cpp:388) */
 static int has_out_edge(const oracle_sim* s, uint32_t u, uint32_t c) {
     uint64_t lo = s->rp[u], hi = s->rp[u + 1];            /* rows are sorted */
     while (lo < hi) {
         uint64_t mid = (lo + hi) / 2;
         if (s->col[mid] < c) lo = mid + 1; else hi = mid;
     }
-    if (lo < s->rp[u + 1] && s->col[lo] == c) return 1;
+    if (lo < s->rp[u + 1] && s->col[lo] == c && !s->masked[lo]) return 1;
     for (uint32_t k = 0; k < s->ex_cnt[u]; ++k)
-        if (s->ex_col[(uint64_t)u * s->K + k] == c) return 1;
+        if (s->ex_col[(uint64_t)u * s->K + k] == c && !s->ex_masked[(uint64_t)u * s->K + k]) return 1;
     return 0;
 }
 
@@ -722,7 +785,12 @@ int oracle_sim_step(oracle_sim* s, oracle_stats* out) {
     memset(&st, 0, sizeof(st));
     uint32_t r = s->round;
     st.round = r;
+    uint64_t n_rj = 0;
+    uint32_t* rj = do_rejoin(s, r, &n_rj);
+    st.rejoined = n_rj;
     st.died = do_churn(s, r);
+    rejoin_select(s, r, rj, n_rj, &st);
+    free(rj);
     if (s->cfg.ping_every && r % s->cfg.ping_every == 0) {
         st.flags |= 1;
         do_liveness(s, r, &st);
@@ -799,7 +867,7 @@ void oracle_sim_registered(const oracle_sim* s, uint8_t* out) { memcpy(out, s->r
 
 uint64_t oracle_sim_sent_to_total(const oracle_sim* s) {
     if (!s->lists) return 0;
-    uint64_t t = 0;
+    uint64_t t = s->sent_lost;
     for (uint64_t v = 0; v < s->n; ++v)
         for (uint32_t i = 0; i < s->lists[v].cap; ++i)
             if (s->lists[v].key[i] != 0xFFFFFFFFu) t += s->lists[v].sent_to[i];
@@ -832,7 +900,8 @@ struct oracle_part {
 
 oracle_part* oracle_part_create(const oracle_sim_cfg* cfg, uint64_t b, uint64_t e, const uint64_t* row_ptr,
                                 const uint32_t* col) {
-    if (!cfg || b >= e || e > cfg->n || cfg->extra_cap) return NULL;  /* no re-bootstrap in the emulation */
+    if (!cfg || b >= e || e > cfg->n || cfg->extra_cap || cfg->rejoin_threshold || cfg->n_started)
+        return NULL; /* no re-bootstrap, rejoin or failed registrations in the emulation */
     oracle_part* p = (oracle_part*)calloc(1, sizeof(oracle_part));
     p->cfg = *cfg;
     if (p->cfg.max_rounds == 0) p->cfg.max_rounds = 1u << 20;

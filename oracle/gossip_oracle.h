@@ -42,7 +42,9 @@ enum {
     ORACLE_P_SHUFFLE = 3, /* ctr {3, response, d>>2, 0}[d&3] -> Fisher-Yates draw d (peer.cpp:224-225) */
     ORACLE_P_CHURN = 4,   /* ctr {4, round, 0, 0}.x -> peer dies if < churn_threshold */
     ORACLE_P_ORIGIN = 5,  /* key {seed, 0xFFFFFFFF}, ctr {5, k, attempt, 0}.x -> origin k */
-    ORACLE_P_REBOOT = 6   /* ctr {6, round, dead, 0}.x -> k draw; ctr {6, round, dead, 1+(i>>2)}[i&3] -> candidate i */
+    ORACLE_P_REBOOT = 6,  /* ctr {6, round, dead, 0}.x -> k draw; ctr {6, round, dead, 1+(i>>2)}[i&3] -> candidate i */
+    ORACLE_P_REJOIN = 7   /* ctr {7, round, 0, 0}.x -> a dead peer restarts if < rejoin_threshold, .y -> k draw;
+                             ctr {7, round, 1+(i>>2), 0}[i&3] -> candidate i */
 };
 
 /* Integer threshold for the reference's power-law pick
@@ -98,6 +100,7 @@ typedef struct oracle_stats {
     uint64_t digest;        /* sum g(v*W+w) * seen[v][w] mod 2^64 at push start */
     uint64_t covered;       /* sum popcount(seen) at push start */
     uint64_t reconnects;    /* out-edges added by re-bootstrap this round (extra_cap > 0) */
+    uint64_t rejoined;      /* dead peers restarted this round (rejoin_threshold > 0) */
 } oracle_stats;
 
 typedef struct oracle_report {
@@ -118,6 +121,8 @@ typedef struct oracle_sim_cfg {
     uint32_t extra_cap;        /* re-bootstrap after a death: up to this many extra out-edges per peer (0 = off) */
     uint32_t list_len;         /* re-bootstrap: candidates per seed response (powerlaw list_len) */
     uint64_t n_started;        /* peers >= n_started never start (failed registration, F10); 0 = all start */
+    uint32_t rejoin_threshold; /* join churn: a dead peer restarts in round r if philox < threshold; 0 = never */
+    uint32_t pad0;
 } oracle_sim_cfg;
 
 typedef struct oracle_sim oracle_sim;

@@ -119,6 +119,8 @@ struct gossip_ctx {
     void* rb_temp = nullptr;
     size_t rb_temp_bytes = 0;
     RebootArgs reboot{};
+    uint32_t* rj_list = nullptr;          // join churn: this round's restarted owned peers (local ids)
+    unsigned long long* rj_n = nullptr;   // their count
     BinState bins;               // binned dense rounds: slot layout (gossip_bins.hip)
     bool bins_ready = false;
     bool last_bin = false;       // the pull round in flight runs binned
@@ -210,6 +212,10 @@ void free_state(gossip_ctx* c) {
     hipFree(c->rb_keys);
     hipFree(c->rb_keys2);
     hipFree(c->rb_temp);
+    hipFree(c->rj_list);
+    hipFree(c->rj_n);
+    c->rj_list = nullptr;
+    c->rj_n = nullptr;
     c->ex_col = c->ex_cnt = nullptr;
     c->ex_miss = nullptr;
     c->rb_keys = c->rb_keys2 = nullptr;
@@ -460,6 +466,14 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
     if (c->round >= c->cfg.max_rounds) return fail(GOSSIP_ESTATE, "max_rounds reached");
     RoundArgs a = make_args(c);
     const uint32_t pw = pack_w(c);
+    if (c->cfg.rejoin_threshold) {  // restarts first: a peer dying this round cannot restart in it
+        HIPCHK(hipMemsetAsync(c->rj_n, 0, sizeof(unsigned long long), c->stream));
+        HIPCHK(timed(c, "rejoin", [&] {
+            return launch_rejoin(a, pw, c->cfg.rng_seed, c->cfg.rejoin_threshold, c->n_started, c->rj_list, c->rj_n,
+                                 c->stream);
+        }));
+        c->any_masked = true;
+    }
     uint32_t first = 0, cnt = kills_in_round(c, c->round, &first);
     if (cnt) {
         c->any_dead = true;
@@ -469,6 +483,10 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
         c->any_dead = true;
         HIPCHK(timed(c, "churn", [&] { return launch_churn(a, pw, c->cfg.rng_seed, c->cfg.churn_threshold, c->stream); }));
     }
+    if (c->cfg.rejoin_threshold && c->cfg.extra_cap)  // the restarted peers' new out-edges, after the deaths
+        HIPCHK(timed(c, "rejoin", [&] {
+            return launch_rejoin_select(a, c->reboot, c->rj_list, c->rj_n, c->n_local, c->stream);
+        }));
     if (c->cfg.ping_every && c->round % c->cfg.ping_every == 0) {
         HIPCHK(timed(c, "liveness", [&] {
             hipError_t e = launch_liveness(a, c->stream, 1);
@@ -496,7 +514,8 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
     // dead peers are fine for pull / binned rounds (a live peer's in-edges from
     // live peers are never masked: only edges to dead peers are); re-bootstrap
     // edges are not (they break the symmetry the pull relies on)
-    const bool pull_ok = c->symmetric && (!c->any_dead || !c->cfg.extra_cap) &&
+    // (nor are restarted peers: their dropped rows break it too)
+    const bool pull_ok = c->symmetric && (!c->any_dead || (!c->cfg.extra_cap && !c->cfg.rejoin_threshold)) &&
                          !(c->cfg.flags & GOSSIP_FLAG_FORCE_PUSH) && (!remote || c->gather != nullptr);
     a.dead_mode = c->any_dead ? 1u : 0u;
     bool pull;
@@ -654,6 +673,7 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
     s.reports = d.reports;
     s.seed_removals = d.seed_removals;
     s.reconnects = d.reconnects;
+    s.rejoined = d.rejoined;
     if (cumulative) {
         c->cum_digest += d.digest;
         c->cum_covered += d.covered;
@@ -704,7 +724,8 @@ gossip_status gossip_create(const gossip_config* cfg, gossip_ctx** out) {
     uint64_t b = cfg->part_begin, e = cfg->part_end;
     if (b == 0 && e == 0) e = cfg->n_peers;
     if (b >= e || e > cfg->n_peers) return fail(GOSSIP_EINVAL, "bad partition range");
-    if (cfg->reserved1) return fail(GOSSIP_EINVAL, "reserved1 must be 0");
+    if (cfg->rejoin_threshold && !(b == 0 && e == cfg->n_peers))
+        return fail(GOSSIP_EINVAL, "rejoin_threshold needs a single partition");
     if (cfg->graph_model == GOSSIP_GRAPH_REF_BOOTSTRAP && cfg->n_peers > 4096)
         return fail(GOSSIP_EINVAL, "ref_bootstrap supports n_peers <= 4096");
     int ndev = 0;
@@ -776,6 +797,10 @@ gossip_status gossip_create(const gossip_config* cfg, gossip_ctx** out) {
         c->reboot.L = c->cfg.list_len;
         c->reboot.seed = c->cfg.rng_seed;
         for (uint32_t j = 1; j < c->cfg.list_len && j < 64; ++j) c->reboot.thr[j] = (uint32_t)pick_threshold(j, c->cfg.list_len);
+    }
+    if (c->cfg.rejoin_threshold) {
+        if ((err = hipMalloc((void**)&c->rj_list, c->n_local * 4 + 4)) != hipSuccess) return bail("rejoin list", err);
+        if ((err = hipMalloc((void**)&c->rj_n, sizeof(unsigned long long))) != hipSuccess) return bail("rejoin count", err);
     }
     if (c->cfg.flags & GOSSIP_FLAG_COVERAGE_HISTORY) {
         if ((err = hipMalloc((void**)&c->cov_hist, (uint64_t)c->cfg.max_rounds * 64 * c->Wp * 8)) != hipSuccess)

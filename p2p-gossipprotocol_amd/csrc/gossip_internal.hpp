@@ -19,9 +19,9 @@ constexpr int kPullNT = 0x100;                 // launch_pull_light unroll flag:
 struct DevStats {
     unsigned long long frontier, traversals, deliveries, undelivered, new_receipts, injected, died, reports,
         seed_removals, digest, covered, heavy_traversals, live_checked, activated, pull_edges, pull_gathers,
-        reconnects;
+        reconnects, rejoined;
 };
-constexpr int kStatFields = 17;
+constexpr int kStatFields = 18;
 static_assert(sizeof(DevStats) == kStatFields * 8, "DevStats layout");
 
 struct HeavyChunk {
@@ -161,6 +161,14 @@ hipError_t launch_reboot_keys(const RoundArgs& a, uint64_t first, uint64_t n, un
 hipError_t launch_rebootstrap(const RoundArgs& a, const RebootArgs& r, const unsigned long long* keys, uint64_t n,
                               hipStream_t s);
 hipError_t launch_src_count(const RoundArgs& a, uint32_t W, hipStream_t s);
+// join churn, before the round's kills and deaths: peers dead at round start
+// restart (alive, registered, seen cleared, row dropped, overflow row emptied);
+// owned ones are appended to list (count in *n_list)
+hipError_t launch_rejoin(const RoundArgs& a, uint32_t W, uint32_t seed, uint32_t thr, uint64_t n_boot, uint32_t* list,
+                         unsigned long long* n_list, hipStream_t s);
+// after the round's deaths: the restarted peers' fresh out-edges (extra_cap > 0)
+hipError_t launch_rejoin_select(const RoundArgs& a, const RebootArgs& r, const uint32_t* list,
+                                const unsigned long long* n_list, uint64_t max_list, hipStream_t s);
 hipError_t launch_coverage(const uint64_t* words, uint64_t n_local, uint32_t W, unsigned long long* counts,
                            hipStream_t s);
 hipError_t launch_heavy_count(const uint64_t* rp, uint64_t n_local, uint32_t heavy, unsigned long long* n_chunks,

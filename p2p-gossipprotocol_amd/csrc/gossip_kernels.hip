@@ -42,7 +42,7 @@ __device__ __forceinline__ uint32_t lane_rank(unsigned long long mask) {
 struct Acc {
     unsigned long long frontier = 0, trav = 0, deliv = 0, undeliv = 0, fresh = 0, digest = 0, covered = 0, died = 0,
                        reports = 0, removals = 0, injected = 0, htrav = 0, checked = 0,
-                       activated = 0, pulled = 0, gathered = 0, reconnects = 0;
+                       activated = 0, pulled = 0, gathered = 0, reconnects = 0, rejoined = 0;
 };
 
 // Block-level flush: wave sums -> LDS -> one atomic per nonzero field per
@@ -59,7 +59,8 @@ __device__ __forceinline__ void flush(Acc& acc, DevStats* st) {
     // DevStats field order
     const unsigned long long v[kF] = {acc.frontier, acc.trav,     acc.deliv,   acc.undeliv, acc.fresh,  acc.injected,
                                       acc.died,     acc.reports,  acc.removals, acc.digest, acc.covered, acc.htrav,
-                                      acc.checked,  acc.activated, acc.pulled,  acc.gathered, acc.reconnects};
+                                      acc.checked,  acc.activated, acc.pulled,  acc.gathered, acc.reconnects,
+                                      acc.rejoined};
 #pragma unroll
     for (int f = 0; f < kF; ++f) {
         const unsigned long long s_ = wave_sum(v[f]);
@@ -949,7 +950,8 @@ __global__ void k_reboot_keys(DeadReport* rep, uint64_t first, uint64_t n, uint6
     }
 }
 
-// u already has an out-edge to c (its sorted row, masked or not, or an extra)
+// u holds a connection to c: an unmasked entry of its sorted row or of its
+// overflow row (a dropped edge is erased from connectedPeers, peer.cpp:388)
 __device__ __forceinline__ bool has_out_edge(const RoundArgs& a, uint64_t u, uint32_t c) {
     uint64_t lo = a.rp[u], hi = a.rp[u + 1];
     while (lo < hi) {
@@ -957,10 +959,10 @@ __device__ __forceinline__ bool has_out_edge(const RoundArgs& a, uint64_t u, uin
         if ((a.col[mid] & ~kMaskedEdge) < c) lo = mid + 1;
         else hi = mid;
     }
-    if (lo < a.rp[u + 1] && (a.col[lo] & ~kMaskedEdge) == c) return true;
+    if (lo < a.rp[u + 1] && a.col[lo] == c) return true;  // equal and unmasked
     const uint32_t cnt = a.ex_cnt[u];
     for (uint32_t k = 0; k < cnt; ++k)
-        if ((a.ex_col[u * a.ex_cap + k] & ~kMaskedEdge) == c) return true;
+        if (a.ex_col[u * a.ex_cap + k] == c) return true;
     return false;
 }
 
@@ -992,6 +994,85 @@ __global__ __launch_bounds__(kBlock) void k_rebootstrap(RoundArgs a, RebootArgs 
                 a.ex_cnt[u] = cnt + 1;
                 acc.reconnects++;
             }
+        }
+    }
+    flush(acc, a.st);
+}
+
+// ---------------------------------------------------------------------------
+// Join churn (the reference has no rejoin path).  A peer
+// dead at the start of round r restarts at its address in r with probability
+// threshold / 2^32 -- PeerNode::start again (peer.cpp:28-101): re-registered
+// (seed.cpp:153-156), an empty Message-List, its old connections gone (its row
+// is dropped) and, once the round's deaths are known, fresh out-edges from one
+// seed response in its overflow row.  Runs before the round's kills and churn
+// deaths; one thread per 32-peer word of the alive bitset.
+// ---------------------------------------------------------------------------
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_rejoin(RoundArgs a, uint32_t wd, uint32_t seed, uint32_t thr,
+                                                   uint64_t n_boot, uint32_t* list, unsigned long long* n_list) {
+    Acc acc;
+    const uint64_t n_words = (n_boot + 31) >> 5;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n_words; i += (uint64_t)gridDim.x * kBlock) {
+        const uint32_t valid = (i + 1) * 32 <= n_boot ? ~0u : (1u << (n_boot & 31)) - 1u;
+        const uint32_t word = a.alive[i];
+        uint32_t back = 0;
+        for (uint32_t x = ~word & valid; x; x &= x - 1) {
+            const uint32_t b = (uint32_t)__builtin_ctz(x);
+            if (philox4x32_10(P_REJOIN, a.round, 0, 0, seed, (uint32_t)(i * 32 + b)).x < thr) back |= 1u << b;
+        }
+        if (!back) continue;
+        a.alive[i] = word | back;
+        a.registered[i] |= back;  // one thread per word: plain stores
+        for (uint32_t x = back; x; x &= x - 1) {
+            const uint32_t v = (uint32_t)(i * 32 + __builtin_ctz(x));
+            if (v < a.begin || v >= a.end) continue;
+            const uint64_t lv = v - a.begin;
+            acc.rejoined++;
+            // the old Message-List is gone: its words leave the digest and coverage
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                const uint64_t mm = a.seen[lv * W + w];
+                a.seen[lv * W + w] = 0ull;
+                a.nw[lv * W + w] = 0ull;
+                if (!mm) continue;
+                if (w < (int)wd) acc.digest -= digest_weight((uint64_t)v * wd + w) * mm;
+                acc.covered -= (unsigned long long)__popcll(mm);
+                if (a.cov)
+                    for (uint64_t y = mm; y; y &= y - 1) atomicAdd(&a.cov[w * 64 + __builtin_ctzll(y)], ~0ull);
+            }
+            for (uint64_t e = a.rp[lv]; e < a.rp[lv + 1]; ++e) a.col[e] |= kMaskedEdge;  // old connections
+            if (a.ex_cap) a.ex_cnt[lv] = 0;
+            list[atomicAdd(n_list, 1ull)] = (uint32_t)lv;
+        }
+    }
+    flush(acc, a.st);
+}
+
+// the restarted peers' selectAndConnectPeers (peer.cpp:214-253) once the
+// round's deaths are known: one response of L candidates keyed by the round,
+// self / dead / repeated candidates skipped, at most ex_cap kept
+__global__ __launch_bounds__(kBlock) void k_rejoin_select(RoundArgs a, RebootArgs rb, const uint32_t* list,
+                                                          const unsigned long long* n_list) {
+    Acc acc;
+    const uint64_t n = *n_list;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t lv = list[i];
+        const uint32_t v = (uint32_t)(a.begin + lv);
+        if (!bit_alive(a.alive, v)) continue;  // died again in the same round
+        const uint32_t y = philox4x32_10(P_REJOIN, a.round, 0, 0, rb.seed, v).y;
+        uint32_t k = 0;
+        for (uint32_t t = 1; t < rb.L; ++t) k += y >= rb.thr[t];
+        for (uint32_t c_i = 0; c_i < k; ++c_i) {
+            const u32x4 r = philox4x32_10(P_REJOIN, a.round, 1 + (c_i >> 2), 0, rb.seed, v);
+            const uint32_t c = skew_pick(lane_of(r, c_i & 3), a.n_global);
+            if (c == v || !bit_alive(a.alive, c) || has_out_edge(a, lv, c)) continue;
+            const uint32_t cnt = a.ex_cnt[lv];
+            if (cnt >= a.ex_cap) continue;
+            a.ex_col[lv * a.ex_cap + cnt] = c;
+            a.ex_miss[lv * a.ex_cap + cnt] = 0;
+            a.ex_cnt[lv] = cnt + 1;
+            acc.reconnects++;
         }
     }
     flush(acc, a.st);
@@ -1426,6 +1507,21 @@ hipError_t launch_rebootstrap(const RoundArgs& a, const RebootArgs& r, const uns
                               hipStream_t s) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_rebootstrap, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, a, r, keys, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_rejoin(const RoundArgs& a, uint32_t W_, uint32_t seed, uint32_t thr, uint64_t n_boot, uint32_t* list,
+                         unsigned long long* n_list, hipStream_t s) {
+    const uint32_t wd = wd_of(W_);
+    GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_rejoin<W>, dim3(grid_for((n_boot + 31) / 32, kBlock)), dim3(kBlock),
+                                                   0, s, a, wd, seed, thr, n_boot, list, n_list));
+    return hipGetLastError();
+}
+
+hipError_t launch_rejoin_select(const RoundArgs& a, const RebootArgs& r, const uint32_t* list,
+                                const unsigned long long* n_list, uint64_t max_list, hipStream_t s) {
+    if (!a.ex_cap || !max_list) return hipSuccess;
+    hipLaunchKernelGGL(k_rejoin_select, dim3(grid_for(max_list, kBlock)), dim3(kBlock), 0, s, a, r, list, n_list);
     return hipGetLastError();
 }
 

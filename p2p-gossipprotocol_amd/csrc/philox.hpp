@@ -18,6 +18,7 @@ enum : uint32_t {
     P_CHURN = 4,    // {4, round, 0, 0}.x           death test
     P_ORIGIN = 5,   // key {seed, ~0u}, {5, k, attempt, 0}.x  origin pick
     P_REBOOT = 6,   // {6, round, dead, 0}.x k draw; {6, round, dead, 1+(i>>2)}[i&3] candidate i (re-bootstrap)
+    P_REJOIN = 7,   // {7, round, 0, 0}.x restart test, .y k draw; {7, round, 1+(i>>2), 0}[i&3] candidate i
 };
 
 struct u32x4 {

@@ -58,12 +58,12 @@ class GossipConfig(C.Structure):
         ("bin_permille", C.c_uint32),
         ("extra_cap", C.c_uint32),
         ("list_cap", C.c_uint32),
-        ("reserved1", C.c_uint32),
+        ("rejoin_threshold", C.c_uint32),
     ]
 
 
 STAT_FIELDS = ("frontier", "traversals", "deliveries", "undelivered", "new_receipts", "duplicates", "injected",
-               "died", "reports", "seed_removals", "digest", "covered", "reconnects")
+               "died", "reports", "seed_removals", "digest", "covered", "reconnects", "rejoined")
 
 
 class RoundStats(C.Structure):

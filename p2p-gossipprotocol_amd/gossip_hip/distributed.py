@@ -41,7 +41,7 @@ import torch.distributed as dist
 from ._abi import STAT_FIELDS
 
 _SUM_FIELDS = ("frontier", "traversals", "deliveries", "undelivered", "new_receipts", "injected", "died", "reports",
-               "reconnects")
+               "reconnects", "rejoined")
 MASK32 = (1 << 32) - 1
 MASK64 = (1 << 64) - 1
 

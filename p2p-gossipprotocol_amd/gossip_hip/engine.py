@@ -17,7 +17,7 @@ from ._abi import DeadReport, GossipConfig, RoundStats, check
 
 _GRAPHS = {"powerlaw": _abi.GRAPH_POWERLAW, "ref_bootstrap": _abi.GRAPH_REF_BOOTSTRAP}
 KERNELS = ("push_light", "push_heavy", "push_extra", "src_count", "frontier_bits", "pull_light", "pull_heavy", "bin_scatter",
-           "bin_apply", "liveness", "rebootstrap", "churn", "kills", "inject", "apply_remote")
+           "bin_apply", "liveness", "rebootstrap", "rejoin", "churn", "kills", "inject", "apply_remote")
 
 
 def _u32(a) -> np.ndarray:
@@ -40,7 +40,7 @@ class Engine:
                  max_rounds: int = 4096, min_rounds: int = 0, device: int = -1, coverage_history: bool = False,
                  part: tuple[int, int] = (0, 0), report_capacity: int = 0, mode: str = "auto",
                  pull_permille: int = 0, front_permille: int = 0, bin_permille: int = 0, bins: bool = True,
-                 extra_cap: int = 0, list_cap: int = 0):
+                 extra_cap: int = 0, list_cap: int = 0, rejoin_threshold: int = 0):
         self._L = _abi.lib()
         cfg = GossipConfig()
         cfg.n_peers = n_peers
@@ -64,6 +64,7 @@ class Engine:
         cfg.bin_permille = bin_permille
         cfg.extra_cap = extra_cap
         cfg.list_cap = list_cap
+        cfg.rejoin_threshold = rejoin_threshold
         self.cfg = cfg
         ctx = C.c_void_p()
         check(self._L.gossip_create(C.byref(cfg), C.byref(ctx)), "gossip_create")

@@ -38,11 +38,13 @@ class Workload:
     min_rounds: int = 0
     extra_cap: int = 0   # re-bootstrap after a death; 0 = drop-only (the literal reference)
     list_cap: int = 0    # ref_bootstrap: peer_list bytes a peer reads (4095 = the reference's recv, F10); 0 = no cap
+    rejoin_threshold: int = 0  # join churn: a dead peer restarts iff philox.x < this; 0 = never
 
     def engine_kwargs(self) -> dict:
         return dict(rng_seed=self.rng_seed, graph=self.graph, list_len=self.list_len, n_seeds=self.n_seeds,
                     churn_threshold=self.churn_threshold, ping_every=self.ping_every, max_missed=self.max_missed,
-                    min_rounds=self.min_rounds, extra_cap=self.extra_cap, list_cap=self.list_cap)
+                    min_rounds=self.min_rounds, extra_cap=self.extra_cap, list_cap=self.list_cap,
+                    rejoin_threshold=self.rejoin_threshold)
 
 
 def _batches(origins: np.ndarray, per_origin: int, every: int) -> tuple[np.ndarray, np.ndarray]:

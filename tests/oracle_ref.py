@@ -11,7 +11,7 @@ from pathlib import Path
 import numpy as np
 
 STAT_FIELDS = ("frontier", "traversals", "deliveries", "undelivered", "new_receipts", "duplicates", "injected",
-               "died", "reports", "seed_removals", "digest", "covered", "reconnects")
+               "died", "reports", "seed_removals", "digest", "covered", "reconnects", "rejoined")
 
 
 class OStats(C.Structure):
@@ -25,7 +25,8 @@ class OCfg(C.Structure):
     _fields_ = [("n", C.c_uint64), ("n_msgs", C.c_uint32), ("seed", C.c_uint32), ("churn_threshold", C.c_uint32),
                 ("ping_every", C.c_uint32), ("max_missed", C.c_uint32), ("max_rounds", C.c_uint32),
                 ("min_rounds", C.c_uint32), ("threads", C.c_int), ("variant", C.c_int), ("extra_cap", C.c_uint32),
-                ("list_len", C.c_uint32), ("n_started", C.c_uint64)]
+                ("list_len", C.c_uint32), ("n_started", C.c_uint64), ("rejoin_threshold", C.c_uint32),
+                ("pad0", C.c_uint32)]
 
 
 class OReport(C.Structure):
@@ -88,11 +89,11 @@ class Oracle:
 
     def simulate(self, rp, col, n, n_msgs, origins, inject_rounds, *, seed=0, churn_threshold=0, ping_every=0,
                  max_missed=3, max_rounds=4096, min_rounds=0, kills=(), variant=0, threads=8, extra_cap=0,
-                 list_len=6, n_started=0):
+                 list_len=6, n_started=0, rejoin_threshold=0):
         rp = np.ascontiguousarray(rp, dtype=np.uint64)
         col = np.ascontiguousarray(col if len(col) else np.zeros(1), dtype=np.uint32)
         cfg = OCfg(n, n_msgs, seed, churn_threshold, ping_every, max_missed, max_rounds, min_rounds, threads, variant,
-                   extra_cap, list_len, n_started)
+                   extra_cap, list_len, n_started, rejoin_threshold)
         s = self.L.oracle_sim_create(C.byref(cfg), _p(rp, C.c_uint64), _p(col, C.c_uint32))
         assert s, "oracle_sim_create failed"
         s = C.c_void_p(s)
@@ -134,7 +135,8 @@ class Oracle:
                              churn_threshold=w.churn_threshold, ping_every=w.ping_every, max_missed=w.max_missed,
                              min_rounds=w.min_rounds, kills=w.kills, variant=variant, threads=threads,
                              max_rounds=max_rounds, extra_cap=w.extra_cap, list_len=w.list_len,
-                             n_started=self.started_under_cap(w.n, w.list_cap) if w.graph == "ref_bootstrap" else 0)
+                             n_started=self.started_under_cap(w.n, w.list_cap) if w.graph == "ref_bootstrap" else 0,
+                             rejoin_threshold=w.rejoin_threshold)
 
     def started_under_cap(self, n, list_cap):
         return int(self.L.oracle_started_under_cap(C.c_uint64(n), C.c_uint32(list_cap)))

@@ -36,6 +36,8 @@ def test_create_rejects_bad_config(hip_lib):
     cfg.n_peers = 10
     cfg.n_msgs = 513
     assert hip_lib.gossip_create(C.byref(cfg), C.byref(ctx)) == _abi.GOSSIP_EINVAL
+    cfg.n_peers, cfg.n_msgs, cfg.part_begin, cfg.part_end, cfg.rejoin_threshold = 64, 8, 0, 32, 1000
+    assert hip_lib.gossip_create(C.byref(cfg), C.byref(ctx)) == _abi.GOSSIP_EINVAL  # rejoin: single partition only
 
 
 def test_pick_origins_matches_oracle(oracle):

@@ -193,6 +193,34 @@ def test_f10_list_cap_parity(oracle, n, cap):
         _compare(e, ref, w)
 
 
+@pytest.mark.parametrize("idx,n,cap,mode", [(5, 1 << 14, 0, "auto"), (5, 1 << 14, 8, "auto"), (5, 50_000, 4, "push"),
+                                            (5, 20_000, 0, "pull"), (1, None, 8, "auto"), (1, 40, 0, "auto")])
+def test_rejoin_parity(oracle, idx, n, cap, mode):
+    """Join churn (rejoin_threshold): restarted peers --
+    re-registered, empty Message-List, dropped row, fresh out-edges in the
+    overflow row -- bit-exact against the oracle, with and without
+    re-bootstrap; digest and coverage lose the restarted peers' old words."""
+    w = config(idx, n, pick=oracle.pick_origins, rebootstrap=cap)
+    w = dataclasses.replace(w, rejoin_threshold=int((0.05 if idx == 5 else 0.3) * 2**32),
+                            min_rounds=max(w.min_rounds, 30))
+    rp, col = oracle.gen_workload(w)
+    ref = oracle.simulate_workload(w, rp, col)
+    assert sum(s["rejoined"] for s in ref["stats"]) > 0
+    with _engine(w, mode=mode) as e:
+        e.build_graph()
+        e.inject(w.origins, w.inject_rounds)
+        if w.kills:
+            e.schedule_kills([k[0] for k in w.kills], [k[1] for k in w.kills])
+        e.reset()
+        first = _compare(e, ref, w)
+        cnt, ex = e.read_extra()
+        if cap:
+            assert np.array_equal(cnt, ref["extra_counts"])
+            assert np.array_equal(ex, ref["extra_cols"])
+        e.reset()
+        assert e.run() == first
+
+
 @pytest.mark.parametrize("idx,n,cap", [(5, 1 << 14, 4), (5, 50_000, 16), (1, None, 8), (1, 40, 3)])
 def test_rebootstrap_parity(oracle, idx, n, cap):
     """Re-bootstrap after a death (handleDeadPeer

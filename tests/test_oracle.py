@@ -205,3 +205,23 @@ def test_f10_started_count(oracle):
     for k in (1, 2, 50):
         assert oracle.started_under_cap(4096, 30 + 53 * k) == k
         assert oracle.started_under_cap(4096, 30 + 53 * k - 1) == k - 1
+
+
+@pytest.mark.parametrize("cap", [0, 8])
+def test_rejoin_literal_equals_fast(oracle, cap):
+    """Join churn (rejoin_threshold): restarted peers with an
+    empty Message-List, a dropped row and (cap > 0) fresh out-edges; both
+    drivers agree, and sum |sentTo| (restarts included) = sum deliveries."""
+    w = replace(config(5, 4096, pick=oracle.pick_origins, rebootstrap=cap), rejoin_threshold=int(0.05 * 2**32),
+                min_rounds=30)
+    rp, col = oracle.gen_workload(w)
+    fast = oracle.simulate_workload(w, rp, col, variant=0)
+    lit = oracle.simulate_workload(w, rp, col, variant=1)
+    assert fast["stats"] == lit["stats"]
+    assert np.array_equal(fast["seen"], lit["seen"])
+    assert np.array_equal(fast["extra_cols"], lit["extra_cols"])
+    assert sum(s["rejoined"] for s in fast["stats"]) > 100
+    assert lit["sent_to_total"] == sum(s["deliveries"] for s in lit["stats"])
+    off = oracle.simulate_workload(replace(w, rejoin_threshold=0), rp, col)
+    assert all(s["rejoined"] == 0 for s in off["stats"])
+    assert int(fast["alive"].sum()) > int(off["alive"].sum())
