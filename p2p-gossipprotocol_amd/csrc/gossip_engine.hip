@@ -119,6 +119,12 @@ struct gossip_ctx {
     void* rb_temp = nullptr;
     size_t rb_temp_bytes = 0;
     RebootArgs reboot{};
+    // closed-form liveness + per-source dead-edge counters (single partition, symmetric, no rejoin)
+    bool closed_live = false;
+    uint16_t* death_r = nullptr;
+    uint32_t* dgone = nullptr;
+    uint32_t* dmask = nullptr;
+    uint32_t* rev = nullptr;              // reverse-edge positions (closed-form liveness); per overlay
     uint32_t* rj_list = nullptr;          // join churn: this round's restarted owned peers (local ids)
     unsigned long long* rj_n = nullptr;   // their count
     BinState bins;               // binned dense rounds: slot layout (gossip_bins.hip)
@@ -127,6 +133,7 @@ struct gossip_ctx {
     uint64_t last_fresh = 0;     // new receipts of the previous round
     bool bin_noskip = false;     // GOSSIP_BIN_NOSKIP: rewrite every slot each binned round (A/B measurement)
     uint32_t scatter_probe = 0;  // GOSSIP_SCATTER_PROBE: partial scatter for timing breakdowns (wrong results)
+    bool full_liveness = false;  // GOSSIP_FULL_LIVENESS: ping every edge each ping round (A/B against closed form)
     uint64_t* seg = nullptr;     // sparse push: per-destination record segments (world x chunk records)
     unsigned long long* d_counts = nullptr;  // records per destination rank
     uint64_t* h_counts = nullptr;            // pinned copy
@@ -201,6 +208,12 @@ void free_state(gossip_ctx* c) {
     hipFree(c->alive);
     hipFree(c->registered);
     hipFree(c->miss);
+    hipFree(c->death_r);
+    hipFree(c->dgone);
+    hipFree(c->dmask);
+    hipFree(c->rev);
+    c->death_r = nullptr;
+    c->dgone = c->dmask = c->rev = nullptr;
     hipFree(c->st);
     if (c->h_st) hipHostFree(c->h_st);
     hipFree(c->cov_hist);
@@ -237,9 +250,11 @@ void free_graph(gossip_ctx* c) {
     hipFree(c->rp);
     hipFree(c->col);
     hipFree(c->chunks);
+    hipFree(c->rev);
     c->rp = nullptr;
     c->col = nullptr;
     c->chunks = nullptr;
+    c->rev = nullptr;
     c->n_edges = c->n_chunks = 0;
     c->graph_ready = false;
 }
@@ -276,6 +291,10 @@ RoundArgs make_args(gossip_ctx* c) {
     a.ex_cnt = c->ex_cnt;
     a.ex_miss = c->ex_miss;
     a.ex_cap = c->cfg.extra_cap;
+    a.death_r = c->death_r;
+    a.dgone = c->dgone;
+    a.dmask = c->dmask;
+    a.rev = c->rev;
     return a;
 }
 
@@ -464,6 +483,19 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
     if (!c->has_schedule) return fail(GOSSIP_ESTATE, "no schedule: call gossip_inject");
     if (c->finished) return fail(GOSSIP_ESTATE, "run finished: call gossip_reset");
     if (c->round >= c->cfg.max_rounds) return fail(GOSSIP_ESTATE, "max_rounds reached");
+    if (c->closed_live && !c->death_r && (c->cfg.churn_threshold || !c->kill_round_sorted.empty())) {
+        HIPCHK(hipMalloc((void**)&c->death_r, c->n_local * 2 + 2));
+        HIPCHK(hipMalloc((void**)&c->dgone, c->n_local * 4 + 4));
+        HIPCHK(hipMalloc((void**)&c->dmask, c->n_local * 4 + 4));
+        HIPCHK(hipMemsetAsync(c->death_r, 0xFF, c->n_local * 2 + 2, c->stream));
+        HIPCHK(hipMemsetAsync(c->dgone, 0, c->n_local * 4 + 4, c->stream));
+        HIPCHK(hipMemsetAsync(c->dmask, 0, c->n_local * 4 + 4, c->stream));
+        if (c->cfg.ping_every && !c->rev) {  // the ping rounds find u -> v from v's row through rev
+            HIPCHK(hipMalloc((void**)&c->rev, c->n_edges * 4 + 4));
+            RoundArgs r0 = make_args(c);
+            HIPCHK(launch_reverse_edges(r0, c->stream));
+        }
+    }
     RoundArgs a = make_args(c);
     const uint32_t pw = pack_w(c);
     if (c->cfg.rejoin_threshold) {  // restarts first: a peer dying this round cannot restart in it
@@ -483,14 +515,25 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
         c->any_dead = true;
         HIPCHK(timed(c, "churn", [&] { return launch_churn(a, pw, c->cfg.rng_seed, c->cfg.churn_threshold, c->stream); }));
     }
+    if (c->death_r && (cnt || c->cfg.churn_threshold))  // this round's deaths -> their in-neighbours' dgone
+        HIPCHK(timed(c, "churn", [&] { return launch_dead_edges(a, c->stream); }));
     if (c->cfg.rejoin_threshold && c->cfg.extra_cap)  // the restarted peers' new out-edges, after the deaths
         HIPCHK(timed(c, "rejoin", [&] {
             return launch_rejoin_select(a, c->reboot, c->rj_list, c->rj_n, c->n_local, c->stream);
         }));
     if (c->cfg.ping_every && c->round % c->cfg.ping_every == 0) {
         HIPCHK(timed(c, "liveness", [&] {
-            hipError_t e = launch_liveness(a, c->stream, 1);
-            if (e == hipSuccess) e = launch_liveness(a, c->stream, 0);
+            hipError_t e = hipSuccess;
+            if (c->closed_live) {
+                // the in-edges of peers whose max_missed-th ping round since death is this one
+                const int64_t pe = c->cfg.ping_every, mm = std::max<uint32_t>(c->cfg.max_missed, 1u);
+                const int64_t hi = (int64_t)c->round - (mm - 1) * pe;
+                if (c->rev && hi >= 0)
+                    e = launch_liveness_window(a, (uint32_t)std::max<int64_t>(0, hi - pe + 1), (uint32_t)hi, c->stream);
+            } else {
+                e = launch_liveness(a, c->stream, 1);
+                if (e == hipSuccess) e = launch_liveness(a, c->stream, 0);
+            }
             if (e == hipSuccess && c->cfg.extra_cap) e = launch_liveness_extra(a, c->stream);
             return e;
         }));
@@ -588,7 +631,7 @@ gossip_status round_compute(gossip_ctx* c) {
     RoundArgs a = c->cur;
     const uint32_t pw = pack_w(c);
     c->in_round = false;
-    if (c->last_pull && a.dead_mode)
+    if (c->last_pull && a.dead_mode && !a.dgone)  // else the per-source counters give the source side
         HIPCHK(timed(c, "src_count", [&] { return launch_src_count(a, pw, c->stream); }));
     if (c->last_bin) {
         BinArgs b{c->bins.bins,        c->bins.n_bins,   c->bins.cb_slot, c->bins.cb_src, c->bins.chunk_begin,
@@ -752,6 +795,7 @@ gossip_status gossip_create(const gossip_config* cfg, gossip_ctx** out) {
     if (const char* h = std::getenv("GOSSIP_HEAVY_DEGREE")) c->heavy = (uint32_t)std::max(1, std::atoi(h));
     if (const char* u = std::getenv("GOSSIP_BIN_NOSKIP"); u && std::atoi(u)) c->bin_noskip = true;
     if (const char* u = std::getenv("GOSSIP_SCATTER_PROBE")) c->scatter_probe = (uint32_t)std::atoi(u);
+    if (const char* u = std::getenv("GOSSIP_FULL_LIVENESS"); u && std::atoi(u)) c->full_liveness = true;
     if (const char* b = std::getenv("GOSSIP_BIN_PERMILLE"); b && !cfg->bin_permille) c->cfg.bin_permille = (uint32_t)std::atoi(b);
     c->n = cfg->n_peers;
     c->begin = b;
@@ -1040,6 +1084,14 @@ gossip_status gossip_reset(gossip_ctx* c) {
     if (c->cfg.extra_cap) {
         HIPCHK(hipMemsetAsync(c->ex_cnt, 0, c->n_local * 4 + 4, s));
         HIPCHK(hipMemsetAsync(c->ex_miss, 0, c->n_local * c->cfg.extra_cap + 1, s));
+    }
+    // closed-form liveness: deaths are permanent and every in-edge of a peer is in its own row
+    c->closed_live = c->n_local == c->n && c->symmetric && !c->cfg.rejoin_threshold && c->cfg.max_rounds < 0xFFFF &&
+                     !c->full_liveness;
+    if (c->death_r) {
+        HIPCHK(hipMemsetAsync(c->death_r, 0xFF, c->n_local * 2 + 2, s));
+        HIPCHK(hipMemsetAsync(c->dgone, 0, c->n_local * 4 + 4, s));
+        HIPCHK(hipMemsetAsync(c->dmask, 0, c->n_local * 4 + 4, s));
     }
     c->n_rep_seen = 0;
     c->any_masked = false;

@@ -125,6 +125,12 @@ struct RoundArgs {
     uint8_t* ex_miss;              // n_local * ex_cap
     uint32_t ex_cap;
     uint32_t pad1;
+    // single-partition symmetric overlays without rejoin (DESIGN.md section 6,
+    // "closed-form liveness"): per-peer death round and per-source edge counters
+    uint16_t* death_r;             // n_local: round of death, 0xFFFF = alive (null: not kept)
+    uint32_t* dgone;               // n_local: out-edges whose target has died (masked or not)
+    uint32_t* dmask;               // n_local: out-edges masked by liveness
+    uint32_t* rev;                 // n_edges: rev[e] for e = (v -> u) is the position of v in u's row
 };
 
 // Re-bootstrap draw (handleDeadPeer peer.cpp:398-404 -> selectAndConnectPeers
@@ -161,6 +167,15 @@ hipError_t launch_reboot_keys(const RoundArgs& a, uint64_t first, uint64_t n, un
 hipError_t launch_rebootstrap(const RoundArgs& a, const RebootArgs& r, const unsigned long long* keys, uint64_t n,
                               hipStream_t s);
 hipError_t launch_src_count(const RoundArgs& a, uint32_t W, hipStream_t s);
+// after the round's deaths: dgone[u]++ for every in-neighbour u of a peer
+// that died this round (its own row, the overlay being symmetric)
+hipError_t launch_dead_edges(const RoundArgs& a, hipStream_t s);
+// closed-form liveness of a ping round: the in-edges of peers that died in
+// death rounds [lo, hi] reach max_missed misses now; alive reporters mask them,
+// report and (dmask) count them
+hipError_t launch_liveness_window(const RoundArgs& a, uint32_t lo, uint32_t hi, hipStream_t s);
+// rev[] of the symmetric overlay (once per overlay)
+hipError_t launch_reverse_edges(const RoundArgs& a, hipStream_t s);
 // join churn, before the round's kills and deaths: peers dead at round start
 // restart (alive, registered, seen cleared, row dropped, overflow row emptied);
 // owned ones are appended to list (count in *n_list)

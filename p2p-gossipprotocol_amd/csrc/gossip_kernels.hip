@@ -334,9 +334,14 @@ __global__ __launch_bounds__(kBlock) void k_pull_light(RoundArgs a, uint32_t wd)
             }
             acc.frontier++;
             acc.covered += pc;
-            if (!a.dead_mode) {  // every edge alive and unmasked; else k_src_count books them
+            if (!a.dead_mode) {  // every edge alive and unmasked
                 acc.trav += d;
                 acc.deliv += (unsigned long long)pc * d;
+            } else if (a.dgone) {  // from the per-source counters; else k_src_count books them
+                const uint32_t g = a.dgone[v], k = a.dmask[v];
+                acc.trav += d - k;
+                acc.deliv += (unsigned long long)pc * (d - g);
+                acc.undeliv += (unsigned long long)pc * (g - k);
             }
         }
         const bool light = d <= a.heavy;
@@ -534,7 +539,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_lds(RoundArgs a, 
         // chunk's first unit, the source side of its pushes (broadcastMessage,
         // peer.cpp:310-316) for the owned sources; row lengths loaded together
         constexpr int kSrcIt = (kBinChunkWords / W + kScatterBlock - 1) / kScatterBlock;
-        constexpr int kB = 6;  // sources whose row lengths are loaded together (register budget)
+        constexpr int kB = 5;  // sources whose row lengths are loaded together (register budget)
 #pragma unroll
         for (int k0 = 0; k0 < kSrcIt; k0 += kB) {
             uint32_t pcs[kB];
@@ -564,20 +569,26 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_lds(RoundArgs a, 
                 }
             }
             uint64_t d0[kB], d1[kB];
+            uint32_t dg[kB], dk[kB];  // per-source counters (dead mode); else k_src_count books them
+            const bool cnt = a.dead_mode && a.dgone;
 #pragma unroll
             for (int kk = 0; kk < kB; ++kk) {
                 const uint64_t lv = vb + threadIdx.x + (uint64_t)(k0 + kk) * kScatterBlock - a.begin;
                 d0[kk] = pcs[kk] ? a.rp[lv] : 0ull;
                 d1[kk] = pcs[kk] ? a.rp[lv + 1] : 0ull;
+                dg[kk] = pcs[kk] && cnt ? a.dgone[lv] : 0u;
+                dk[kk] = pcs[kk] && cnt ? a.dmask[lv] : 0u;
             }
 #pragma unroll
             for (int kk = 0; kk < kB; ++kk) {
                 if (!pcs[kk]) continue;
                 acc.frontier++;
                 acc.covered += pcs[kk];
-                if (!a.dead_mode) {  // else k_src_count books them
-                    acc.trav += d1[kk] - d0[kk];
-                    acc.deliv += (unsigned long long)pcs[kk] * (d1[kk] - d0[kk]);
+                const uint64_t d = d1[kk] - d0[kk];
+                if (!a.dead_mode || cnt) {
+                    acc.trav += d - dk[kk];
+                    acc.deliv += (unsigned long long)pcs[kk] * (d - dg[kk]);
+                    acc.undeliv += (unsigned long long)pcs[kk] * (dg[kk] - dk[kk]);
                 }
             }
         }
@@ -798,12 +809,20 @@ __device__ __forceinline__ void emit_reports(const RoundArgs& a, bool emit, uint
                                              Acc& acc, RepStage& rs) {
     const unsigned long long mask = __ballot(emit);
     if (!mask) return;
+    // one registry atomic per run of emitting lanes reporting the same peer (the
+    // in-edges of one dead peer sit in consecutive lanes of a row walk)
+    const int lane = threadIdx.x & 63;
+    const unsigned long long below = mask & ((1ull << lane) - 1ull);
+    const int pl = below ? 63 - __builtin_clzll(below) : lane;
+    const uint32_t prev_dead = __shfl(dead, pl);
     if (emit) {
         rs.buf[rs.n + lane_rank(mask)] = DeadReport{a.round, reporter, dead};
         acc.reports++;
-        const uint32_t bit = 1u << (dead & 31);
-        const uint32_t old = atomicAnd(&a.registered[dead >> 5], ~bit);
-        if (old & bit) acc.removals++;  // peerList.erase > 0 (seed.cpp:162)
+        if (pl == lane || prev_dead != dead) {
+            const uint32_t bit = 1u << (dead & 31);
+            const uint32_t old = atomicAnd(&a.registered[dead >> 5], ~bit);
+            if (old & bit) acc.removals++;  // peerList.erase > 0 (seed.cpp:162)
+        }
     }
     rs.n += (uint32_t)__popcll(mask);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -869,6 +888,132 @@ __global__ __launch_bounds__(kBlock) void k_liveness_heavy(RoundArgs a) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     flush_reports(a, rs);
+    flush(acc, a.st);
+}
+
+// ---------------------------------------------------------------------------
+// Closed-form liveness (single partition, symmetric overlay, no rejoin).
+// Deaths are permanent, so an edge u->v misses exactly at the ping rounds from
+// v's death on while u is alive: every alive in-neighbour of v reaches
+// max_missed at the same ping round p*(v) -- the max_missed-th ping round at or
+// after v's death -- and a miss counter per edge carries no information.  A
+// ping round then only visits the in-edges of the peers whose p* it is (by
+// symmetry, their own rows), instead of pinging every edge of every alive
+// peer: same masks, reports and registry removals as pingLoop's counters
+// (peer.cpp:328-346, handleDeadPeer :383-397, seed.cpp:158-167).
+// The same death rounds keep two per-source counters -- dgone (out-edges to
+// peers that died) and dmask (out-edges masked) -- from which the source side
+// of a dense round follows without an alive test per edge:
+// traversals = deg - dmask, undelivered = pc (dgone - dmask), deliveries =
+// pc (deg - dgone).
+// ---------------------------------------------------------------------------
+
+// position of c in u's sorted row (mask bits stripped), or ~0
+__device__ __forceinline__ uint64_t find_in_row(const RoundArgs& a, uint64_t u, uint32_t c) {
+    uint64_t lo = a.rp[u], hi = a.rp[u + 1];
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if ((a.col[mid] & ~kMaskedEdge) < c) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo < a.rp[u + 1] && (a.col[lo] & ~kMaskedEdge) == c ? lo : ~0ull;
+}
+
+// Row walks over the symmetric overlay: for each selected row v, each entry
+// e (v -> u) stands for the in-edge u -> v, found at rev[e] in u's row.
+enum : int {
+    kRowsDead = 0,  // v died this round: one more out-edge of u points at a dead peer (dgone[u]++)
+    kRowsLive = 1,  // ping round, v's p* is now: alive u masks u -> v, counts it (dmask[u]++) and reports v
+    kRowsRev = 2,   // every row: rev[e] = position of v in u's row (once per overlay)
+};
+
+template <int MODE>
+__device__ __forceinline__ void row_entry(const RoundArgs& a, bool valid, uint64_t e, uint32_t v, bool& emit,
+                                          uint32_t& reporter, Acc& acc) {
+    emit = false;
+    if (!valid) return;
+    const uint32_t u = a.col[e] & ~kMaskedEdge;
+    reporter = u;
+    if (MODE == kRowsDead) {
+        atomicAdd(&a.dgone[u - a.begin], 1u);
+    } else if (MODE == kRowsRev) {
+        a.rev[e] = (uint32_t)find_in_row(a, u - a.begin, v);
+    } else {
+        acc.checked++;
+        if (!bit_alive(a.alive, u)) return;  // a dead reporter stopped pinging before its count reached max_missed
+        const uint64_t f = a.rev[e];
+        if (a.col[f] & kMaskedEdge) return;
+        a.col[f] = v | kMaskedEdge;  // connectedPeers.erase (peer.cpp:388)
+        atomicAdd(&a.dmask[u - a.begin], 1u);
+        emit = true;
+    }
+}
+
+template <int MODE>
+__device__ __forceinline__ bool row_selected(const RoundArgs& a, uint64_t lv, uint32_t lo, uint32_t hi) {
+    if (MODE == kRowsRev) return true;
+    const uint32_t d = a.death_r[lv];
+    return d != 0xFFFFu && d >= lo && d <= hi;
+}
+
+// light rows (one wave per 64-peer tile, edge-space expansion)
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_rows_light(RoundArgs a, uint32_t lo, uint32_t hi) {
+    GOSSIP_REP_STAGE;
+    Acc acc;
+    const int lane = threadIdx.x & 63;
+    const uint64_t n_tiles = (a.n_local + 63) >> 6;
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); t < n_tiles; t += nwaves) {
+        const uint64_t v = (t << 6) + lane;
+        const bool act = v < a.n_local && row_selected<MODE>(a, v, lo, hi);
+        if (!__any(act)) continue;
+        uint32_t deg = 0;
+        uint64_t rb = 0;
+        if (act) {
+            rb = a.rp[v];
+            const uint64_t d = a.rp[v + 1] - rb;
+            deg = d <= a.heavy ? (uint32_t)d : 0u;
+        }
+        const uint32_t tile_base = (uint32_t)(a.begin + (t << 6));
+        tile_edges(deg, rb, [&](int s, bool valid, uint64_t e) {
+            bool emit;
+            uint32_t u = 0;
+            const uint32_t dv = tile_base + (uint32_t)s;
+            row_entry<MODE>(a, valid, e, dv, emit, u, acc);
+            if (MODE == kRowsLive) emit_reports(a, emit, u, dv, acc, rs);
+        });
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (MODE == kRowsLive) flush_reports(a, rs);
+    flush(acc, a.st);
+}
+
+// heavy rows (one wave per 1024-edge chunk)
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_rows_heavy(RoundArgs a, uint32_t lo, uint32_t hi) {
+    GOSSIP_REP_STAGE;
+    Acc acc;
+    const int lane = threadIdx.x & 63;
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    for (uint64_t ci = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); ci < a.n_chunks; ci += nwaves) {
+        const HeavyChunk ch = a.chunks[ci];
+        if (!row_selected<MODE>(a, ch.v, lo, hi)) continue;
+        const uint32_t dv = (uint32_t)(a.begin + ch.v);
+        for (uint64_t base = ch.e0; base < ch.e1; base += 64) {
+            const uint64_t e = base + lane;
+            bool emit;
+            uint32_t u = 0;
+            row_entry<MODE>(a, e < ch.e1, e, dv, emit, u, acc);
+            if (MODE == kRowsLive) emit_reports(a, emit, u, dv, acc, rs);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (MODE == kRowsLive) flush_reports(a, rs);
     flush(acc, a.st);
 }
 
@@ -1088,6 +1233,7 @@ __device__ __forceinline__ void retire_peer(const RoundArgs& a, uint32_t v, uint
     if (v < a.begin || v >= a.end) return;
     acc.died++;
     const uint64_t lv = v - a.begin;
+    if (a.death_r) a.death_r[lv] = (uint16_t)a.round;
 #pragma unroll
     for (int w = 0; w < W; ++w) {
         const uint64_t mm = a.nw[lv * W + w];
@@ -1524,6 +1670,23 @@ hipError_t launch_rejoin_select(const RoundArgs& a, const RebootArgs& r, const u
     hipLaunchKernelGGL(k_rejoin_select, dim3(grid_for(max_list, kBlock)), dim3(kBlock), 0, s, a, r, list, n_list);
     return hipGetLastError();
 }
+
+template <int MODE>
+static hipError_t launch_rows(const RoundArgs& a, uint32_t lo, uint32_t hi, hipStream_t s) {
+    if (a.n_chunks)
+        hipLaunchKernelGGL(k_rows_heavy<MODE>, dim3(grid_for(a.n_chunks, kWavesPerBlock)), dim3(kBlock), 0, s, a, lo, hi);
+    hipLaunchKernelGGL(k_rows_light<MODE>, dim3(grid_for((a.n_local + 63) / 64, kWavesPerBlock)), dim3(kBlock), 0, s, a,
+                       lo, hi);
+    return hipGetLastError();
+}
+
+hipError_t launch_dead_edges(const RoundArgs& a, hipStream_t s) { return launch_rows<kRowsDead>(a, a.round, a.round, s); }
+
+hipError_t launch_liveness_window(const RoundArgs& a, uint32_t lo, uint32_t hi, hipStream_t s) {
+    return launch_rows<kRowsLive>(a, lo, hi, s);
+}
+
+hipError_t launch_reverse_edges(const RoundArgs& a, hipStream_t s) { return launch_rows<kRowsRev>(a, 0, 0, s); }
 
 hipError_t launch_src_count(const RoundArgs& a, uint32_t W_, hipStream_t s) {
     const uint64_t tiles = (a.n_local + 63) / 64;
