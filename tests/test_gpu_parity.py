@@ -241,3 +241,33 @@ def test_rebootstrap_parity(oracle, idx, n, cap):
         assert np.array_equal(ex, ref["extra_cols"])
         e.reset()
         assert e.run() == first
+
+
+@pytest.mark.parametrize("max_missed,ping", [(3, 3), (1, 2), (2, 5)])
+def test_closed_form_liveness_kills_and_hubs(oracle, max_missed, ping):
+    """Closed-form liveness (single partition, symmetric overlay): the in-edges
+    of a dead peer are visited through its own row at its max_missed-th ping
+    round; hubs (heavy rows, chunked) and light peers killed at various
+    rounds, with churn on top; bit-exact against the oracle's per-edge miss
+    counters, and equal to the engine's own per-edge scan (GOSSIP_FULL_LIVENESS)."""
+    import os
+    base = config(2, 1 << 14, pick=oracle.pick_origins)
+    kills = [(0, 1), (1, 2), (5, 2), (100, 4), (7777, 0), (2, 6)]
+    w = dataclasses.replace(base, kills=kills, ping_every=ping, max_missed=max_missed, min_rounds=24,
+                            churn_threshold=int(0.01 * 2**32))
+    rp, col = oracle.gen_workload(w)
+    ref = oracle.simulate_workload(w, rp, col)
+    assert sum(s["reports"] for s in ref["stats"]) > 0
+    runs = []
+    for full in ("0", "1"):
+        os.environ["GOSSIP_FULL_LIVENESS"] = full
+        try:
+            with _engine(w) as e:
+                e.build_graph()
+                e.inject(w.origins, w.inject_rounds)
+                e.schedule_kills([k[0] for k in w.kills], [k[1] for k in w.kills])
+                e.reset()
+                runs.append(_compare(e, ref, w))
+        finally:
+            del os.environ["GOSSIP_FULL_LIVENESS"]
+    assert runs[0] == runs[1]
