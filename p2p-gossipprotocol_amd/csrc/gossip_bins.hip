@@ -24,7 +24,11 @@
 //   bins    : whole 64-peer tiles, <= kBinWords/Wp peers and <= kBinSlotCap slots
 //   bdst    : u16 per slot -> destination - bin.v0 (padding slots: 0, val 0)
 //   val     : Wp u64 per slot (the source's words of the last binned round)
-//   cb_slot, cb_src : u32 slot / u16 chunk-local source per binned edge, (source chunk, bin) order
+//   cb_src  : u16 chunk-local source per binned edge, (source chunk, bin) order;
+//             bit 15 marks the first entry of a run of consecutive slots
+//   cb_run  : u32 per run: slot - position (the slot of entry p is p + cb_run[run])
+//   cb_grp  : u32 per 64 entries: the run of the group's first entry, so a
+//             wave finds each lane's run with one ballot of the bit-15 flags
 //   chunk_begin     : offsets of each (global) source chunk's cb entries
 //   units, xcd_units: scatter work units and their split over the 8 XCDs
 // Construction: (a) 64-bit key (bin << 32 | source) per edge of a light row,
@@ -32,7 +36,8 @@
 // in source order; (b) key = chunk(source) * n_bins + bin per slot-order
 // position, stable sort -> cb order.  The (chunk, bin) slots are contiguous
 // because chunks are source ranges, and the cb entries of a pair are in slot
-// order, so a run of consecutive entries stores to consecutive slots.
+// order, so a run of consecutive entries stores to consecutive slots; (c) the
+// slots are stored once per run (about 7 entries at config 4), not per entry.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -129,6 +134,27 @@ __global__ void k_cb_fill(const uint32_t* svals, uint64_t n_binned, const unsign
     }
 }
 
+// (c) run encoding: an entry starts a run unless its slot follows the previous
+// entry's; the slot of entry p of run r is p + cb_run[r] (mod 2^32).
+__global__ void k_run_flags(const uint32_t* cb_slot, uint64_t n_binned, uint16_t* cb_src, uint32_t* flag) {
+    for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n_binned;
+         p += (uint64_t)gridDim.x * blockDim.x) {
+        const bool st = p == 0 || cb_slot[p] != cb_slot[p - 1] + 1;
+        flag[p] = st;
+        if (st) cb_src[p] |= kRunStart;
+    }
+}
+
+// ids: inclusive prefix sum of the flags (run of entry p = ids[p] - 1)
+__global__ void k_run_fill(const uint32_t* cb_slot, const uint32_t* flag, const uint32_t* ids, uint64_t n_binned,
+                           uint32_t* cb_run, uint32_t* cb_grp) {
+    for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n_binned;
+         p += (uint64_t)gridDim.x * blockDim.x) {
+        if (flag[p]) cb_run[ids[p] - 1] = cb_slot[p] - (uint32_t)p;
+        if ((p & 63) == 0) cb_grp[p >> 6] = ids[p] - 1;
+    }
+}
+
 // chunk_begin[c] = first cb position whose key >= c * n_bins (keys sorted).
 __global__ void k_chunk_bounds(const uint32_t* skeys, uint64_t n_binned, uint32_t n_bins, uint64_t n_chunks,
                                uint64_t* chunk_begin) {
@@ -162,15 +188,15 @@ __global__ void k_chunk_bounds(const uint32_t* skeys, uint64_t n_binned, uint32_
 
 void free_bins(BinState* b) {
     hipFree(b->bins);
-    hipFree(b->cb_slot);
     hipFree(b->cb_src);
+    hipFree(b->cb_run);
+    hipFree(b->cb_grp);
     hipFree(b->chunk_begin);
     hipFree(b->units);
     hipFree(b->xcd_units);
-    hipFree(b->nz[0]);
-    hipFree(b->nz[1]);
     hipFree(b->bdst);
     hipFree(b->val);
+    hipFree(b->dummy);
     *b = BinState{};
 }
 
@@ -191,6 +217,7 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
     unsigned long long *keys64_in = nullptr, *keys64_out = nullptr;
     uint32_t *keys_in = nullptr, *vals_in = nullptr, *keys_out = nullptr, *vals_out = nullptr;
     uint32_t* row = nullptr;
+    uint32_t* cb_slot = nullptr;  // per cb entry, until the run encoding is built
     uint64_t chunk_words = kBinChunkWords;
     if (const char* c = std::getenv("GOSSIP_BIN_CHUNK"))
         chunk_words = std::max<uint64_t>(512, std::min<uint64_t>(kBinChunkWords, std::strtoull(c, nullptr, 0) / 512 * 512));
@@ -293,6 +320,7 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
     BCHECK(hipMalloc((void**)&st.val, (slots + kBinSlotPad) * Wp * sizeof(uint64_t)));
     BCHECK(hipMemsetAsync(st.bdst, 0, (slots + kBinSlotPad) * sizeof(uint16_t), s));
     BCHECK(hipMemsetAsync(st.val, 0, (slots + kBinSlotPad) * Wp * sizeof(uint64_t), s));
+    BCHECK(hipMalloc((void**)&st.dummy, (uint64_t)kScatterGrid * kScatterBlock * Wp * sizeof(uint64_t)));
     hipLaunchKernelGGL(k_bin_assign, dim3(gridn(m)), dim3(256), 0, s, keys64_out, vals_out, m, st.bins,
                        (uint32_t)st.n_bins, row, st.bdst);
     BCHECK(hipGetLastError());
@@ -318,11 +346,11 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
     hipFree(temp);
     keys_in = vals_in = nullptr;
     temp = nullptr;
-    BCHECK(hipMalloc((void**)&st.cb_slot, (upos + 1) * sizeof(uint32_t)));
+    BCHECK(hipMalloc((void**)&cb_slot, (upos + 1) * sizeof(uint32_t)));
     BCHECK(hipMalloc((void**)&st.cb_src, (upos + 1) * sizeof(uint16_t)));
     BCHECK(hipMalloc((void**)&st.chunk_begin, (n_chunks + 1) * sizeof(uint64_t)));
     hipLaunchKernelGGL(k_cb_fill, dim3(gridn(upos)), dim3(256), 0, s, vals_out, upos, keys64_out, st.bins,
-                       (uint32_t)chunk, st.cb_slot, st.cb_src);
+                       (uint32_t)chunk, cb_slot, st.cb_src);
     BCHECK(hipGetLastError());
     hipLaunchKernelGGL(k_chunk_bounds, dim3(gridn(n_chunks + 1)), dim3(256), 0, s, keys_out, upos,
                        (uint32_t)st.n_bins, n_chunks, st.chunk_begin);
@@ -330,6 +358,34 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
     BCHECK(hipStreamSynchronize(s));
     hipFree(keys64_out);
     keys64_out = nullptr;
+
+    // (c) runs: flags into keys_out, their inclusive sum into vals_out (both >= upos + 1 words)
+    {
+        uint32_t n_runs = 0;
+        if (upos) {
+            hipLaunchKernelGGL(k_run_flags, dim3(gridn(upos)), dim3(256), 0, s, cb_slot, upos, st.cb_src, keys_out);
+            BCHECK(hipGetLastError());
+            temp_bytes = 0;
+            BCHECK(hipcub::DeviceScan::InclusiveSum(nullptr, temp_bytes, keys_out, vals_out, upos, s));
+            BCHECK(hipMalloc(&temp, temp_bytes + 16));
+            BCHECK(hipcub::DeviceScan::InclusiveSum(temp, temp_bytes, keys_out, vals_out, upos, s));
+            BCHECK(hipMemcpyAsync(&n_runs, vals_out + upos - 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+            BCHECK(hipStreamSynchronize(s));
+            hipFree(temp);
+            temp = nullptr;
+        }
+        st.n_runs = n_runs;
+        BCHECK(hipMalloc((void**)&st.cb_run, ((uint64_t)n_runs + 1) * sizeof(uint32_t)));
+        BCHECK(hipMalloc((void**)&st.cb_grp, ((upos + 63) / 64 + 1) * sizeof(uint32_t)));
+        if (upos) {
+            hipLaunchKernelGGL(k_run_fill, dim3(gridn(upos)), dim3(256), 0, s, cb_slot, keys_out, vals_out, upos,
+                               st.cb_run, st.cb_grp);
+            BCHECK(hipGetLastError());
+        }
+        BCHECK(hipStreamSynchronize(s));
+        hipFree(cb_slot);
+        cb_slot = nullptr;
+    }
 
     // scatter work units: chunks split into <= kBinUnitCap entries (every chunk
     // has at least one: its first unit books the chunk's source-side stats);
@@ -359,10 +415,6 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
         BCHECK(hipMemcpy(st.units, units.data(), units.size() * sizeof(BinUnit), hipMemcpyHostToDevice));
         BCHECK(hipMalloc((void**)&st.xcd_units, 9 * sizeof(uint64_t)));
         BCHECK(hipMemcpy(st.xcd_units, xu.data(), 9 * sizeof(uint64_t), hipMemcpyHostToDevice));
-        for (int k = 0; k < 2; ++k) {  // val starts zeroed: no slot holds anything yet
-            BCHECK(hipMalloc((void**)&st.nz[k], (n_global / 64 + 2) * sizeof(uint64_t)));
-            BCHECK(hipMemset(st.nz[k], 0, (n_global / 64 + 2) * sizeof(uint64_t)));
-        }
     }
 
 done:
@@ -377,6 +429,7 @@ done:
     hipFree(vals_out);
     hipFree(temp);
     hipFree(row);
+    hipFree(cb_slot);
     if (rc != hipSuccess) {
         hipGetLastError();  // clear a sticky allocation error
         free_bins(&st);

@@ -131,6 +131,10 @@ struct gossip_ctx {
     bool bins_ready = false;
     bool last_bin = false;       // the pull round in flight runs binned
     uint64_t last_fresh = 0;     // new receipts of the previous round
+    hipStream_t aux = nullptr;           // side stream: slot clears of gossip_reset
+    hipEvent_t ev_main = nullptr, ev_clear = nullptr;
+    bool clear_pending = false;          // the next binned round waits for ev_clear
+    bool bins_dirty = false;             // a binned round wrote slots since the last clear
     bool bin_noskip = false;     // GOSSIP_BIN_NOSKIP: rewrite every slot each binned round (A/B measurement)
     uint32_t scatter_probe = 0;  // GOSSIP_SCATTER_PROBE: partial scatter for timing breakdowns (wrong results)
     bool full_liveness = false;  // GOSSIP_FULL_LIVENESS: ping every edge each ping round (A/B against closed form)
@@ -411,6 +415,8 @@ gossip_status upload_csr(gossip_ctx* c, const uint64_t* rp, const uint32_t* col,
 // Slot layout for binned dense rounds: only for a full, symmetric overlay
 // (pull-eligible); skipped, not failed, when it does not fit in HBM.
 gossip_status prepare_bins(gossip_ctx* c) {
+    if (c->aux) HIPCHK(hipStreamSynchronize(c->aux));  // no slot clear in flight
+    c->clear_pending = c->bins_dirty = false;
     free_bins(&c->bins);
     c->bins_ready = false;
     if (!c->symmetric || (c->cfg.flags & GOSSIP_FLAG_NO_BIN) || !c->n_edges) return GOSSIP_OK;
@@ -419,8 +425,11 @@ gossip_status prepare_bins(gossip_ctx* c) {
         build_bins(c->rp, c->col, c->n_local, c->n, c->n_edges, c->heavy, c->Wp, c->stream, &c->bins, &err);
     if (e == hipErrorOutOfMemory || e == hipErrorInvalidValue) return GOSSIP_OK;  // dense rounds gather instead
     if (e != hipSuccess) return fail(GOSSIP_EHIP, "bin layout: " + err);
-    if (c->bin_noskip)  // nz[0] stays "every slot may hold something": every slot is rewritten each round
-        HIPCHK(hipMemset(c->bins.nz[0], 0xFF, (c->n / 64 + 2) * sizeof(uint64_t)));
+    if (!c->aux) {
+        HIPCHK(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&c->ev_main, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&c->ev_clear, hipEventDisableTiming));
+    }
     c->bins_ready = true;
     return GOSSIP_OK;
 }
@@ -624,6 +633,22 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
     return GOSSIP_OK;
 }
 
+// Slot words of binned rounds are zeroed on the side stream at a reset,
+// overlapping the early (push) rounds of the next run; its first binned round
+// waits for it (k_bin_scatter_lds writes only the slots of active sources).
+// (Launched instead when a run leaves its binned rounds, the clear slowed the
+// following gather-pull rounds by more: 85.7 against 73.7 ms per step.)
+gossip_status clear_slots(gossip_ctx* c) {
+    if (!c->bins_ready || !c->bins_dirty) return GOSSIP_OK;
+    HIPCHK(hipEventRecord(c->ev_main, c->stream));
+    HIPCHK(hipStreamWaitEvent(c->aux, c->ev_main, 0));
+    HIPCHK(hipMemsetAsync(c->bins.val, 0, (c->bins.n_slots + kBinSlotPad) * c->Wp * 8, c->aux));
+    HIPCHK(hipEventRecord(c->ev_clear, c->aux));
+    c->clear_pending = true;
+    c->bins_dirty = false;
+    return GOSSIP_OK;
+}
+
 // Round phase 2: the push or pull kernels (after the caller's all-gather in a
 // partitioned pull round).
 gossip_status round_compute(gossip_ctx* c) {
@@ -634,12 +659,17 @@ gossip_status round_compute(gossip_ctx* c) {
     if (c->last_pull && a.dead_mode && !a.dgone)  // else the per-source counters give the source side
         HIPCHK(timed(c, "src_count", [&] { return launch_src_count(a, pw, c->stream); }));
     if (c->last_bin) {
-        BinArgs b{c->bins.bins,        c->bins.n_bins,   c->bins.cb_slot, c->bins.cb_src, c->bins.chunk_begin,
-                  c->bins.n_chunks,    c->bins.chunk,    c->bins.units,   c->bins.xcd_units, c->bins.bdst,
-                  c->bins.val,         c->bins.bin_words, c->bins.nz[c->bins.nz_cur], c->bins.nz[c->bins.nz_cur ^ 1], c->scatter_probe};
+        if (c->clear_pending) {  // clear_slots (side stream)
+            HIPCHK(hipStreamWaitEvent(c->stream, c->ev_clear, 0));
+            c->clear_pending = false;
+        }
+        c->bins_dirty = true;
+        BinArgs b{c->bins.bins,     c->bins.n_bins,    c->bins.cb_src,  c->bins.cb_run,    c->bins.cb_grp,
+                  c->bins.n_binned, c->bins.chunk_begin, c->bins.n_chunks, c->bins.chunk,    c->bins.units,
+                  c->bins.xcd_units, c->bins.bdst,     c->bins.val,     c->bins.bin_words, c->bins.dummy,   c->bin_noskip,
+                  c->scatter_probe};
         HIPCHK(timed(c, "bin_scatter", [&] { return launch_bin_scatter(a, b, pw, c->stream); }));
         HIPCHK(timed(c, "bin_apply", [&] { return launch_bin_apply(a, b, pw, c->stream); }));
-        if (!c->bin_noskip) c->bins.nz_cur ^= 1;
         HIPCHK(timed(c, "pull_heavy", [&] { return launch_pull_heavy(a, pw, c->stream); }));
         return GOSSIP_OK;
     }
@@ -683,9 +713,11 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
     if (c->timing) {
         if (c->last_bin) {
             const double wb = 8.0 * c->Wp;
-            // slices of every source chunk + row bounds of the frontier + 6 B cb entry per binned edge + slot writes
+            // slices of every source chunk + row bounds of the frontier + the run-encoded cb list (2 B per
+            // binned edge, 4 B per run, 4 B per 64 entries) + slot writes
             const double n_src = c->gather ? (double)c->n : (double)c->n_local;
-            c->kbytes["bin_scatter"] += wb * n_src + 16.0 * d.frontier + 6.0 * c->bins.n_binned + wb * (double)d.pull_gathers;
+            const double cb = 2.0 * c->bins.n_binned + 4.0 * c->bins.n_runs + 4.0 * ((c->bins.n_binned + 63) / 64);
+            c->kbytes["bin_scatter"] += wb * n_src + 16.0 * d.frontier + cb + wb * (double)d.pull_gathers;
             c->kbytes["bin_apply"] += (2.0 + wb) * (double)d.pull_edges + 2.0 * wb * c->n_local;
             c->kbytes["pull_heavy"] += 12.0 * (double)d.heavy_traversals;
         }
@@ -858,6 +890,12 @@ void gossip_destroy(gossip_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
+    if (c->aux) {
+        hipStreamSynchronize(c->aux);
+        hipStreamDestroy(c->aux);
+        hipEventDestroy(c->ev_main);
+        hipEventDestroy(c->ev_clear);
+    }
     drain_timers(c);
     free_state(c);
     free_graph(c);
@@ -1076,7 +1114,7 @@ gossip_status gossip_reset(gossip_ctx* c) {
     HIPCHK(hipMemsetAsync(c->n_reports, 0, sizeof(unsigned long long), s));
     if (c->cov_hist) HIPCHK(hipMemsetAsync(c->cov_hist, 0, (uint64_t)c->cfg.max_rounds * 64 * c->Wp * 8, s));
     if (c->miss) HIPCHK(hipMemsetAsync(c->miss, 0, c->n_edges + 1, s));
-    // the slot words survive a reset; nz[nz_cur] still says which of them are nonzero
+    if (gossip_status st = clear_slots(c)) return st;
     if (c->any_masked && c->col && c->n_edges) {
         hipLaunchKernelGGL(k_unmask, dim3(2048), dim3(256), 0, s, c->col, c->n_edges);
         HIPCHK(hipGetLastError());

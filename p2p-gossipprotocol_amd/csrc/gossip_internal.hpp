@@ -37,7 +37,10 @@ constexpr uint64_t kBinSlotCap = 1u << 18;  // slots per bin (load balance betwe
 constexpr uint32_t kBinChunkWords = 18432;     // source chunk: its new words (144 KB) are staged in LDS
 constexpr uint64_t kBinUnitCap = 1u << 17;     // cb entries per scatter work unit (hub chunks are split)
 constexpr int kScatterBlock = 1024;            // k_bin_scatter_lds: one 16-wave workgroup per CU
+constexpr int kScatterGrid = 256;              // one workgroup per CU
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
+constexpr uint16_t kRunStart = 0x8000u;        // cb_src flag; chunk-local sources are < kBinChunkWords < 2^15
+static_assert(kBinChunkWords < kRunStart, "chunk-local sources fit 15 bits");
 
 struct Bin {
     uint32_t v0, v1;  // destination peers [v0, v1) (local ids, whole 64-peer tiles)
@@ -53,8 +56,11 @@ struct BinUnit {        // one scatter work unit: cb entries [p0, p1) of source 
 struct BinArgs {
     const Bin* bins;
     uint64_t n_bins;
-    const uint32_t* cb_slot;      // per binned edge, chunk-major order: its slot
-    const uint16_t* cb_src;       // per binned edge, chunk-major order: its source peer, local to the chunk
+    const uint16_t* cb_src;       // per binned edge, chunk-major order: its source peer, local to the chunk;
+                                  // bit 15 (kRunStart): the entry starts a run of consecutive slots
+    const uint32_t* cb_run;       // per run: slot - position of its entries (mod 2^32)
+    const uint32_t* cb_grp;       // per 64-entry group: the run of its first entry
+    uint64_t n_binned;            // cb entries
     const uint64_t* chunk_begin;  // n_chunks + 1 offsets into cb_*
     uint64_t n_chunks, chunk;     // source chunks of `chunk` peers
     const BinUnit* units;         // scatter work units, in chunk order
@@ -62,17 +68,18 @@ struct BinArgs {
     const uint16_t* bdst;         // per slot: destination - bin.v0
     uint64_t* val;                // per slot: Wp words, the source's new words of this round
     uint32_t bin_words;           // LDS accumulator words of a bin (kBinWords or kBinWords / 2)
-    const uint64_t* nz_prev;      // per source bit: its slots hold nonzero words (previous binned round)
-    uint64_t* nz_next;            // the same bits for this round's words
-    uint32_t probe;               // measurement only (GOSSIP_SCATTER_PROBE): 1 staging only, 2 + entry loads,
-                                  // 3 + LDS reads; results are then wrong
+    uint64_t* dummy;              // kScatterGrid * kScatterBlock * Wp words: stores of lanes with no slot
+    uint32_t noskip;              // GOSSIP_BIN_NOSKIP: every slot is rewritten (A/B measurement)
+    uint32_t probe;               // measurement only (GOSSIP_SCATTER_PROBE=1: staging only; results are then wrong)
 };
 
 struct BinState {
     Bin* bins = nullptr;
     uint64_t n_bins = 0;
-    uint32_t* cb_slot = nullptr;
     uint16_t* cb_src = nullptr;
+    uint32_t* cb_run = nullptr;
+    uint32_t* cb_grp = nullptr;
+    uint64_t n_runs = 0;
     uint64_t* chunk_begin = nullptr;
     uint64_t n_chunks = 0, chunk = 0;
     BinUnit* units = nullptr;
@@ -80,8 +87,7 @@ struct BinState {
     uint64_t n_units = 0;
     uint16_t* bdst = nullptr;
     uint64_t* val = nullptr;
-    uint64_t* nz[2] = {nullptr, nullptr};  // per-source "slots hold nonzero" bits; nz[nz_cur] = previous round
-    int nz_cur = 0;
+    uint64_t* dummy = nullptr;
     uint32_t bin_words = kBinWords;
     uint64_t n_slots = 0;   // padded
     uint64_t n_binned = 0;  // edges with a slot (light destinations)

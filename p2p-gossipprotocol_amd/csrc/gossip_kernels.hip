@@ -503,9 +503,12 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_lds(RoundArgs a, 
     constexpr int kSliceIt = kBinChunkWords / kScatterBlock;  // slice words per lane
     static_assert(kBinChunkWords % kScatterBlock == 0, "slice split");
     __shared__ unsigned long long slice[kBinChunkWords];
-    // which of the chunk's sources have anything to write: nonzero new words
-    // now, or nonzero in the previous binned round (their slots still hold
-    // it).  A source with neither finds zeros in its slots and skips them.
+    // which of the chunk's sources have anything to write: nonzero new words.
+    // An idle source leaves its slots alone.  A slot may thus keep a word of
+    // an earlier binned round of the same run: that round OR-ed it into
+    // seen[dst] (deaths are permanent and dead peers never receive, so seen
+    // still holds it), and the apply masks with ~seen.  gossip_reset zeroes
+    // the slots (side stream) before the first binned round of a run.
     __shared__ unsigned long long live_s[kBinChunkWords / 64];
     __shared__ unsigned int cov_s[COV ? 64 * W : 1];
     if (COV) {
@@ -529,11 +532,10 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_lds(RoundArgs a, 
             const uint64_t i = threadIdx.x + (uint64_t)k * kScatterBlock;
             r[k] = i < nwords ? a.nw_src[vb * W + i] : 0ull;
         }
-        const uint64_t prev = threadIdx.x < (n_src + 63) / 64 ? b.nz_prev[(vb >> 6) + threadIdx.x] : 0ull;
         __syncthreads();  // previous unit's readers are done with the slice
 #pragma unroll
         for (int k = 0; k < kSliceIt; ++k) slice[threadIdx.x + k * kScatterBlock] = r[k];
-        if (threadIdx.x < kBinChunkWords / 64) live_s[threadIdx.x] = prev;
+        if (threadIdx.x < kBinChunkWords / 64) live_s[threadIdx.x] = b.noskip ? ~0ull : 0ull;
         __syncthreads();
         // per source (a wave covers 64 consecutive ones): live bits and, in the
         // chunk's first unit, the source side of its pushes (broadcastMessage,
@@ -563,10 +565,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_lds(RoundArgs a, 
                         for (uint64_t x = m; x; x &= x - 1) atomicAdd(&cov_s[w * 64 + __builtin_ctzll(x)], 1u);
                 }
                 const unsigned long long bits = __ballot(nz);
-                if (lane == 0) {
-                    live_s[j >> 6] |= bits;
-                    if (un.first) b.nz_next[v >> 6] = bits;
-                }
+                if (lane == 0) live_s[j >> 6] |= bits;
             }
             uint64_t d0[kB], d1[kB];
             uint32_t dg[kB], dk[kB];  // per-source counters (dead mode); else k_src_count books them
@@ -597,45 +596,82 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_lds(RoundArgs a, 
         // consecutive lanes take consecutive entries: the stores of one
         // instruction fall into a few slot runs (measured at config 4: 37 ms
         // per step against 57 ms with 8 consecutive entries per lane; u16
-        // chunk-local sources 36-41 ms against 43-47 ms with u32 global ids)
-        // software-pipelined: the next kU entries are loaded before this
-        // batch's LDS reads and stores, so every wave keeps two batches of
-        // loads in flight
-        const uint64_t step = (uint64_t)kScatterBlock * kU;
-        uint32_t sl[kU], u[kU];
-        auto load = [&](uint64_t p, uint32_t (&s_)[kU], uint32_t (&u_)[kU]) {
+        // chunk-local sources 36-41 ms against 43-47 ms with u32 global ids).
+        // Each wave walks whole 64-entry groups (aligned), so a lane finds its
+        // run with one ballot of the run-start flags: run = cb_grp[group] +
+        // number of starts at lanes 1..lane; slot = position + cb_run[run].
+        // Three-stage software pipeline per wave, ordered so that every wait
+        // is for loads issued before the previous batch's stores (vmcnt
+        // counts loads and stores in issue order): resolve batch i+1 (its
+        // cb_run loads), load the entries of batch i+2, store batch i.  The
+        // loop has no branches -- loads use clamped addresses, raw values are
+        // masked only when resolved, and a lane with nothing to write stores
+        // to its own line of a small L2-resident dummy array -- so the
+        // compiler's waits count exactly instead of draining to vmcnt(0).
+        // positions fit 32 bits (build_bins: fewer than kNoSlot edges)
+        constexpr uint32_t step = (uint32_t)kScatterBlock * kU;
+        const uint32_t p0 = (uint32_t)un.p0, p1 = (uint32_t)un.p1, nb = (uint32_t)b.n_binned;
+        if (p0 >= p1) continue;  // block-uniform; nb >= 1 below
+        const uint32_t base0 = (p0 & ~63u) + threadIdx.x;
+        const uint32_t n_grp = (nb + 63) >> 6;
+        const unsigned long long below = (lane == 63 ? ~0ull : ((2ull << lane) - 1)) & ~1ull;  // lanes 1..lane
+        uint64_t* const sink = b.dummy + ((uint64_t)blockIdx.x * kScatterBlock + threadIdx.x) * W;
+        using Buf = uint32_t[kU];
+        auto load = [&](uint32_t p, Buf& s_, Buf& g_) {
 #pragma unroll
             for (int j = 0; j < kU; ++j) {
-                const uint64_t q = p + (uint64_t)j * kScatterBlock;
-                s_[j] = q < un.p1 ? __builtin_nontemporal_load(b.cb_slot + q) : kNoSlot;
-                u_[j] = q < un.p1 ? (uint32_t)__builtin_nontemporal_load(b.cb_src + q) : 0u;
+                const uint32_t q = p + (uint32_t)j * kScatterBlock;
+                const uint32_t g = __builtin_amdgcn_readfirstlane(q >> 6);  // wave-uniform group
+                s_[j] = (uint32_t)__builtin_nontemporal_load(b.cb_src + min(q, nb - 1));  // raw: masked in resolve
+                g_[j] = b.cb_grp[min(g, n_grp - 1)];
             }
         };
-        load(un.p0 + threadIdx.x, sl, u);
-        for (uint64_t p = un.p0 + threadIdx.x; p < un.p1; p += step) {
-            uint32_t sn[kU], un_[kU];
-            load(p + step, sn, un_);
-            if (b.probe == 2) {
-#pragma unroll
-                for (int j = 0; j < kU; ++j) acc.gathered += sl[j] != kNoSlot && u[j] != 0xFFFFu;
-            } else if (b.probe == 3) {
-#pragma unroll
-                for (int j = 0; j < kU; ++j)
-                    if (sl[j] != kNoSlot && ((live_s[u[j] >> 6] >> (u[j] & 63)) & 1ull))
-                        acc.gathered += slice[(uint64_t)u[j] * W] & 1;
-            } else
+        // runs of a loaded batch: issues the cb_run loads (r_, used one
+        // iteration later), the chunk-local sources (u_) and the lanes with a
+        // slot to write (a_: inside the unit and an active source); past the
+        // end the flags are 0, so the run stays in range
+        auto resolve = [&](uint32_t p, const Buf& s_, const Buf& g_, Buf& r_, Buf& u_, uint32_t& a_) {
+            a_ = 0;
 #pragma unroll
             for (int j = 0; j < kU; ++j) {
-                if (sl[j] == kNoSlot || !((live_s[u[j] >> 6] >> (u[j] & 63)) & 1ull)) continue;
-#pragma unroll
-                for (int w = 0; w < W; ++w) b.val[(uint64_t)sl[j] * W + w] = slice[(uint64_t)u[j] * W + w];
-                acc.gathered++;  // slots written (byte accounting)
+                const uint32_t q = p + (uint32_t)j * kScatterBlock;
+                const uint32_t sv = q < nb ? s_[j] : 0u;
+                const unsigned long long starts = __ballot((sv & kRunStart) != 0);
+                const uint32_t run = g_[j] + (uint32_t)__popcll(starts & below);
+                const uint32_t u = sv & (kRunStart - 1u);  // < chunk: in range of the slice
+                const uint32_t live = (uint32_t)(live_s[u >> 6] >> (u & 63)) & 1u;  // unconditional (no branch)
+                a_ |= ((uint32_t)(q >= p0) & (uint32_t)(q < p1) & live) << j;
+                u_[j] = u;
+                r_[j] = b.cb_run[run];
             }
+        };
+        auto store = [&](uint32_t p, const Buf& r_, const Buf& u_, uint32_t a_) {
 #pragma unroll
             for (int j = 0; j < kU; ++j) {
-                sl[j] = sn[j];
-                u[j] = un_[j];
+                const uint32_t q = p + (uint32_t)j * kScatterBlock;
+                uint64_t* const dst = (a_ >> j) & 1u ? b.val + (uint64_t)(r_[j] + q) * W : sink;
+#pragma unroll
+                for (int w = 0; w < W; ++w) dst[w] = slice[(uint64_t)u_[j] * W + w];
             }
+            acc.gathered += __popc(a_);  // slots written (byte accounting)
+        };
+        // two register sets, alternating (no loop-carried copies, which would
+        // wait for the loads just issued)
+        Buf s0, g0, r0, u0, s1, g1, r1, u1;
+        uint32_t a0, a1;
+        load(base0, s1, g1);
+        resolve(base0, s1, g1, r0, u0, a0);
+        load(base0 + step, s0, g0);
+        for (uint32_t base = p0 & ~63u;; base += 2 * step) {  // block-uniform: ballots see every lane
+            const uint32_t p = base + threadIdx.x;
+            resolve(p + step, s0, g0, r1, u1, a1);
+            load(p + 2 * step, s1, g1);
+            store(p, r0, u0, a0);
+            if (base + step >= p1) break;
+            resolve(p + 2 * step, s1, g1, r0, u0, a0);
+            load(p + 3 * step, s0, g0);
+            store(p + step, r1, u1, a1);
+            if (base + 2 * step >= p1) break;
         }
     }
     flush<kWaves>(acc, a.st);
@@ -1602,10 +1638,11 @@ static int scatter_u() {
 hipError_t launch_bin_scatter(const RoundArgs& a, const BinArgs& b, uint32_t W_, hipStream_t s) {
     const uint32_t wd = wd_of(W_);
     GOSSIP_DISPATCH_W(wp_of(W_), {  // one workgroup per CU (128 KB of LDS each)
-        if (a.cov) hipLaunchKernelGGL((k_bin_scatter_lds<W, true, 4>), dim3(256), dim3(kScatterBlock), 0, s, a, b, wd);
+        if (a.cov)
+            hipLaunchKernelGGL((k_bin_scatter_lds<W, true, 4>), dim3(kScatterGrid), dim3(kScatterBlock), 0, s, a, b, wd);
         else if (scatter_u() == 8)
-            hipLaunchKernelGGL((k_bin_scatter_lds<W, false, 8>), dim3(256), dim3(kScatterBlock), 0, s, a, b, wd);
-        else hipLaunchKernelGGL((k_bin_scatter_lds<W, false, 4>), dim3(256), dim3(kScatterBlock), 0, s, a, b, wd);
+            hipLaunchKernelGGL((k_bin_scatter_lds<W, false, 8>), dim3(kScatterGrid), dim3(kScatterBlock), 0, s, a, b, wd);
+        else hipLaunchKernelGGL((k_bin_scatter_lds<W, false, 4>), dim3(kScatterGrid), dim3(kScatterBlock), 0, s, a, b, wd);
     });
     return hipGetLastError();
 }
