@@ -72,6 +72,11 @@ struct gossip_ctx {
     // dynamic state
     uint64_t *seen = nullptr, *nw = nullptr, *nx = nullptr;
     uint64_t* front = nullptr;  // pull-round frontier bitmap
+    uint64_t* tact[2] = {nullptr, nullptr};  // push-round frontier tiles (1 bit per 64 peers), this / next round
+    int tcur = 0;                            // tact[tcur]: this round's
+    uint64_t prev_frontier_est = 0;          // frontier_est of the round before
+    bool tact_ok = true;                     // tact[tcur] covers every tile with nonzero new words
+    bool tact_marked = false;                // this round's activations mark tact[tcur ^ 1]
     uint32_t* alive = nullptr;
     uint32_t* registered = nullptr;
     uint8_t* miss = nullptr;
@@ -131,10 +136,7 @@ struct gossip_ctx {
     bool bins_ready = false;
     bool last_bin = false;       // the pull round in flight runs binned
     uint64_t last_fresh = 0;     // new receipts of the previous round
-    hipStream_t aux = nullptr;           // side stream: slot clears of gossip_reset
-    hipEvent_t ev_main = nullptr, ev_clear = nullptr;
-    bool clear_pending = false;          // the next binned round waits for ev_clear
-    bool bins_dirty = false;             // a binned round wrote slots since the last clear
+    bool bins_first = false;             // no binned round since the last reset: rewrite every slot
     bool bin_noskip = false;     // GOSSIP_BIN_NOSKIP: rewrite every slot each binned round (A/B measurement)
     uint32_t scatter_probe = 0;  // GOSSIP_SCATTER_PROBE: partial scatter for timing breakdowns (wrong results)
     bool full_liveness = false;  // GOSSIP_FULL_LIVENESS: ping every edge each ping round (A/B against closed form)
@@ -209,6 +211,9 @@ void free_state(gossip_ctx* c) {
     hipFree(c->nw);
     hipFree(c->nx);
     hipFree(c->front);
+    hipFree(c->tact[0]);
+    hipFree(c->tact[1]);
+    c->tact[0] = c->tact[1] = nullptr;
     hipFree(c->alive);
     hipFree(c->registered);
     hipFree(c->miss);
@@ -263,6 +268,8 @@ void free_graph(gossip_ctx* c) {
     c->graph_ready = false;
 }
 
+uint64_t tact_bytes(const gossip_ctx* c) { return (((c->n_local + 63) / 64 + 63) / 64 + 1) * 8; }
+
 RoundArgs make_args(gossip_ctx* c) {
     RoundArgs a{};
     a.rp = c->rp;
@@ -275,6 +282,18 @@ RoundArgs make_args(gossip_ctx* c) {
     a.n_src = c->n_local;
     a.nx = c->nx;
     a.front = c->front;
+    if (c->tact[0] && c->n_local == c->n && c->world == 1) {  // single partition: remote applies keep no marks
+        a.tcur = c->tact[c->tcur];
+        // the marked-tile sweep only for a nearly empty frontier (it walks 64 tiles per wave in turn;
+        // at a 1.3 % frontier, 57 % of the tiles, the full sweep was faster: 3.1 against 4.4 ms)
+        a.tsparse = c->tact_ok && c->frontier_est * 500 < c->n_local ? 1u : 0u;
+        // marks cost a check per activation (push_heavy +2 ms per step at config 4 when kept in every
+        // round): kept only where the next frontier is likely small -- a tiny frontier, or a shrinking one
+        const bool small = c->frontier_est * 500 < c->n_local ||
+                           (c->frontier_est < c->prev_frontier_est && c->frontier_est * 100 < c->n_local);
+        a.tnx = small ? c->tact[c->tcur ^ 1] : nullptr;
+        c->tact_marked = small;
+    }
     a.send = c->send;
     a.miss = c->miss;
     a.st = c->st;
@@ -415,8 +434,7 @@ gossip_status upload_csr(gossip_ctx* c, const uint64_t* rp, const uint32_t* col,
 // Slot layout for binned dense rounds: only for a full, symmetric overlay
 // (pull-eligible); skipped, not failed, when it does not fit in HBM.
 gossip_status prepare_bins(gossip_ctx* c) {
-    if (c->aux) HIPCHK(hipStreamSynchronize(c->aux));  // no slot clear in flight
-    c->clear_pending = c->bins_dirty = false;
+    c->bins_first = false;  // a fresh layout holds zeros
     free_bins(&c->bins);
     c->bins_ready = false;
     if (!c->symmetric || (c->cfg.flags & GOSSIP_FLAG_NO_BIN) || !c->n_edges) return GOSSIP_OK;
@@ -425,11 +443,6 @@ gossip_status prepare_bins(gossip_ctx* c) {
         build_bins(c->rp, c->col, c->n_local, c->n, c->n_edges, c->heavy, c->Wp, c->stream, &c->bins, &err);
     if (e == hipErrorOutOfMemory || e == hipErrorInvalidValue) return GOSSIP_OK;  // dense rounds gather instead
     if (e != hipSuccess) return fail(GOSSIP_EHIP, "bin layout: " + err);
-    if (!c->aux) {
-        HIPCHK(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
-        HIPCHK(hipEventCreateWithFlags(&c->ev_main, hipEventDisableTiming));
-        HIPCHK(hipEventCreateWithFlags(&c->ev_clear, hipEventDisableTiming));
-    }
     c->bins_ready = true;
     return GOSSIP_OK;
 }
@@ -601,6 +614,11 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
     c->last_bin = bin;
     c->last_front = false;
     if (pull) {
+        if (a.tcur) {  // pull / binned rounds set no tile marks: this round's go, the next push round scans
+            HIPCHK(hipMemsetAsync(a.tcur, 0, tact_bytes(c), c->stream));
+            a.tcur = a.tnx = nullptr;
+            a.tsparse = 0;
+        }
         a.nw_src = c->nw;
         a.n_src = c->n_local;
         if (remote) {  // publish this block's new words; the caller all-gathers c->gather
@@ -633,22 +651,6 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
     return GOSSIP_OK;
 }
 
-// Slot words of binned rounds are zeroed on the side stream at a reset,
-// overlapping the early (push) rounds of the next run; its first binned round
-// waits for it (k_bin_scatter_lds writes only the slots of active sources).
-// (Launched instead when a run leaves its binned rounds, the clear slowed the
-// following gather-pull rounds by more: 85.7 against 73.7 ms per step.)
-gossip_status clear_slots(gossip_ctx* c) {
-    if (!c->bins_ready || !c->bins_dirty) return GOSSIP_OK;
-    HIPCHK(hipEventRecord(c->ev_main, c->stream));
-    HIPCHK(hipStreamWaitEvent(c->aux, c->ev_main, 0));
-    HIPCHK(hipMemsetAsync(c->bins.val, 0, (c->bins.n_slots + kBinSlotPad) * c->Wp * 8, c->aux));
-    HIPCHK(hipEventRecord(c->ev_clear, c->aux));
-    c->clear_pending = true;
-    c->bins_dirty = false;
-    return GOSSIP_OK;
-}
-
 // Round phase 2: the push or pull kernels (after the caller's all-gather in a
 // partitioned pull round).
 gossip_status round_compute(gossip_ctx* c) {
@@ -659,17 +661,13 @@ gossip_status round_compute(gossip_ctx* c) {
     if (c->last_pull && a.dead_mode && !a.dgone)  // else the per-source counters give the source side
         HIPCHK(timed(c, "src_count", [&] { return launch_src_count(a, pw, c->stream); }));
     if (c->last_bin) {
-        if (c->clear_pending) {  // clear_slots (side stream)
-            HIPCHK(hipStreamWaitEvent(c->stream, c->ev_clear, 0));
-            c->clear_pending = false;
-        }
-        c->bins_dirty = true;
         BinArgs b{c->bins.bins,     c->bins.n_bins,    c->bins.cb_src,  c->bins.cb_run,    c->bins.cb_grp,
                   c->bins.n_binned, c->bins.chunk_begin, c->bins.n_chunks, c->bins.chunk,    c->bins.units,
-                  c->bins.xcd_units, c->bins.bdst,     c->bins.val,     c->bins.bin_words, c->bins.dummy,   c->bin_noskip,
+                  c->bins.xcd_units, c->bins.bdst,     c->bins.val,     c->bins.bin_words, c->bins.dummy,   c->bin_noskip || c->bins_first,
                   c->scatter_probe};
         HIPCHK(timed(c, "bin_scatter", [&] { return launch_bin_scatter(a, b, pw, c->stream); }));
         HIPCHK(timed(c, "bin_apply", [&] { return launch_bin_apply(a, b, pw, c->stream); }));
+        c->bins_first = false;
         HIPCHK(timed(c, "pull_heavy", [&] { return launch_pull_heavy(a, pw, c->stream); }));
         return GOSSIP_OK;
     }
@@ -684,6 +682,7 @@ gossip_status round_compute(gossip_ctx* c) {
     if (c->cfg.extra_cap)
         HIPCHK(timed(c, "push_extra", [&] { return launch_push_extra(a, pw, c->any_dead, remote, c->stream); }));
     HIPCHK(timed(c, "push_heavy", [&] { return launch_push_heavy(a, pw, c->any_dead, remote, c->stream); }));
+    if (a.tcur && !a.tsparse) HIPCHK(hipMemsetAsync(a.tcur, 0, tact_bytes(c), c->stream));  // unread marks go
     HIPCHK(timed(c, "push_light", [&] { return launch_push_light(a, pw, c->any_dead, remote, c->stream); }));
     if (c->cur_sparse) {
         HIPCHK(timed(c, "compact_send", [&] {
@@ -708,6 +707,7 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
         c->last_st_round = c->round;
     }
     const DevStats d = c->last_st;
+    c->prev_frontier_est = c->frontier_est;
     c->frontier_est = d.activated;
     c->last_fresh = d.new_receipts;
     if (c->timing) {
@@ -764,6 +764,8 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
 
 void advance(gossip_ctx* c, uint64_t fresh_global) {
     std::swap(c->nw, c->nx);  // push: nw was cleared by push_light; pull: the old nw is stale
+    c->tcur ^= 1;             // push with marks: every activation marked its tile; otherwise no marks
+    c->tact_ok = !c->last_pull && c->tact_marked;
     c->nx_dirty = c->last_pull;
     const uint32_t r = c->round;
     c->round++;
@@ -853,6 +855,8 @@ gossip_status gossip_create(const gossip_config* cfg, gossip_ctx** out) {
     if ((err = hipMalloc((void**)&c->nw, words * 8)) != hipSuccess) return bail("new", err);
     if ((err = hipMalloc((void**)&c->nx, words * 8)) != hipSuccess) return bail("next", err);
     if ((err = hipMalloc((void**)&c->front, ((c->n_local + 63) / 64 + 1) * 8)) != hipSuccess) return bail("front", err);
+    for (int k = 0; k < 2; ++k)
+        if ((err = hipMalloc((void**)&c->tact[k], tact_bytes(c))) != hipSuccess) return bail("frontier tiles", err);
     if ((err = hipMalloc((void**)&c->alive, bitwords * 4)) != hipSuccess) return bail("alive", err);
     if ((err = hipMalloc((void**)&c->registered, bitwords * 4)) != hipSuccess) return bail("registry", err);
     if ((err = hipMalloc((void**)&c->st, kStatLines * sizeof(DevStats))) != hipSuccess)
@@ -890,12 +894,6 @@ void gossip_destroy(gossip_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
-    if (c->aux) {
-        hipStreamSynchronize(c->aux);
-        hipStreamDestroy(c->aux);
-        hipEventDestroy(c->ev_main);
-        hipEventDestroy(c->ev_clear);
-    }
     drain_timers(c);
     free_state(c);
     free_graph(c);
@@ -1094,6 +1092,9 @@ gossip_status gossip_reset(gossip_ctx* c) {
     HIPCHK(hipMemsetAsync(c->seen, 0, words * 8, s));
     HIPCHK(hipMemsetAsync(c->nw, 0, words * 8, s));
     HIPCHK(hipMemsetAsync(c->nx, 0, words * 8, s));
+    for (int k = 0; k < 2; ++k) HIPCHK(hipMemsetAsync(c->tact[k], 0, tact_bytes(c), s));
+    c->tact_ok = true;  // no new words anywhere
+    c->tact_marked = false;
     HIPCHK(hipMemsetAsync(c->alive, 0xFF, bitwords * 4, s));
     HIPCHK(hipMemsetAsync(c->registered, 0xFF, bitwords * 4, s));
     if (c->n % 32) {
@@ -1114,7 +1115,8 @@ gossip_status gossip_reset(gossip_ctx* c) {
     HIPCHK(hipMemsetAsync(c->n_reports, 0, sizeof(unsigned long long), s));
     if (c->cov_hist) HIPCHK(hipMemsetAsync(c->cov_hist, 0, (uint64_t)c->cfg.max_rounds * 64 * c->Wp * 8, s));
     if (c->miss) HIPCHK(hipMemsetAsync(c->miss, 0, c->n_edges + 1, s));
-    if (gossip_status st = clear_slots(c)) return st;
+    // slots still hold words of the last run: the first binned round of the next rewrites every slot
+    c->bins_first = true;
     if (c->any_masked && c->col && c->n_edges) {
         hipLaunchKernelGGL(k_unmask, dim3(2048), dim3(256), 0, s, c->col, c->n_edges);
         HIPCHK(hipGetLastError());
@@ -1137,7 +1139,7 @@ gossip_status gossip_reset(gossip_ctx* c) {
     c->last_pull = false;
     c->last_bin = false;
     c->last_fresh = 0;
-    c->frontier_est = 0;
+    c->frontier_est = c->prev_frontier_est = 0;
     c->round = 0;
     c->finished = false;
     c->any_dead = c->n_started < c->n;

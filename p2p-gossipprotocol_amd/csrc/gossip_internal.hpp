@@ -69,8 +69,9 @@ struct BinArgs {
     uint64_t* val;                // per slot: Wp words, the source's new words of this round
     uint32_t bin_words;           // LDS accumulator words of a bin (kBinWords or kBinWords / 2)
     uint64_t* dummy;              // kScatterGrid * kScatterBlock * Wp words: stores of lanes with no slot
-    uint32_t noskip;              // GOSSIP_BIN_NOSKIP: every slot is rewritten (A/B measurement)
-    uint32_t probe;               // measurement only (GOSSIP_SCATTER_PROBE=1: staging only; results are then wrong)
+    uint32_t noskip;              // every slot is rewritten: first binned round after a reset (or GOSSIP_BIN_NOSKIP)
+    uint32_t probe;               // measurement only (GOSSIP_SCATTER_PROBE=1: staging only, 2: slot stores to the
+                                  // sink; results are then wrong)
 };
 
 struct BinState {
@@ -122,6 +123,10 @@ struct RoundArgs {
     uint32_t dead_mode;            // some peers are dead: dense rounds skip dead destinations and the
                                    // traversal stats come from k_src_count (per-edge alive test)
     uint64_t inj_mask[kMaxWords];  // messages injected so far (pull: bits a peer can still learn)
+    uint64_t* tcur;                // push rounds (P = 1): 1 bit per 64-peer tile, a superset of the tiles with
+                                   // nonzero new words; cleared as consumed (nullptr: not kept)
+    uint64_t* tnx;                 // the same bits for the next round's words, set at activation
+    uint32_t tsparse;              // tcur is valid: push_light visits only its tiles
     uint64_t* front;               // pull rounds: 1 bit per source peer, set iff its new words are nonzero
     const uint64_t* nw_src;        // pull rounds: new words of every source, indexed by (global) peer id
     uint64_t n_src;                // peers covered by nw_src / front

@@ -139,6 +139,11 @@ __device__ __forceinline__ void deliver(const RoundArgs& a, uint32_t c, const ui
         if (fr) {
             const unsigned long long onx = atomicOr(reinterpret_cast<unsigned long long*>(a.nx) + lv * W + w, fr);
             acc.activated += onx == 0;
+            if (a.tnx && onx == 0) {  // the peer's tile joins the next round's frontier tiles
+                const unsigned long long tb = 1ull << ((lv >> 6) & 63);
+                unsigned long long* tw = reinterpret_cast<unsigned long long*>(a.tnx) + (lv >> 12);
+                if (!(*tw & tb)) atomicOr(tw, tb);  // read first: most tiles are already marked
+            }
             acc.fresh += (unsigned long long)__popcll(fr);
         }
     }
@@ -149,7 +154,7 @@ __device__ __forceinline__ void deliver(const RoundArgs& a, uint32_t c, const ui
 // round's push-start bookkeeping: frontier, digest and coverage increments
 // (the new words ARE the bits added to seen since the last push start).
 // ---------------------------------------------------------------------------
-template <int W, bool CA, bool RM, bool COV>
+template <int W, bool CA, bool RM, bool COV, bool SP>  // SP: visit only the tiles marked in tcur
 __global__ __launch_bounds__(kBlock) void k_push_light(RoundArgs a, uint32_t wd) {
     __shared__ unsigned int cov_s[COV ? 64 * W : 1];
     if (COV) {
@@ -160,7 +165,7 @@ __global__ __launch_bounds__(kBlock) void k_push_light(RoundArgs a, uint32_t wd)
     const int lane = threadIdx.x & 63;
     const uint64_t n_tiles = (a.n_local + 63) >> 6;
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
-    for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); t < n_tiles; t += nwaves) {
+    auto tile = [&](uint64_t t) {
         const uint64_t v = (t << 6) + lane;
         uint64_t m[W];
         bool act = false;
@@ -169,7 +174,7 @@ __global__ __launch_bounds__(kBlock) void k_push_light(RoundArgs a, uint32_t wd)
             m[w] = v < a.n_local ? a.nw[v * W + w] : 0ull;
             act |= m[w] != 0;
         }
-        if (!__any(act)) continue;
+        if (!__any(act)) return;
         uint32_t pc = 0, deg = 0;
         uint64_t rb = 0;
         if (act) {
@@ -195,6 +200,20 @@ __global__ __launch_bounds__(kBlock) void k_push_light(RoundArgs a, uint32_t wd)
             const uint32_t pcs = __shfl(pc, s);
             if (valid) deliver<W, CA, RM>(a, a.col[e], ms, pcs, acc);
         });
+    };
+    const uint64_t wave0 = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if constexpr (SP) {  // only the tiles marked in tcur (64 per bitmap word), clearing the words
+        const uint64_t n_words = (n_tiles + 63) >> 6;
+        for (uint64_t i = wave0; i < n_words; i += nwaves) {
+            const unsigned long long word = a.tcur[i];
+            unsigned long long bits = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(word >> 32)) << 32) |
+                                      __builtin_amdgcn_readfirstlane((uint32_t)word);  // wave-uniform
+            if (!bits) continue;
+            if (lane == 0) a.tcur[i] = 0ull;
+            for (; bits; bits &= bits - 1) tile((i << 6) + (uint64_t)__builtin_ctzll(bits));
+        }
+    } else {
+        for (uint64_t t = wave0; t < n_tiles; t += nwaves) tile(t);  // (the engine clears tcur)
     }
     flush(acc, a.st);
     if (COV) {
@@ -507,8 +526,8 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_lds(RoundArgs a, 
     // An idle source leaves its slots alone.  A slot may thus keep a word of
     // an earlier binned round of the same run: that round OR-ed it into
     // seen[dst] (deaths are permanent and dead peers never receive, so seen
-    // still holds it), and the apply masks with ~seen.  gossip_reset zeroes
-    // the slots (side stream) before the first binned round of a run.
+    // still holds it), and the apply masks with ~seen.  The first binned round
+    // after a reset (noskip) rewrites every slot, clearing the last run's words.
     __shared__ unsigned long long live_s[kBinChunkWords / 64];
     __shared__ unsigned int cov_s[COV ? 64 * W : 1];
     if (COV) {
@@ -649,7 +668,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_lds(RoundArgs a, 
 #pragma unroll
             for (int j = 0; j < kU; ++j) {
                 const uint32_t q = p + (uint32_t)j * kScatterBlock;
-                uint64_t* const dst = (a_ >> j) & 1u ? b.val + (uint64_t)(r_[j] + q) * W : sink;
+                uint64_t* const dst = ((a_ >> j) & 1u) && b.probe != 2 ? b.val + (uint64_t)(r_[j] + q) * W : sink;
 #pragma unroll
                 for (int w = 0; w < W; ++w) dst[w] = slice[(uint64_t)u_[j] * W + w];
             }
@@ -1332,6 +1351,7 @@ __global__ __launch_bounds__(kBlock) void k_inject(RoundArgs a, const uint32_t* 
             const unsigned long long bit = 1ull << (m & 63);
             atomicOr(reinterpret_cast<unsigned long long*>(a.seen) + idx, bit);
             atomicOr(reinterpret_cast<unsigned long long*>(a.nw) + idx, bit);
+            if (a.tcur) atomicOr(reinterpret_cast<unsigned long long*>(a.tcur) + ((o - a.begin) >> 12), 1ull << (((o - a.begin) >> 6) & 63));
             acc.injected++;
         }
     }
@@ -1549,7 +1569,20 @@ hipError_t launch_push_light(const RoundArgs& a, uint32_t W_, bool check_alive, 
     const uint32_t wd = wd_of(W_);
     const bool cov = a.cov != nullptr;
 #define GOSSIP_LIGHT(CA, RM, COV) \
-    hipLaunchKernelGGL((k_push_light<W, CA, RM, COV>), dim3(g), dim3(kBlock), 0, s, a, wd)
+    hipLaunchKernelGGL((k_push_light<W, CA, RM, COV, false>), dim3(g), dim3(kBlock), 0, s, a, wd)
+    if (a.tsparse && !remote) {  // a nearly empty frontier: only the marked tiles
+        const unsigned gs = grid_for((tiles + 63) / 64, kWavesPerBlock);
+        GOSSIP_DISPATCH_W(wp_of(W_), {
+            if (cov) {
+                if (check_alive) hipLaunchKernelGGL((k_push_light<W, true, false, true, true>), dim3(gs), dim3(kBlock), 0, s, a, wd);
+                else hipLaunchKernelGGL((k_push_light<W, false, false, true, true>), dim3(gs), dim3(kBlock), 0, s, a, wd);
+            } else {
+                if (check_alive) hipLaunchKernelGGL((k_push_light<W, true, false, false, true>), dim3(gs), dim3(kBlock), 0, s, a, wd);
+                else hipLaunchKernelGGL((k_push_light<W, false, false, false, true>), dim3(gs), dim3(kBlock), 0, s, a, wd);
+            }
+        });
+        return hipGetLastError();
+    }
     GOSSIP_DISPATCH_W(wp_of(W_), {
         if (cov) {
             if (check_alive) { if (remote) GOSSIP_LIGHT(true, true, true); else GOSSIP_LIGHT(true, false, true); }

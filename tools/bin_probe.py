@@ -1,6 +1,7 @@
-"""Times the first binned round of config 4 (per-kernel ms): once on a fresh
-layout (clean slots) and once after a full run (slots hold the last run's
-words).  Run once per GOSSIP_BIN_* setting."""
+"""Times every binned round of config 4 (per-kernel ms, cumulative counters
+differenced per round): once on a fresh layout and once after a full run.
+Run once per GOSSIP_* setting (GOSSIP_SCATTER_PROBE=1: staging only; 2: slot
+stores go to the sink)."""
 import os
 import sys
 from pathlib import Path
@@ -20,10 +21,15 @@ for label in ("clean", "after-run"):
         e.run()
     e.reset()
     e.enable_timing(True)
+    prev = {k: e.kernel_time(k) for k in ("bin_scatter", "bin_apply")}
+    parts = []
     while True:
         st, fin = e.step()
-        t = e.kernel_time("bin_scatter")
-        if t[1] or fin:
+        cur = {k: e.kernel_time(k) for k in prev}
+        if cur["bin_scatter"][1] != prev["bin_scatter"][1]:
+            parts.append(f"r{st['round']} scatter {cur['bin_scatter'][0] - prev['bin_scatter'][0]:.3f} "
+                         f"apply {cur['bin_apply'][0] - prev['bin_apply'][0]:.3f}")
+        prev = cur
+        if fin:
             break
-    print(f"[{tag}] {label} round {st['round']} scatter {t[0]:.3f} ms apply {e.kernel_time('bin_apply')[0]:.3f} ms",
-          flush=True)
+    print(f"[{tag}] {label}: " + "; ".join(parts), flush=True)

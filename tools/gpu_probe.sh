@@ -1,10 +1,10 @@
 #!/bin/bash
-# Scatter timing breakdown at config 4: staging only (1), + entry loads (2), + LDS reads (3), full (0); U=8.
+# Scatter timing breakdown per binned round at config 4: full (0), staging only (1), stores to the sink (2).
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/probe
-for p in 0 1 2 3; do
+: > gpurun_out/probe/probe.log
+for p in 0 1 2; do
   GOSSIP_SCATTER_PROBE=$p timeout -k 10 240 python -u tools/bin_probe.py 4 >> gpurun_out/probe/probe.log 2>&1 || { tail -5 gpurun_out/probe/probe.log; exit 1; }
 done
-GOSSIP_SCATTER_U=8 timeout -k 10 240 python -u tools/bin_probe.py 4 >> gpurun_out/probe/probe.log 2>&1 || { tail -5 gpurun_out/probe/probe.log; exit 1; }
 cat gpurun_out/probe/probe.log
