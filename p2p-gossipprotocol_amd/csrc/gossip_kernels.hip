@@ -670,13 +670,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_lds(RoundArgs a, 
                 const uint32_t q = p + (uint32_t)j * kScatterBlock;
                 uint64_t* const dst = ((a_ >> j) & 1u) && b.probe != 2 ? b.val + (uint64_t)(r_[j] + q) * W : sink;
 #pragma unroll
-                for (int w = 0; w < W; ++w) {
-#if GOSSIP_SCATTER_NT
-                    __builtin_nontemporal_store(slice[(uint64_t)u_[j] * W + w], dst + w);
-#else
-                    dst[w] = slice[(uint64_t)u_[j] * W + w];
-#endif
-                }
+                for (int w = 0; w < W; ++w) dst[w] = slice[(uint64_t)u_[j] * W + w];
             }
             acc.gathered += __popc(a_);  // slots written (byte accounting)
         };

@@ -4,7 +4,7 @@ set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/abn
 : > gpurun_out/abn/ab.log
-for i in 1 2; do
+for i in $(seq 1 ${PASSES:-2}); do
   for v in ${VARIANTS:-base}; do
     export GOSSIP_HIP_LIB=$PWD/abtest/$v/libgossip_hip.so
     timeout -k 10 300 python -u bench.py --no-cpu-baseline ${AB_ARGS} > gpurun_out/abn/$v$i.json 2> gpurun_out/abn/$v$i.err || { tail -20 gpurun_out/abn/$v$i.err; exit 1; }
