@@ -98,6 +98,32 @@ uint64_t oracle_digest_weight(uint64_t idx) {
 
 void oracle_free(void* p) { free(p); }
 
+/* Fixture checksums (tests/golden/make_fullsize_golden.py): sum_i g(i) * x[i]
+ * mod 2^64 with the digest weights, so order and position matter. */
+uint64_t oracle_hash_u64(const uint64_t* x, uint64_t n, int threads) {
+    uint64_t h = 0;
+    if (threads <= 0) threads = 1;
+#pragma omp parallel for reduction(+ : h) schedule(static, 1 << 16) num_threads(threads)
+    for (int64_t i = 0; i < (int64_t)n; ++i) h += oracle_digest_weight((uint64_t)i) * x[i];
+    return h;
+}
+
+uint64_t oracle_hash_u32(const uint32_t* x, uint64_t n, int threads) {
+    uint64_t h = 0;
+    if (threads <= 0) threads = 1;
+#pragma omp parallel for reduction(+ : h) schedule(static, 1 << 16) num_threads(threads)
+    for (int64_t i = 0; i < (int64_t)n; ++i) h += oracle_digest_weight((uint64_t)i) * x[i];
+    return h;
+}
+
+uint64_t oracle_hash_u8(const uint8_t* x, uint64_t n, int threads) {
+    uint64_t h = 0;
+    if (threads <= 0) threads = 1;
+#pragma omp parallel for reduction(+ : h) schedule(static, 1 << 16) num_threads(threads)
+    for (int64_t i = 0; i < (int64_t)n; ++i) h += oracle_digest_weight((uint64_t)i) * x[i];
+    return h;
+}
+
 /* ------------------------------------------------------------------------ */
 /* CSR assembly: sort rows, drop duplicates and self loops                  */
 /* ------------------------------------------------------------------------ */

@@ -82,6 +82,10 @@ void oracle_free(void* p);
 
 /* ---- digest weight g(i) ------------------------- */
 uint64_t oracle_digest_weight(uint64_t idx);
+/* fixture checksums: sum_i g(i) * x[i] mod 2^64 (OpenMP) */
+uint64_t oracle_hash_u64(const uint64_t* x, uint64_t n, int threads);
+uint64_t oracle_hash_u32(const uint32_t* x, uint64_t n, int threads);
+uint64_t oracle_hash_u8(const uint8_t* x, uint64_t n, int threads);
 
 /* ---- round driver ------------------------------------------------------ */
 typedef struct oracle_stats {

@@ -144,6 +144,7 @@ struct gossip_ctx {
     unsigned long long* d_counts = nullptr;  // records per destination rank
     uint64_t* h_counts = nullptr;            // pinned copy
     bool cur_sparse = false;
+    bool send_dirty = false;     // the dense staging buffer holds a dense push round's masks
     int pull_unroll = 2;         // 64-edge batches in flight per wave in pull_light (GOSSIP_PULL_UNROLL)
     uint32_t heavy = kHeavyDegree;  // light/heavy row threshold (GOSSIP_HEAVY_DEGREE)
     uint64_t frontier_est = 0;   // activated peers of the previous round
@@ -160,6 +161,7 @@ struct gossip_ctx {
     bool timing = false;
     std::map<std::string, TimerRec> timers;
     std::map<std::string, double> kbytes;
+    std::vector<hipEvent_t> event_pool;
 };
 
 namespace {
@@ -178,12 +180,23 @@ gossip_status set_dev(gossip_ctx* c) {
     return GOSSIP_OK;
 }
 
+// Events come from a per-ctx pool (creating two events per launch inside a
+// timed loop cost more than recording them).
+hipEvent_t take_event(gossip_ctx* c) {
+    hipEvent_t e = nullptr;
+    if (!c->event_pool.empty()) {
+        e = c->event_pool.back();
+        c->event_pool.pop_back();
+    } else {
+        hipEventCreate(&e);
+    }
+    return e;
+}
+
 template <class F>
 hipError_t timed(gossip_ctx* c, const char* name, F&& launch) {
     if (!c->timing) return launch();
-    hipEvent_t a, b;
-    hipEventCreate(&a);
-    hipEventCreate(&b);
+    hipEvent_t a = take_event(c), b = take_event(c);
     hipEventRecord(a, c->stream);
     hipError_t e = launch();
     hipEventRecord(b, c->stream);
@@ -199,8 +212,8 @@ void drain_timers(gossip_ctx* c) {
             hipEventElapsedTime(&ms, ev.first, ev.second);
             kv.second.ms += ms;
             kv.second.launches++;
-            hipEventDestroy(ev.first);
-            hipEventDestroy(ev.second);
+            c->event_pool.push_back(ev.first);
+            c->event_pool.push_back(ev.second);
         }
         kv.second.pending.clear();
     }
@@ -259,7 +272,14 @@ void free_graph(gossip_ctx* c) {
     hipFree(c->rp);
     hipFree(c->col);
     hipFree(c->chunks);
+    // closed-form liveness state belongs to the overlay: round_begin rebuilds
+    // all of it (rev included) for the next one
     hipFree(c->rev);
+    hipFree(c->death_r);
+    hipFree(c->dgone);
+    hipFree(c->dmask);
+    c->death_r = nullptr;
+    c->dgone = c->dmask = nullptr;
     c->rp = nullptr;
     c->col = nullptr;
     c->chunks = nullptr;
@@ -350,6 +370,7 @@ gossip_status install_graph(gossip_ctx* c, uint64_t* d_rp, uint32_t* d_col, uint
     if (c->cfg.ping_every) {
         hipFree(c->miss);
         HIPCHK(hipMalloc((void**)&c->miss, m + 1));
+        HIPCHK(hipMemsetAsync(c->miss, 0, m + 1, c->stream));
     }
     c->graph_ready = true;
     return GOSSIP_OK;
@@ -641,7 +662,12 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
             c->nx_dirty = false;
         }
         // dense exchange: clear the staging buffer; sparse: it is kept clear by the compaction pass
-        if (remote && !c->cur_sparse) HIPCHK(hipMemsetAsync(c->send, 0, c->n * c->Wp * sizeof(uint64_t), c->stream));
+        // (a sparse round after a dense one first clears what the dense round left)
+        if (remote && (!c->cur_sparse || c->send_dirty)) {
+            HIPCHK(hipMemsetAsync(c->send, 0, c->n * c->Wp * sizeof(uint64_t), c->stream));
+            c->send_dirty = false;
+        }
+        if (remote && !c->cur_sparse) c->send_dirty = true;
         if (c->cur_sparse) HIPCHK(hipMemsetAsync(c->d_counts, 0, c->world * sizeof(unsigned long long), c->stream));
     }
     c->cur = a;
@@ -886,8 +912,16 @@ gossip_status gossip_create(const gossip_config* cfg, gossip_ctx** out) {
         if ((err = hipMalloc((void**)&c->cov_hist, (uint64_t)c->cfg.max_rounds * 64 * c->Wp * 8)) != hipSuccess)
             return bail("coverage history", err);
     }
+    c->n_started = c->n;  // every peer starts until an overlay with a list_cap says otherwise
+    if (gossip_status rs = gossip_reset(c)) {
+        const std::string m = g_last_error;
+        free_state(c);
+        if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
+        delete c;
+        return fail(rs, m);
+    }
     *out = c;
-    return gossip_reset(c);
+    return GOSSIP_OK;
 }
 
 void gossip_destroy(gossip_ctx* c) {
@@ -895,6 +929,7 @@ void gossip_destroy(gossip_ctx* c) {
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
     drain_timers(c);
+    for (hipEvent_t e : c->event_pool) hipEventDestroy(e);
     free_state(c);
     free_graph(c);
     hipFree(c->d_inj_origin);
@@ -937,7 +972,7 @@ gossip_status gossip_build_graph(gossip_ctx* c) {
         gossip_status st = upload_csr(c, rp.data(), col.data(), col.size());
         c->symmetric = false;  // the literal bootstrap overlay is a DAG (F8)
         c->n_started = started_under_cap(c->n, c->cfg.list_cap);
-        return st;
+        return st ? st : gossip_reset(c);  // round 0 state of the new overlay
     }
     if (c->cfg.graph_model != GOSSIP_GRAPH_POWERLAW) return fail(GOSSIP_EINVAL, "unknown graph_model");
     if (c->cfg.list_len < 2 || c->cfg.list_len > 64) return fail(GOSSIP_EINVAL, "list_len must be 2..64");
@@ -951,7 +986,8 @@ gossip_status gossip_build_graph(gossip_ctx* c) {
         return fail(GOSSIP_EHIP, "overlay generator: " + err);
     gossip_status st = install_graph(c, rp, col, m);
     c->symmetric = true;  // powerlaw overlay is symmetrised by construction
-    return st ? st : prepare_bins(c);
+    if (!st) st = prepare_bins(c);
+    return st ? st : gossip_reset(c);  // round 0 state of the new overlay
 }
 
 gossip_status gossip_load_csr(gossip_ctx* c, const uint64_t* rp, const uint32_t* col, uint64_t n_rows,
@@ -978,7 +1014,8 @@ gossip_status gossip_load_csr(gossip_ctx* c, const uint64_t* rp, const uint32_t*
     if (set_dev(c)) return GOSSIP_EHIP;
     gossip_status st = upload_csr(c, rp, col, n_edges);
     c->symmetric = sym;
-    return st ? st : prepare_bins(c);
+    if (!st) st = prepare_bins(c);
+    return st ? st : gossip_reset(c);  // round 0 state of the new overlay
 }
 
 gossip_status gossip_read_csr(gossip_ctx* c, uint64_t* rp, uint32_t* col) {

@@ -226,10 +226,10 @@ class Engine:
         cnt = C.c_uint64()
         check(self._L.gossip_read_reports(self._ctx, None, 0, C.byref(cnt)), "gossip_read_reports")
         n = cnt.value
-        buf = (DeadReport * max(n, 1))()
-        check(self._L.gossip_read_reports(self._ctx, buf, n, C.byref(cnt)), "gossip_read_reports")
-        return np.array([(buf[i].round, buf[i].reporter, buf[i].dead) for i in range(n)],
-                        dtype=np.uint32).reshape(n, 3)
+        buf = np.zeros((max(n, 1), 3), dtype=np.uint32)  # DeadReport = 3 x u32
+        check(self._L.gossip_read_reports(self._ctx, buf.ctypes.data_as(C.POINTER(DeadReport)), n, C.byref(cnt)),
+              "gossip_read_reports")
+        return buf[:n]
 
     def alive(self) -> np.ndarray:
         out = np.zeros(self.n_peers, dtype=np.uint8)

@@ -46,6 +46,9 @@ class Oracle:
         L.oracle_skew_pick.argtypes = [C.c_uint32, C.c_uint64]
         L.oracle_digest_weight.restype = C.c_uint64
         L.oracle_digest_weight.argtypes = [C.c_uint64]
+        for name, t in (("oracle_hash_u64", C.c_uint64), ("oracle_hash_u32", C.c_uint32), ("oracle_hash_u8", C.c_uint8)):
+            getattr(L, name).restype = C.c_uint64
+            getattr(L, name).argtypes = [C.POINTER(t), C.c_uint64, C.c_int]
         L.oracle_sim_create.restype = C.c_void_p
         L.oracle_sim_reports.restype = C.c_uint64
         L.oracle_sim_sent_to_total.restype = C.c_uint64
@@ -57,6 +60,13 @@ class Oracle:
         out = (C.c_uint32 * 4)()
         self.L.oracle_philox4x32_10((C.c_uint32 * 4)(*ctr), (C.c_uint32 * 2)(*key), out)
         return [int(x) for x in out]
+
+    def hash(self, a, threads=8) -> int:
+        """Fixture checksum: sum_i g(i) * a[i] mod 2^64 (g = the digest weights)."""
+        a = np.ascontiguousarray(a).reshape(-1)
+        fn, t = {8: (self.L.oracle_hash_u64, C.c_uint64), 4: (self.L.oracle_hash_u32, C.c_uint32),
+                 1: (self.L.oracle_hash_u8, C.c_uint8)}[a.dtype.itemsize]
+        return int(fn(_p(a, t), C.c_uint64(a.size), C.c_int(threads)))
 
     def threshold(self, j, L):
         return int(self.L.oracle_threshold(C.c_uint32(j), C.c_uint32(L)))
@@ -112,11 +122,10 @@ class Oracle:
             self.L.oracle_sim_seen(s, _p(seen, C.c_uint64))
             cov = np.zeros(n_msgs, dtype=np.uint64)
             self.L.oracle_sim_coverage(s, _p(cov, C.c_uint64))
-            nrep = self.L.oracle_sim_reports(s, None, C.c_uint64(0))
-            rb = (OReport * max(int(nrep), 1))()
-            self.L.oracle_sim_reports(s, rb, C.c_uint64(nrep))
-            reps = np.array([(rb[i].round, rb[i].reporter, rb[i].dead) for i in range(int(nrep))],
-                            dtype=np.uint32).reshape(int(nrep), 3)
+            nrep = int(self.L.oracle_sim_reports(s, None, C.c_uint64(0)))
+            reps = np.zeros((max(nrep, 1), 3), dtype=np.uint32)
+            self.L.oracle_sim_reports(s, reps.ctypes.data_as(C.POINTER(OReport)), C.c_uint64(nrep))
+            reps = reps[:nrep]
             alive = np.zeros(n, dtype=np.uint8)
             self.L.oracle_sim_alive(s, _p(alive, C.c_uint8))
             reg = np.zeros(n, dtype=np.uint8)

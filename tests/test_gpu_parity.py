@@ -271,3 +271,35 @@ def test_closed_form_liveness_kills_and_hubs(oracle, max_missed, ping):
         finally:
             del os.environ["GOSSIP_FULL_LIVENESS"]
     assert runs[0] == runs[1]
+
+
+def test_steps_right_after_build_graph(oracle):
+    """create -> build_graph -> inject -> run with no explicit reset: the
+    overlay install leaves the round-0 state (every peer alive, miss counters
+    zero), so the run equals the oracle's."""
+    w = config(5, 1 << 14, pick=oracle.pick_origins)
+    rp, col = oracle.gen_workload(w)
+    ref = oracle.simulate_workload(w, rp, col)
+    with _engine(w) as e:
+        e.build_graph()
+        e.inject(w.origins, w.inject_rounds)
+        _compare(e, ref, w)
+
+
+@pytest.mark.parametrize("mode", ["auto", "push"])
+def test_reload_overlay_with_kills(oracle, mode):
+    """One ctx, the overlay loaded twice (a second load_csr after a run with
+    deaths): the closed-form liveness state is rebuilt for the new overlay,
+    so the ping rounds still mask and report exactly as the oracle does."""
+    base = config(2, 1 << 13, pick=oracle.pick_origins)
+    w = dataclasses.replace(base, kills=[(0, 1), (9, 2), (77, 3)], ping_every=2, max_missed=2, min_rounds=16,
+                            churn_threshold=int(0.01 * 2**32))
+    rp, col = oracle.gen_workload(w)
+    ref = oracle.simulate_workload(w, rp, col)
+    assert sum(s["reports"] for s in ref["stats"]) > 0
+    with _engine(w, mode=mode) as e:
+        for _ in range(2):
+            e.load_csr(rp, col)
+            e.inject(w.origins, w.inject_rounds)
+            e.schedule_kills([k[0] for k in w.kills], [k[1] for k in w.kills])
+            _compare(e, ref, w)
