@@ -10,7 +10,8 @@ Default workload (N=1): BASELINE.json configs[3] -- 2^28 peers, power-law
 overlay, 64 concurrent messages from Philox-chosen origins, run to full
 coverage -- the largest configuration, and the one the metric's 1/2/4/8-GPU
 series is quoted on.  With --gpus N the same 2^28-peer overlay is
-vertex-partitioned over N ranks (strong scaling, RCCL all-to-all per round).
+vertex-partitioned over N ranks (strong scaling); libgossip_hip issues each
+round's RCCL collectives itself (gossip_comm_init).
 
 One JSON line on rank 0; see DESIGN.md section 7 for every field.
 """
@@ -36,7 +37,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", type=int, default=4, help="BASELINE.json config index (1-5)")
     ap.add_argument("--n", type=int, default=0, help="override peer count")
-    ap.add_argument("--cpu-sample-n", type=int, default=1 << 25)
+    ap.add_argument("--cpu-sample-n", type=int, default=1 << 25, help="CPU baseline sample size (all threads)")
+    ap.add_argument("--cpu-sample-n1", type=int, default=1 << 21, help="CPU baseline sample size (1 thread)")
+    ap.add_argument("--cpu-repeats", type=int, default=5)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP event timing")
@@ -46,7 +49,7 @@ def parse():
     ap.add_argument("--rebootstrap", type=int, default=0,
                     help="re-bootstrap after a death with this many extra out-edges per peer (configs 1, 5)")
     ap.add_argument("--force-partitioned", action="store_true",
-                    help="use the multi-rank driver (RCCL collectives) even at WORLD_SIZE 1")
+                    help="use the library's multi-GPU driver (RCCL collectives) even at WORLD_SIZE 1")
     return ap.parse_args()
 
 
@@ -96,26 +99,73 @@ def rounds_to_full(stats: list[dict]) -> int:
     return last - min(s["round"] for s in stats if s["injected"] > 0) if any(s["injected"] for s in stats) else 0
 
 
+def _cpu_model() -> str:
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(args, cfg_idx: int) -> dict:
-    """The oracle's 64-bit-mask round driver (g++ -O3 -fopenmp) on a bounded
-    sample of the same workload, timed on this host's cores (rounds only)."""
+    """The oracle's 64-bit-mask round driver (gcc -O3 -fopenmp; the restatement
+    of peer.cpp:255-318 that the GPU is checked against) on bounded samples of
+    the same workload, timed on this host: oracle_sim_run only (the rounds;
+    overlay generation, sim allocation and read-backs untimed), median of
+    --cpu-repeats fresh runs, at the host's thread budget and at 1 thread."""
+    import statistics
     sys.path.insert(0, str(REPO / "tests"))
     import oracle_ref  # noqa: E402  (checker / baseline only)
     from gossip_hip.workloads import config
 
     so = REPO / "oracle" / "_build" / "libgossip_oracle.so"
     orc = oracle_ref.Oracle(so)
-    threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", 0) or min(16, os.cpu_count() or 1))
-    n = args.cpu_sample_n
-    w = config(cfg_idx if cfg_idx != 1 else 3, n, pick=orc.pick_origins)
-    rp, col = orc.gen_workload(w, threads=threads)
-    t0 = time.perf_counter()
-    out = orc.simulate_workload(w, rp, col, variant=0, threads=threads)
-    dt = time.perf_counter() - t0
-    d = sum(s["deliveries"] for s in out["stats"])
-    return {"value": round(d / dt / 1e9, 4), "unit": "GTEPS", "cores": threads, "kind": "port",
-            "sample": f"{w.name} workload at n=2^{n.bit_length() - 1} ({n} peers, {len(col)} edges, "
-                      f"{len(out['stats'])} rounds), oracle fast driver, {dt:.2f} s incl. state setup"}
+    nproc = os.cpu_count() or 1
+    threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", 0) or nproc)
+    idx = cfg_idx if cfg_idx != 1 else 3
+    out = {}
+    for label, n, th in (("all", args.cpu_sample_n, threads), ("one", args.cpu_sample_n1, 1)):
+        w = config(idx, n, pick=orc.pick_origins)
+        rp, col = orc.gen_workload(w, threads=threads)
+        secs, stats = orc.time_rounds(w, rp, col, threads=th, repeats=args.cpu_repeats)
+        med = statistics.median(secs)
+        d = sum(s["deliveries"] for s in stats)
+        t = sum(s["traversals"] for s in stats)
+        out[label] = {"gteps": d / med / 1e9, "traversal_gteps": t / med / 1e9, "n": n, "edges": int(len(col)),
+                      "rounds": len(stats), "median_s": med, "runs_s": [round(x, 3) for x in secs], "threads": th}
+    a, o = out["all"], out["one"]
+    return {"value": round(a["gteps"], 4), "unit": "GTEPS", "cores": threads, "kind": "port",
+            "traversal_gteps": round(a["traversal_gteps"], 4),
+            "single_thread": {"value": round(o["gteps"], 4), "traversal_gteps": round(o["traversal_gteps"], 4),
+                              "median_s": round(o["median_s"], 3), "runs_s": o["runs_s"],
+                              "sample": f"n=2^{o['n'].bit_length() - 1}, {o['edges']} edges, {o['rounds']} rounds"},
+            "nproc": nproc, "cpu_model": _cpu_model(), "median_s": round(a["median_s"], 3), "runs_s": a["runs_s"],
+            "timed": "oracle_sim_run only (rounds); generation, allocation and read-backs excluded",
+            "sample": f"{config(idx, 1024).name} workload at n=2^{a['n'].bit_length() - 1} ({a['n']} peers, "
+                      f"{a['edges']} edges, {a['rounds']} rounds), oracle fast driver, {threads} threads of {nproc} "
+                      f"visible CPUs, median of {args.cpu_repeats}"}
+
+
+def per_round_profile(eng) -> list[dict]:
+    """One run, stepped round by round with per-kernel timing (untimed pass)."""
+    from gossip_hip.engine import KERNELS
+    eng.reset()
+    eng.enable_timing(True)
+    prev = {k: eng.kernel_time(k)[0] for k in KERNELS}
+    rows = []
+    while True:
+        st, fin = eng.step()
+        cur = {k: eng.kernel_time(k)[0] for k in KERNELS}
+        d = {k: cur[k] - prev[k] for k in KERNELS if cur[k] - prev[k] > 0}
+        prev = cur
+        mode = "bin" if "bin_scatter" in d else "pull" if "pull_light" in d else "push"
+        rows.append({"round": st["round"], "mode": mode, "frontier_frac": round(st["frontier"] / eng.n_peers, 4),
+                     "traversals": st["traversals"], "alg_bytes": 32 * st["frontier"] + 20 * st["traversals"],
+                     "kernel_ms": round(sum(d.values()), 3)})
+        if fin:
+            return rows
 
 
 def main():
@@ -137,29 +187,33 @@ def main():
     tune = dict(pull_permille=args.pull_permille, front_permille=args.front_permille, mode=args.mode)
     partitioned = world > 1 or args.force_partitioned
     if partitioned:
+        # one process per GPU; libgossip_hip drives every round's RCCL collectives
+        # itself (gossip_comm_init); torch.distributed (gloo, host side) only hands
+        # out the RCCL unique id and keeps the barrier and max-over-ranks timing
         import torch.distributed as dist
 
-        from gossip_hip.distributed import PartitionedRun, partition
+        from gossip_hip import comm_unique_id, partition
 
         for k, v in (("RANK", "0"), ("WORLD_SIZE", "1"), ("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29511")):
             os.environ.setdefault(k, v)  # --force-partitioned run without a launcher
-        dist.init_process_group("nccl", device_id=dev)
+        dist.init_process_group("gloo")
         part = partition(w.n, world)
         eng = Engine(w.n, w.n_msgs, device=local, part=(part[rank], part[rank + 1]), **tune, **w.engine_kwargs())
         eng.build_graph()
         eng.inject(w.origins, w.inject_rounds)
         if w.kills:
             eng.schedule_kills([k[0] for k in w.kills], [k[1] for k in w.kills])
-        runner = PartitionedRun(eng, w.n, rank, world, dev)
+        uid = [comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        eng.comm_init(uid[0], world, rank)
 
         def one_step():
             eng.reset()
-            return runner.run()
+            return eng.run()
 
         def barrier():
             torch.cuda.synchronize()
             dist.barrier()
-            torch.cuda.synchronize()
     else:
         eng = Engine(w.n, w.n_msgs, device=local, **tune, **w.engine_kwargs())
         eng.build_graph()
@@ -177,7 +231,7 @@ def main():
     shape = eng.shape()
     n_edges = shape["n_edges"]
     if partitioned:
-        t = torch.tensor([n_edges], dtype=torch.int64, device=dev)
+        t = torch.tensor([n_edges], dtype=torch.int64)
         dist.all_reduce(t)
         n_edges = int(t.item())
     for _ in range(args.warmup):
@@ -192,8 +246,7 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     if partitioned:
-        import torch.distributed as dist
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
@@ -220,6 +273,25 @@ def main():
                         "kernel_frac": {k: round(k_b[k] / (v[0] / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
                                         for k, v in k_ms.items() if v[0] > 0 and k_b[k] > 0}}
 
+    # per-round pass (untimed, P = 1): one step round by round with per-kernel
+    # deltas -- which rounds ran binned / pull / push, and SURVEY 8(d)'s
+    # algorithmic bytes B_r = 32 F_r + 20 T_r against the kernels' device time
+    rounds_prof = None
+    if not partitioned and not args.no_timing:
+        rounds_prof = per_round_profile(eng)
+        traversals = sum(s["traversals"] for s in stats)
+        alg = sum(r["alg_bytes"] for r in rounds_prof)
+        dense = [r for r in rounds_prof if r["mode"] == "bin"]
+        if roofline is not None:
+            roofline["step_frac"] = round(alg / (dt / args.steps) / 1e9 / HBM_PEAK_GBS, 4)
+            if dense:
+                d_b = sum(r["alg_bytes"] for r in dense)
+                d_ms = sum(r["kernel_ms"] for r in dense)
+                roofline["dense_round"] = {"rounds": [r["round"] for r in dense], "alg_bytes": d_b,
+                                           "kernel_ms": round(d_ms, 3),
+                                           "frac": round(d_b / (d_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                                           "kernels": "bin_scatter + bin_apply + pull_heavy"}
+
     if rank == 0:
         line = {
             "metric": "gossip edge-deliveries/sec (GTEPS) + rounds-to-full-coverage",
@@ -237,18 +309,24 @@ def main():
             "config": {"workload": w.name, "peers": w.n, "edges": n_edges,
                        "messages": w.n_msgs, "rounds": len(stats),
                        "rounds_to_full_coverage": rounds_to_full(stats),
-                       "deliveries_per_step": deliveries, "parallelism": f"vertex-partition x{world}"},
+                       "deliveries_per_step": deliveries,
+                       "traversals_per_step": sum(s["traversals"] for s in stats),
+                       "parallelism": f"vertex-partition x{world}"},
+            "traversal_gteps": round(args.steps * sum(s["traversals"] for s in stats) / dt / 1e9, 3),
         }
+        if rounds_prof:
+            line["rounds"] = [{k: r[k] for k in ("round", "mode", "frontier_frac", "traversals", "kernel_ms")}
+                              for r in rounds_prof]
         if roofline:
             line["roofline"] = roofline
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args, args.config)
         print(json.dumps(line), flush=True)
     if partitioned:
-        import torch.distributed as dist
-        reps = runner.finalize(stats)
+        reps = eng.comm_finalize(stats)
         if rank == 0 and args.force_partitioned:
-            print(json.dumps({"partitioned_check": {"modes": runner.modes, "reports": int(len(reps))}}), flush=True)
+            print(json.dumps({"partitioned_check": {"modes": eng.comm_modes(), "reports": int(len(reps))}}), flush=True)
+        eng.close()
         dist.destroy_process_group()
 
 

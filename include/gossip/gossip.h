@@ -207,6 +207,61 @@ gossip_status gossip_round_push(gossip_ctx* ctx);
 gossip_status gossip_round_finish(gossip_ctx* ctx, gossip_round_stats* local_out);
 gossip_status gossip_round_commit(gossip_ctx* ctx, uint64_t global_new_receipts, int* finished);
 
+/* ---- multi-GPU rounds driven by the library (RCCL over xGMI) --------------
+ * Replaces the reference's cross-process send of a gossip message
+ * (broadcastMessage peer.cpp:310-316 over TCP to another PeerNode process):
+ * peers are 1D vertex-partitioned into the blocks of gossip_partition
+ * (ceil(n/world) peers each) and every round exchanges the cross-block
+ * frontier words with RCCL -- an all-gather of the new words in dense
+ * (pull / binned) rounds, an all-to-all of staged masks (or of compacted
+ * {peer, words} records) in push rounds, and one all-reduce of the stats.
+ * The schedule is chosen from the previous round's GLOBAL stats, so every
+ * rank runs the same one; results equal the single-partition run. */
+#define GOSSIP_ECOMM (-7)           /* RCCL error */
+#define GOSSIP_COMM_ID_BYTES 128    /* ncclUniqueId */
+/* begins[world+1]: rank p owns peers [begins[p], begins[p+1]) */
+gossip_status gossip_partition(uint64_t n_peers, uint32_t world, uint64_t* begins);
+/* One process per GPU: rank 0 creates the id, every rank receives it out of band. */
+gossip_status gossip_comm_unique_id(uint8_t* id /* GOSSIP_COMM_ID_BYTES */);
+/* Makes ctx (created with the rank's block of gossip_partition as its part range)
+ * rank `rank` of `world`: allocates the exchange buffers, joins the RCCL
+ * communicator (collective: every rank calls it), after which gossip_step /
+ * gossip_run issue the collectives themselves (call them in lockstep on every
+ * rank).  Their stats are global; seed_removals are filled in by
+ * gossip_comm_finalize.  Reads (gossip_read_*) stay per block. */
+gossip_status gossip_comm_init(gossip_ctx* ctx, const uint8_t* id, uint32_t world, uint32_t rank);
+/* Collective, after a run: gathers every rank's dead-node reports (sorted by
+ * (round, reporter, dead); reports may be NULL) and sets per_round[i].seed_removals
+ * (the registry drops a peer on its first report, SeedNode::handleDeadNode seed.cpp:158-167). */
+gossip_status gossip_comm_finalize(gossip_ctx* ctx, gossip_round_stats* per_round, uint32_t rounds,
+                                   gossip_dead_report* reports, uint64_t cap, uint64_t* count);
+/* Exchange mode of every round run since the last reset (GOSSIP_MODE_*). */
+gossip_status gossip_comm_modes(gossip_ctx* ctx, int32_t* modes, uint32_t cap, uint32_t* n);
+
+/* One process, several GPUs (one ctx per part; RCCL communicators from
+ * ncclCommInitAll).  devices[p] is part p's device; when every part names the
+ * same device the parts exchange by device copies instead (a single-GPU
+ * rehearsal of the partitioned path).  The group's calls drive all parts. */
+typedef struct gossip_group gossip_group;
+gossip_status gossip_group_create(const gossip_config* cfg, uint32_t n_parts, const int32_t* devices,
+                                  gossip_group** out);
+void gossip_group_destroy(gossip_group* g);
+gossip_status gossip_group_part(gossip_group* g, uint32_t p, gossip_ctx** ctx);
+gossip_status gossip_group_build_graph(gossip_group* g);
+gossip_status gossip_group_inject(gossip_group* g, const uint32_t* origin, const uint32_t* inject_round,
+                                  uint32_t n_msgs);
+gossip_status gossip_group_schedule_kills(gossip_group* g, const uint32_t* kill_peer, const uint32_t* kill_round,
+                                          uint32_t n_kills);
+gossip_status gossip_group_reset(gossip_group* g);
+/* one round on every part; 1 when finished, 0 if not, < 0 on error (seed_removals: 0 until the run ends) */
+gossip_status gossip_group_step(gossip_group* g, gossip_round_stats* out);
+/* steps until finished; per_round gets global stats with seed_removals */
+gossip_status gossip_group_run(gossip_group* g, gossip_round_stats* per_round, uint32_t cap, uint32_t* rounds);
+/* seen words of all n_peers peers (n_peers * W) */
+gossip_status gossip_group_read_seen(gossip_group* g, uint64_t* host_seen);
+/* every part's reports, merged and sorted by (round, reporter, dead) */
+gossip_status gossip_group_read_reports(gossip_group* g, gossip_dead_report* buf, uint64_t cap, uint64_t* count);
+
 /* ---- results ------------------------------------------------------------- */
 /* Owned seen words (n_local * W): bit m of peer v = v's Message-List holds m (peer.hpp:52). */
 gossip_status gossip_read_seen(gossip_ctx* ctx, uint64_t* host_seen);

@@ -9,6 +9,7 @@
 // have logged is appended to seed_<port>_output.txt when logging is enabled.
 #pragma once
 
+#include <atomic>
 #include <chrono>
 #include <mutex>
 #include <string>
@@ -46,10 +47,10 @@ public:
 private:
     std::string ip_;
     int port_;
-    bool running_ = false;
+    std::atomic<bool> running_{false};  // stop() may come from another thread (main.cpp:14-22)
     std::unordered_map<PeerInfo, std::chrono::system_clock::time_point, PeerInfoHash> peers_;
     std::vector<PeerInfo> order_;  // registration order (a deterministic peer_list)
     std::mutex mu_;
     std::string logPath_;
-    long long clock_ = 0;
+    std::atomic<long long> clock_{0};  // simulation clock of the log stamps (set while peers register)
 };

@@ -666,7 +666,7 @@ static void do_liveness(oracle_sim* s, uint32_t r, oracle_stats* st) {
     }
     if (!s->K) return;
     /* this round's reports in (reporter, dead) order */
-    qsort(s->rep + first, s->n_rep - first, sizeof(oracle_report), cmp_rep);
+    if (s->n_rep > first) qsort(s->rep + first, s->n_rep - first, sizeof(oracle_report), cmp_rep);
     for (uint64_t i = first; i < s->n_rep; ++i) rebootstrap(s, r, s->rep[i].reporter, s->rep[i].dead, st);
 }
 
@@ -871,7 +871,7 @@ void oracle_sim_coverage(const oracle_sim* s, uint64_t* out) {
 
 
 uint64_t oracle_sim_reports(const oracle_sim* s, oracle_report* buf, uint64_t cap) {
-    qsort(s->rep, s->n_rep, sizeof(oracle_report), cmp_rep);
+    if (s->n_rep) qsort(s->rep, s->n_rep, sizeof(oracle_report), cmp_rep);
     uint64_t k = s->n_rep < cap ? s->n_rep : cap;
     if (buf && k) memcpy(buf, s->rep, k * sizeof(oracle_report));
     return s->n_rep;
@@ -1190,7 +1190,7 @@ void oracle_part_reset(oracle_part* p) {
 void oracle_part_seen(const oracle_part* p, uint64_t* out) { memcpy(out, p->seen, p->nl * p->W * 8); }
 
 uint64_t oracle_part_reports(const oracle_part* p, oracle_report* buf, uint64_t cap) {
-    qsort(p->rep, p->n_rep, sizeof(oracle_report), cmp_rep);
+    if (p->n_rep) qsort(p->rep, p->n_rep, sizeof(oracle_report), cmp_rep);
     uint64_t k = p->n_rep < cap ? p->n_rep : cap;
     if (buf && k) memcpy(buf, p->rep, k * sizeof(oracle_report));
     return p->n_rep;

@@ -197,6 +197,7 @@ void free_bins(BinState* b) {
     hipFree(b->bdst);
     hipFree(b->val);
     hipFree(b->dummy);
+    hipFree(b->sync);
     *b = BinState{};
 }
 
@@ -387,30 +388,62 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
         cb_slot = nullptr;
     }
 
-    // scatter work units: chunks split into <= kBinUnitCap entries (every chunk
-    // has at least one: its first unit books the chunk's source-side stats);
-    // the unit list is cut into 8 contiguous ranges of equal entry counts (one per XCD)
+    // scatter work units (every chunk has at least one: its first unit books
+    // the chunk's source-side stats).  The chunk sequence is cut into 8
+    // contiguous ranges of equal entry counts, one per XCD.  Row mode (the
+    // default): inside an XCD's range a unit is a whole chunk, except hub
+    // chunks (more than kHubFactor times the mean), which are cut into units
+    // of about the mean; the list is padded to rows of kScatterGrid / 8 units,
+    // member j of the XCD takes unit j of every row, so the workgroups of a
+    // row stage consecutive chunks and write adjacent slot runs in every bin
+    // at about the same time (merged into whole lines in the XCD's L2; the
+    // kernel's row barrier keeps them together).  GOSSIP_BIN_UNIT = cap
+    // restores capped units dealt round-robin with no padding (the round-1
+    // layout, A/B only).
     {
         std::vector<uint64_t> cbeg(n_chunks + 1);
         BCHECK(hipMemcpy(cbeg.data(), st.chunk_begin, (n_chunks + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost));
         std::vector<BinUnit> units;
-        uint64_t cap = kBinUnitCap;
-        if (const char* e = std::getenv("GOSSIP_BIN_UNIT")) cap = std::max<uint64_t>(1024, std::strtoull(e, nullptr, 0));
-        for (uint64_t c = 0; c < n_chunks; ++c) {
-            const uint64_t len = cbeg[c + 1] - cbeg[c];
-            const uint64_t k = std::max<uint64_t>(1, (len + cap - 1) / cap);
-            for (uint64_t j = 0; j < k; ++j)
-                units.push_back(BinUnit{(uint32_t)c, j == 0 ? 1u : 0u, cbeg[c] + len * j / k, cbeg[c] + len * (j + 1) / k});
-        }
-        std::vector<uint64_t> xu(9, units.size());
-        xu[0] = 0;
-        uint64_t acc = 0;
-        int x = 1;
-        for (uint64_t i = 0; i < units.size() && x < 8; ++i) {
-            acc += units[i].p1 - units[i].p0;
-            while (x < 8 && acc * 8 >= upos * (uint64_t)x) xu[x++] = i + 1;
+        std::vector<uint64_t> xu(9, 0);
+        const uint64_t members = kScatterGrid / 8;
+        if (const char* e = std::getenv("GOSSIP_BIN_UNIT")) {
+            const uint64_t cap = std::max<uint64_t>(1024, std::strtoull(e, nullptr, 0));
+            for (uint64_t c = 0; c < n_chunks; ++c) {
+                const uint64_t len = cbeg[c + 1] - cbeg[c];
+                const uint64_t k = std::max<uint64_t>(1, (len + cap - 1) / cap);
+                for (uint64_t j = 0; j < k; ++j)
+                    units.push_back(
+                        BinUnit{(uint32_t)c, j == 0 ? 1u : 0u, cbeg[c] + len * j / k, cbeg[c] + len * (j + 1) / k});
+            }
+            xu.assign(9, units.size());
+            xu[0] = 0;
+            uint64_t acc = 0;
+            int x = 1;
+            for (uint64_t i = 0; i < units.size() && x < 8; ++i) {
+                acc += units[i].p1 - units[i].p0;
+                while (x < 8 && acc * 8 >= upos * (uint64_t)x) xu[x++] = i + 1;
+            }
+        } else {
+            const uint64_t mean = std::max<uint64_t>(1024, upos / std::max<uint64_t>(1, n_chunks));
+            uint64_t c = 0, acc = 0;
+            for (int x = 0; x < 8; ++x) {
+                xu[x] = units.size();
+                const uint64_t want = upos * (uint64_t)(x + 1) / 8;
+                for (; c < n_chunks && (x == 7 || acc < want); ++c) {
+                    const uint64_t len = cbeg[c + 1] - cbeg[c];
+                    acc += len;
+                    const uint64_t k = len > kHubFactor * mean ? (len + mean - 1) / mean : 1;
+                    for (uint64_t j = 0; j < k; ++j)
+                        units.push_back(
+                            BinUnit{(uint32_t)c, j == 0 ? 1u : 0u, cbeg[c] + len * j / k, cbeg[c] + len * (j + 1) / k});
+                }
+                while ((units.size() - xu[x]) % members) units.push_back(BinUnit{0u, 0u, 0, 0});  // empty: skipped
+            }
+            xu[8] = units.size();
         }
         st.n_units = units.size();
+        BCHECK(hipMalloc((void**)&st.sync, 8 * kScatterSyncStride * sizeof(uint32_t)));
+        BCHECK(hipMemset(st.sync, 0, 8 * kScatterSyncStride * sizeof(uint32_t)));
         BCHECK(hipMalloc((void**)&st.units, units.size() * sizeof(BinUnit)));
         BCHECK(hipMemcpy(st.units, units.data(), units.size() * sizeof(BinUnit), hipMemcpyHostToDevice));
         BCHECK(hipMalloc((void**)&st.xcd_units, 9 * sizeof(uint64_t)));

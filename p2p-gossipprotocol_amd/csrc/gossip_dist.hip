@@ -1,0 +1,738 @@
+// gossip_dist.hip -- multi-GPU rounds driven by libgossip_hip itself (RCCL over xGMI).
+//
+// The reference sends every gossip message to another PeerNode process over
+// TCP (broadcastMessage peer.cpp:310-316 -> handleClient peer.cpp:255-295).
+// Here peers are 1D vertex-partitioned into blocks of ceil(n/P) (SURVEY.md
+// 8(e)) and one round's cross-block traffic is ONE exchange, issued by this
+// driver on the block's HIP stream:
+//   dense rounds (PULL / BIN): in-place ncclAllGather of every block's new
+//     words into a buffer indexed by global peer; each block then pulls or
+//     streams its in-edges from it (no second exchange, no atomics);
+//   push rounds: the block's pushes to remote peers are OR-ed into a dense
+//     staging buffer indexed by global peer, and an all-to-all of ncclSend /
+//     ncclRecv pairs (all ranks' sends and receives in one group, every link
+//     of the xGMI mesh at once) hands rank q its slice; narrow rounds
+//     (PUSH_SPARSE) first compact the staging buffer into {peer, words}
+//     records and exchange only those (counts first, then the records);
+//   then one ncclAllReduce (uint64 sum, so the digest wraps mod 2^64 exactly
+//   as on one GPU) of the round's stats drives the common termination.
+// The mode is chosen from the previous round's GLOBAL stats, so every rank
+// picks the same one.  Results equal the single-partition run bit for bit
+// (set semantics; tests/test_gpu_group.py).
+//
+// Two deployments share this code:
+//   gossip_comm_init: one process per GPU (the bench's torchrun launch), one
+//     local rank per driver, communicator from ncclCommInitRank;
+//   gossip_group_*:   one process driving several GPUs,
+//     communicators from ncclCommInitAll, every collective of the local ranks
+//     inside one ncclGroupStart/End; when all parts sit on ONE device the
+//     exchange is done by device copies on one shared stream (a single-GPU
+//     rehearsal of the partitioned path: the remote staging, record
+//     compaction and remote-apply kernels and this driver's schedule).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/gossip/gossip.h"
+#include "gossip_internal.hpp"
+
+namespace gossip {
+
+namespace {
+
+constexpr int kStatSlots = 12;  // all-reduced stat fields (see pack_stats)
+
+struct DistRank {
+    gossip_ctx* ctx = nullptr;
+    uint32_t rank = 0;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    ncclComm_t comm = nullptr;
+    uint64_t begin = 0, n_local = 0;
+    uint64_t *send = nullptr, *recv = nullptr, *gather = nullptr, *seg = nullptr, *rec_in = nullptr;
+    uint64_t* d_io = nullptr;  // device scratch: stats all-reduce, record counts
+    uint64_t* h_io = nullptr;  // pinned mirror
+    std::vector<uint64_t> counts_out, counts_in;
+    gossip_round_stats local{};
+};
+
+}  // namespace
+
+struct DistDriver {
+    std::vector<DistRank> ranks;  // the ranks this process drives
+    uint32_t world = 1;
+    bool emulate = false;         // every rank local on one device: device copies, one stream
+    std::vector<uint64_t> part;
+    uint64_t n = 0, chunk = 0;
+    uint32_t X = 1, R = 2;
+    uint32_t pull_pm = 50, sparse_pm = 250, bin_pm = 4000, bin_front_pm = 100;
+    // schedule state, from global stats (identical on every rank)
+    uint64_t prev_new = 0, injected = 0, cum_digest = 0, cum_covered = 0;
+    bool finished = false;
+    std::vector<int32_t> modes;
+};
+
+namespace {
+
+#define DHIP(call)                                                                                  \
+    do {                                                                                            \
+        hipError_t e_ = (call);                                                                     \
+        if (e_ != hipSuccess) return set_error(GOSSIP_EHIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+#define DNCCL(call)                                                                                 \
+    do {                                                                                            \
+        ncclResult_t r_ = (call);                                                                   \
+        if (r_ != ncclSuccess) return set_error(GOSSIP_ECOMM, std::string(#call) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+std::vector<uint64_t> blocks(uint64_t n, uint32_t world) {
+    const uint64_t chunk = (n + world - 1) / world;
+    std::vector<uint64_t> b(world + 1);
+    for (uint32_t p = 0; p <= world; ++p) b[p] = std::min<uint64_t>((uint64_t)p * chunk, n);
+    return b;
+}
+
+// Buffers and communicator of one rank (its stream is released by dist_free).
+void free_rank(DistRank& r) {
+    hipSetDevice(r.device);
+    if (r.stream) hipStreamSynchronize(r.stream);
+    if (r.comm) ncclCommDestroy(r.comm);
+    hipFree(r.send);
+    hipFree(r.recv);
+    hipFree(r.gather);
+    hipFree(r.seg);
+    hipFree(r.rec_in);
+    hipFree(r.d_io);
+    if (r.h_io) hipHostFree(r.h_io);
+    r.send = r.recv = r.gather = r.seg = r.rec_in = r.d_io = r.h_io = nullptr;
+    r.comm = nullptr;
+}
+
+// Exchange buffers of one rank (device memory of its GPU) and their
+// registration with its ctx; the ctx then issues its work on r.stream.
+gossip_status setup_rank(DistDriver* d, DistRank& r) {
+    DHIP(hipSetDevice(r.device));
+    const uint64_t X = d->X, R = d->R, W = d->world;
+    auto alloc = [&](uint64_t** p, uint64_t words) -> hipError_t {
+        hipError_t e = hipMalloc((void**)p, std::max<uint64_t>(words, 1) * 8);
+        return e == hipSuccess ? hipMemsetAsync(*p, 0, std::max<uint64_t>(words, 1) * 8, r.stream) : e;
+    };
+    DHIP(alloc(&r.send, d->n * X));
+    DHIP(alloc(&r.recv, W * r.n_local * X));
+    DHIP(alloc(&r.gather, W * d->chunk * X));
+    DHIP(alloc(&r.seg, W * d->chunk * R));
+    DHIP(alloc(&r.rec_in, W * r.n_local * R));
+    DHIP(alloc(&r.d_io, 2 * std::max<uint64_t>(W, kStatSlots)));
+    DHIP(hipHostMalloc((void**)&r.h_io, 2 * std::max<uint64_t>(W, kStatSlots) * 8));
+    r.counts_out.assign(W, 0);
+    r.counts_in.assign(W, 0);
+    DHIP(hipStreamSynchronize(r.stream));
+    gossip_status s = gossip_set_stream(r.ctx, r.stream);
+    if (!s) s = gossip_set_exchange(r.ctx, r.send, r.recv, d->world, d->part.data());
+    if (!s) s = gossip_set_gather(r.ctx, r.gather);
+    if (!s) s = gossip_set_sparse(r.ctx, r.seg);
+    return s;
+}
+
+// Checks the ctx's block against the partition and fills the rank's shape.
+gossip_status bind_rank(DistDriver* d, DistRank& r) {
+    uint64_t b = 0, e = 0;
+    ctx_range(r.ctx, &b, &e);
+    if (b != d->part[r.rank] || e != d->part[r.rank + 1])
+        return set_error(GOSSIP_EINVAL, "ctx part range is not rank " + std::to_string(r.rank) +
+                                            "'s block of gossip_partition(n_peers, world)");
+    r.begin = b;
+    r.n_local = e - b;
+    r.device = ctx_device(r.ctx);
+    uint32_t words = 0, x = 0;
+    gossip_status s = gossip_get_shape(r.ctx, &words, &x, nullptr, nullptr);
+    if (s) return s;
+    d->X = x;
+    d->R = 1 + x;
+    return GOSSIP_OK;
+}
+
+void init_schedule(DistDriver* d, const gossip_config& cfg) {
+    d->n = cfg.n_peers;
+    d->part = blocks(d->n, d->world);
+    d->chunk = d->part[1];
+    if (cfg.pull_permille) d->pull_pm = cfg.pull_permille;
+    if (cfg.bin_permille) d->bin_pm = cfg.bin_permille;
+}
+
+// The round's exchange mode from the previous round's GLOBAL stats (the
+// single-partition engine's switch points).
+int choose_mode(const DistDriver* d) {
+    const uint64_t n = d->n;
+    if (d->prev_new * 1000 >= (uint64_t)d->pull_pm * n) {
+        const uint64_t have = d->cum_covered + d->prev_new, total = d->injected * n;
+        const uint64_t missing = total > have ? total - have : 0;
+        const bool wide = d->prev_new * 1000 >= (uint64_t)d->bin_front_pm * n;
+        return wide && missing * 1000 >= (uint64_t)d->bin_pm * n ? GOSSIP_MODE_BIN : GOSSIP_MODE_PULL;
+    }
+    return d->prev_new * 1000 < (uint64_t)d->sparse_pm * n ? GOSSIP_MODE_PUSH_SPARSE : GOSSIP_MODE_PUSH;
+}
+
+// ---- collectives (RCCL, or device copies when emulating on one GPU) ----
+
+// every block's new words (published at gather + rank * chunk * X) to every rank
+gossip_status all_gather(DistDriver* d) {
+    const uint64_t words = d->chunk * d->X;
+    if (d->emulate) {
+        for (auto& q : d->ranks)
+            for (auto& p : d->ranks)
+                if (p.rank != q.rank)
+                    DHIP(hipMemcpyAsync(q.gather + p.rank * words, p.gather + p.rank * words, words * 8,
+                                        hipMemcpyDeviceToDevice, q.stream));
+        return GOSSIP_OK;
+    }
+    DNCCL(ncclGroupStart());
+    for (auto& r : d->ranks) {
+        hipSetDevice(r.device);
+        DNCCL(ncclAllGather(r.gather + r.rank * words, r.gather, words, ncclUint64, r.comm, r.stream));
+    }
+    DNCCL(ncclGroupEnd());
+    return GOSSIP_OK;
+}
+
+// dense push: rank p's staged masks for block q (send + begins[q] * X) to q,
+// received at recv + p * n_local(q) * X
+gossip_status all_to_all(DistDriver* d) {
+    const uint64_t X = d->X;
+    if (d->emulate) {
+        for (auto& q : d->ranks)
+            for (auto& p : d->ranks)
+                if (p.rank != q.rank)  // own pushes went straight to seen; the own slice of recv stays zero
+                    DHIP(hipMemcpyAsync(q.recv + p.rank * q.n_local * X, p.send + d->part[q.rank] * X,
+                                        q.n_local * X * 8, hipMemcpyDeviceToDevice, q.stream));
+        return GOSSIP_OK;
+    }
+    DNCCL(ncclGroupStart());
+    for (auto& r : d->ranks) {
+        hipSetDevice(r.device);
+        for (uint32_t q = 0; q < d->world; ++q) {
+            if (q == r.rank && d->world > 1) continue;  // own pushes went straight to seen (world 1 still exchanges)
+            DNCCL(ncclSend(r.send + d->part[q] * X, (d->part[q + 1] - d->part[q]) * X, ncclUint64, (int)q, r.comm,
+                           r.stream));
+            DNCCL(ncclRecv(r.recv + (uint64_t)q * r.n_local * X, r.n_local * X, ncclUint64, (int)q, r.comm, r.stream));
+        }
+    }
+    DNCCL(ncclGroupEnd());
+    return GOSSIP_OK;
+}
+
+// sparse push: record counts (per destination) then the records themselves;
+// rank q receives sender p's records after those of senders < p
+gossip_status exchange_records(DistDriver* d, std::vector<uint64_t>& total_in) {
+    const uint32_t W = d->world;
+    const uint64_t R = d->R, chunk = d->chunk;
+    for (auto& r : d->ranks) {
+        gossip_status s = gossip_sparse_counts(r.ctx, r.counts_out.data());
+        if (s) return s;
+    }
+    if (d->emulate) {
+        for (auto& q : d->ranks)
+            for (auto& p : d->ranks) q.counts_in[p.rank] = p.counts_out[q.rank];
+    } else {
+        for (auto& r : d->ranks) {
+            hipSetDevice(r.device);
+            std::memcpy(r.h_io, r.counts_out.data(), W * 8);
+            DHIP(hipMemcpyAsync(r.d_io, r.h_io, W * 8, hipMemcpyHostToDevice, r.stream));
+        }
+        DNCCL(ncclGroupStart());
+        for (auto& r : d->ranks) {
+            hipSetDevice(r.device);
+            for (uint32_t q = 0; q < W; ++q) {
+                DNCCL(ncclSend(r.d_io + q, 1, ncclUint64, (int)q, r.comm, r.stream));
+                DNCCL(ncclRecv(r.d_io + W + q, 1, ncclUint64, (int)q, r.comm, r.stream));
+            }
+        }
+        DNCCL(ncclGroupEnd());
+        for (auto& r : d->ranks) {
+            hipSetDevice(r.device);
+            DHIP(hipMemcpyAsync(r.h_io + W, r.d_io + W, W * 8, hipMemcpyDeviceToHost, r.stream));
+            DHIP(hipStreamSynchronize(r.stream));
+            std::memcpy(r.counts_in.data(), r.h_io + W, W * 8);
+        }
+    }
+    total_in.assign(d->ranks.size(), 0);
+    if (d->emulate) {
+        for (size_t i = 0; i < d->ranks.size(); ++i) {
+            DistRank& q = d->ranks[i];
+            uint64_t off = 0;
+            for (auto& p : d->ranks) {
+                const uint64_t c = p.counts_out[q.rank];
+                if (c)
+                    DHIP(hipMemcpyAsync(q.rec_in + off * R, p.seg + (uint64_t)q.rank * chunk * R, c * R * 8,
+                                        hipMemcpyDeviceToDevice, q.stream));
+                off += c;
+            }
+            total_in[i] = off;
+        }
+        return GOSSIP_OK;
+    }
+    DNCCL(ncclGroupStart());
+    for (size_t i = 0; i < d->ranks.size(); ++i) {
+        DistRank& r = d->ranks[i];
+        hipSetDevice(r.device);
+        uint64_t off = 0;
+        for (uint32_t q = 0; q < W; ++q) {  // both sides know every count: zero-length pairs are skipped on both
+            if (r.counts_out[q])
+                DNCCL(ncclSend(r.seg + (uint64_t)q * chunk * R, r.counts_out[q] * R, ncclUint64, (int)q, r.comm, r.stream));
+            if (r.counts_in[q])
+                DNCCL(ncclRecv(r.rec_in + off * R, r.counts_in[q] * R, ncclUint64, (int)q, r.comm, r.stream));
+            off += r.counts_in[q];
+        }
+        total_in[i] = off;
+    }
+    DNCCL(ncclGroupEnd());
+    return GOSSIP_OK;
+}
+
+void pack_stats(const gossip_round_stats& s, uint64_t* v) {
+    const uint64_t f[kStatSlots] = {s.frontier, s.traversals, s.deliveries, s.undelivered, s.new_receipts, s.injected,
+                                    s.died,     s.reports,    s.reconnects, s.rejoined,    s.digest,       s.covered};
+    std::memcpy(v, f, sizeof(f));
+}
+
+gossip_status all_reduce_stats(DistDriver* d, uint64_t* g) {
+    if (d->emulate) {
+        std::fill(g, g + kStatSlots, 0ull);
+        for (auto& r : d->ranks) {
+            uint64_t v[kStatSlots];
+            pack_stats(r.local, v);
+            for (int i = 0; i < kStatSlots; ++i) g[i] += v[i];  // mod 2^64, like ncclSum on uint64
+        }
+        return GOSSIP_OK;
+    }
+    for (auto& r : d->ranks) {
+        hipSetDevice(r.device);
+        pack_stats(r.local, r.h_io);
+        DHIP(hipMemcpyAsync(r.d_io, r.h_io, kStatSlots * 8, hipMemcpyHostToDevice, r.stream));
+    }
+    DNCCL(ncclGroupStart());
+    for (auto& r : d->ranks) {
+        hipSetDevice(r.device);
+        DNCCL(ncclAllReduce(r.d_io, r.d_io, kStatSlots, ncclUint64, ncclSum, r.comm, r.stream));
+    }
+    DNCCL(ncclGroupEnd());
+    for (auto& r : d->ranks) {
+        hipSetDevice(r.device);
+        DHIP(hipMemcpyAsync(r.h_io, r.d_io, kStatSlots * 8, hipMemcpyDeviceToHost, r.stream));
+        DHIP(hipStreamSynchronize(r.stream));
+    }
+    std::memcpy(g, d->ranks[0].h_io, kStatSlots * 8);
+    return GOSSIP_OK;
+}
+
+// One round on every local rank, lockstep phases.
+gossip_status dist_step(DistDriver* d, gossip_round_stats* out) {
+    if (d->finished) return set_error(GOSSIP_ESTATE, "run finished: call gossip_reset");
+    const int want = choose_mode(d);
+    int mode = -1;
+    for (auto& r : d->ranks) {
+        int m = 0;
+        gossip_status s = gossip_round_begin(r.ctx, want, &m);
+        if (s) return s;
+        if (mode >= 0 && m != mode) return set_error(GOSSIP_ESTATE, "ranks chose different round modes");
+        mode = m;
+    }
+    d->modes.push_back(mode);
+    gossip_status s = GOSSIP_OK;
+    if (mode == GOSSIP_MODE_PULL || mode == GOSSIP_MODE_BIN) {
+        if ((s = all_gather(d))) return s;
+        for (auto& r : d->ranks)
+            if ((s = gossip_round_compute(r.ctx))) return s;
+        for (auto& r : d->ranks)
+            if ((s = gossip_round_finish(r.ctx, &r.local))) return s;
+    } else if (mode == GOSSIP_MODE_PUSH_SPARSE) {
+        for (auto& r : d->ranks)
+            if ((s = gossip_round_compute(r.ctx))) return s;
+        std::vector<uint64_t> total_in;
+        if ((s = exchange_records(d, total_in))) return s;
+        for (size_t i = 0; i < d->ranks.size(); ++i)
+            if ((s = gossip_round_finish_sparse(d->ranks[i].ctx, d->ranks[i].rec_in, total_in[i], &d->ranks[i].local)))
+                return s;
+    } else {
+        for (auto& r : d->ranks)
+            if ((s = gossip_round_compute(r.ctx))) return s;
+        if ((s = all_to_all(d))) return s;
+        for (auto& r : d->ranks)
+            if ((s = gossip_round_finish(r.ctx, &r.local))) return s;
+    }
+    uint64_t g[kStatSlots];
+    if ((s = all_reduce_stats(d, g))) return s;
+    gossip_round_stats o{};
+    o.round = d->ranks[0].local.round;
+    o.flags = d->ranks[0].local.flags;
+    o.frontier = g[0];
+    o.traversals = g[1];
+    o.deliveries = g[2];
+    o.undelivered = g[3];
+    o.new_receipts = g[4];
+    o.injected = g[5];
+    o.died = g[6];
+    o.reports = g[7];
+    o.reconnects = g[8];
+    o.rejoined = g[9];
+    d->cum_digest += g[10];
+    d->cum_covered += g[11];
+    o.digest = d->cum_digest;
+    o.covered = d->cum_covered;
+    o.duplicates = o.deliveries - o.new_receipts;
+    o.seed_removals = 0;  // from the gathered reports (gossip_comm_finalize)
+    d->prev_new = o.new_receipts;
+    d->injected += o.injected;
+    int fin = -1;
+    for (auto& r : d->ranks) {
+        int f = 0;
+        if ((s = gossip_round_commit(r.ctx, o.new_receipts, &f))) return s;
+        if (fin >= 0 && f != fin) return set_error(GOSSIP_ESTATE, "ranks disagree on termination");
+        fin = f;
+    }
+    d->finished = fin == 1;
+    if (out) *out = o;
+    return d->finished ? 1 : 0;
+}
+
+bool report_less(const gossip_dead_report& x, const gossip_dead_report& y) {
+    if (x.round != y.round) return x.round < y.round;
+    if (x.reporter != y.reporter) return x.reporter < y.reporter;
+    return x.dead < y.dead;
+}
+
+gossip_status local_reports(DistRank& r, std::vector<gossip_dead_report>& out) {
+    uint64_t n = 0;
+    gossip_status s = gossip_read_reports(r.ctx, nullptr, 0, &n);
+    if (s) return s;
+    out.resize(n);
+    return n ? gossip_read_reports(r.ctx, out.data(), n, &n) : GOSSIP_OK;
+}
+
+// Every rank's reports to every rank, merged and sorted; seed_removals of a
+// round = peers whose first report falls in it (seed.cpp:158-167).
+gossip_status dist_finalize(DistDriver* d, gossip_round_stats* per_round, uint32_t rounds,
+                            std::vector<gossip_dead_report>& all) {
+    all.clear();
+    gossip_status s = GOSSIP_OK;
+    if (d->world == (uint32_t)d->ranks.size()) {  // this process holds every rank: no collective needed
+        for (auto& r : d->ranks) {
+            std::vector<gossip_dead_report> mine;
+            if ((s = local_reports(r, mine))) return s;
+            all.insert(all.end(), mine.begin(), mine.end());
+        }
+    } else {
+        // one local rank (gossip_comm_init): counts, then the padded lists, all-gathered
+        DistRank& r = d->ranks[0];
+        std::vector<gossip_dead_report> mine;
+        if ((s = local_reports(r, mine))) return s;
+        const uint32_t W = d->world;
+        DHIP(hipSetDevice(r.device));
+        r.h_io[0] = mine.size();
+        DHIP(hipMemcpyAsync(r.d_io, r.h_io, 8, hipMemcpyHostToDevice, r.stream));
+        DNCCL(ncclAllGather(r.d_io, r.d_io + W, 1, ncclUint64, r.comm, r.stream));
+        DHIP(hipMemcpyAsync(r.h_io + W, r.d_io + W, W * 8, hipMemcpyDeviceToHost, r.stream));
+        DHIP(hipStreamSynchronize(r.stream));
+        std::vector<uint64_t> cnt(r.h_io + W, r.h_io + 2 * W);
+        const uint64_t mx = std::max<uint64_t>(1, *std::max_element(cnt.begin(), cnt.end()));
+        uint32_t *d_mine = nullptr, *d_all = nullptr;
+        DHIP(hipMalloc((void**)&d_mine, mx * 12));
+        if (hipMalloc((void**)&d_all, mx * 12 * W) != hipSuccess) {
+            hipFree(d_mine);
+            return set_error(GOSSIP_ENOMEM, "report gather buffer");
+        }
+        hipError_t he = mine.empty() ? hipSuccess
+                                     : hipMemcpyAsync(d_mine, mine.data(), mine.size() * 12, hipMemcpyHostToDevice, r.stream);
+        ncclResult_t nr = he == hipSuccess ? ncclAllGather(d_mine, d_all, mx * 3, ncclUint32, r.comm, r.stream)
+                                           : ncclSuccess;
+        std::vector<gossip_dead_report> buf(mx * W);
+        if (he == hipSuccess && nr == ncclSuccess)
+            he = hipMemcpyAsync(buf.data(), d_all, mx * 12 * W, hipMemcpyDeviceToHost, r.stream);
+        if (he == hipSuccess) he = hipStreamSynchronize(r.stream);
+        hipFree(d_mine);
+        hipFree(d_all);
+        if (he != hipSuccess) return set_error(GOSSIP_EHIP, std::string("report gather: ") + hipGetErrorString(he));
+        if (nr != ncclSuccess) return set_error(GOSSIP_ECOMM, std::string("report gather: ") + ncclGetErrorString(nr));
+        for (uint32_t p = 0; p < W; ++p) all.insert(all.end(), buf.begin() + p * mx, buf.begin() + p * mx + cnt[p]);
+    }
+    std::sort(all.begin(), all.end(), report_less);
+    if (per_round) {
+        std::vector<std::pair<uint32_t, uint32_t>> firsts;  // (dead, round) of its first report
+        std::vector<gossip_dead_report> byv(all);
+        std::stable_sort(byv.begin(), byv.end(),
+                         [](const gossip_dead_report& x, const gossip_dead_report& y) { return x.dead < y.dead; });
+        for (size_t i = 0; i < byv.size(); ++i)
+            if (i == 0 || byv[i].dead != byv[i - 1].dead) firsts.emplace_back(byv[i].dead, byv[i].round);
+        for (uint32_t i = 0; i < rounds; ++i) per_round[i].seed_removals = 0;
+        for (const auto& f : firsts)
+            for (uint32_t i = 0; i < rounds; ++i)
+                if (per_round[i].round == f.second) {
+                    per_round[i].seed_removals++;
+                    break;
+                }
+    }
+    return GOSSIP_OK;
+}
+
+}  // namespace
+
+gossip_status dist_step_ctx(gossip_ctx* c, gossip_round_stats* out) {
+    DistDriver* d = ctx_dist(c);
+    if (d->ranks.size() != 1) return set_error(GOSSIP_ESTATE, "this ctx is a part of a group: use gossip_group_step");
+    return dist_step(d, out);
+}
+
+void dist_reset(DistDriver* d) {
+    d->prev_new = d->injected = d->cum_digest = d->cum_covered = 0;
+    d->finished = false;
+    d->modes.clear();
+}
+
+void dist_free(DistDriver* d) {
+    if (!d) return;
+    for (auto& r : d->ranks) free_rank(r);
+    std::vector<hipStream_t> done;  // emulated groups share one stream
+    for (auto& r : d->ranks) {
+        if (!r.stream || std::find(done.begin(), done.end(), r.stream) != done.end()) continue;
+        hipSetDevice(r.device);
+        hipStreamDestroy(r.stream);
+        done.push_back(r.stream);
+    }
+    delete d;
+}
+
+}  // namespace gossip
+
+using namespace gossip;
+
+struct gossip_group {
+    DistDriver* d = nullptr;
+    std::vector<gossip_ctx*> parts;
+    uint64_t n = 0;
+    uint32_t W = 0;
+};
+
+extern "C" {
+
+gossip_status gossip_partition(uint64_t n_peers, uint32_t world, uint64_t* begins) {
+    if (!begins || world < 1 || n_peers < world) return set_error(GOSSIP_EINVAL, "need 1 <= world <= n_peers");
+    const std::vector<uint64_t> b = blocks(n_peers, world);
+    for (uint32_t p = 0; p < world; ++p)
+        if (b[p + 1] <= b[p]) return set_error(GOSSIP_EINVAL, "peers do not split into non-empty ceil(n/world) blocks");
+    std::copy(b.begin(), b.end(), begins);
+    return GOSSIP_OK;
+}
+
+gossip_status gossip_comm_unique_id(uint8_t* id) {
+    if (!id) return set_error(GOSSIP_EINVAL, "null argument");
+    ncclUniqueId u;
+    DNCCL(ncclGetUniqueId(&u));
+    static_assert(sizeof(u) == GOSSIP_COMM_ID_BYTES, "ncclUniqueId size");
+    std::memcpy(id, &u, sizeof(u));
+    return GOSSIP_OK;
+}
+
+gossip_status gossip_comm_init(gossip_ctx* ctx, const uint8_t* id, uint32_t world, uint32_t rank) {
+    if (!ctx || !id || world < 1 || rank >= world) return set_error(GOSSIP_EINVAL, "bad argument");
+    if (ctx_dist(ctx)) return set_error(GOSSIP_ESTATE, "ctx already has a communicator");
+    const gossip_config& cfg = ctx_config(ctx);
+    if (cfg.rejoin_threshold) return set_error(GOSSIP_EINVAL, "rejoin_threshold needs a single partition");
+    DistDriver* d = new DistDriver();
+    d->world = world;
+    init_schedule(d, cfg);
+    d->ranks.resize(1);
+    DistRank& r = d->ranks[0];
+    r.ctx = ctx;
+    r.rank = rank;
+    gossip_status s = bind_rank(d, r);
+    if (!s) {
+        hipSetDevice(r.device);
+        if (hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking) != hipSuccess)
+            s = set_error(GOSSIP_EHIP, "stream");
+    }
+    if (!s) s = setup_rank(d, r);
+    if (!s) {
+        ncclUniqueId u;
+        std::memcpy(&u, id, sizeof(u));
+        const ncclResult_t nr = ncclCommInitRank(&r.comm, (int)world, u, (int)rank);
+        if (nr != ncclSuccess) s = set_error(GOSSIP_ECOMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(nr));
+    }
+    if (s) {
+        gossip_set_stream(ctx, nullptr);  // back to the null stream before ours goes
+        dist_free(d);
+        return s;
+    }
+    ctx_attach_dist(ctx, d, true);
+    return GOSSIP_OK;
+}
+
+gossip_status gossip_comm_finalize(gossip_ctx* ctx, gossip_round_stats* per_round, uint32_t rounds,
+                                   gossip_dead_report* reports, uint64_t cap, uint64_t* count) {
+    if (!ctx) return set_error(GOSSIP_EINVAL, "null ctx");
+    DistDriver* d = ctx_dist(ctx);
+    if (!d) return set_error(GOSSIP_ESTATE, "no communicator: gossip_comm_init first");
+    std::vector<gossip_dead_report> all;
+    gossip_status s = dist_finalize(d, per_round, rounds, all);
+    if (s) return s;
+    if (count) *count = all.size();
+    if (reports) std::copy(all.begin(), all.begin() + std::min<uint64_t>(cap, all.size()), reports);
+    return GOSSIP_OK;
+}
+
+gossip_status gossip_comm_modes(gossip_ctx* ctx, int32_t* modes, uint32_t cap, uint32_t* n) {
+    if (!ctx || !n) return set_error(GOSSIP_EINVAL, "null argument");
+    DistDriver* d = ctx_dist(ctx);
+    if (!d) return set_error(GOSSIP_ESTATE, "no communicator");
+    *n = (uint32_t)d->modes.size();
+    if (modes) std::copy(d->modes.begin(), d->modes.begin() + std::min<size_t>(cap, d->modes.size()), modes);
+    return GOSSIP_OK;
+}
+
+gossip_status gossip_group_create(const gossip_config* cfg, uint32_t n_parts, const int32_t* devices,
+                                  gossip_group** out) {
+    if (!cfg || !devices || !out || n_parts < 1) return set_error(GOSSIP_EINVAL, "bad argument");
+    *out = nullptr;
+    if (cfg->rejoin_threshold && n_parts > 1) return set_error(GOSSIP_EINVAL, "rejoin_threshold needs a single partition");
+    bool same = true, distinct = true;
+    for (uint32_t p = 0; p < n_parts; ++p)
+        for (uint32_t q = 0; q < p; ++q) {
+            same &= devices[p] == devices[q];
+            distinct &= devices[p] != devices[q];
+        }
+    same &= devices[0] == devices[n_parts - 1];
+    if (!same && !distinct) return set_error(GOSSIP_EINVAL, "devices must be all distinct or all the same");
+    std::vector<uint64_t> part(n_parts + 1);
+    gossip_status s = gossip_partition(cfg->n_peers, n_parts, part.data());
+    if (s) return s;
+    gossip_group* g = new gossip_group();
+    g->n = cfg->n_peers;
+    g->W = (cfg->n_msgs + 63) / 64;
+    DistDriver* d = new DistDriver();
+    g->d = d;
+    d->world = n_parts;
+    d->emulate = same && n_parts > 1;
+    init_schedule(d, *cfg);
+    d->ranks.resize(n_parts);
+    auto bail = [&](gossip_status st) {
+        for (auto& r : d->ranks)
+            if (r.ctx) ctx_attach_dist(r.ctx, nullptr, false);
+        gossip_group_destroy(g);
+        return st;
+    };
+    for (uint32_t p = 0; p < n_parts; ++p) {
+        gossip_config c = *cfg;
+        c.part_begin = part[p];
+        c.part_end = part[p + 1];
+        c.device = devices[p];
+        if ((s = gossip_create(&c, &d->ranks[p].ctx))) return bail(s);
+        g->parts.push_back(d->ranks[p].ctx);
+        d->ranks[p].rank = p;
+        if ((s = bind_rank(d, d->ranks[p]))) return bail(s);
+        hipSetDevice(d->ranks[p].device);
+        if (!d->emulate || p == 0) {
+            if (hipStreamCreateWithFlags(&d->ranks[p].stream, hipStreamNonBlocking) != hipSuccess)
+                return bail(set_error(GOSSIP_EHIP, "stream"));
+        } else {
+            d->ranks[p].stream = d->ranks[0].stream;  // one stream orders every part's work and copies
+        }
+    }
+    for (auto& r : d->ranks)
+        if ((s = setup_rank(d, r))) return bail(s);
+    if (!d->emulate) {
+        std::vector<ncclComm_t> comms(n_parts);
+        std::vector<int> devs(devices, devices + n_parts);
+        const ncclResult_t nr = ncclCommInitAll(comms.data(), (int)n_parts, devs.data());
+        if (nr != ncclSuccess) return bail(set_error(GOSSIP_ECOMM, std::string("ncclCommInitAll: ") + ncclGetErrorString(nr)));
+        for (uint32_t p = 0; p < n_parts; ++p) d->ranks[p].comm = comms[p];
+    }
+    for (auto& r : d->ranks) ctx_attach_dist(r.ctx, d, false);
+    *out = g;
+    return GOSSIP_OK;
+}
+
+void gossip_group_destroy(gossip_group* g) {
+    if (!g) return;
+    for (gossip_ctx* c : g->parts) {
+        ctx_attach_dist(c, nullptr, false);
+        gossip_set_stream(c, nullptr);  // the driver's streams go with it
+    }
+    if (g->d) {
+        for (auto& r : g->d->ranks) r.ctx = nullptr;
+        dist_free(g->d);
+    }
+    for (gossip_ctx* c : g->parts) gossip_destroy(c);
+    delete g;
+}
+
+gossip_status gossip_group_part(gossip_group* g, uint32_t p, gossip_ctx** ctx) {
+    if (!g || !ctx || p >= g->parts.size()) return set_error(GOSSIP_EINVAL, "bad argument");
+    *ctx = g->parts[p];
+    return GOSSIP_OK;
+}
+
+#define GROUP_EACH(g, call)                              \
+    do {                                                 \
+        if (!(g)) return set_error(GOSSIP_EINVAL, "null group"); \
+        for (gossip_ctx* c_ : (g)->parts) {              \
+            gossip_status s_ = call;                     \
+            if (s_) return s_;                           \
+        }                                                \
+        return GOSSIP_OK;                                \
+    } while (0)
+
+gossip_status gossip_group_build_graph(gossip_group* g) { GROUP_EACH(g, gossip_build_graph(c_)); }
+gossip_status gossip_group_inject(gossip_group* g, const uint32_t* origin, const uint32_t* inject_round, uint32_t n) {
+    GROUP_EACH(g, gossip_inject(c_, origin, inject_round, n));
+}
+gossip_status gossip_group_schedule_kills(gossip_group* g, const uint32_t* peer, const uint32_t* round, uint32_t n) {
+    GROUP_EACH(g, gossip_schedule_kills(c_, peer, round, n));
+}
+gossip_status gossip_group_reset(gossip_group* g) { GROUP_EACH(g, gossip_reset(c_)); }
+
+gossip_status gossip_group_step(gossip_group* g, gossip_round_stats* out) {
+    if (!g) return set_error(GOSSIP_EINVAL, "null group");
+    return dist_step(g->d, out);
+}
+
+gossip_status gossip_group_run(gossip_group* g, gossip_round_stats* per_round, uint32_t cap, uint32_t* rounds) {
+    if (!g) return set_error(GOSSIP_EINVAL, "null group");
+    std::vector<gossip_round_stats> all;
+    while (!g->d->finished) {
+        gossip_round_stats st{};
+        const gossip_status s = dist_step(g->d, &st);
+        if (s < 0) return s;
+        all.push_back(st);
+    }
+    std::vector<gossip_dead_report> reps;
+    const gossip_status s = dist_finalize(g->d, all.data(), (uint32_t)all.size(), reps);
+    if (s) return s;
+    if (per_round) std::copy(all.begin(), all.begin() + std::min<size_t>(cap, all.size()), per_round);
+    if (rounds) *rounds = (uint32_t)all.size();
+    return GOSSIP_OK;
+}
+
+gossip_status gossip_group_read_seen(gossip_group* g, uint64_t* host_seen) {
+    if (!g || !host_seen) return set_error(GOSSIP_EINVAL, "null argument");
+    for (auto& r : g->d->ranks) {
+        const gossip_status s = gossip_read_seen(r.ctx, host_seen + r.begin * g->W);
+        if (s) return s;
+    }
+    return GOSSIP_OK;
+}
+
+gossip_status gossip_group_read_reports(gossip_group* g, gossip_dead_report* buf, uint64_t cap, uint64_t* count) {
+    if (!g || !count) return set_error(GOSSIP_EINVAL, "null argument");
+    std::vector<gossip_dead_report> all;
+    const gossip_status s = dist_finalize(g->d, nullptr, 0, all);
+    if (s) return s;
+    *count = all.size();
+    if (buf) std::copy(all.begin(), all.begin() + std::min<uint64_t>(cap, all.size()), buf);
+    return GOSSIP_OK;
+}
+
+}  // extern "C"

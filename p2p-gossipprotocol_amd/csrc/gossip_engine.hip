@@ -33,6 +33,14 @@ gossip_status fail(gossip_status s, const std::string& msg) {
     return s;
 }
 
+}  // namespace
+
+namespace gossip {
+gossip_status set_error(gossip_status s, const std::string& msg) { return fail(s, msg); }
+}  // namespace gossip
+
+namespace {
+
 #define HIPCHK(call)                                                                              \
     do {                                                                                          \
         hipError_t e_ = (call);                                                                   \
@@ -139,6 +147,7 @@ struct gossip_ctx {
     bool bins_first = false;             // no binned round since the last reset: rewrite every slot
     bool bin_noskip = false;     // GOSSIP_BIN_NOSKIP: rewrite every slot each binned round (A/B measurement)
     uint32_t scatter_probe = 0;  // GOSSIP_SCATTER_PROBE: partial scatter for timing breakdowns (wrong results)
+    uint32_t scatter_sync_us = kScatterSyncUs;  // GOSSIP_SCATTER_SYNC: scatter row-barrier spin bound (0 = off)
     bool full_liveness = false;  // GOSSIP_FULL_LIVENESS: ping every edge each ping round (A/B against closed form)
     uint64_t* seg = nullptr;     // sparse push: per-destination record segments (world x chunk records)
     unsigned long long* d_counts = nullptr;  // records per destination rank
@@ -162,7 +171,27 @@ struct gossip_ctx {
     std::map<std::string, TimerRec> timers;
     std::map<std::string, double> kbytes;
     std::vector<hipEvent_t> event_pool;
+
+    // library-driven multi-GPU rounds (gossip_dist.hip): the driver that issues
+    // this ctx's collectives; owned here for gossip_comm_init, by the group otherwise
+    gossip::DistDriver* dist = nullptr;
+    bool dist_owned = false;
 };
+
+namespace gossip {
+hipStream_t ctx_stream(gossip_ctx* c) { return c->stream; }
+int ctx_device(gossip_ctx* c) { return c->device; }
+const gossip_config& ctx_config(gossip_ctx* c) { return c->cfg; }
+void ctx_range(gossip_ctx* c, uint64_t* begin, uint64_t* end) {
+    *begin = c->begin;
+    *end = c->end;
+}
+void ctx_attach_dist(gossip_ctx* c, DistDriver* d, bool owned) {
+    c->dist = d;
+    c->dist_owned = owned;
+}
+DistDriver* ctx_dist(gossip_ctx* c) { return c->dist; }
+}  // namespace gossip
 
 namespace {
 
@@ -690,7 +719,9 @@ gossip_status round_compute(gossip_ctx* c) {
         BinArgs b{c->bins.bins,     c->bins.n_bins,    c->bins.cb_src,  c->bins.cb_run,    c->bins.cb_grp,
                   c->bins.n_binned, c->bins.chunk_begin, c->bins.n_chunks, c->bins.chunk,    c->bins.units,
                   c->bins.xcd_units, c->bins.bdst,     c->bins.val,     c->bins.bin_words, c->bins.dummy,   c->bin_noskip || c->bins_first,
-                  c->scatter_probe};
+                  c->scatter_probe,  c->bins.n_runs ? c->bins.n_runs - 1 : 0, c->bins.sync,
+                  c->scatter_sync_us};
+        if (b.sync_us) HIPCHK(hipMemsetAsync(c->bins.sync, 0, 8 * kScatterSyncStride * sizeof(uint32_t), c->stream));
         HIPCHK(timed(c, "bin_scatter", [&] { return launch_bin_scatter(a, b, pw, c->stream); }));
         HIPCHK(timed(c, "bin_apply", [&] { return launch_bin_apply(a, b, pw, c->stream); }));
         c->bins_first = false;
@@ -813,6 +844,7 @@ const char* gossip_strerror(gossip_status s) {
         case GOSSIP_ESTATE: return "call out of order";
         case GOSSIP_ENODEV: return "no gfx950 device";
         case GOSSIP_EOVERFLOW: return "report buffer overflow";
+        case GOSSIP_ECOMM: return "RCCL error";
         default: return "unknown status";
     }
 }
@@ -855,6 +887,7 @@ gossip_status gossip_create(const gossip_config* cfg, gossip_ctx** out) {
     if (const char* h = std::getenv("GOSSIP_HEAVY_DEGREE")) c->heavy = (uint32_t)std::max(1, std::atoi(h));
     if (const char* u = std::getenv("GOSSIP_BIN_NOSKIP"); u && std::atoi(u)) c->bin_noskip = true;
     if (const char* u = std::getenv("GOSSIP_SCATTER_PROBE")) c->scatter_probe = (uint32_t)std::atoi(u);
+    if (const char* u = std::getenv("GOSSIP_SCATTER_SYNC")) c->scatter_sync_us = (uint32_t)std::atoi(u);
     if (const char* u = std::getenv("GOSSIP_FULL_LIVENESS"); u && std::atoi(u)) c->full_liveness = true;
     if (const char* b = std::getenv("GOSSIP_BIN_PERMILLE"); b && !cfg->bin_permille) c->cfg.bin_permille = (uint32_t)std::atoi(b);
     c->n = cfg->n_peers;
@@ -938,6 +971,7 @@ void gossip_destroy(gossip_ctx* c) {
     hipFree(c->d_counts);
     if (c->h_counts) hipHostFree(c->h_counts);
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
+    if (c->dist && c->dist_owned) gossip::dist_free(c->dist);
     delete c;
 }
 
@@ -1181,6 +1215,7 @@ gossip_status gossip_reset(gossip_ctx* c) {
     c->finished = false;
     c->any_dead = c->n_started < c->n;
     c->cum_digest = c->cum_covered = 0;
+    if (c->dist) gossip::dist_reset(c->dist);
     HIPCHK(hipStreamSynchronize(s));
     return GOSSIP_OK;
 }
@@ -1188,7 +1223,8 @@ gossip_status gossip_reset(gossip_ctx* c) {
 gossip_status gossip_step(gossip_ctx* c, gossip_round_stats* out) {
     if (!c) return fail(GOSSIP_EINVAL, "null ctx");
     if (set_dev(c)) return GOSSIP_EHIP;
-    if (c->world > 1) return fail(GOSSIP_ESTATE, "partitioned ctx: use gossip_round_push/finish/commit");
+    if (c->dist) return gossip::dist_step_ctx(c, out);  // the library's own collectives (gossip_comm_init)
+    if (c->world > 1) return fail(GOSSIP_ESTATE, "partitioned ctx: use gossip_comm_init or gossip_round_*");
     gossip_status s = round_begin(c, false, GOSSIP_MODE_AUTO, nullptr);
     if (!s) s = round_compute(c);
     if (s) return s;

@@ -5,6 +5,8 @@
 
 #include <string>
 
+#include "../../include/gossip/gossip.h"
+
 namespace gossip {
 
 constexpr uint32_t kMaskedEdge = 0x80000000u;  // col[e] bit 31: edge dropped by liveness (peer.cpp:388)
@@ -35,7 +37,7 @@ constexpr uint32_t kBinWords = 18432;       // LDS accumulator words per bin (14
 constexpr uint32_t kBinSlotPad = 8;         // bin slot ranges padded to 8 slots (16-B loads)
 constexpr uint64_t kBinSlotCap = 1u << 18;  // slots per bin (load balance between bins)
 constexpr uint32_t kBinChunkWords = 18432;     // source chunk: its new words (144 KB) are staged in LDS
-constexpr uint64_t kBinUnitCap = 1u << 17;     // cb entries per scatter work unit (hub chunks are split)
+constexpr uint64_t kHubFactor = 4;             // chunks with more than 4x the mean cb entries are split into units
 constexpr int kScatterBlock = 1024;            // k_bin_scatter_lds: one 16-wave workgroup per CU
 constexpr int kScatterGrid = 256;              // one workgroup per CU
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
@@ -72,7 +74,13 @@ struct BinArgs {
     uint32_t noskip;              // every slot is rewritten: first binned round after a reset (or GOSSIP_BIN_NOSKIP)
     uint32_t probe;               // measurement only (GOSSIP_SCATTER_PROBE=1: staging only, 2: slot stores to the
                                   // sink; results are then wrong)
+    uint64_t n_runs_m1;           // cb_run entries - 1 (clamp for the run index of past-the-end lanes)
+    uint32_t* sync;               // kScatterSyncStride words per XCD: units finished (zeroed before each scatter)
+    uint32_t sync_us;             // row barrier between the XCD's workgroups, spin bound in us (0 = none).
+                                  // Speed only: no result depends on it, and every wait is bounded
 };
+constexpr int kScatterSyncStride = 32;  // one 128-B line per XCD counter
+constexpr uint32_t kScatterSyncUs = 50;  // default spin bound of the scatter row barrier
 
 struct BinState {
     Bin* bins = nullptr;
@@ -92,6 +100,7 @@ struct BinState {
     uint32_t bin_words = kBinWords;
     uint64_t n_slots = 0;   // padded
     uint64_t n_binned = 0;  // edges with a slot (light destinations)
+    uint32_t* sync = nullptr;  // 8 * kScatterSyncStride words (scatter row barrier)
 };
 
 struct DeadReport {
@@ -216,6 +225,19 @@ hipError_t build_powerlaw_device(uint64_t n_global, uint64_t begin, uint64_t end
 hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local, uint64_t n_global, uint64_t n_edges,
                       uint32_t heavy, uint32_t Wp, hipStream_t s, BinState* out, std::string* err);
 void free_bins(BinState* b);
+
+// ---- library-driven multi-GPU rounds (gossip_dist.hip) ----
+struct DistDriver;
+gossip_status set_error(gossip_status s, const std::string& msg);
+hipStream_t ctx_stream(gossip_ctx* c);
+int ctx_device(gossip_ctx* c);
+const gossip_config& ctx_config(gossip_ctx* c);
+void ctx_range(gossip_ctx* c, uint64_t* begin, uint64_t* end);
+void ctx_attach_dist(gossip_ctx* c, DistDriver* d, bool owned);
+DistDriver* ctx_dist(gossip_ctx* c);
+gossip_status dist_step_ctx(gossip_ctx* c, gossip_round_stats* out);
+void dist_reset(DistDriver* d);
+void dist_free(DistDriver* d);
 
 // Exact integer threshold ceil(2^32 (j/L)^2.5) (host only).
 uint64_t pick_threshold(uint32_t j, uint32_t L);

@@ -50,11 +50,20 @@ struct Acc {
 // atomics serialise (~9 ns each measured); one line per round hit by every
 // wave cost ~0.65 ms per pull round at 2^20 peers.  Must be reached by every
 // wave of the block (it holds a barrier).
+// flush_into: the same with caller-provided LDS scratch (kWaves * kStatFields words).
+template <int kWaves>
+__device__ __forceinline__ void flush_into(Acc& acc, DevStats* st, unsigned long long (*red)[kStatFields]);
+
 template <int kWaves = kWavesPerBlock>
 __device__ __forceinline__ void flush(Acc& acc, DevStats* st) {
+    __shared__ unsigned long long red[kWaves][kStatFields];
+    flush_into<kWaves>(acc, st, red);
+}
+
+template <int kWaves>
+__device__ __forceinline__ void flush_into(Acc& acc, DevStats* st, unsigned long long (*red)[kStatFields]) {
     constexpr int kF = kStatFields;
     static_assert(sizeof(DevStats) == kF * 8, "one u64 per stat field");
-    __shared__ unsigned long long red[kWaves][kF];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     // DevStats field order
     const unsigned long long v[kF] = {acc.frontier, acc.trav,     acc.deliv,   acc.undeliv, acc.fresh,  acc.injected,
@@ -516,11 +525,123 @@ __global__ __launch_bounds__(kBlock) void k_pull_heavy(RoundArgs a) {
 // consecutive, and their slot runs inside each bin are adjacent, so the lines
 // of a bin fill up in that XCD's L2 from several workgroups before they are
 // written back.
+// Staging of one scatter unit's source chunk (every thread of the block):
+// the chunk's new words into the LDS slice, the live bits of its sources and,
+// in the chunk's first unit, the source side of its pushes (broadcastMessage,
+// peer.cpp:310-316).  Ends before the block barrier that publishes the slice.
+template <int W, bool COV>
+__device__ __forceinline__ void scatter_stage(const RoundArgs& a, const BinArgs& b, const BinUnit& un, uint32_t wd,
+                                              unsigned long long* slice, unsigned long long* live_s,
+                                              unsigned int* cov_s, Acc& acc) {
+    constexpr int kSliceIt = kBinChunkWords / kScatterBlock;  // slice words per lane
+    static_assert(kBinChunkWords % kScatterBlock == 0, "slice split");
+    const int lane = threadIdx.x & 63;
+    // global source chunk; words from nw_src (own words at P = 1, the all-gathered ones at P > 1)
+    const uint64_t vb = (uint64_t)un.c * b.chunk, ve = min(vb + b.chunk, a.n_src);  // vb % 64 == 0
+    const uint64_t nwords = (ve - vb) * W;
+    // stage the slice (and the previous round's live bits): every load of
+    // the lane in flight at once
+    const uint64_t n_src = ve - vb;
+    uint64_t r[kSliceIt];
+#pragma unroll
+    for (int k = 0; k < kSliceIt; ++k) {
+        const uint64_t i = threadIdx.x + (uint64_t)k * kScatterBlock;
+        r[k] = i < nwords ? a.nw_src[vb * W + i] : 0ull;
+    }
+    __syncthreads();  // previous unit's readers are done with the slice
+#pragma unroll
+    for (int k = 0; k < kSliceIt; ++k) slice[threadIdx.x + k * kScatterBlock] = r[k];
+    if (threadIdx.x < kBinChunkWords / 64 / W) live_s[threadIdx.x] = b.noskip ? ~0ull : 0ull;
+    __syncthreads();
+    // per source (a wave covers 64 consecutive ones): live bits and, in the
+    // chunk's first unit, the source side of its pushes (broadcastMessage,
+    // peer.cpp:310-316) for the owned sources; row lengths loaded together
+    constexpr int kSrcIt = (kBinChunkWords / W + kScatterBlock - 1) / kScatterBlock;
+    constexpr int kB = 5;  // sources whose row lengths are loaded together (register budget)
+#pragma unroll
+    for (int k0 = 0; k0 < kSrcIt; k0 += kB) {
+        uint32_t pcs[kB];
+#pragma unroll
+        for (int kk = 0; kk < kB; ++kk) {
+            const uint64_t j = threadIdx.x + (uint64_t)(k0 + kk) * kScatterBlock;
+            pcs[kk] = 0;
+            if (k0 + kk >= kSrcIt || j >= ((n_src + 63) & ~63ull)) continue;  // wave-uniform
+            const uint64_t v = vb + j;
+            const bool vv = j < n_src;
+            const bool own = vv && un.first && v >= a.begin && v < a.end;
+            bool nz = false;
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                const uint64_t m = vv ? slice[j * W + w] : 0ull;
+                nz |= m != 0;
+                if (!own || !m) continue;
+                pcs[kk] += (uint32_t)__popcll(m);
+                if (w < (int)wd) acc.digest += digest_weight(v * wd + w) * m;
+                if (COV)
+                    for (uint64_t x = m; x; x &= x - 1) atomicAdd(&cov_s[w * 64 + __builtin_ctzll(x)], 1u);
+            }
+            const unsigned long long bits = __ballot(nz);
+            if (lane == 0) live_s[j >> 6] |= bits;
+        }
+        uint64_t d0[kB], d1[kB];
+        uint32_t dg[kB], dk[kB];  // per-source counters (dead mode); else k_src_count books them
+        const bool cnt = a.dead_mode && a.dgone;
+#pragma unroll
+        for (int kk = 0; kk < kB; ++kk) {
+            const uint64_t lv = vb + threadIdx.x + (uint64_t)(k0 + kk) * kScatterBlock - a.begin;
+            d0[kk] = pcs[kk] ? a.rp[lv] : 0ull;
+            d1[kk] = pcs[kk] ? a.rp[lv + 1] : 0ull;
+            dg[kk] = pcs[kk] && cnt ? a.dgone[lv] : 0u;
+            dk[kk] = pcs[kk] && cnt ? a.dmask[lv] : 0u;
+        }
+#pragma unroll
+        for (int kk = 0; kk < kB; ++kk) {
+            if (!pcs[kk]) continue;
+            acc.frontier++;
+            acc.covered += pcs[kk];
+            const uint64_t d = d1[kk] - d0[kk];
+            if (!a.dead_mode || cnt) {
+                acc.trav += d - dk[kk];
+                acc.deliv += (unsigned long long)pcs[kk] * (d - dg[kk]);
+                acc.undeliv += (unsigned long long)pcs[kk] * (dg[kk] - dk[kk]);
+            }
+        }
+    }
+}
+
+// The row loop shared by both scatters: member j of XCD x takes unit j of each
+// row of the XCD's unit list (gossip_bins.hip); with sync_us the XCD's
+// workgroups finish a row together before the next, so the slot runs they
+// write into a bin stay adjacent in time (and merge in the XCD's L2).  The
+// wait is bounded: placement of workgroups on XCDs and their residency are not
+// guaranteed, and no result depends on it.
+template <class F>
+__device__ __forceinline__ void scatter_rows(const BinArgs& b, F&& unit) {
+    const uint32_t xcd = blockIdx.x & 7, member = blockIdx.x >> 3, members = gridDim.x >> 3;
+    const uint64_t ubase = b.xcd_units[xcd], u1 = b.xcd_units[xcd + 1];
+    const uint64_t n_rows = (u1 - ubase + members - 1) / members;
+    for (uint64_t row = 0; row < n_rows; ++row) {
+        const uint64_t ui = ubase + row * members + member;
+        if (ui < u1) unit(ui);
+        if (b.sync_us) {
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                uint32_t* ctr = b.sync + xcd * kScatterSyncStride;
+                __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t target = (uint32_t)((row + 1) * members);
+                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+                while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target &&
+                       __builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)b.sync_us * 100u)
+                    __builtin_amdgcn_s_sleep(2);
+            }
+            __syncthreads();
+        }
+    }
+}
+
 template <int W, bool COV, int kU>  // kU: cb entries in flight per lane
 __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_lds(RoundArgs a, BinArgs b, uint32_t wd) {
     constexpr int kWaves = kScatterBlock / 64;
-    constexpr int kSliceIt = kBinChunkWords / kScatterBlock;  // slice words per lane
-    static_assert(kBinChunkWords % kScatterBlock == 0, "slice split");
     __shared__ unsigned long long slice[kBinChunkWords];
     // which of the chunk's sources have anything to write: nonzero new words.
     // An idle source leaves its slots alone.  A slot may thus keep a word of
@@ -535,83 +656,12 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_lds(RoundArgs a, 
     }
     Acc acc;
     const int lane = threadIdx.x & 63;
-    const uint32_t xcd = blockIdx.x & 7, member = blockIdx.x >> 3, members = gridDim.x >> 3;
-    const uint64_t u1 = b.xcd_units[xcd + 1];
-    for (uint64_t ui = b.xcd_units[xcd] + member; ui < u1; ui += members) {
+    auto scatter_unit = [&](const uint64_t ui) {
         const BinUnit un = b.units[ui];
-        // global source chunk; words from nw_src (own words at P = 1, the all-gathered ones at P > 1)
-        const uint64_t vb = (uint64_t)un.c * b.chunk, ve = min(vb + b.chunk, a.n_src);  // vb % 64 == 0
-        const uint64_t nwords = (ve - vb) * W;
-        // stage the slice (and the previous round's live bits): every load of
-        // the lane in flight at once
-        const uint64_t n_src = ve - vb;
-        uint64_t r[kSliceIt];
-#pragma unroll
-        for (int k = 0; k < kSliceIt; ++k) {
-            const uint64_t i = threadIdx.x + (uint64_t)k * kScatterBlock;
-            r[k] = i < nwords ? a.nw_src[vb * W + i] : 0ull;
-        }
-        __syncthreads();  // previous unit's readers are done with the slice
-#pragma unroll
-        for (int k = 0; k < kSliceIt; ++k) slice[threadIdx.x + k * kScatterBlock] = r[k];
-        if (threadIdx.x < kBinChunkWords / 64) live_s[threadIdx.x] = b.noskip ? ~0ull : 0ull;
+        if (un.p0 >= un.p1 && !un.first) return;  // padding of a row (block-uniform)
+        scatter_stage<W, COV>(a, b, un, wd, slice, live_s, cov_s, acc);
         __syncthreads();
-        // per source (a wave covers 64 consecutive ones): live bits and, in the
-        // chunk's first unit, the source side of its pushes (broadcastMessage,
-        // peer.cpp:310-316) for the owned sources; row lengths loaded together
-        constexpr int kSrcIt = (kBinChunkWords / W + kScatterBlock - 1) / kScatterBlock;
-        constexpr int kB = 5;  // sources whose row lengths are loaded together (register budget)
-#pragma unroll
-        for (int k0 = 0; k0 < kSrcIt; k0 += kB) {
-            uint32_t pcs[kB];
-#pragma unroll
-            for (int kk = 0; kk < kB; ++kk) {
-                const uint64_t j = threadIdx.x + (uint64_t)(k0 + kk) * kScatterBlock;
-                pcs[kk] = 0;
-                if (k0 + kk >= kSrcIt || j >= ((n_src + 63) & ~63ull)) continue;  // wave-uniform
-                const uint64_t v = vb + j;
-                const bool vv = j < n_src;
-                const bool own = vv && un.first && v >= a.begin && v < a.end;
-                bool nz = false;
-#pragma unroll
-                for (int w = 0; w < W; ++w) {
-                    const uint64_t m = vv ? slice[j * W + w] : 0ull;
-                    nz |= m != 0;
-                    if (!own || !m) continue;
-                    pcs[kk] += (uint32_t)__popcll(m);
-                    if (w < (int)wd) acc.digest += digest_weight(v * wd + w) * m;
-                    if (COV)
-                        for (uint64_t x = m; x; x &= x - 1) atomicAdd(&cov_s[w * 64 + __builtin_ctzll(x)], 1u);
-                }
-                const unsigned long long bits = __ballot(nz);
-                if (lane == 0) live_s[j >> 6] |= bits;
-            }
-            uint64_t d0[kB], d1[kB];
-            uint32_t dg[kB], dk[kB];  // per-source counters (dead mode); else k_src_count books them
-            const bool cnt = a.dead_mode && a.dgone;
-#pragma unroll
-            for (int kk = 0; kk < kB; ++kk) {
-                const uint64_t lv = vb + threadIdx.x + (uint64_t)(k0 + kk) * kScatterBlock - a.begin;
-                d0[kk] = pcs[kk] ? a.rp[lv] : 0ull;
-                d1[kk] = pcs[kk] ? a.rp[lv + 1] : 0ull;
-                dg[kk] = pcs[kk] && cnt ? a.dgone[lv] : 0u;
-                dk[kk] = pcs[kk] && cnt ? a.dmask[lv] : 0u;
-            }
-#pragma unroll
-            for (int kk = 0; kk < kB; ++kk) {
-                if (!pcs[kk]) continue;
-                acc.frontier++;
-                acc.covered += pcs[kk];
-                const uint64_t d = d1[kk] - d0[kk];
-                if (!a.dead_mode || cnt) {
-                    acc.trav += d - dk[kk];
-                    acc.deliv += (unsigned long long)pcs[kk] * (d - dg[kk]);
-                    acc.undeliv += (unsigned long long)pcs[kk] * (dg[kk] - dk[kk]);
-                }
-            }
-        }
-        __syncthreads();
-        if (b.probe == 1) continue;
+        if (b.probe == 1) return;
         // consecutive lanes take consecutive entries: the stores of one
         // instruction fall into a few slot runs (measured at config 4: 37 ms
         // per step against 57 ms with 8 consecutive entries per lane; u16
@@ -630,7 +680,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_lds(RoundArgs a, 
         // positions fit 32 bits (build_bins: fewer than kNoSlot edges)
         constexpr uint32_t step = (uint32_t)kScatterBlock * kU;
         const uint32_t p0 = (uint32_t)un.p0, p1 = (uint32_t)un.p1, nb = (uint32_t)b.n_binned;
-        if (p0 >= p1) continue;  // block-uniform; nb >= 1 below
+        if (p0 >= p1) return;  // block-uniform; nb >= 1 below
         const uint32_t base0 = (p0 & ~63u) + threadIdx.x;
         const uint32_t n_grp = (nb + 63) >> 6;
         const unsigned long long below = (lane == 63 ? ~0ull : ((2ull << lane) - 1)) & ~1ull;  // lanes 1..lane
@@ -668,7 +718,9 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_lds(RoundArgs a, 
 #pragma unroll
             for (int j = 0; j < kU; ++j) {
                 const uint32_t q = p + (uint32_t)j * kScatterBlock;
-                uint64_t* const dst = ((a_ >> j) & 1u) && b.probe != 2 ? b.val + (uint64_t)(r_[j] + q) * W : sink;
+                // probe 3 (timing only, wrong results): entry p stores to val[p], i.e. sequentially
+                const uint64_t slot = b.probe == 3 ? (uint64_t)q : (uint64_t)(r_[j] + q);
+                uint64_t* const dst = ((a_ >> j) & 1u) && b.probe != 2 ? b.val + slot * W : sink;
 #pragma unroll
                 for (int w = 0; w < W; ++w) dst[w] = slice[(uint64_t)u_[j] * W + w];
             }
@@ -692,8 +744,172 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_lds(RoundArgs a, 
             store(p + step, r1, u1, a1);
             if (base + 2 * step >= p1) break;
         }
-    }
+    };
+    scatter_rows(b, scatter_unit);
     flush<kWaves>(acc, a.st);
+    if (COV) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < 64 * W; i += kScatterBlock)
+            if (cov_s[i]) atomicAdd(&a.cov[i], (unsigned long long)cov_s[i]);
+    }
+}
+
+// Producer/consumer scatter (the default; GOSSIP_SCATTER_PC=0 selects
+// k_bin_scatter_lds).  Measured on the single-role kernel: a wave that both
+// loads and stores cannot keep stores in flight -- vmcnt counts loads and
+// stores in issue order, and every wait for a load (the next cb entries)
+// also waited for the stores issued before it (the compiled loop drained to
+// vmcnt(1)-vmcnt(0) every iteration), so each wave had one batch of stores in
+// flight per HBM write latency.  Here the 16 waves split the work:
+//   producers (waves 0-7) load the unit's cb entries and resolve their slots
+//     (cb_grp + a ballot of the run-start flags + cb_run), and hand
+//     {slot, chunk-local source | active} to their consumer through an LDS
+//     ring; they issue only loads, so their waits are exact;
+//   consumers (waves 8-15) read the ring and the staged slice and store --
+//     they issue no global loads, never wait on vmcnt, and keep as many slot
+//     stores in flight as the memory system takes.
+// Producer k and consumer k share a private ring of kPcRing 64-entry slots;
+// each side publishes a counter in LDS (its own wave writes it, after
+// s_waitcnt lgkmcnt(0) on the ring data).  Both sides walk the unit's
+// 64-entry groups g0 + k, g0 + k + 8, ... in the same order, so consecutive
+// groups go out through different consumer waves at about the same time.
+__device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// kPcProd producer waves, the other 16 - kPcProd consume; consumer c serves the
+// producers p = c (mod consumers) in turn.  kPcG: groups a producer resolves per
+// pipeline stage; kPcRing: ring slots (64 entries each) per producer.
+template <int W, bool COV, int kPcProd, int kPcG, int kPcRing>
+__global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_pc(RoundArgs a, BinArgs b, uint32_t wd) {
+    constexpr int kWaves = kScatterBlock / 64;
+    constexpr int kPcCons = kWaves - kPcProd;
+    static_assert(kPcProd % kPcCons == 0, "every consumer serves the same number of producers");
+    static_assert(kPcRing % kPcG == 0, "a stage fills whole ring slots");
+    __shared__ unsigned long long slice[kBinChunkWords];
+    __shared__ unsigned long long live_s[kBinChunkWords / 64 / W];  // the chunk has kBinChunkWords / W sources
+    __shared__ unsigned int cov_s[COV ? 64 * W : 1];
+    // (the final stat reduction reuses the ring: LDS is 160 KB and the slice takes 144 KB)
+    __shared__ __attribute__((aligned(16))) uint32_t ring_slot[kPcProd][kPcRing][64];
+    __shared__ uint16_t ring_src[kPcProd][kPcRing][64];  // chunk-local source | 0x8000 = a slot to write
+    __shared__ uint32_t prod_cnt[kPcProd], cons_cnt[kPcProd];  // groups handed over / taken, per pair
+    if (COV) {
+        for (int i = threadIdx.x; i < 64 * W; i += kScatterBlock) cov_s[i] = 0;
+    }
+    Acc acc;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const bool producer = wave < kPcProd;
+    const int pair = producer ? wave : wave - kPcProd;  // producer index, or the consumer's first producer
+    // hand-over counters: relaxed workgroup-scope atomics on LDS (ds_read / ds_write; a generic
+    // volatile pointer compiles to flat accesses, which wait for vmcnt(0) as well)
+    auto ld_prod = [&](int p) { return __hip_atomic_load(&prod_cnt[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+    auto ld_cons = [&] { return __hip_atomic_load(&cons_cnt[pair], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+    const unsigned long long below = (lane == 63 ? ~0ull : ((2ull << lane) - 1)) & ~1ull;  // lanes 1..lane
+    auto scatter_unit = [&](const uint64_t ui) {
+        const BinUnit un = b.units[ui];
+        if (un.p0 >= un.p1 && !un.first) return;  // padding of a row (block-uniform)
+        scatter_stage<W, COV>(a, b, un, wd, slice, live_s, cov_s, acc);
+        if (threadIdx.x < kPcProd) prod_cnt[threadIdx.x] = cons_cnt[threadIdx.x] = 0;
+        __syncthreads();
+        if (b.probe == 1) return;
+        // positions fit 32 bits (build_bins: fewer than kNoSlot edges)
+        const uint32_t p0 = (uint32_t)un.p0, p1 = (uint32_t)un.p1, nb = (uint32_t)b.n_binned;
+        if (p0 >= p1) return;  // block-uniform; nb >= 1 below
+        const uint32_t g0 = p0 >> 6, n_groups = ((p1 - 1) >> 6) - g0 + 1;
+        // producer p's groups: g0 + p + kPcProd * i, i < items(p)
+        auto items = [&](int p) { return n_groups > (uint32_t)p ? (n_groups - p + kPcProd - 1) / kPcProd : 0u; };
+        const uint32_t n_items = items(pair);
+        if (producer) {
+            const uint32_t n_grp = (nb + 63) >> 6;
+            // three register sets: loads of stage j+2 | run resolution of j+1 | hand-over of j
+            uint32_t sv[3][kPcG], gr[3][kPcG], rv[3][kPcG], uu[3][kPcG];
+            auto load = [&](int set, uint32_t j) {  // stage j = items j*kPcG .. j*kPcG + kPcG - 1
+#pragma unroll
+                for (int t = 0; t < kPcG; ++t) {
+                    const uint32_t i = j * kPcG + t;
+                    const uint32_t g = min(g0 + pair + kPcProd * i, n_grp - 1);  // clamped past the end
+                    const uint32_t q = g * 64 + lane;
+                    sv[set][t] = (uint32_t)__builtin_nontemporal_load(b.cb_src + min(q, nb - 1));
+                    gr[set][t] = b.cb_grp[g];
+                }
+            };
+            auto resolve = [&](int set, uint32_t j) {
+#pragma unroll
+                for (int t = 0; t < kPcG; ++t) {
+                    const uint32_t i = j * kPcG + t;
+                    const uint32_t g = g0 + pair + kPcProd * i;
+                    const uint32_t q = g * 64 + lane;
+                    const uint32_t v = i < n_items && q < nb ? sv[set][t] : 0u;  // past the end: no run starts
+                    const uint32_t u = v & (kRunStart - 1u);
+                    const uint32_t live = (uint32_t)(live_s[u >> 6] >> (u & 63)) & 1u;
+                    const uint32_t act = (uint32_t)(i < n_items) & (uint32_t)(q >= p0) & (uint32_t)(q < p1) & live;
+                    uu[set][t] = u | (act << 15);
+                    const unsigned long long starts = __ballot((v & kRunStart) != 0);
+                    const uint32_t run = gr[set][t] + (uint32_t)__popcll(starts & below);
+                    rv[set][t] = q + b.cb_run[min(run, (uint32_t)b.n_runs_m1)];  // the slot
+                }
+            };
+            auto hand_over = [&](int set, uint32_t j) {
+                const uint32_t i0 = j * kPcG;
+                if (i0 >= n_items) return;  // wave-uniform
+                while (i0 + kPcG - ld_cons() > (uint32_t)kPcRing) __builtin_amdgcn_s_sleep(2);  // ring full
+                asm volatile("" ::: "memory");
+#pragma unroll
+                for (int t = 0; t < kPcG; ++t) {
+                    const uint32_t i = i0 + t;
+                    ring_slot[pair][i % kPcRing][lane] = rv[set][t];
+                    ring_src[pair][i % kPcRing][lane] = (uint16_t)uu[set][t];
+                }
+                lds_wait();
+                if (lane == 0)
+                    __hip_atomic_store(&prod_cnt[pair], min(i0 + kPcG, n_items), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+            };
+            const uint32_t n_stages = (n_items + kPcG - 1) / kPcG;
+            load(0, 0);
+            load(1, 1);
+            resolve(0, 0);
+            for (uint32_t j = 0; j < n_stages; j += 3) {  // sets rotate 0,1,2 with no register copies
+                load(2, j + 2);
+                resolve(1, j + 1);
+                hand_over(0, j);
+                if (j + 1 >= n_stages) break;
+                load(0, j + 3);
+                resolve(2, j + 2);
+                hand_over(1, j + 1);
+                if (j + 2 >= n_stages) break;
+                load(1, j + 4);
+                resolve(0, j + 3);
+                hand_over(2, j + 2);
+            }
+        } else {
+            const uint32_t n_max = items(pair);  // the first producer served has the most items
+            for (uint32_t i = 0; i < n_max; ++i) {
+                for (int pp = pair; pp < kPcProd; pp += kPcCons) {
+                    if (i >= items(pp)) break;  // wave-uniform; later producers have no more items either
+                    while (ld_prod(pp) <= i) __builtin_amdgcn_s_sleep(2);  // not handed over yet
+                    asm volatile("" ::: "memory");                        // the ring reads stay behind the poll
+                    const uint32_t slot = ring_slot[pp][i % kPcRing][lane];
+                    const uint32_t su = ring_src[pp][i % kPcRing][lane];
+                    uint64_t x[W];
+#pragma unroll
+                    for (int w = 0; w < W; ++w) x[w] = slice[(uint64_t)(su & (kRunStart - 1u)) * W + w];
+                    lds_wait();
+                    if (lane == 0)  // the ring slot is free again
+                        __hip_atomic_store(&cons_cnt[pp], i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    const bool act = (su & kRunStart) && b.probe != 2;
+                    if (act) {
+                        const uint64_t at = b.probe == 3 ? (uint64_t)((g0 + pp + kPcProd * i) * 64 + lane) : slot;
+#pragma unroll
+                        for (int w = 0; w < W; ++w) b.val[at * W + w] = x[w];
+                    }
+                    acc.gathered += (su & kRunStart) ? 1u : 0u;  // slots written (byte accounting)
+                }
+            }
+        }
+    };
+    scatter_rows(b, scatter_unit);
+    static_assert(sizeof(ring_slot) >= kWaves * kStatFields * 8, "stat scratch fits the ring");
+    __syncthreads();  // the ring is idle
+    flush_into<kWaves>(acc, a.st, reinterpret_cast<unsigned long long (*)[kStatFields]>(&ring_slot[0][0][0]));
     if (COV) {
         __syncthreads();
         for (int i = threadIdx.x; i < 64 * W; i += kScatterBlock)
@@ -1668,8 +1884,36 @@ static int scatter_u() {
     return u;
 }
 
+// producer/consumer scatter (default) or the single-role one (GOSSIP_SCATTER_PC=0)
+// (GOSSIP_SCATTER_PC: 0 single-role kernel; 1 = 8 producers resolving 2 groups per stage
+// into 4-slot rings (the default; measured best); 2 = 12 producers, 2 groups, 2 slots;
+// 4 = 8 producers, 4 groups, 4 slots)
+static int scatter_pc() {
+    static const int pc = [] {
+        const char* e = getenv("GOSSIP_SCATTER_PC");
+        return e ? atoi(e) : 1;
+    }();
+    return pc;
+}
+
 hipError_t launch_bin_scatter(const RoundArgs& a, const BinArgs& b, uint32_t W_, hipStream_t s) {
     const uint32_t wd = wd_of(W_);
+    if (const int v = scatter_pc()) {
+#define GOSSIP_PC(P, G, R)                                                                                 \
+        do {                                                                                               \
+            if (a.cov) hipLaunchKernelGGL((k_bin_scatter_pc<W, true, P, G, R>), dim3(kScatterGrid),          \
+                                          dim3(kScatterBlock), 0, s, a, b, wd);                            \
+            else hipLaunchKernelGGL((k_bin_scatter_pc<W, false, P, G, R>), dim3(kScatterGrid),               \
+                                    dim3(kScatterBlock), 0, s, a, b, wd);                                  \
+        } while (0)
+        GOSSIP_DISPATCH_W(wp_of(W_), {
+            if (v == 2) GOSSIP_PC(12, 2, 2);
+            else if (v == 4) GOSSIP_PC(8, 4, 4);
+            else GOSSIP_PC(8, 2, 4);
+        });
+#undef GOSSIP_PC
+        return hipGetLastError();
+    }
     GOSSIP_DISPATCH_W(wp_of(W_), {  // one workgroup per CU (128 KB of LDS each)
         if (a.cov)
             hipLaunchKernelGGL((k_bin_scatter_lds<W, true, 4>), dim3(kScatterGrid), dim3(kScatterBlock), 0, s, a, b, wd);

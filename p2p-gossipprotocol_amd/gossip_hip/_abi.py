@@ -21,6 +21,8 @@ GOSSIP_EHIP = -3
 GOSSIP_ESTATE = -4
 GOSSIP_ENODEV = -5
 GOSSIP_EOVERFLOW = -6
+GOSSIP_ECOMM = -7
+COMM_ID_BYTES = 128
 
 GRAPH_POWERLAW = 1
 GRAPH_REF_BOOTSTRAP = 2
@@ -33,6 +35,7 @@ MODE_AUTO = -1
 MODE_PUSH = 0
 MODE_PULL = 1
 MODE_PUSH_SPARSE = 2
+MODE_BIN = 3
 
 
 class GossipConfig(C.Structure):
@@ -133,6 +136,23 @@ def lib() -> C.CDLL:
         "gossip_enable_timing": (i32, [P, i32]),
         "gossip_kernel_time": (i32, [P, C.c_char_p, C.POINTER(C.c_double), pu64]),
         "gossip_kernel_bytes": (i32, [P, C.c_char_p, C.POINTER(C.c_double)]),
+        # library-driven multi-GPU rounds (gossip_dist.hip)
+        "gossip_partition": (i32, [u64, u32, pu64]),
+        "gossip_comm_unique_id": (i32, [pu8]),
+        "gossip_comm_init": (i32, [P, pu8, u32, u32]),
+        "gossip_comm_finalize": (i32, [P, C.POINTER(RoundStats), u32, C.POINTER(DeadReport), u64, pu64]),
+        "gossip_comm_modes": (i32, [P, C.POINTER(C.c_int32), u32, pu32]),
+        "gossip_group_create": (i32, [C.POINTER(GossipConfig), u32, C.POINTER(C.c_int32), C.POINTER(P)]),
+        "gossip_group_destroy": (None, [P]),
+        "gossip_group_part": (i32, [P, u32, C.POINTER(P)]),
+        "gossip_group_build_graph": (i32, [P]),
+        "gossip_group_inject": (i32, [P, pu32, pu32, u32]),
+        "gossip_group_schedule_kills": (i32, [P, pu32, pu32, u32]),
+        "gossip_group_reset": (i32, [P]),
+        "gossip_group_step": (i32, [P, C.POINTER(RoundStats)]),
+        "gossip_group_run": (i32, [P, C.POINTER(RoundStats), u32, pu32]),
+        "gossip_group_read_seen": (i32, [P, pu64]),
+        "gossip_group_read_reports": (i32, [P, C.POINTER(DeadReport), u64, pu64]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(L, name)

@@ -28,43 +28,63 @@ def _ptr(a: np.ndarray, ctype):
     return a.ctypes.data_as(C.POINTER(ctype))
 
 
+def comm_unique_id() -> bytes:
+    """A fresh RCCL unique id (rank 0 makes it; the others receive it out of band)."""
+    buf = (C.c_uint8 * _abi.COMM_ID_BYTES)()
+    check(_abi.lib().gossip_comm_unique_id(buf), "gossip_comm_unique_id")
+    return bytes(buf)
+
+
+def partition(n_peers: int, world: int) -> list[int]:
+    """The library's vertex blocks: begins[world+1] (ceil(n/world) peers each)."""
+    out = np.zeros(world + 1, dtype=np.uint64)
+    check(_abi.lib().gossip_partition(n_peers, world, _ptr(out, C.c_uint64)), "gossip_partition")
+    return [int(x) for x in out]
+
+
 def pick_origins(n_peers: int, rng_seed: int, count: int) -> np.ndarray:
     out = np.zeros(max(count, 1), dtype=np.uint32)
     check(_abi.lib().gossip_pick_origins(n_peers, rng_seed, count, _ptr(out, C.c_uint32)), "gossip_pick_origins")
     return out[:count]
 
 
+def make_config(n_peers: int, n_msgs: int, *, rng_seed: int = 0, graph: str = "powerlaw", list_len: int = 6,
+                n_seeds: int = 20, churn_threshold: int = 0, ping_every: int = 0, max_missed: int = 3,
+                max_rounds: int = 4096, min_rounds: int = 0, device: int = -1, coverage_history: bool = False,
+                part: tuple[int, int] = (0, 0), report_capacity: int = 0, mode: str = "auto",
+                pull_permille: int = 0, front_permille: int = 0, bin_permille: int = 0, bins: bool = True,
+                extra_cap: int = 0, list_cap: int = 0, rejoin_threshold: int = 0) -> GossipConfig:
+    """gossip_config from keyword arguments (the fields of include/gossip/gossip.h)."""
+    cfg = GossipConfig()
+    cfg.n_peers = n_peers
+    cfg.part_begin, cfg.part_end = part
+    cfg.n_msgs = n_msgs
+    cfg.rng_seed = rng_seed
+    cfg.graph_model = _GRAPHS[graph]
+    cfg.list_len = list_len
+    cfg.n_seeds = n_seeds
+    cfg.churn_threshold = churn_threshold
+    cfg.ping_every = ping_every
+    cfg.max_missed = max_missed
+    cfg.max_rounds = max_rounds
+    cfg.min_rounds = min_rounds
+    cfg.device = device
+    cfg.flags = (_abi.FLAG_COVERAGE_HISTORY if coverage_history else 0) | (0 if bins else _abi.FLAG_NO_BIN) | {
+        "auto": 0, "push": _abi.FLAG_FORCE_PUSH, "pull": _abi.FLAG_FORCE_PULL, "bin": _abi.FLAG_FORCE_BIN}[mode]
+    cfg.report_capacity = report_capacity
+    cfg.pull_permille = pull_permille
+    cfg.front_permille = front_permille
+    cfg.bin_permille = bin_permille
+    cfg.extra_cap = extra_cap
+    cfg.list_cap = list_cap
+    cfg.rejoin_threshold = rejoin_threshold
+    return cfg
+
+
 class Engine:
-    def __init__(self, n_peers: int, n_msgs: int, *, rng_seed: int = 0, graph: str = "powerlaw", list_len: int = 6,
-                 n_seeds: int = 20, churn_threshold: int = 0, ping_every: int = 0, max_missed: int = 3,
-                 max_rounds: int = 4096, min_rounds: int = 0, device: int = -1, coverage_history: bool = False,
-                 part: tuple[int, int] = (0, 0), report_capacity: int = 0, mode: str = "auto",
-                 pull_permille: int = 0, front_permille: int = 0, bin_permille: int = 0, bins: bool = True,
-                 extra_cap: int = 0, list_cap: int = 0, rejoin_threshold: int = 0):
+    def __init__(self, n_peers: int, n_msgs: int, *, part: tuple[int, int] = (0, 0), **kw):
         self._L = _abi.lib()
-        cfg = GossipConfig()
-        cfg.n_peers = n_peers
-        cfg.part_begin, cfg.part_end = part
-        cfg.n_msgs = n_msgs
-        cfg.rng_seed = rng_seed
-        cfg.graph_model = _GRAPHS[graph]
-        cfg.list_len = list_len
-        cfg.n_seeds = n_seeds
-        cfg.churn_threshold = churn_threshold
-        cfg.ping_every = ping_every
-        cfg.max_missed = max_missed
-        cfg.max_rounds = max_rounds
-        cfg.min_rounds = min_rounds
-        cfg.device = device
-        cfg.flags = (_abi.FLAG_COVERAGE_HISTORY if coverage_history else 0) | (0 if bins else _abi.FLAG_NO_BIN) | {
-            "auto": 0, "push": _abi.FLAG_FORCE_PUSH, "pull": _abi.FLAG_FORCE_PULL, "bin": _abi.FLAG_FORCE_BIN}[mode]
-        cfg.report_capacity = report_capacity
-        cfg.pull_permille = pull_permille
-        cfg.front_permille = front_permille
-        cfg.bin_permille = bin_permille
-        cfg.extra_cap = extra_cap
-        cfg.list_cap = list_cap
-        cfg.rejoin_threshold = rejoin_threshold
+        cfg = make_config(n_peers, n_msgs, part=part, **kw)
         self.cfg = cfg
         ctx = C.c_void_p()
         check(self._L.gossip_create(C.byref(cfg), C.byref(ctx)), "gossip_create")
@@ -203,6 +223,36 @@ class Engine:
         check(self._L.gossip_round_commit(self._ctx, global_new_receipts, C.byref(fin)), "gossip_round_commit")
         return bool(fin.value)
 
+    # library-driven multi-GPU rounds (RCCL inside libgossip_hip)
+    def comm_init(self, unique_id: bytes, world: int, rank: int) -> None:
+        """Join the library's RCCL communicator as `rank` of `world` (collective);
+        afterwards step()/run() issue every round's collectives themselves."""
+        buf = (C.c_uint8 * _abi.COMM_ID_BYTES).from_buffer_copy(unique_id)
+        check(self._L.gossip_comm_init(self._ctx, buf, world, rank), "gossip_comm_init")
+
+    def comm_finalize(self, rounds: list[dict]) -> np.ndarray:
+        """Collective: every rank's dead-node reports (sorted) and the global
+        seed_removals of each round (filled into `rounds`)."""
+        buf = (RoundStats * max(len(rounds), 1))()
+        for i, r in enumerate(rounds):
+            for f, _ in RoundStats._fields_:
+                setattr(buf[i], f, r[f])
+        cnt = C.c_uint64()
+        check(self._L.gossip_comm_finalize(self._ctx, buf, len(rounds), None, 0, C.byref(cnt)), "gossip_comm_finalize")
+        reps = np.zeros((max(cnt.value, 1), 3), dtype=np.uint32)
+        check(self._L.gossip_comm_finalize(self._ctx, buf, len(rounds), reps.ctypes.data_as(C.POINTER(DeadReport)),
+                                           cnt.value, C.byref(cnt)), "gossip_comm_finalize")
+        for i, r in enumerate(rounds):
+            r["seed_removals"] = int(buf[i].seed_removals)
+        return reps[: cnt.value]
+
+    def comm_modes(self) -> list[int]:
+        n = C.c_uint32()
+        check(self._L.gossip_comm_modes(self._ctx, None, 0, C.byref(n)), "gossip_comm_modes")
+        out = (C.c_int32 * max(n.value, 1))()
+        check(self._L.gossip_comm_modes(self._ctx, out, n.value, C.byref(n)), "gossip_comm_modes")
+        return list(out)[: n.value]
+
     # -- results ----------------------------------------------------------------
     def read_seen(self) -> np.ndarray:
         s = self.shape()
@@ -254,3 +304,86 @@ class Engine:
         b = C.c_double()
         check(self._L.gossip_kernel_bytes(self._ctx, name.encode(), C.byref(b)), "gossip_kernel_bytes")
         return b.value
+
+
+class Group:
+    """One process driving several vertex blocks (gossip_group_*): one part
+    per entry of `devices` (distinct GPUs: RCCL communicators from
+    ncclCommInitAll; all the same GPU: device-copy exchange).  Takes the
+    Engine's keyword arguments (except part/device)."""
+
+    def __init__(self, n_peers: int, n_msgs: int, devices, **kw):
+        self._L = _abi.lib()
+        cfg = make_config(n_peers, n_msgs, **kw)
+        devs = (C.c_int32 * len(devices))(*devices)
+        g = C.c_void_p()
+        check(self._L.gossip_group_create(C.byref(cfg), len(devices), devs, C.byref(g)), "gossip_group_create")
+        self._g = g
+        self.n_peers, self.n_msgs = n_peers, n_msgs
+        self.W = (n_msgs + 63) // 64
+        self.n_parts = len(devices)
+
+    def close(self) -> None:
+        if getattr(self, "_g", None) and self._g.value:
+            self._L.gossip_group_destroy(self._g)
+            self._g = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def build_graph(self) -> None:
+        check(self._L.gossip_group_build_graph(self._g), "gossip_group_build_graph")
+
+    def inject(self, origin, inject_round) -> None:
+        o, r = _u32(origin), _u32(inject_round)
+        check(self._L.gossip_group_inject(self._g, _ptr(o, C.c_uint32), _ptr(r, C.c_uint32), o.size),
+              "gossip_group_inject")
+
+    def schedule_kills(self, peers, rounds) -> None:
+        p, r = _u32(peers), _u32(rounds)
+        n = p.size
+        if n == 0:
+            p = r = np.zeros(1, dtype=np.uint32)
+        check(self._L.gossip_group_schedule_kills(self._g, _ptr(p, C.c_uint32), _ptr(r, C.c_uint32), n),
+              "gossip_group_schedule_kills")
+
+    def reset(self) -> None:
+        check(self._L.gossip_group_reset(self._g), "gossip_group_reset")
+
+    def step(self) -> tuple[dict, bool]:
+        st = RoundStats()
+        rc = check(self._L.gossip_group_step(self._g, C.byref(st)), "gossip_group_step")
+        return st.as_dict(), rc == 1
+
+    def run(self, cap: int = 4096) -> list[dict]:
+        buf = (RoundStats * cap)()
+        rounds = C.c_uint32()
+        check(self._L.gossip_group_run(self._g, buf, cap, C.byref(rounds)), "gossip_group_run")
+        return [buf[i].as_dict() for i in range(min(rounds.value, cap))]
+
+    def read_seen(self) -> np.ndarray:
+        out = np.zeros((self.n_peers, self.W), dtype=np.uint64)
+        check(self._L.gossip_group_read_seen(self._g, _ptr(out, C.c_uint64)), "gossip_group_read_seen")
+        return out
+
+    def reports(self) -> np.ndarray:
+        cnt = C.c_uint64()
+        check(self._L.gossip_group_read_reports(self._g, None, 0, C.byref(cnt)), "gossip_group_read_reports")
+        buf = np.zeros((max(cnt.value, 1), 3), dtype=np.uint32)
+        check(self._L.gossip_group_read_reports(self._g, buf.ctypes.data_as(C.POINTER(DeadReport)), cnt.value,
+                                                C.byref(cnt)), "gossip_group_read_reports")
+        return buf[: cnt.value]
+
+    def part_ctx(self, p: int) -> C.c_void_p:
+        ctx = C.c_void_p()
+        check(self._L.gossip_group_part(self._g, p, C.byref(ctx)), "gossip_group_part")
+        return ctx

@@ -18,7 +18,10 @@ import numpy as np
 
 from ._abi import PKG_ROOT
 
-BINARY = PKG_ROOT / "build" / "gossip_loopback"
+import os  # noqa: E402
+
+# (GOSSIP_LOOPBACK_BIN: another build of the harness, e.g. the sanitizer build of tests/sanitize/)
+BINARY = Path(os.environ.get("GOSSIP_LOOPBACK_BIN", PKG_ROOT / "build" / "gossip_loopback"))
 
 
 def msg_numbers(origins: np.ndarray) -> np.ndarray:

@@ -147,6 +147,36 @@ class Oracle:
                              n_started=self.started_under_cap(w.n, w.list_cap) if w.graph == "ref_bootstrap" else 0,
                              rejoin_threshold=w.rejoin_threshold)
 
+    def time_rounds(self, w, rp, col, threads=8, variant=0, repeats=5, max_rounds=4096):
+        """CPU baseline: wall seconds of oracle_sim_run alone (the rounds; create,
+        schedule and every read-back untimed), `repeats` fresh sims.  Returns
+        (list of seconds, per-round stats of the last run)."""
+        import time
+        rp = np.ascontiguousarray(rp, dtype=np.uint64)
+        col = np.ascontiguousarray(col if len(col) else np.zeros(1), dtype=np.uint32)
+        cfg = OCfg(w.n, w.n_msgs, w.rng_seed, w.churn_threshold, w.ping_every, w.max_missed, max_rounds,
+                   w.min_rounds, threads, variant, w.extra_cap, w.list_len,
+                   self.started_under_cap(w.n, w.list_cap) if w.graph == "ref_bootstrap" else 0, w.rejoin_threshold)
+        o = np.ascontiguousarray(w.origins, dtype=np.uint32)
+        r = np.ascontiguousarray(w.inject_rounds, dtype=np.uint32)
+        kp = np.array([k[0] for k in w.kills] + [0], dtype=np.uint32)
+        kr = np.array([k[1] for k in w.kills] + [0], dtype=np.uint32)
+        secs, stats = [], []
+        for _ in range(repeats):
+            s = C.c_void_p(self.L.oracle_sim_create(C.byref(cfg), _p(rp, C.c_uint64), _p(col, C.c_uint32)))
+            assert s.value, "oracle_sim_create failed"
+            try:
+                assert self.L.oracle_sim_schedule(s, _p(o, C.c_uint32), _p(r, C.c_uint32), C.c_uint32(len(w.kills)),
+                                                  _p(kp, C.c_uint32), _p(kr, C.c_uint32)) == 0
+                buf = (OStats * max_rounds)()
+                t0 = time.perf_counter()
+                nr = self.L.oracle_sim_run(s, buf, C.c_uint32(max_rounds))
+                secs.append(time.perf_counter() - t0)
+                stats = [buf[i].as_dict() for i in range(nr)]
+            finally:
+                self.L.oracle_sim_destroy(s)
+        return secs, stats
+
     def started_under_cap(self, n, list_cap):
         return int(self.L.oracle_started_under_cap(C.c_uint64(n), C.c_uint32(list_cap)))
 

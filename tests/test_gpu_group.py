@@ -1,0 +1,84 @@
+"""Library-driven multi-GPU rounds (gossip_dist.hip, RCCL inside
+libgossip_hip) against the single-partition oracle run -- the partitioned
+run must be bit-exact (P-invariance).
+
+On one GPU: a group of P parts on the same device exchanges by device copies
+(the C++ driver's schedule, the remote staging / record compaction /
+remote-apply kernels and the report merge); a one-part group on device 0
+(ncclCommInitAll) and an Engine joined with gossip_comm_init at world 1
+(ncclCommInitRank) run the real RCCL calls (all-gather, send/recv all-to-all,
+all-reduce, report all-gather)."""
+import numpy as np
+import pytest
+
+from gossip_hip import Engine, Group, comm_unique_id, partition
+from gossip_hip.workloads import config
+
+pytestmark = pytest.mark.gpu
+
+
+def _run_group(w, devices, **kw):
+    with Group(w.n, w.n_msgs, devices, **w.engine_kwargs(), **kw) as g:
+        g.build_graph()
+        g.inject(w.origins, w.inject_rounds)
+        if w.kills:
+            g.schedule_kills([k[0] for k in w.kills], [k[1] for k in w.kills])
+        g.reset()
+        stats = g.run()
+        seen, reps = g.read_seen(), g.reports()
+        g.reset()
+        again = g.run()
+    return stats, seen, reps, again
+
+
+@pytest.mark.parametrize("P", [2, 3, 4])
+@pytest.mark.parametrize("idx,n", [(2, 1 << 15), (3, 100_000), (5, 1 << 15)])
+def test_group_on_one_device_equals_oracle(oracle, idx, n, P):
+    w = config(idx, n, pick=oracle.pick_origins)
+    rp, col = oracle.gen_workload(w)
+    ref = oracle.simulate_workload(w, rp, col)
+    stats, seen, reps, again = _run_group(w, [0] * P)
+    assert stats == ref["stats"]
+    assert np.array_equal(seen, ref["seen"])
+    assert np.array_equal(reps, ref["reports"])
+    assert again == stats
+
+
+@pytest.mark.parametrize("idx,n", [(2, 1 << 15), (5, 1 << 15)])
+def test_group_one_part_rccl_equals_oracle(oracle, idx, n):
+    """ncclCommInitAll over device 0: every collective of the driver through RCCL."""
+    w = config(idx, n, pick=oracle.pick_origins)
+    rp, col = oracle.gen_workload(w)
+    ref = oracle.simulate_workload(w, rp, col)
+    stats, seen, reps, again = _run_group(w, [0])
+    assert stats == ref["stats"]
+    assert np.array_equal(seen, ref["seen"])
+    assert np.array_equal(reps, ref["reports"])
+
+
+@pytest.mark.parametrize("idx,n", [(3, 1 << 16), (5, 1 << 15)])
+def test_comm_init_world1_equals_oracle(oracle, idx, n):
+    """One process per GPU path (bench --gpus N): ncclCommInitRank at world 1,
+    gossip_run issuing the collectives, gossip_comm_finalize gathering reports."""
+    w = config(idx, n, pick=oracle.pick_origins)
+    rp, col = oracle.gen_workload(w)
+    ref = oracle.simulate_workload(w, rp, col)
+    part = partition(w.n, 1)
+    with Engine(w.n, w.n_msgs, part=(part[0], part[1]), **w.engine_kwargs()) as e:
+        e.build_graph()
+        e.inject(w.origins, w.inject_rounds)
+        e.comm_init(comm_unique_id(), 1, 0)
+        e.reset()
+        stats = e.run()
+        reps = e.comm_finalize(stats)
+        modes = e.comm_modes()
+        assert stats == ref["stats"]
+        assert np.array_equal(e.read_seen(), ref["seen"])
+        assert np.array_equal(reps, ref["reports"])
+        assert len(modes) == len(stats)
+
+
+def test_group_rejects_mixed_devices():
+    from gossip_hip import GossipError
+    with pytest.raises(GossipError):
+        Group(1 << 12, 64, [0, 0, 1])
