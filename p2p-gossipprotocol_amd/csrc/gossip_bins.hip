@@ -197,7 +197,6 @@ void free_bins(BinState* b) {
     hipFree(b->bdst);
     hipFree(b->val);
     hipFree(b->dummy);
-    hipFree(b->sync);
     *b = BinState{};
 }
 
@@ -396,8 +395,9 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
     // of about the mean; the list is padded to rows of kScatterGrid / 8 units,
     // member j of the XCD takes unit j of every row, so the workgroups of a
     // row stage consecutive chunks and write adjacent slot runs in every bin
-    // at about the same time (merged into whole lines in the XCD's L2; the
-    // kernel's row barrier keeps them together).  GOSSIP_BIN_UNIT = cap
+    // at about the same time (adjacent runs can merge in the XCD's L2; with
+    // the single-role scatter 36.0 against 39.2 ms per step for capped units
+    // dealt round-robin).  GOSSIP_BIN_UNIT = cap
     // restores capped units dealt round-robin with no padding (the round-1
     // layout, A/B only).
     {
@@ -442,8 +442,6 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
             xu[8] = units.size();
         }
         st.n_units = units.size();
-        BCHECK(hipMalloc((void**)&st.sync, 8 * kScatterSyncStride * sizeof(uint32_t)));
-        BCHECK(hipMemset(st.sync, 0, 8 * kScatterSyncStride * sizeof(uint32_t)));
         BCHECK(hipMalloc((void**)&st.units, units.size() * sizeof(BinUnit)));
         BCHECK(hipMemcpy(st.units, units.data(), units.size() * sizeof(BinUnit), hipMemcpyHostToDevice));
         BCHECK(hipMalloc((void**)&st.xcd_units, 9 * sizeof(uint64_t)));

@@ -147,7 +147,8 @@ struct gossip_ctx {
     bool bins_first = false;             // no binned round since the last reset: rewrite every slot
     bool bin_noskip = false;     // GOSSIP_BIN_NOSKIP: rewrite every slot each binned round (A/B measurement)
     uint32_t scatter_probe = 0;  // GOSSIP_SCATTER_PROBE: partial scatter for timing breakdowns (wrong results)
-    uint32_t scatter_sync_us = kScatterSyncUs;  // GOSSIP_SCATTER_SYNC: scatter row-barrier spin bound (0 = off)
+    uint32_t bin_front_pm = 100;  // binned rounds need a frontier of >= this per-mille (GOSSIP_BIN_FRONT_PM)
+    bool heavy_exit = true;       // k_pull_heavy early exit (GOSSIP_HEAVY_EXIT=0: off, A/B)
     bool full_liveness = false;  // GOSSIP_FULL_LIVENESS: ping every edge each ping round (A/B against closed form)
     uint64_t* seg = nullptr;     // sparse push: per-destination record segments (world x chunk records)
     unsigned long long* d_counts = nullptr;  // records per destination rank
@@ -363,6 +364,7 @@ RoundArgs make_args(gossip_ctx* c) {
     a.ex_cnt = c->ex_cnt;
     a.ex_miss = c->ex_miss;
     a.ex_cap = c->cfg.extra_cap;
+    a.heavy_exit = c->heavy_exit ? 1u : 0u;
     a.death_r = c->death_r;
     a.dgone = c->dgone;
     a.dmask = c->dmask;
@@ -656,7 +658,8 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
             const uint64_t missing = total > have ? total - have : 0;
             const uint32_t bpm = c->cfg.bin_permille ? c->cfg.bin_permille : 4000;
             // and only on a wide frontier: a narrow one is cheaper to gather from (frontier bitmap)
-            bin = missing * 1000 >= c->n_local * (uint64_t)bpm && (c->frontier_est + cnt) * 10 >= c->n_local;
+            bin = missing * 1000 >= c->n_local * (uint64_t)bpm &&
+                  (c->frontier_est + cnt) * 1000 >= c->n_local * (uint64_t)c->bin_front_pm;
         }
     }
     c->cur_sparse = !pull && remote && requested == GOSSIP_MODE_PUSH_SPARSE && c->seg != nullptr;
@@ -719,9 +722,7 @@ gossip_status round_compute(gossip_ctx* c) {
         BinArgs b{c->bins.bins,     c->bins.n_bins,    c->bins.cb_src,  c->bins.cb_run,    c->bins.cb_grp,
                   c->bins.n_binned, c->bins.chunk_begin, c->bins.n_chunks, c->bins.chunk,    c->bins.units,
                   c->bins.xcd_units, c->bins.bdst,     c->bins.val,     c->bins.bin_words, c->bins.dummy,   c->bin_noskip || c->bins_first,
-                  c->scatter_probe,  c->bins.n_runs ? c->bins.n_runs - 1 : 0, c->bins.sync,
-                  c->scatter_sync_us};
-        if (b.sync_us) HIPCHK(hipMemsetAsync(c->bins.sync, 0, 8 * kScatterSyncStride * sizeof(uint32_t), c->stream));
+                  c->scatter_probe,  c->bins.n_runs ? c->bins.n_runs - 1 : 0};
         HIPCHK(timed(c, "bin_scatter", [&] { return launch_bin_scatter(a, b, pw, c->stream); }));
         HIPCHK(timed(c, "bin_apply", [&] { return launch_bin_apply(a, b, pw, c->stream); }));
         c->bins_first = false;
@@ -887,7 +888,8 @@ gossip_status gossip_create(const gossip_config* cfg, gossip_ctx** out) {
     if (const char* h = std::getenv("GOSSIP_HEAVY_DEGREE")) c->heavy = (uint32_t)std::max(1, std::atoi(h));
     if (const char* u = std::getenv("GOSSIP_BIN_NOSKIP"); u && std::atoi(u)) c->bin_noskip = true;
     if (const char* u = std::getenv("GOSSIP_SCATTER_PROBE")) c->scatter_probe = (uint32_t)std::atoi(u);
-    if (const char* u = std::getenv("GOSSIP_SCATTER_SYNC")) c->scatter_sync_us = (uint32_t)std::atoi(u);
+    if (const char* u = std::getenv("GOSSIP_BIN_FRONT_PM")) c->bin_front_pm = (uint32_t)std::atoi(u);
+    if (const char* u = std::getenv("GOSSIP_HEAVY_EXIT")) c->heavy_exit = std::atoi(u) != 0;
     if (const char* u = std::getenv("GOSSIP_FULL_LIVENESS"); u && std::atoi(u)) c->full_liveness = true;
     if (const char* b = std::getenv("GOSSIP_BIN_PERMILLE"); b && !cfg->bin_permille) c->cfg.bin_permille = (uint32_t)std::atoi(b);
     c->n = cfg->n_peers;

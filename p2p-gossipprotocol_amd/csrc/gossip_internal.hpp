@@ -16,6 +16,7 @@ constexpr int kBlock = 256;                    // 4 waves of 64
 constexpr int kMaxWords = 8;                   // M <= 512 concurrent messages
 constexpr int kStatLines = 64;                 // striped DevStats lines per round (summed at read)
 constexpr int kPullNT = 0x100;                 // launch_pull_light unroll flag: non-temporal streamed accesses
+constexpr uint32_t kHeavyExitEvery = 4;        // k_pull_heavy checks its early exit every 4 batches of 64 edges
 
 // Per-round device counters (all integer; order-independent sums).
 struct DevStats {
@@ -75,12 +76,7 @@ struct BinArgs {
     uint32_t probe;               // measurement only (GOSSIP_SCATTER_PROBE=1: staging only, 2: slot stores to the
                                   // sink; results are then wrong)
     uint64_t n_runs_m1;           // cb_run entries - 1 (clamp for the run index of past-the-end lanes)
-    uint32_t* sync;               // kScatterSyncStride words per XCD: units finished (zeroed before each scatter)
-    uint32_t sync_us;             // row barrier between the XCD's workgroups, spin bound in us (0 = none).
-                                  // Speed only: no result depends on it, and every wait is bounded
 };
-constexpr int kScatterSyncStride = 32;  // one 128-B line per XCD counter
-constexpr uint32_t kScatterSyncUs = 50;  // default spin bound of the scatter row barrier
 
 struct BinState {
     Bin* bins = nullptr;
@@ -100,7 +96,6 @@ struct BinState {
     uint32_t bin_words = kBinWords;
     uint64_t n_slots = 0;   // padded
     uint64_t n_binned = 0;  // edges with a slot (light destinations)
-    uint32_t* sync = nullptr;  // 8 * kScatterSyncStride words (scatter row barrier)
 };
 
 struct DeadReport {
@@ -144,7 +139,7 @@ struct RoundArgs {
     uint32_t* ex_cnt;              // n_local
     uint8_t* ex_miss;              // n_local * ex_cap
     uint32_t ex_cap;
-    uint32_t pad1;
+    uint32_t heavy_exit;           // k_pull_heavy stops a chunk once it holds every needed bit
     // single-partition symmetric overlays without rejoin (DESIGN.md section 6,
     // "closed-form liveness"): per-peer death round and per-source edge counters
     uint16_t* death_r;             // n_local: round of death, 0xFFFF = alive (null: not kept)
