@@ -37,8 +37,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", type=int, default=4, help="BASELINE.json config index (1-5)")
     ap.add_argument("--n", type=int, default=0, help="override peer count")
-    ap.add_argument("--cpu-sample-n", type=int, default=1 << 25, help="CPU baseline sample size (all threads)")
-    ap.add_argument("--cpu-sample-n1", type=int, default=1 << 21, help="CPU baseline sample size (1 thread)")
+    ap.add_argument("--cpu-sample-n", type=int, default=0, help="CPU baseline sample size, all threads (0: per config)")
+    ap.add_argument("--cpu-sample-n1", type=int, default=0, help="CPU baseline sample size, 1 thread (0: per config)")
     ap.add_argument("--cpu-repeats", type=int, default=5)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -54,21 +54,26 @@ def parse():
 
 
 # kernel timer name -> rocprofv3 kernel-name prefix in the PMC summary
-PMC_KERNELS = {"bin_scatter": "k_bin_scatter_lds", "bin_apply": "k_bin_apply", "pull_light": "k_pull_light",
+PMC_KERNELS = {"bin_scatter": "k_bin_scatter_pc", "bin_apply": "k_bin_apply", "pull_light": "k_pull_light",
                "push_light": "k_push_light", "push_heavy": "k_push_heavy", "pull_heavy": "k_pull_heavy"}
 
 
 def pmc_traffic(workload: str, kernel: str, alg_bytes_per_launch: float, n_local: int):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
-    (FETCH_SIZE and WRITE_SIZE, separate runs of this same command) with the
+    (FETCH_SIZE and WRITE_SIZE, separate runs of this bench command on the same
+    config: tools/gpu_profile_r02.sh, newest round first) with the
     gfx950 corrections measured by tools/calib_fetch.hip (profiles/r01/
     calib_fetch_timing.log): FETCH_SIZE counts 1/2 of coalesced streamed bytes
     and one 64-B line per random 8-B gather; WRITE_SIZE counts stores 1:1.
     bin_scatter / bin_apply read only coalesced streams (traffic = 2 x fetch +
     write); pull_light mixes streams with random gathers (only its streamed
     reads are doubled)."""
-    path = REPO / "profiles" / "r01" / "config4_pmc_summary.json"
-    if not workload.startswith("config4") or not path.exists() or kernel not in PMC_KERNELS:
+    if kernel not in PMC_KERNELS:
+        return None, None
+    cfg = workload.split("_")[0]  # "config4" ...
+    cands = [REPO / "profiles" / r / f"{cfg}_pmc_summary.json" for r in ("r02", "r01")]
+    path = next((p for p in cands if p.exists()), None)
+    if path is None:
         return None, None
     prof = json.loads(path.read_text())
     keys = [k for k in prof["kernels"] if k.startswith(PMC_KERNELS[kernel] + "<") or k == PMC_KERNELS[kernel]]
@@ -109,12 +114,19 @@ def _cpu_model() -> str:
     return "unknown"
 
 
+# CPU baseline samples per BASELINE.json config: (all-threads n, 1-thread n, literal-driver n or 0)
+CPU_SAMPLES = {1: (8, 8, 8), 2: (1 << 20, 1 << 18, 1 << 18), 3: (1 << 24, 1 << 20, 0), 4: (1 << 25, 1 << 21, 0),
+               5: (1 << 22, 1 << 19, 0)}
+
+
 def cpu_baseline(args, cfg_idx: int) -> dict:
     """The oracle's 64-bit-mask round driver (gcc -O3 -fopenmp; the restatement
     of peer.cpp:255-318 that the GPU is checked against) on bounded samples of
     the same workload, timed on this host: oracle_sim_run only (the rounds;
     overlay generation, sim allocation and read-backs untimed), median of
-    --cpu-repeats fresh runs, at the host's thread budget and at 1 thread."""
+    --cpu-repeats fresh runs, at the host's thread budget and at 1 thread.
+    Configs 1-2 also time the literal driver (per-peer Message-List hash sets
+    with sentTo counts, peer.hpp:23-26,52), single-threaded."""
     import statistics
     sys.path.insert(0, str(REPO / "tests"))
     import oracle_ref  # noqa: E402  (checker / baseline only)
@@ -124,28 +136,37 @@ def cpu_baseline(args, cfg_idx: int) -> dict:
     orc = oracle_ref.Oracle(so)
     nproc = os.cpu_count() or 1
     threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", 0) or nproc)
-    idx = cfg_idx if cfg_idx != 1 else 3
+    n_all, n_one, n_lit = CPU_SAMPLES[cfg_idx]
+    n_all = args.cpu_sample_n or n_all
+    n_one = args.cpu_sample_n1 or n_one
     out = {}
-    for label, n, th in (("all", args.cpu_sample_n, threads), ("one", args.cpu_sample_n1, 1)):
-        w = config(idx, n, pick=orc.pick_origins)
+    legs = [("all", n_all, threads, 0, args.cpu_repeats), ("one", n_one, 1, 0, args.cpu_repeats)]
+    if n_lit:
+        legs.append(("literal", n_lit, 1, 1, 1 if n_lit > 4096 else args.cpu_repeats))
+    for label, n, th, variant, reps in legs:
+        w = config(cfg_idx, n, pick=orc.pick_origins)
         rp, col = orc.gen_workload(w, threads=threads)
-        secs, stats = orc.time_rounds(w, rp, col, threads=th, repeats=args.cpu_repeats)
+        secs, stats = orc.time_rounds(w, rp, col, threads=th, variant=variant, repeats=reps)
         med = statistics.median(secs)
         d = sum(s["deliveries"] for s in stats)
         t = sum(s["traversals"] for s in stats)
-        out[label] = {"gteps": d / med / 1e9, "traversal_gteps": t / med / 1e9, "n": n, "edges": int(len(col)),
-                      "rounds": len(stats), "median_s": med, "runs_s": [round(x, 3) for x in secs], "threads": th}
+        out[label] = {"gteps": d / med / 1e9, "traversal_gteps": t / med / 1e9, "n": w.n, "edges": int(len(col)),
+                      "rounds": len(stats), "median_s": med, "runs_s": [round(x, 4) for x in secs], "threads": th,
+                      "sample": f"{w.name} at n={w.n} ({len(col)} edges, {len(stats)} rounds)"}
     a, o = out["all"], out["one"]
-    return {"value": round(a["gteps"], 4), "unit": "GTEPS", "cores": threads, "kind": "port",
-            "traversal_gteps": round(a["traversal_gteps"], 4),
-            "single_thread": {"value": round(o["gteps"], 4), "traversal_gteps": round(o["traversal_gteps"], 4),
-                              "median_s": round(o["median_s"], 3), "runs_s": o["runs_s"],
-                              "sample": f"n=2^{o['n'].bit_length() - 1}, {o['edges']} edges, {o['rounds']} rounds"},
-            "nproc": nproc, "cpu_model": _cpu_model(), "median_s": round(a["median_s"], 3), "runs_s": a["runs_s"],
-            "timed": "oracle_sim_run only (rounds); generation, allocation and read-backs excluded",
-            "sample": f"{config(idx, 1024).name} workload at n=2^{a['n'].bit_length() - 1} ({a['n']} peers, "
-                      f"{a['edges']} edges, {a['rounds']} rounds), oracle fast driver, {threads} threads of {nproc} "
-                      f"visible CPUs, median of {args.cpu_repeats}"}
+    res = {"value": round(a["gteps"], 4), "unit": "GTEPS", "cores": threads, "kind": "port",
+           "traversal_gteps": round(a["traversal_gteps"], 4),
+           "single_thread": {"value": round(o["gteps"], 4), "traversal_gteps": round(o["traversal_gteps"], 4),
+                             "median_s": round(o["median_s"], 4), "runs_s": o["runs_s"], "sample": o["sample"]},
+           "nproc": nproc, "cpu_model": _cpu_model(), "median_s": round(a["median_s"], 4), "runs_s": a["runs_s"],
+           "timed": "oracle_sim_run only (rounds); generation, allocation and read-backs excluded",
+           "sample": f"{a['sample']}, oracle fast driver, {threads} threads of {nproc} visible CPUs, "
+                     f"median of {args.cpu_repeats}"}
+    if "literal" in out:
+        lt = out["literal"]
+        res["literal_driver"] = {"value": round(lt["gteps"], 6), "median_s": round(lt["median_s"], 4),
+                                 "runs_s": lt["runs_s"], "threads": 1, "sample": lt["sample"]}
+    return res
 
 
 def per_round_profile(eng) -> list[dict]:

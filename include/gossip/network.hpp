@@ -37,13 +37,17 @@ struct SimOptions {
     uint32_t min_rounds = 0;
     std::vector<std::pair<uint32_t, uint32_t>> kills;  // (peer, round): "Ctrl+C" (README.md:6)
     int device = -1;
+    // vertex partitions (gossip_group_*: one per GPU 0..n_gpus-1, RCCL collectives inside the library;
+    // when fewer GPUs are visible, every part on `device` with device-copy exchange).  Traced
+    // networks (<= kTraceMax peers) keep one partition: their per-peer views read the whole overlay.
+    uint32_t n_gpus = 1;
     std::string log_dir;                  // reference-format logs (small networks)
     std::vector<std::pair<std::string, int>> addresses;  // optional ip:port per peer (default: peer_address())
 
     // Reference keys (ping_interval, message_interval, max_messages,
     // max_missed_pings) plus simulation keys: n_peers, rng_seed, graph,
     // list_len, origins, churn_ppm, max_rounds, min_rounds, kills=p@r,...,
-    // device, log_dir.
+    // device, n_gpus, log_dir.
     static SimOptions fromConfig(const NetworkConfig& cfg);
 };
 
@@ -74,7 +78,8 @@ public:
     std::vector<gossip_dead_report> reports() const;
     std::vector<SeedNode*> seeds();
     std::shared_ptr<PeerNode> peer(uint64_t id);
-    gossip_ctx* ctx() const { return ctx_; }
+    gossip_ctx* ctx() const { return ctx_; }        // single partition (null when partitioned)
+    gossip_group* group() const { return group_; }  // partitioned (n_gpus > 1)
 
     // traced views (size() <= kTraceMax)
     bool traced() const { return trace_; }
@@ -90,6 +95,7 @@ private:
     SimOptions opt_;
     uint32_t M_ = 0, W_ = 0;
     gossip_ctx* ctx_ = nullptr;
+    gossip_group* group_ = nullptr;
     bool started_ = false, finished_ = false, trace_ = false;
     std::atomic<bool> stop_{false};
     std::vector<uint32_t> origin_, injectRound_;
@@ -106,4 +112,5 @@ private:
     std::vector<int32_t> deathRound_;          // per peer
 
     void captureRound(uint32_t r);
+    void seedRemovalsFromReports();  // partitioned runs: each round's removals from the merged reports
 };

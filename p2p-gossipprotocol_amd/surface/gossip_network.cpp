@@ -48,6 +48,7 @@ SimOptions SimOptions::fromConfig(const NetworkConfig& c) {
     o.min_rounds = (uint32_t)c.getInt("min_rounds", 0);
     o.kills = parse_kills(c.getString("kills", ""));
     o.device = (int)c.getInt("device", -1);
+    o.n_gpus = (uint32_t)std::max<long long>(1, c.getInt("n_gpus", 1));
     o.log_dir = c.getString("log_dir", "");
     return o;
 }
@@ -60,6 +61,7 @@ GossipNetwork::GossipNetwork(const NetworkConfig& cfg, SimOptions opt) : opt_(st
 
 GossipNetwork::~GossipNetwork() {
     if (ctx_) gossip_destroy(ctx_);
+    if (group_) gossip_group_destroy(group_);
 }
 
 PeerInfo GossipNetwork::peerInfo(uint64_t id) const {
@@ -113,8 +115,22 @@ bool GossipNetwork::start() {
     cfg.max_rounds = opt_.max_rounds;
     cfg.min_rounds = opt_.min_rounds;
     cfg.device = opt_.device;
-    gossip_status st = gossip_create(&cfg, &ctx_);
-    if (st == GOSSIP_OK) st = gossip_build_graph(ctx_);
+    trace_ = n <= kTraceMax;
+    const uint32_t parts = trace_ ? 1u : std::max<uint32_t>(1, opt_.n_gpus);
+    gossip_status st = GOSSIP_OK;
+    if (parts > 1) {
+        std::vector<int32_t> devs(parts);
+        for (uint32_t p = 0; p < parts; ++p) devs[p] = (int32_t)p;
+        st = gossip_group_create(&cfg, parts, devs.data(), &group_);
+        if (st != GOSSIP_OK) {  // fewer GPUs than parts: all parts on one device, exchanged by device copies
+            std::fill(devs.begin(), devs.end(), (int32_t)std::max(opt_.device, 0));
+            st = gossip_group_create(&cfg, parts, devs.data(), &group_);
+        }
+        if (st == GOSSIP_OK) st = gossip_group_build_graph(group_);
+    } else {
+        st = gossip_create(&cfg, &ctx_);
+        if (st == GOSSIP_OK) st = gossip_build_graph(ctx_);
+    }
     // messageGenerationLoop (peer.cpp:357-379): origin o's k-th message at round k * message_every
     std::vector<uint32_t> origins(n_origins);
     if (st == GOSSIP_OK) {
@@ -129,16 +145,19 @@ bool GossipNetwork::start() {
             origin_[oi * opt_.messages_per_origin + k] = origins[oi];
             injectRound_[oi * opt_.messages_per_origin + k] = k * opt_.message_every;
         }
-    if (st == GOSSIP_OK) st = gossip_inject(ctx_, origin_.data(), injectRound_.data(), M_);
+    if (st == GOSSIP_OK)
+        st = group_ ? gossip_group_inject(group_, origin_.data(), injectRound_.data(), M_)
+                    : gossip_inject(ctx_, origin_.data(), injectRound_.data(), M_);
     if (st == GOSSIP_OK && !opt_.kills.empty()) {
         std::vector<uint32_t> kp, kr;
         for (const auto& k : opt_.kills) {
             kp.push_back(k.first);
             kr.push_back(k.second);
         }
-        st = gossip_schedule_kills(ctx_, kp.data(), kr.data(), (uint32_t)kp.size());
+        st = group_ ? gossip_group_schedule_kills(group_, kp.data(), kr.data(), (uint32_t)kp.size())
+                    : gossip_schedule_kills(ctx_, kp.data(), kr.data(), (uint32_t)kp.size());
     }
-    if (st == GOSSIP_OK) st = gossip_reset(ctx_);
+    if (st == GOSSIP_OK) st = group_ ? gossip_group_reset(group_) : gossip_reset(ctx_);
     if (st != GOSSIP_OK) {
         std::cerr << "Error starting gossip network: " << gossip_strerror(st) << ": " << gossip_last_error() << std::endl;
         return false;
@@ -150,7 +169,6 @@ bool GossipNetwork::start() {
         seedNodes_.back()->setClock(gossip::kEpochSeconds);
         seedNodes_.back()->start();
     }
-    trace_ = n <= kTraceMax;
     if (trace_) {
         const size_t q = std::min(seedNodes_.size(), seedNodes_.size() / 2 + 1);
         for (uint64_t i = 0; i < n; ++i) {
@@ -216,7 +234,7 @@ int GossipNetwork::step() {
     if (!started_ && !start()) return GOSSIP_ESTATE;
     if (finished_) return 1;
     gossip_round_stats st{};
-    const int rc = gossip_step(ctx_, &st);
+    const int rc = group_ ? gossip_group_step(group_, &st) : gossip_step(ctx_, &st);
     if (rc < 0) {
         std::cerr << "Error in gossip round: " << gossip_strerror(rc) << ": " << gossip_last_error() << std::endl;
         return rc;
@@ -232,16 +250,41 @@ bool GossipNetwork::run() {
     while (!finished_ && !stop_) {
         if (step() < 0) return false;
     }
+    if (finished_ && group_) seedRemovalsFromReports();
     if (finished_ && !opt_.log_dir.empty() && trace_) writeLogs(opt_.log_dir);
     return true;
 }
 
 std::vector<gossip_dead_report> GossipNetwork::reports() const {
     uint64_t count = 0;
+    if (group_) {
+        if (gossip_group_read_reports(group_, nullptr, 0, &count) != GOSSIP_OK || count == 0) return {};
+        std::vector<gossip_dead_report> out(count);
+        gossip_group_read_reports(group_, out.data(), count, &count);
+        return out;
+    }
     if (!ctx_ || gossip_read_reports(ctx_, nullptr, 0, &count) != GOSSIP_OK || count == 0) return {};
     std::vector<gossip_dead_report> out(count);
     gossip_read_reports(ctx_, out.data(), count, &count);
     return out;
+}
+
+// The registry drops a peer on its first report (SeedNode::handleDeadNode,
+// seed.cpp:158-167): a partitioned run's per-round stats get their seed
+// removals from the merged report list.
+void GossipNetwork::seedRemovalsFromReports() {
+    std::map<uint32_t, uint32_t> first;  // dead peer -> round of its first report
+    for (const gossip_dead_report& r : reports()) {
+        auto it = first.find(r.dead);
+        if (it == first.end() || r.round < it->second) first[r.dead] = r.round;
+    }
+    for (gossip_round_stats& st : rounds_) st.seed_removals = 0;
+    for (const auto& kv : first)
+        for (gossip_round_stats& st : rounds_)
+            if (st.round == kv.second) {
+                st.seed_removals++;
+                break;
+            }
 }
 
 std::vector<SeedNode*> GossipNetwork::seeds() {

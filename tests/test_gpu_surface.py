@@ -49,3 +49,27 @@ def test_cli_reference_run(oracle, tmp_path):
     assert s0.count("Received dead node notification for: 127.0.0.1:5003") == 4
     assert s0.count("Removed dead peer: 127.0.0.1:5003") == 1
     assert "Registered new peer" not in (logs / "seed_8019_output.txt").read_text()  # quorum reached at seed 10
+
+
+@pytest.mark.parametrize("n_gpus", [1, 2, 3])
+def test_cli_partitioned_network(oracle, tmp_path, n_gpus):
+    """network.txt with n_gpus: the drop-in CLI runs the overlay vertex-partitioned
+    through the library's own multi-GPU driver (gossip_group_*; on a one-GPU box
+    every part sits on device 0 and the parts exchange by device copies) -- the
+    rounds equal the single-partition oracle's."""
+    from gossip_hip.workloads import CHURN_1PCT
+    cfg = tmp_path / "network.txt"
+    cfg.write_text((REPO / "tests" / "golden" / "network.txt").read_text() +
+                   f"n_peers=20000\ngraph=powerlaw\norigins=6\nrng_seed=0x5EED0002\nn_gpus={n_gpus}\n"
+                   f"churn_ppm=10000\nping_interval=13\nmin_rounds=40\n")
+    r = subprocess.run([str(EXE), str(cfg)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    rounds = [json.loads(l) for l in r.stdout.splitlines() if l.startswith('{"round"')]
+    import dataclasses
+    w = config(2, 20000, pick=oracle.pick_origins)
+    w = dataclasses.replace(w, churn_threshold=CHURN_1PCT, ping_every=15, min_rounds=40)  # churn_ppm=10000
+    rp, col = oracle.gen_workload(w)
+    ref = oracle.simulate_workload(w, rp, col)
+    assert [(x["round"], x["frontier"], x["deliveries"], x["new_receipts"], x["died"], x["reports"], x["covered"])
+            for x in rounds] == [(s["round"], s["frontier"], s["deliveries"], s["new_receipts"], s["died"],
+                                  s["reports"], s["covered"]) for s in ref["stats"]]
