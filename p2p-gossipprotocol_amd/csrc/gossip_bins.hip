@@ -147,11 +147,37 @@ __global__ void k_run_flags(const uint32_t* cb_slot, uint64_t n_binned, uint16_t
 
 // ids: inclusive prefix sum of the flags (run of entry p = ids[p] - 1)
 __global__ void k_run_fill(const uint32_t* cb_slot, const uint32_t* flag, const uint32_t* ids, uint64_t n_binned,
-                           uint32_t* cb_run, uint32_t* cb_grp) {
+                           uint32_t* cb_run, uint32_t* cb_grp, uint32_t* run_start) {
     for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n_binned;
          p += (uint64_t)gridDim.x * blockDim.x) {
-        if (flag[p]) cb_run[ids[p] - 1] = cb_slot[p] - (uint32_t)p;
+        if (flag[p]) {
+            cb_run[ids[p] - 1] = cb_slot[p] - (uint32_t)p;
+            run_start[ids[p] - 1] = cb_slot[p];
+        }
         if ((p & 63) == 0) cb_grp[p >> 6] = ids[p] - 1;
+    }
+}
+
+// (d) the apply side of the streamed layout (val in cb order): the runs in
+// slot order (ap_start sorted, ap_run = slot - position as cb_run), the first
+// slot of each run flagged in bdst, and per 64-slot group the number of runs
+// that start before it.  The value of slot q of run r sits at q - ap_run[r].
+__global__ void k_ap_flags(const uint32_t* ap_start, uint64_t n_runs, uint16_t* bdst) {
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n_runs; r += (uint64_t)gridDim.x * blockDim.x)
+        bdst[ap_start[r]] |= kRunStart;
+}
+
+__global__ void k_ap_grp(const uint32_t* ap_start, uint64_t n_runs, uint64_t n_groups, uint32_t* ap_grp) {
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n_groups;
+         g += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t want = g * 64;
+        uint64_t lo = 0, hi = n_runs;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) / 2;
+            if (ap_start[mid] < want) lo = mid + 1;
+            else hi = mid;
+        }
+        ap_grp[g] = (uint32_t)lo;
     }
 }
 
@@ -191,6 +217,8 @@ void free_bins(BinState* b) {
     hipFree(b->cb_src);
     hipFree(b->cb_run);
     hipFree(b->cb_grp);
+    hipFree(b->ap_run);
+    hipFree(b->ap_grp);
     hipFree(b->chunk_begin);
     hipFree(b->units);
     hipFree(b->xcd_units);
@@ -201,7 +229,7 @@ void free_bins(BinState* b) {
 }
 
 hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local, uint64_t n_global, uint64_t m,
-                      uint32_t heavy, uint32_t Wp, hipStream_t s, BinState* out, std::string* err) {
+                      uint32_t heavy, uint32_t Wp, bool stream, hipStream_t s, BinState* out, std::string* err) {
     hipError_t rc = hipSuccess;
     const uint64_t n_tiles = (n_local + 63) / 64;
     // bigger bins -> longer slot runs per (source chunk, bin) in the scatter
@@ -316,10 +344,11 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
     st.n_binned = upos;
     st.n_chunks = n_chunks;
     st.chunk = chunk;
-    BCHECK(hipMalloc((void**)&st.bdst, (slots + kBinSlotPad) * sizeof(uint16_t)));
-    BCHECK(hipMalloc((void**)&st.val, (slots + kBinSlotPad) * Wp * sizeof(uint64_t)));
-    BCHECK(hipMemsetAsync(st.bdst, 0, (slots + kBinSlotPad) * sizeof(uint16_t), s));
-    BCHECK(hipMemsetAsync(st.val, 0, (slots + kBinSlotPad) * Wp * sizeof(uint64_t), s));
+    // (+64: the apply reads whole 64-slot groups; val is indexed by slot or, streamed, by cb position)
+    BCHECK(hipMalloc((void**)&st.bdst, (slots + 64) * sizeof(uint16_t)));
+    BCHECK(hipMalloc((void**)&st.val, (slots + 64) * Wp * sizeof(uint64_t)));
+    BCHECK(hipMemsetAsync(st.bdst, 0, (slots + 64) * sizeof(uint16_t), s));
+    BCHECK(hipMemsetAsync(st.val, 0, (slots + 64) * Wp * sizeof(uint64_t), s));
     BCHECK(hipMalloc((void**)&st.dummy, (uint64_t)kScatterGrid * kScatterBlock * Wp * sizeof(uint64_t)));
     hipLaunchKernelGGL(k_bin_assign, dim3(gridn(m)), dim3(256), 0, s, keys64_out, vals_out, m, st.bins,
                        (uint32_t)st.n_bins, row, st.bdst);
@@ -347,7 +376,7 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
     keys_in = vals_in = nullptr;
     temp = nullptr;
     BCHECK(hipMalloc((void**)&cb_slot, (upos + 1) * sizeof(uint32_t)));
-    BCHECK(hipMalloc((void**)&st.cb_src, (upos + 1) * sizeof(uint16_t)));
+    BCHECK(hipMalloc((void**)&st.cb_src, (upos + 16) * sizeof(uint16_t)));  // k_bin_stream reads aligned 8-entry blocks
     BCHECK(hipMalloc((void**)&st.chunk_begin, (n_chunks + 1) * sizeof(uint64_t)));
     hipLaunchKernelGGL(k_cb_fill, dim3(gridn(upos)), dim3(256), 0, s, vals_out, upos, keys64_out, st.bins,
                        (uint32_t)chunk, cb_slot, st.cb_src);
@@ -377,14 +406,42 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
         st.n_runs = n_runs;
         BCHECK(hipMalloc((void**)&st.cb_run, ((uint64_t)n_runs + 1) * sizeof(uint32_t)));
         BCHECK(hipMalloc((void**)&st.cb_grp, ((upos + 63) / 64 + 1) * sizeof(uint32_t)));
+        // run starts (slot of each run's first entry) in cb_slot's place once it is consumed: keys_in
+        BCHECK(hipMalloc((void**)&keys_in, ((uint64_t)n_runs + 1) * sizeof(uint32_t)));
         if (upos) {
             hipLaunchKernelGGL(k_run_fill, dim3(gridn(upos)), dim3(256), 0, s, cb_slot, keys_out, vals_out, upos,
-                               st.cb_run, st.cb_grp);
+                               st.cb_run, st.cb_grp, keys_in);
             BCHECK(hipGetLastError());
         }
         BCHECK(hipStreamSynchronize(s));
         hipFree(cb_slot);
         cb_slot = nullptr;
+        // (d) apply side of the streamed layout: runs sorted by first slot (keys_out / vals_out are free again)
+        const uint64_t n_groups = (slots + 63) / 64 + 1;
+        if (!stream) goto no_stream;
+        BCHECK(hipMalloc((void**)&st.ap_run, ((uint64_t)n_runs + 1) * sizeof(uint32_t)));
+        BCHECK(hipMalloc((void**)&st.ap_grp, n_groups * sizeof(uint32_t)));
+        if (n_runs) {
+            int end_bit3 = 1;
+            while (end_bit3 < 32 && (1ull << end_bit3) <= slots) ++end_bit3;
+            temp_bytes = 0;
+            BCHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, keys_in, keys_out, st.cb_run, st.ap_run,
+                                                      (size_t)n_runs, 0, end_bit3, s));
+            BCHECK(hipMalloc(&temp, temp_bytes + 16));
+            BCHECK(hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys_in, keys_out, st.cb_run, st.ap_run,
+                                                      (size_t)n_runs, 0, end_bit3, s));
+            hipLaunchKernelGGL(k_ap_flags, dim3(gridn(n_runs)), dim3(256), 0, s, keys_out, (uint64_t)n_runs, st.bdst);
+            BCHECK(hipGetLastError());
+        }
+        hipLaunchKernelGGL(k_ap_grp, dim3(gridn(n_groups)), dim3(256), 0, s, keys_out, (uint64_t)n_runs, n_groups,
+                           st.ap_grp);
+        BCHECK(hipGetLastError());
+        BCHECK(hipStreamSynchronize(s));
+        hipFree(temp);
+        temp = nullptr;
+    no_stream:
+        hipFree(keys_in);
+        keys_in = nullptr;
     }
 
     // scatter work units (every chunk has at least one: its first unit books

@@ -149,6 +149,12 @@ struct gossip_ctx {
     uint32_t scatter_probe = 0;  // GOSSIP_SCATTER_PROBE: partial scatter for timing breakdowns (wrong results)
     uint32_t bin_front_pm = 100;  // binned rounds need a frontier of >= this per-mille (GOSSIP_BIN_FRONT_PM)
     bool heavy_exit = true;       // k_pull_heavy early exit (GOSSIP_HEAVY_EXIT=0: off, A/B)
+    bool bin_stream = false;      // streamed binned layout (GOSSIP_BIN_STREAM=1; A/B: 1-1.5 ms per binned
+                                  // round slower at config 4)
+    uint32_t defer_pm = 0;        // push rounds with a frontier of >= this per-mille defer the seen update
+                                  // (GOSSIP_DEFER_PM; 0: never -- measured slower at config 4, A/B only)
+    bool pull_diag = false;       // GOSSIP_PULL_DIAG: count the gathers of an early-exit row scan (measurement)
+    bool cur_defer = false;       // this round defers: advance() folds nx into seen
     bool full_liveness = false;  // GOSSIP_FULL_LIVENESS: ping every edge each ping round (A/B against closed form)
     uint64_t* seg = nullptr;     // sparse push: per-destination record segments (world x chunk records)
     unsigned long long* d_counts = nullptr;  // records per destination rank
@@ -365,6 +371,7 @@ RoundArgs make_args(gossip_ctx* c) {
     a.ex_miss = c->ex_miss;
     a.ex_cap = c->cfg.extra_cap;
     a.heavy_exit = c->heavy_exit ? 1u : 0u;
+    a.defer = c->cur_defer ? 1u : 0u;
     a.death_r = c->death_r;
     a.dgone = c->dgone;
     a.dmask = c->dmask;
@@ -492,7 +499,7 @@ gossip_status prepare_bins(gossip_ctx* c) {
     if (!c->symmetric || (c->cfg.flags & GOSSIP_FLAG_NO_BIN) || !c->n_edges) return GOSSIP_OK;
     std::string err;
     const hipError_t e =
-        build_bins(c->rp, c->col, c->n_local, c->n, c->n_edges, c->heavy, c->Wp, c->stream, &c->bins, &err);
+        build_bins(c->rp, c->col, c->n_local, c->n, c->n_edges, c->heavy, c->Wp, c->bin_stream, c->stream, &c->bins, &err);
     if (e == hipErrorOutOfMemory || e == hipErrorInvalidValue) return GOSSIP_OK;  // dense rounds gather instead
     if (e != hipSuccess) return fail(GOSSIP_EHIP, "bin layout: " + err);
     c->bins_ready = true;
@@ -663,6 +670,11 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
         }
     }
     c->cur_sparse = !pull && remote && requested == GOSSIP_MODE_PUSH_SPARSE && c->seg != nullptr;
+    // a wide push round (the explosion before the dense rounds) is bound by memory-side atomics, two per
+    // fresh delivery (seen, then nx); deferring the seen update halves them for one streamed pass
+    // (k_commit_nx).  A per-rank choice: results do not depend on it.
+    c->cur_defer = !pull && c->defer_pm && (c->frontier_est + cnt) * 1000 >= c->n_local * (uint64_t)c->defer_pm;
+    a.defer = c->cur_defer ? 1u : 0u;
     c->last_pull = pull;
     c->last_bin = bin;
     c->last_front = false;
@@ -722,7 +734,8 @@ gossip_status round_compute(gossip_ctx* c) {
         BinArgs b{c->bins.bins,     c->bins.n_bins,    c->bins.cb_src,  c->bins.cb_run,    c->bins.cb_grp,
                   c->bins.n_binned, c->bins.chunk_begin, c->bins.n_chunks, c->bins.chunk,    c->bins.units,
                   c->bins.xcd_units, c->bins.bdst,     c->bins.val,     c->bins.bin_words, c->bins.dummy,   c->bin_noskip || c->bins_first,
-                  c->scatter_probe,  c->bins.n_runs ? c->bins.n_runs - 1 : 0};
+                  c->scatter_probe,  c->bins.n_runs ? c->bins.n_runs - 1 : 0, c->bins.ap_run, c->bins.ap_grp,
+                  c->bin_stream ? 1u : 0u};
         HIPCHK(timed(c, "bin_scatter", [&] { return launch_bin_scatter(a, b, pw, c->stream); }));
         HIPCHK(timed(c, "bin_apply", [&] { return launch_bin_apply(a, b, pw, c->stream); }));
         c->bins_first = false;
@@ -731,6 +744,7 @@ gossip_status round_compute(gossip_ctx* c) {
     }
     if (c->last_pull) {
         if (a.front) HIPCHK(timed(c, "frontier_bits", [&] { return launch_frontier_bits(a, pw, c->stream); }));
+        if (c->pull_diag) HIPCHK(launch_pull_diag(a, pw, c->stream));
         // nx is written whole by pull_light; heavy rows are OR-ed in afterwards
         HIPCHK(timed(c, "pull_light", [&] { return launch_pull_light(a, pw, c->pull_unroll, c->stream); }));
         HIPCHK(timed(c, "pull_heavy", [&] { return launch_pull_heavy(a, pw, c->stream); }));
@@ -774,9 +788,13 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
             // slices of every source chunk + row bounds of the frontier + the run-encoded cb list (2 B per
             // binned edge, 4 B per run, 4 B per 64 entries) + slot writes
             const double n_src = c->gather ? (double)c->n : (double)c->n_local;
-            const double cb = 2.0 * c->bins.n_binned + 4.0 * c->bins.n_runs + 4.0 * ((c->bins.n_binned + 63) / 64);
+            // the run tables (4 B per run + 4 B per 64 entries or slots): the scatter's in slot order,
+            // the apply's when streamed
+            const double runs = 4.0 * c->bins.n_runs + 4.0 * ((c->bins.n_binned + 63) / 64);
+            const double cb = 2.0 * c->bins.n_binned + (c->bin_stream ? 0.0 : runs);
             c->kbytes["bin_scatter"] += wb * n_src + 16.0 * d.frontier + cb + wb * (double)d.pull_gathers;
-            c->kbytes["bin_apply"] += (2.0 + wb) * (double)d.pull_edges + 2.0 * wb * c->n_local;
+            c->kbytes["bin_apply"] += (2.0 + wb) * (double)d.pull_edges + 2.0 * wb * c->n_local +
+                                      (c->bin_stream && d.pull_edges ? runs : 0.0);
             c->kbytes["pull_heavy"] += 12.0 * (double)d.heavy_traversals;
         }
         if (c->last_pull && c->cur.dead_mode) c->kbytes["src_count"] += 32.0 * d.frontier + 4.125 * (double)d.traversals;
@@ -791,6 +809,16 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
             c->kbytes["push_heavy"] += 20.0 * (double)d.heavy_traversals;
         }
         c->kbytes["liveness"] += 6.125 * (double)d.live_checked;
+        // counters (not bytes): device-scope atomics on peer state, traversals by row class
+        c->kbytes["#atomics"] += (double)d.atomics;
+        c->kbytes["#heavy_trav"] += (double)d.heavy_traversals;
+        c->kbytes["#trav"] += (double)d.traversals;
+        if (c->last_pull && !c->last_bin) {  // pull rounds: edges whose row still wanted something, gathers issued
+            c->kbytes["#pulled"] += (double)d.pull_edges;
+            c->kbytes["#gathers"] += (double)d.pull_gathers;
+            c->kbytes["#needy_rows"] += (double)(d.diag & 0xFFFFFFFFull);
+            c->kbytes["#exit_gathers"] += (double)(d.diag >> 32);
+        }
     }
     gossip_round_stats s{};
     s.round = c->round;
@@ -820,7 +848,11 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
     return GOSSIP_OK;
 }
 
-void advance(gossip_ctx* c, uint64_t fresh_global) {
+gossip_status advance(gossip_ctx* c, uint64_t fresh_global) {
+    if (c->cur_defer) {  // every delivery of the round is in nx (remote applies included): fold it into seen
+        HIPCHK(timed(c, "commit", [&] { return launch_commit_nx(c->seen, c->nx, c->n_local * c->Wp, c->stream); }));
+        c->cur_defer = false;
+    }
     std::swap(c->nw, c->nx);  // push: nw was cleared by push_light; pull: the old nw is stale
     c->tcur ^= 1;             // push with marks: every activation marked its tile; otherwise no marks
     c->tact_ok = !c->last_pull && c->tact_marked;
@@ -830,6 +862,7 @@ void advance(gossip_ctx* c, uint64_t fresh_global) {
     const bool pending = c->has_schedule && c->last_inject_round > r;
     if ((fresh_global == 0 && !pending && c->round >= c->cfg.min_rounds) || c->round >= c->cfg.max_rounds)
         c->finished = true;
+    return GOSSIP_OK;
 }
 
 }  // namespace
@@ -885,11 +918,16 @@ gossip_status gossip_create(const gossip_config* cfg, gossip_ctx** out) {
     c->device = dev;
     if (const char* u = std::getenv("GOSSIP_PULL_UNROLL")) c->pull_unroll = std::atoi(u);
     if (const char* u = std::getenv("GOSSIP_PULL_NT"); u && std::atoi(u)) c->pull_unroll |= kPullNT;
+    if (const char* u = std::getenv("GOSSIP_PULL_ROWS"); !u || std::atoi(u)) c->pull_unroll |= kPullRows;
+    if (const char* u = std::getenv("GOSSIP_ROW_B")) c->pull_unroll |= (std::atoi(u) & 7) << 12;
     if (const char* h = std::getenv("GOSSIP_HEAVY_DEGREE")) c->heavy = (uint32_t)std::max(1, std::atoi(h));
     if (const char* u = std::getenv("GOSSIP_BIN_NOSKIP"); u && std::atoi(u)) c->bin_noskip = true;
     if (const char* u = std::getenv("GOSSIP_SCATTER_PROBE")) c->scatter_probe = (uint32_t)std::atoi(u);
     if (const char* u = std::getenv("GOSSIP_BIN_FRONT_PM")) c->bin_front_pm = (uint32_t)std::atoi(u);
     if (const char* u = std::getenv("GOSSIP_HEAVY_EXIT")) c->heavy_exit = std::atoi(u) != 0;
+    if (const char* u = std::getenv("GOSSIP_DEFER_PM")) c->defer_pm = (uint32_t)std::atoi(u);
+    if (const char* u = std::getenv("GOSSIP_BIN_STREAM")) c->bin_stream = std::atoi(u) != 0;
+    if (const char* u = std::getenv("GOSSIP_PULL_DIAG")) c->pull_diag = std::atoi(u) != 0;
     if (const char* u = std::getenv("GOSSIP_FULL_LIVENESS"); u && std::atoi(u)) c->full_liveness = true;
     if (const char* b = std::getenv("GOSSIP_BIN_PERMILLE"); b && !cfg->bin_permille) c->cfg.bin_permille = (uint32_t)std::atoi(b);
     c->n = cfg->n_peers;
@@ -911,10 +949,11 @@ gossip_status gossip_create(const gossip_config* cfg, gossip_ctx** out) {
     if ((err = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) return bail("stream", err);
     c->own_stream = true;
     const uint64_t words = c->n_local * c->Wp;
+    const uint64_t words2 = (words + 1) & ~1ull;  // k_commit_nx streams 16-B pairs
     const uint64_t bitwords = (c->n + 31) / 32;
-    if ((err = hipMalloc((void**)&c->seen, words * 8)) != hipSuccess) return bail("seen", err);
-    if ((err = hipMalloc((void**)&c->nw, words * 8)) != hipSuccess) return bail("new", err);
-    if ((err = hipMalloc((void**)&c->nx, words * 8)) != hipSuccess) return bail("next", err);
+    if ((err = hipMalloc((void**)&c->seen, words2 * 8)) != hipSuccess) return bail("seen", err);
+    if ((err = hipMalloc((void**)&c->nw, words2 * 8)) != hipSuccess) return bail("new", err);
+    if ((err = hipMalloc((void**)&c->nx, words2 * 8)) != hipSuccess) return bail("next", err);
     if ((err = hipMalloc((void**)&c->front, ((c->n_local + 63) / 64 + 1) * 8)) != hipSuccess) return bail("front", err);
     for (int k = 0; k < 2; ++k)
         if ((err = hipMalloc((void**)&c->tact[k], tact_bytes(c))) != hipSuccess) return bail("frontier tiles", err);
@@ -1211,6 +1250,7 @@ gossip_status gossip_reset(gossip_ctx* c) {
     c->nx_dirty = false;
     c->last_pull = false;
     c->last_bin = false;
+    c->cur_defer = false;
     c->last_fresh = 0;
     c->frontier_est = c->prev_frontier_est = 0;
     c->round = 0;
@@ -1233,7 +1273,7 @@ gossip_status gossip_step(gossip_ctx* c, gossip_round_stats* out) {
     gossip_round_stats st;
     if ((s = read_slot(c, &st, true))) return s;
     if (out) *out = st;
-    advance(c, st.new_receipts);
+    if ((s = advance(c, st.new_receipts))) return s;
     return c->finished ? 1 : 0;
 }
 
@@ -1352,7 +1392,7 @@ gossip_status gossip_round_finish(gossip_ctx* c, gossip_round_stats* out) {
 
 gossip_status gossip_round_commit(gossip_ctx* c, uint64_t global_new_receipts, int* finished) {
     if (!c) return fail(GOSSIP_EINVAL, "null ctx");
-    advance(c, global_new_receipts);
+    if (gossip_status s = advance(c, global_new_receipts)) return s;
     if (finished) *finished = c->finished ? 1 : 0;
     return GOSSIP_OK;
 }

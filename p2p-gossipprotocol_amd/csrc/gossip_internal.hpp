@@ -16,15 +16,17 @@ constexpr int kBlock = 256;                    // 4 waves of 64
 constexpr int kMaxWords = 8;                   // M <= 512 concurrent messages
 constexpr int kStatLines = 64;                 // striped DevStats lines per round (summed at read)
 constexpr int kPullNT = 0x100;                 // launch_pull_light unroll flag: non-temporal streamed accesses
+constexpr int kPullRows = 0x200;               // launch_pull_light flag: the row-queue kernel (k_pull_rows)
 constexpr uint32_t kHeavyExitEvery = 4;        // k_pull_heavy checks its early exit every 4 batches of 64 edges
 
 // Per-round device counters (all integer; order-independent sums).
 struct DevStats {
     unsigned long long frontier, traversals, deliveries, undelivered, new_receipts, injected, died, reports,
         seed_removals, digest, covered, heavy_traversals, live_checked, activated, pull_edges, pull_gathers,
-        reconnects, rejoined;
+        reconnects, rejoined, atomics,  // atomics: device-scope atomics issued on peer state (seen, nx, marks)
+        diag;                           // measurement counters (GOSSIP_PULL_DIAG)
 };
-constexpr int kStatFields = 18;
+constexpr int kStatFields = 20;
 static_assert(sizeof(DevStats) == kStatFields * 8, "DevStats layout");
 
 struct HeavyChunk {
@@ -76,6 +78,11 @@ struct BinArgs {
     uint32_t probe;               // measurement only (GOSSIP_SCATTER_PROBE=1: staging only, 2: slot stores to the
                                   // sink; results are then wrong)
     uint64_t n_runs_m1;           // cb_run entries - 1 (clamp for the run index of past-the-end lanes)
+    // streamed layout (the default): val is in cb order, written front to back by k_bin_stream; the
+    // apply walks its bin's slots and finds each value through the run of the slot
+    const uint32_t* ap_run;       // per run, in slot order: slot - cb position (as cb_run)
+    const uint32_t* ap_grp;       // per 64-slot group: runs that start before the group
+    uint32_t stream;              // 1: streamed layout, 0: val in slot order (k_bin_scatter_*)
 };
 
 struct BinState {
@@ -85,6 +92,8 @@ struct BinState {
     uint32_t* cb_run = nullptr;
     uint32_t* cb_grp = nullptr;
     uint64_t n_runs = 0;
+    uint32_t* ap_run = nullptr;
+    uint32_t* ap_grp = nullptr;
     uint64_t* chunk_begin = nullptr;
     uint64_t n_chunks = 0, chunk = 0;
     BinUnit* units = nullptr;
@@ -131,6 +140,9 @@ struct RoundArgs {
                                    // nonzero new words; cleared as consumed (nullptr: not kept)
     uint64_t* tnx;                 // the same bits for the next round's words, set at activation
     uint32_t tsparse;              // tcur is valid: push_light visits only its tiles
+    uint32_t defer;                // push round with a deferred seen update: deliveries test against the
+                                   // round-start seen and OR the unseen bits into nx only (one atomic per
+                                   // delivery); k_commit_nx folds nx into seen after the round
     uint64_t* front;               // pull rounds: 1 bit per source peer, set iff its new words are nonzero
     const uint64_t* nw_src;        // pull rounds: new words of every source, indexed by (global) peer id
     uint64_t n_src;                // peers covered by nw_src / front
@@ -165,6 +177,7 @@ hipError_t launch_inject(const RoundArgs& a, uint32_t W, const uint32_t* origin,
 hipError_t launch_push_heavy(const RoundArgs& a, uint32_t W, bool check_alive, bool remote, hipStream_t s);
 hipError_t launch_push_light(const RoundArgs& a, uint32_t W, bool check_alive, bool remote, hipStream_t s);
 hipError_t launch_frontier_bits(const RoundArgs& a, uint32_t W, hipStream_t s);
+hipError_t launch_pull_diag(const RoundArgs& a, uint32_t W, hipStream_t s);
 hipError_t launch_pull_light(const RoundArgs& a, uint32_t W, int unroll, hipStream_t s);
 hipError_t launch_pull_heavy(const RoundArgs& a, uint32_t W, hipStream_t s);
 hipError_t launch_apply_remote(const RoundArgs& a, uint32_t W, const uint64_t* recv, uint32_t world,
@@ -199,6 +212,7 @@ hipError_t launch_rejoin(const RoundArgs& a, uint32_t W, uint32_t seed, uint32_t
 // after the round's deaths: the restarted peers' fresh out-edges (extra_cap > 0)
 hipError_t launch_rejoin_select(const RoundArgs& a, const RebootArgs& r, const uint32_t* list,
                                 const unsigned long long* n_list, uint64_t max_list, hipStream_t s);
+hipError_t launch_commit_nx(uint64_t* seen, const uint64_t* nx, uint64_t n_words, hipStream_t s);
 hipError_t launch_coverage(const uint64_t* words, uint64_t n_local, uint32_t W, unsigned long long* counts,
                            hipStream_t s);
 hipError_t launch_heavy_count(const uint64_t* rp, uint64_t n_local, uint32_t heavy, unsigned long long* n_chunks,
@@ -218,7 +232,7 @@ hipError_t build_powerlaw_device(uint64_t n_global, uint64_t begin, uint64_t end
 // hipErrorOutOfMemory (state untouched) when the layout does not fit next to
 // what is already resident.
 hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local, uint64_t n_global, uint64_t n_edges,
-                      uint32_t heavy, uint32_t Wp, hipStream_t s, BinState* out, std::string* err);
+                      uint32_t heavy, uint32_t Wp, bool stream, hipStream_t s, BinState* out, std::string* err);
 void free_bins(BinState* b);
 
 // ---- library-driven multi-GPU rounds (gossip_dist.hip) ----

@@ -39,10 +39,14 @@ __device__ __forceinline__ uint32_t lane_rank(unsigned long long mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
+
 struct Acc {
     unsigned long long frontier = 0, trav = 0, deliv = 0, undeliv = 0, fresh = 0, digest = 0, covered = 0, died = 0,
                        reports = 0, removals = 0, injected = 0, htrav = 0, checked = 0,
-                       activated = 0, pulled = 0, gathered = 0, reconnects = 0, rejoined = 0;
+                       activated = 0, pulled = 0, gathered = 0, reconnects = 0, rejoined = 0, atomics = 0,
+                       diag = 0;
 };
 
 // Block-level flush: wave sums -> LDS -> one atomic per nonzero field per
@@ -69,7 +73,7 @@ __device__ __forceinline__ void flush_into(Acc& acc, DevStats* st, unsigned long
     const unsigned long long v[kF] = {acc.frontier, acc.trav,     acc.deliv,   acc.undeliv, acc.fresh,  acc.injected,
                                       acc.died,     acc.reports,  acc.removals, acc.digest, acc.covered, acc.htrav,
                                       acc.checked,  acc.activated, acc.pulled,  acc.gathered, acc.reconnects,
-                                      acc.rejoined};
+                                      acc.rejoined, acc.atomics, acc.diag};
 #pragma unroll
     for (int f = 0; f < kF; ++f) {
         const unsigned long long s_ = wave_sum(v[f]);
@@ -112,10 +116,65 @@ __device__ __forceinline__ void tile_edges(uint32_t deg, uint64_t rb, F&& f) {
     }
 }
 
+// Source lane of edge position p within a tile: the number of rows whose
+// inclusive end is <= p (incl = in-wave inclusive scan of row lengths).
+__device__ __forceinline__ int src_lane(uint32_t incl, uint32_t p) {
+    int s = 0;
+#pragma unroll
+    for (int step = 32; step > 0; step >>= 1) {
+        const uint32_t val = __shfl(incl, s + step - 1);
+        if (val <= p) s += step;
+    }
+    return s;
+}
+
 // handleClient's dedup (peer.cpp:277-285) as a 64-bit test-and-set: deliver
-// the source's new words m to peer c.  A plain read first: seen only grows
-// within a round, so a stale read can only cost an extra atomic, never a
-// wrong answer.
+// the source's new words m to local peer lv whose seen words were read as cur.
+// The plain read first: seen only grows within a round, so a stale read can
+// only cost an extra atomic, never a wrong answer.
+template <int W>
+__device__ __forceinline__ void deliver_local(const RoundArgs& a, uint64_t lv, const uint64_t (&m)[W],
+                                              const uint64_t (&cur)[W], Acc& acc) {
+    unsigned long long* sp = reinterpret_cast<unsigned long long*>(a.seen) + lv * W;
+    unsigned long long* np = reinterpret_cast<unsigned long long*>(a.nx) + lv * W;
+    auto mark = [&] {  // the peer's tile joins the next round's frontier tiles
+        const unsigned long long tb = 1ull << ((lv >> 6) & 63);
+        unsigned long long* tw = reinterpret_cast<unsigned long long*>(a.tnx) + (lv >> 12);
+        if (!(*tw & tb)) {  // read first: most tiles are already marked
+            atomicOr(tw, tb);
+            acc.atomics++;
+        }
+    };
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        const unsigned long long u = m[w] & ~cur[w];
+        if (!u) continue;  // all duplicates: dropped (peer.cpp:281)
+        if (a.defer) {     // seen is the round-start set all round: one atomic, on nx
+            const unsigned long long old = atomicOr(np + w, u);
+            acc.atomics++;
+            const unsigned long long fr = u & ~old;  // not yet received this round either
+            if (fr) {
+                acc.activated += old == 0;
+                if (a.tnx && old == 0) mark();
+                acc.fresh += (unsigned long long)__popcll(fr);
+            }
+            continue;
+        }
+        const unsigned long long old = atomicOr(sp + w, (unsigned long long)m[w]);
+        acc.atomics++;
+        const unsigned long long fr = m[w] & ~old;
+        if (fr) {
+            const unsigned long long onx = atomicOr(np + w, fr);
+            acc.atomics++;
+            acc.activated += onx == 0;
+            if (a.tnx && onx == 0) mark();
+            acc.fresh += (unsigned long long)__popcll(fr);
+        }
+    }
+}
+
+// One delivery to global peer c (bit 31: masked edge): liveness, remote
+// staging or the local test-and-set.
 template <int W, bool CA, bool RM>
 __device__ __forceinline__ void deliver(const RoundArgs& a, uint32_t c, const uint64_t (&m)[W], uint32_t pc,
                                         Acc& acc) {
@@ -132,62 +191,223 @@ __device__ __forceinline__ void deliver(const RoundArgs& a, uint32_t c, const ui
         for (int w = 0; w < W; ++w) {
             if (!m[w]) continue;
             const unsigned long long cur = dst[w];
-            if ((cur & m[w]) != m[w]) atomicOr(dst + w, (unsigned long long)m[w]);
+            if ((cur & m[w]) != m[w]) {
+                atomicOr(dst + w, (unsigned long long)m[w]);
+                acc.atomics++;
+            }
         }
         return;
     }
     const uint64_t lv = (uint64_t)(c - (uint32_t)a.begin);
-    unsigned long long* sp = reinterpret_cast<unsigned long long*>(a.seen) + lv * W;
+    uint64_t cur[W];
 #pragma unroll
-    for (int w = 0; w < W; ++w) {
-        if (!m[w]) continue;
-        const unsigned long long cur = sp[w];
-        if (!(m[w] & ~cur)) continue;  // all duplicates: dropped (peer.cpp:281)
-        const unsigned long long old = atomicOr(sp + w, (unsigned long long)m[w]);
-        const unsigned long long fr = m[w] & ~old;
-        if (fr) {
-            const unsigned long long onx = atomicOr(reinterpret_cast<unsigned long long*>(a.nx) + lv * W + w, fr);
-            acc.activated += onx == 0;
-            if (a.tnx && onx == 0) {  // the peer's tile joins the next round's frontier tiles
+    for (int w = 0; w < W; ++w) cur[w] = m[w] ? a.seen[lv * W + w] : ~0ull;
+    deliver_local<W>(a, lv, m, cur, acc);
+}
+
+// kU deliveries per lane at once (one per 64-edge batch), in phases so that
+// every load of a phase is in flight together: the liveness bits, then the
+// seen words, then the atomics.  A sparse push round is otherwise a chain of
+// dependent round trips per batch (col -> seen -> atomic -> atomic).
+template <int W, bool CA, bool RM, int kU>
+__device__ __forceinline__ void deliver_batch(const RoundArgs& a, const uint32_t (&c)[kU],
+                                              const uint64_t (&m)[kU][W], const uint32_t (&pc)[kU], Acc& acc) {
+    bool loc[kU];
+    uint32_t al[kU];
+#pragma unroll
+    for (int j = 0; j < kU; ++j) {
+        const bool ok = !(c[j] & kMaskedEdge);  // invalid lanes carry a masked id
+        acc.trav += ok;
+        loc[j] = ok;
+        if (CA) al[j] = a.alive[ok ? c[j] >> 5 : 0];
+    }
+#pragma unroll
+    for (int j = 0; j < kU; ++j) {
+        if (CA && loc[j] && !((al[j] >> (c[j] & 31)) & 1u)) {  // send() to a dead peer fails (peer.cpp:312)
+            acc.undeliv += pc[j];
+            loc[j] = false;
+        } else if (loc[j]) {
+            acc.deliv += pc[j];  // sentTo.insert (peer.cpp:314)
+        }
+        if (RM && loc[j] && (c[j] < a.begin || c[j] >= a.end)) {
+            unsigned long long* dst = reinterpret_cast<unsigned long long*>(a.send) + (uint64_t)c[j] * W;
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                if (!m[j][w]) continue;
+                if ((dst[w] & m[j][w]) != m[j][w]) {
+                    atomicOr(dst + w, (unsigned long long)m[j][w]);
+                    acc.atomics++;
+                }
+            }
+            loc[j] = false;
+        }
+    }
+    // unconditional loads (lanes without a delivery read word 0): a load under a branch gets its own wait
+    uint64_t cur[kU][W];
+#pragma unroll
+    for (int j = 0; j < kU; ++j)
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            const uint64_t x = a.seen[loc[j] ? (uint64_t)(c[j] - (uint32_t)a.begin) * W + w : 0];
+            cur[j][w] = x | (loc[j] && m[j][w] ? 0ull : ~0ull);  // (a select would sink the load into a branch)
+        }
+    // the test-and-sets, every atomic of a phase issued before any result is used
+    uint64_t old[kU][W];
+#pragma unroll
+    for (int j = 0; j < kU; ++j)
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            const uint64_t lv = (uint64_t)(c[j] - (uint32_t)a.begin);
+            const unsigned long long u = m[j][w] & ~cur[j][w];  // 0: all duplicates, dropped (peer.cpp:281)
+            unsigned long long* p = reinterpret_cast<unsigned long long*>(a.defer ? a.nx : a.seen) + lv * W + w;
+            old[j][w] = u ? atomicOr(p, a.defer ? u : (unsigned long long)m[j][w]) : ~0ull;
+            acc.atomics += u != 0;
+        }
+    uint64_t fr[kU][W], onx[kU][W];
+#pragma unroll
+    for (int j = 0; j < kU; ++j)
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            const uint64_t lv = (uint64_t)(c[j] - (uint32_t)a.begin);
+            // defer: seen is the round-start set and nx holds the round's receipts so far
+            fr[j][w] = (a.defer ? m[j][w] & ~cur[j][w] : m[j][w]) & ~old[j][w];
+            onx[j][w] = a.defer ? old[j][w]
+                        : fr[j][w] ? atomicOr(reinterpret_cast<unsigned long long*>(a.nx) + lv * W + w,
+                                              (unsigned long long)fr[j][w])
+                                   : ~0ull;
+            acc.atomics += !a.defer && fr[j][w];
+        }
+#pragma unroll
+    for (int j = 0; j < kU; ++j)
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            if (!fr[j][w]) continue;
+            acc.fresh += (unsigned long long)__popcll(fr[j][w]);
+            acc.activated += onx[j][w] == 0;
+            if (a.tnx && onx[j][w] == 0) {  // the peer's tile joins the next round's frontier tiles
+                const uint64_t lv = (uint64_t)(c[j] - (uint32_t)a.begin);
                 const unsigned long long tb = 1ull << ((lv >> 6) & 63);
                 unsigned long long* tw = reinterpret_cast<unsigned long long*>(a.tnx) + (lv >> 12);
-                if (!(*tw & tb)) atomicOr(tw, tb);  // read first: most tiles are already marked
+                if (!(*tw & tb)) {  // read first: most tiles are already marked
+                    atomicOr(tw, tb);
+                    acc.atomics++;
+                }
             }
-            acc.fresh += (unsigned long long)__popcll(fr);
         }
+}
+
+// Edge-space expansion of up to 64 rows (one per lane: deg = row length, 0 =
+// skip; rb = row begin; m/pc = the row's new words and their popcount), kU
+// batches of 64 edges at once, every edge delivered through deliver_batch.
+template <int W, bool CA, bool RM, int kU>
+__device__ __forceinline__ void expand_push(const RoundArgs& a, uint32_t deg, uint64_t rb, const uint64_t (&m)[W],
+                                            uint32_t pc, Acc& acc) {
+    const int lane = threadIdx.x & 63;
+    uint32_t incl = deg;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off);
+        if (lane >= off) incl += y;
+    }
+    const uint32_t excl = incl - deg;
+    const uint32_t total = __shfl(incl, 63);
+    for (uint32_t base = 0; base < total; base += 64 * kU) {
+        uint32_t c[kU], pcs[kU];
+        uint64_t ms[kU][W];
+        uint64_t e[kU];
+#pragma unroll
+        for (int j = 0; j < kU; ++j) {
+            const uint32_t p = base + j * 64 + lane;
+            const int s = src_lane(incl, p);
+            e[j] = __shfl(rb, s) + (uint64_t)(p - __shfl(excl, s));
+            pcs[j] = __shfl(pc, s);
+#pragma unroll
+            for (int w = 0; w < W; ++w) ms[j][w] = __shfl(m[w], s);
+            if (p >= total) pcs[j] = 0;
+        }
+#pragma unroll
+        for (int j = 0; j < kU; ++j) c[j] = base + j * 64 + lane < total ? a.col[e[j]] : kMaskedEdge;
+        deliver_batch<W, CA, RM, kU>(a, c, ms, pcs, acc);
     }
 }
 
 // ---------------------------------------------------------------------------
-// push: light rows (<= kHeavyDegree), one wave per 64-peer tile.  Also the
-// round's push-start bookkeeping: frontier, digest and coverage increments
-// (the new words ARE the bits added to seen since the last push start).
+// push: light rows (<= kHeavyDegree).  Each wave sweeps 64-peer tiles and
+// does the round's push-start bookkeeping for their active peers (frontier,
+// digest and coverage increments: the new words ARE the bits added to seen
+// since the last push start); it collects the active peers into a wave-private
+// packet in LDS and expands 64 of them at a time (expand_push).  On a sparse
+// frontier a tile holds about one active peer: expanding tile by tile left
+// each wave one short chain of dependent loads at a time.
 // ---------------------------------------------------------------------------
+constexpr int kPushU = 4;  // 64-edge batches delivered together (W <= 2)
 template <int W, bool CA, bool RM, bool COV, bool SP>  // SP: visit only the tiles marked in tcur
 __global__ __launch_bounds__(kBlock) void k_push_light(RoundArgs a, uint32_t wd) {
+    constexpr int kU = W <= 2 ? kPushU : 1;
     __shared__ unsigned int cov_s[COV ? 64 * W : 1];
+    __shared__ uint32_t pk_v[kWavesPerBlock][128];
+    __shared__ unsigned long long pk_m[kWavesPerBlock][128 * W];
     if (COV) {
         for (int i = threadIdx.x; i < 64 * W; i += kBlock) cov_s[i] = 0;
         __syncthreads();
     }
     Acc acc;
     const int lane = threadIdx.x & 63;
+    uint32_t* pv = pk_v[threadIdx.x >> 6];
+    unsigned long long* pm = pk_m[threadIdx.x >> 6];
+    uint32_t n_pk = 0;  // wave-uniform
     const uint64_t n_tiles = (a.n_local + 63) >> 6;
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
-    auto tile = [&](uint64_t t) {
-        const uint64_t v = (t << 6) + lane;
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    // expand the packet's first min(n_pk, 64) peers; keep the rest
+    auto expand = [&] {
+        wave_sync();
+        const uint32_t cnt = n_pk < 64 ? n_pk : 64;
+        const bool have = (uint32_t)lane < cnt;
+        const uint64_t v = have ? pv[lane] : 0;
         uint64_t m[W];
-        bool act = false;
+        uint32_t pc = 0;
 #pragma unroll
         for (int w = 0; w < W; ++w) {
-            m[w] = v < a.n_local ? a.nw[v * W + w] : 0ull;
-            act |= m[w] != 0;
+            m[w] = have ? pm[lane * W + w] : 0ull;
+            pc += (uint32_t)__popcll(m[w]);
         }
-        if (!__any(act)) return;
-        uint32_t pc = 0, deg = 0;
+        uint32_t deg = 0;
         uint64_t rb = 0;
+        if (have) {
+            rb = a.rp[v];
+            const uint64_t d = a.rp[v + 1] - rb;
+            deg = d <= a.heavy ? (uint32_t)d : 0u;  // heavy rows: k_push_heavy
+        }
+        const uint32_t rest = n_pk - cnt;
+        wave_sync();
+        if ((uint32_t)lane < rest) {  // entries 64.. move down (rest < 64)
+            pv[lane] = pv[64 + lane];
+#pragma unroll
+            for (int w = 0; w < W; ++w) pm[lane * W + w] = pm[(64 + lane) * W + w];
+        }
+        n_pk = rest;
+        expand_push<W, CA, RM, kU>(a, deg, rb, m, pc, acc);
+    };
+    auto load = [&](uint64_t t, uint64_t (&m)[W]) {
+        const uint64_t v = (t << 6) + lane;
+#pragma unroll
+        for (int w = 0; w < W; ++w) m[w] = v < a.n_local ? a.nw[v * W + w] : 0ull;
+    };
+    auto tile = [&](uint64_t t, uint64_t (&m)[W]) {
+        const uint64_t v = (t << 6) + lane;
+        bool act = false;
+#pragma unroll
+        for (int w = 0; w < W; ++w) act |= m[w] != 0;
+        const unsigned long long bal = __ballot(act);
+        if (!bal) return;
         if (act) {
             acc.frontier++;
+            uint32_t pc = 0;
 #pragma unroll
             for (int w = 0; w < W; ++w) {
                 pc += (uint32_t)__popcll(m[w]);
@@ -198,17 +418,14 @@ __global__ __launch_bounds__(kBlock) void k_push_light(RoundArgs a, uint32_t wd)
                 }
             }
             acc.covered += pc;
-            rb = a.rp[v];
-            const uint64_t d = a.rp[v + 1] - rb;
-            deg = d <= a.heavy ? (uint32_t)d : 0u;
-        }
-        tile_edges(deg, rb, [&](int s, bool valid, uint64_t e) {
-            uint64_t ms[W];
+            const uint32_t pos = n_pk + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+            pv[pos] = (uint32_t)v;
 #pragma unroll
-            for (int w = 0; w < W; ++w) ms[w] = __shfl(m[w], s);
-            const uint32_t pcs = __shfl(pc, s);
-            if (valid) deliver<W, CA, RM>(a, a.col[e], ms, pcs, acc);
-        });
+            for (int w = 0; w < W; ++w) pm[pos * W + w] = m[w];
+        }
+        n_pk += (uint32_t)__popcll(bal);
+        if (n_pk >= 64) expand();
     };
     const uint64_t wave0 = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
     if constexpr (SP) {  // only the tiles marked in tcur (64 per bitmap word), clearing the words
@@ -219,11 +436,25 @@ __global__ __launch_bounds__(kBlock) void k_push_light(RoundArgs a, uint32_t wd)
                                       __builtin_amdgcn_readfirstlane((uint32_t)word);  // wave-uniform
             if (!bits) continue;
             if (lane == 0) a.tcur[i] = 0ull;
-            for (; bits; bits &= bits - 1) tile((i << 6) + (uint64_t)__builtin_ctzll(bits));
+            for (; bits; bits &= bits - 1) {
+                uint64_t m[W];
+                load((i << 6) + (uint64_t)__builtin_ctzll(bits), m);
+                tile((i << 6) + (uint64_t)__builtin_ctzll(bits), m);
+            }
         }
-    } else {
-        for (uint64_t t = wave0; t < n_tiles; t += nwaves) tile(t);  // (the engine clears tcur)
+    } else {  // (the engine clears tcur)
+        // kPre tiles' words in flight per wave: a sweep over a sparse frontier is bound by load latency
+        constexpr int kPre = W <= 2 ? 4 : 1;
+        for (uint64_t t0 = wave0; t0 < n_tiles; t0 += kPre * nwaves) {
+            uint64_t m[kPre][W];
+#pragma unroll
+            for (int j = 0; j < kPre; ++j) load(t0 + j * nwaves, m[j]);
+#pragma unroll
+            for (int j = 0; j < kPre; ++j)
+                if (t0 + j * nwaves < n_tiles) tile(t0 + j * nwaves, m[j]);
+        }
     }
+    if (n_pk) expand();  // n_pk < 64 here
     flush(acc, a.st);
     if (COV) {
         __syncthreads();
@@ -251,7 +482,21 @@ __global__ __launch_bounds__(kBlock) void k_push_heavy(RoundArgs a) {
             pc += (uint32_t)__popcll(m[w]);
         }
         if (!act) continue;  // uniform over the wave
-        for (uint64_t e = ch.e0 + lane; e < ch.e1; e += 64) deliver<W, CA, RM>(a, a.col[e], m, pc, acc);
+        constexpr int kU = W <= 2 ? kPushU : 1;
+        uint64_t ms[kU][W];
+        uint32_t pcs[kU];
+#pragma unroll
+        for (int j = 0; j < kU; ++j) {
+            pcs[j] = pc;
+#pragma unroll
+            for (int w = 0; w < W; ++w) ms[j][w] = m[w];
+        }
+        for (uint64_t e0 = ch.e0 + lane; e0 < ch.e1; e0 += 64 * kU) {
+            uint32_t c[kU];
+#pragma unroll
+            for (int j = 0; j < kU; ++j) c[j] = e0 + j * 64 < ch.e1 ? a.col[e0 + j * 64] : kMaskedEdge;
+            deliver_batch<W, CA, RM, kU>(a, c, ms, pcs, acc);
+        }
     }
     acc.htrav = acc.trav;
     flush(acc, a.st);
@@ -288,18 +533,6 @@ __global__ __launch_bounds__(kBlock) void k_frontier_bits(RoundArgs a) {
     }
 }
 
-// Source lane of edge position p within a tile: the number of rows whose
-// inclusive end is <= p (incl = in-wave inclusive scan of row lengths).
-__device__ __forceinline__ int src_lane(uint32_t incl, uint32_t p) {
-    int s = 0;
-#pragma unroll
-    for (int step = 32; step > 0; step >>= 1) {
-        const uint32_t val = __shfl(incl, s + step - 1);
-        if (val <= p) s += step;
-    }
-    return s;
-}
-
 // Streamed (touched-once) loads/stores of a pull round; NT marks them
 // non-temporal so they do not push the gathered new words out of L2/MALL.
 template <bool NT, class T>
@@ -311,6 +544,46 @@ template <bool NT, class T>
 __device__ __forceinline__ void st_s(T* p, T v) {
     if constexpr (NT) __builtin_nontemporal_store(v, p);
     else *p = v;
+}
+
+// Measurement only (GOSSIP_PULL_DIAG=1, before k_pull_light): per light row
+// that can still learn, the gathers a sequential scan of its row with an early
+// exit would issue -- it stops at the edge where its words hold every bit it
+// can learn (need); a row whose need is not covered by its neighbours scans
+// all of them.  Into the round's diag counter: gathers << 32 | needy rows.
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_pull_diag(RoundArgs a) {
+    Acc acc;
+    for (uint64_t v = (uint64_t)blockIdx.x * kBlock + threadIdx.x; v < a.n_local; v += (uint64_t)gridDim.x * kBlock) {
+        uint64_t need[W], got[W];
+        bool needy = false;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            need[w] = a.inj_mask[w] & ~a.seen[v * W + w];
+            got[w] = 0;
+            needy |= need[w] != 0;
+        }
+        if (!needy) continue;
+        const uint64_t rb = a.rp[v], d = a.rp[v + 1] - rb;
+        if (d > a.heavy) continue;
+        uint64_t k = 0;
+        for (; k < d; ++k) {
+            const uint32_t u = a.col[rb + k];
+            if (u & kMaskedEdge) continue;
+            bool done = true;
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                got[w] |= a.nw_src[(uint64_t)u * W + w] & need[w];
+                done &= got[w] == need[w];
+            }
+            if (done) {
+                ++k;
+                break;
+            }
+        }
+        acc.diag += (k << 32) + 1;
+    }
+    flush(acc, a.st);
 }
 
 template <int W, bool COV, bool FRONT, int kPullUnroll, bool NT>  // kPullUnroll: 64-edge batches in flight per wave
@@ -458,6 +731,197 @@ __global__ __launch_bounds__(kBlock) void k_pull_light(RoundArgs a, uint32_t wd)
     }
 }
 
+// pull, light rows, as a row queue with an early exit (the default pull
+// kernel; k_pull_light is the tile-expansion form, GOSSIP_PULL_ROWS=0).  Each
+// wave sweeps 64-peer tiles: source side of the pushes, nx = 0, and every
+// light row that can still learn something (need != 0) joins the wave's queue
+// in LDS.  Lanes take rows from the queue and scan them kRowB edges per step,
+// OR-ing the neighbours' new words into what they got; a row stops as soon as
+// it got every bit it can learn (need) -- most rows need one neighbour (config
+// 4, round 7: 90.1 M needy rows, 101 M gathers with the exit against 479 M
+// for whole rows) -- or at its end.  Finished lanes take the next row.  Same
+// results as k_pull_light: fr = (OR of the scanned neighbours) & need, and a
+// row that stops early already holds all of need.
+constexpr int kRowQ = 128;    // queue entries per wave
+template <int W, bool COV, bool FRONT, int kRowB>  // kRowB: edges per lane per step
+__global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) {
+    __shared__ unsigned int cov_s[COV ? 64 * W : 1];
+    __shared__ uint32_t q_v[kWavesPerBlock][kRowQ];
+    __shared__ uint32_t q_d[kWavesPerBlock][kRowQ];
+    __shared__ unsigned long long q_rb[kWavesPerBlock][kRowQ];
+    __shared__ unsigned long long q_need[kWavesPerBlock][kRowQ * W];
+    if (COV) {
+        for (int i = threadIdx.x; i < 64 * W; i += kBlock) cov_s[i] = 0;
+        __syncthreads();
+    }
+    Acc acc;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t* qv = q_v[wv];
+    uint32_t* qd = q_d[wv];
+    unsigned long long* qrb = q_rb[wv];
+    unsigned long long* qneed = q_need[wv];
+    uint32_t q_head = 0, q_tail = 0;  // wave-uniform ring counters (q_tail - q_head <= kRowQ)
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    // this lane's row
+    bool has = false;
+    uint32_t rv = 0, rd = 0, rk = 0;
+    uint64_t rrb = 0, need[W], got[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) need[w] = got[w] = 0;
+    const uint64_t n_tiles = (a.n_local + 63) >> 6;
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
+    auto sweep_tile = [&](uint64_t tt) {
+        const uint64_t v = (tt << 6) + lane;
+        const bool vv = v < a.n_local;
+        uint64_t m[W], nd[W];
+        bool act = false, needy = false;
+        const bool va = vv && (!a.dead_mode || bit_alive(a.alive, (uint32_t)(a.begin + v)));  // dead: no receive
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            m[w] = vv ? a.nw[v * W + w] : 0ull;
+            const uint64_t sv = vv ? a.seen[v * W + w] : ~0ull;
+            nd[w] = va ? a.inj_mask[w] & ~sv : 0ull;
+            act |= m[w] != 0;
+            needy |= nd[w] != 0;
+            if (vv) a.nx[v * W + w] = 0ull;  // nx is written whole in a pull round; rows that learn rewrite it
+        }
+        uint64_t rb = 0, d = 0;
+        if (act || needy) {
+            rb = a.rp[v];
+            d = a.rp[v + 1] - rb;
+        }
+        if (act) {  // source side of this peer's pushes (broadcastMessage, peer.cpp:310-316)
+            uint32_t pc = 0;
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                pc += (uint32_t)__popcll(m[w]);
+                if (w < (int)wd) acc.digest += digest_weight((a.begin + v) * wd + w) * m[w];
+                if (COV)
+                    for (uint64_t x = m[w]; x; x &= x - 1) atomicAdd(&cov_s[w * 64 + __builtin_ctzll(x)], 1u);
+            }
+            acc.frontier++;
+            acc.covered += pc;
+            if (!a.dead_mode) {  // every edge alive and unmasked
+                acc.trav += d;
+                acc.deliv += (unsigned long long)pc * d;
+            } else if (a.dgone) {  // from the per-source counters; else k_src_count books them
+                const uint32_t g = a.dgone[v], k = a.dmask[v];
+                acc.trav += d - k;
+                acc.deliv += (unsigned long long)pc * (d - g);
+                acc.undeliv += (unsigned long long)pc * (g - k);
+            }
+        }
+        const bool enq = needy && d > 0 && d <= a.heavy;  // heavy rows: k_pull_heavy
+        const unsigned long long bal = __ballot(enq);
+        if (enq) {
+            const uint32_t pos = (q_tail + (uint32_t)__builtin_amdgcn_mbcnt_hi(
+                                               (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))) %
+                                 kRowQ;
+            qv[pos] = (uint32_t)v;
+            qd[pos] = (uint32_t)d;
+            qrb[pos] = rb;
+#pragma unroll
+            for (int w = 0; w < W; ++w) qneed[pos * W + w] = nd[w];
+        }
+        q_tail += (uint32_t)__popcll(bal);
+    };
+    while (true) {
+        // refill the queue while it has room for a whole tile
+        while (t < n_tiles && q_tail - q_head <= (uint32_t)(kRowQ - 64)) {
+            sweep_tile(t);
+            t += nwaves;
+        }
+        // idle lanes take queued rows
+        const unsigned long long idle = __ballot(!has);
+        const uint32_t avail = q_tail - q_head;
+        if (idle && avail) {
+            wave_sync();
+            const uint32_t r = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
+                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+            if (!has && r < avail) {
+                const uint32_t pos = (q_head + r) % kRowQ;
+                has = true;
+                rv = qv[pos];
+                rd = qd[pos];
+                rrb = qrb[pos];
+                rk = 0;
+#pragma unroll
+                for (int w = 0; w < W; ++w) {
+                    need[w] = qneed[pos * W + w];
+                    got[w] = 0;
+                }
+            }
+            const uint32_t taken = min((uint32_t)__popcll(idle), avail);
+            q_head += taken;
+            wave_sync();  // the taken entries are read before a sweep overwrites them
+        }
+        if (!__any(has)) {
+            if (t >= n_tiles && q_tail == q_head) break;
+            continue;
+        }
+        // one step: kRowB edges of this lane's row, every load of the step in flight together
+        uint32_t u[kRowB];
+        bool ok[kRowB];
+#pragma unroll
+        for (int j = 0; j < kRowB; ++j) {
+            ok[j] = has && rk + j < rd;
+            u[j] = a.col[ok[j] ? rrb + rk + j : 0];
+        }
+        acc.pulled += (has ? min(kRowB, (int)(rd - rk)) : 0);
+#pragma unroll
+        for (int j = 0; j < kRowB; ++j) ok[j] = ok[j] && !(u[j] & kMaskedEdge);  // dead neighbour: words are zero
+        if (FRONT) {
+            uint64_t fb[kRowB];
+#pragma unroll
+            for (int j = 0; j < kRowB; ++j) fb[j] = a.front[ok[j] ? u[j] >> 6 : 0];
+#pragma unroll
+            for (int j = 0; j < kRowB; ++j) ok[j] = ok[j] && ((fb[j] >> (u[j] & 63)) & 1ull);  // nothing new: no gather
+        }
+        uint64_t x[kRowB][W];
+#pragma unroll
+        for (int j = 0; j < kRowB; ++j)
+#pragma unroll
+            for (int w = 0; w < W; ++w)  // unconditional (a select would sink the load into a branch)
+                x[j][w] = a.nw_src[(ok[j] ? (uint64_t)u[j] : 0) * W + w] & (ok[j] ? ~0ull : 0ull);
+#pragma unroll
+        for (int j = 0; j < kRowB; ++j) acc.gathered += ok[j];
+        bool done = true;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+#pragma unroll
+            for (int j = 0; j < kRowB; ++j) got[w] |= x[j][w] & need[w];
+            done &= got[w] == need[w];
+        }
+        rk += kRowB;
+        if (has && (done || rk >= rd)) {  // the row is finished: handleClient's test-and-set, owner stores
+            bool any = false;
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                const uint64_t fr = got[w];  // subset of need: bits this peer had not seen
+                if (fr) {
+                    a.seen[(uint64_t)rv * W + w] = (a.inj_mask[w] & ~need[w]) | fr;  // seen is within inj_mask
+                    a.nx[(uint64_t)rv * W + w] = fr;
+                    acc.fresh += (unsigned long long)__popcll(fr);
+                    any = true;
+                }
+            }
+            acc.activated += any;
+            has = false;
+        }
+    }
+    flush(acc, a.st);
+    if (COV) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < 64 * W; i += kBlock)
+            if (cov_s[i]) atomicAdd(&a.cov[i], (unsigned long long)cov_s[i]);
+    }
+}
+
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_pull_heavy(RoundArgs a) {
     Acc acc;
@@ -517,6 +981,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_heavy(RoundArgs a) {
                 if (!part[w]) continue;
                 unsigned long long* sp = reinterpret_cast<unsigned long long*>(a.seen) + (uint64_t)ch.v * W + w;
                 const unsigned long long fr = part[w] & ~atomicOr(sp, (unsigned long long)part[w]);
+                acc.atomics += fr ? 2 : 1;
                 if (fr) {
                     const unsigned long long onx =
                         atomicOr(reinterpret_cast<unsigned long long*>(a.nx) + (uint64_t)ch.v * W + w, fr);
@@ -955,7 +1420,7 @@ __global__ __launch_bounds__(kB) void k_bin_apply(RoundArgs a, BinArgs b) {
         const uint32_t dw[4] = {dd.x, dd.y, dd.z, dd.w};
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const uint32_t dl = (dw[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
+            const uint32_t dl = (dw[k >> 1] >> ((k & 1) * 16)) & (kRunStart - 1u);  // (bit 15: run start)
 #pragma unroll
             for (int w = 0; w < W; ++w)
                 if (x[k * W + w]) atomicOr(&acc_s[dl * W + w], (unsigned long long)x[k * W + w]);
@@ -974,6 +1439,166 @@ __global__ __launch_bounds__(kB) void k_bin_apply(RoundArgs a, BinArgs b) {
         a.nx[v0 * W + i] = fr;  // heavy rows: 0 here, OR-ed by k_pull_heavy afterwards
     }
     flush<kB / 64>(acc, a.st);
+}
+
+// ---------------------------------------------------------------------------
+// Streamed binned rounds (the default layout, gossip_bins.hip (d)): the values
+// live in cb order, so the scatter is a front-to-back stream and the random
+// access moves to the apply, as reads of slot runs (a read of a short run
+// costs no read-modify-write of a partly written line).
+// ---------------------------------------------------------------------------
+// Phase 1: stage each unit's source chunk in LDS (scatter_stage: also the
+// chunk's source-side stats), then val[p] = slice[cb_src[p]] for the unit's cb
+// entries, consecutive lanes on consecutive entries.  Every entry is written
+// every binned round.
+template <int W, bool COV>
+__global__ __launch_bounds__(kScatterBlock) void k_bin_stream(RoundArgs a, BinArgs b, uint32_t wd) {
+    constexpr int kWaves = kScatterBlock / 64;
+    constexpr int kU = W <= 2 ? 2 : 1;  // 8-entry blocks in flight per lane
+    __shared__ unsigned long long slice[kBinChunkWords];
+    __shared__ unsigned long long live_s[kBinChunkWords / 64 / W];
+    __shared__ unsigned int cov_s[COV ? 64 * W : 1];
+    if (COV) {
+        for (int i = threadIdx.x; i < 64 * W; i += kScatterBlock) cov_s[i] = 0;
+    }
+    Acc acc;
+    auto unit = [&](const uint64_t ui) {
+        const BinUnit un = b.units[ui];
+        if (un.p0 >= un.p1 && !un.first) return;  // padding of a row (block-uniform)
+        scatter_stage<W, COV>(a, b, un, wd, slice, live_s, cov_s, acc);
+        // aligned blocks of 8 entries per lane: one 16-B load of cb_src, 8 * W words stored as 16-B pairs
+        const uint64_t k0 = un.p0 >> 3, k1 = (un.p1 + 7) >> 3;
+        for (uint64_t kb = k0 + threadIdx.x; kb < k1; kb += (uint64_t)kScatterBlock * kU) {
+            v4u32 sv[kU];
+#pragma unroll
+            for (int j = 0; j < kU; ++j) {
+                const uint64_t k = kb + (uint64_t)j * kScatterBlock;
+                sv[j] = __builtin_nontemporal_load(reinterpret_cast<const v4u32*>(b.cb_src) + min(k, k1 - 1));
+            }
+#pragma unroll
+            for (int j = 0; j < kU; ++j) {
+                const uint64_t k = kb + (uint64_t)j * kScatterBlock;
+                if (k >= k1) continue;
+                const uint32_t sw[4] = {sv[j].x, sv[j].y, sv[j].z, sv[j].w};
+                uint64_t x[8 * W];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const uint32_t u = (sw[e >> 1] >> ((e & 1) * 16)) & (kRunStart - 1u);
+#pragma unroll
+                    for (int w = 0; w < W; ++w) x[e * W + w] = slice[u * W + w];
+                }
+                const uint64_t p = k * 8;
+                if (p >= un.p0 && p + 8 <= un.p1) {  // whole block: 16-B stores
+                    u64x2* dst = reinterpret_cast<u64x2*>(b.val + p * W);
+#pragma unroll
+                    for (int i = 0; i < 4 * W; ++i) {
+                        u64x2 y;
+                        y.x = x[2 * i];
+                        y.y = x[2 * i + 1];
+                        dst[i] = y;
+                    }
+                } else {  // the unit's ragged ends
+#pragma unroll
+                    for (int e = 0; e < 8; ++e)
+                        if (p + e >= un.p0 && p + e < un.p1)
+#pragma unroll
+                            for (int w = 0; w < W; ++w) b.val[(p + e) * W + w] = x[e * W + w];
+                }
+                acc.gathered += (unsigned)(min(p + 8, un.p1) - max(p, un.p0));
+            }
+        }
+    };
+    scatter_rows(b, unit);
+    flush<kWaves>(acc, a.st);
+    if (COV) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < 64 * W; i += kScatterBlock)
+            if (cov_s[i]) atomicAdd(&a.cov[i], (unsigned long long)cov_s[i]);
+    }
+}
+
+// Phase 2: one workgroup per bin.  Each wave takes 64-slot groups of the bin
+// (kG at once): bdst (destination, bit 15 = a run starts here), the run of
+// each slot from the group's count of earlier runs plus a ballot of the
+// flags, the run's offset, then the value at q - ap_run[run] -- a read from
+// the run's stretch of cb order -- OR-ed into the LDS accumulator.  The end
+// is k_bin_apply's: test-and-set of the bin's peers with plain stores.
+template <int W, int kWords, int kB>
+__global__ __launch_bounds__(kB) void k_bin_apply_runs(RoundArgs a, BinArgs b) {
+    constexpr int kWaves = kB / 64;
+    constexpr int kG = W <= 2 ? 4 : 2;  // groups in flight per wave
+    __shared__ unsigned long long acc_s[kWords];
+    Acc acc;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const Bin bn = b.bins[blockIdx.x];
+    const uint32_t nv = bn.v1 - bn.v0;
+    const uint64_t v0 = bn.v0;
+    bool needy = false;
+    for (uint32_t i = threadIdx.x; i < nv * W; i += kB) {
+        acc_s[i] = 0ull;
+        const bool va = !a.dead_mode || bit_alive(a.alive, (uint32_t)(a.begin + v0 + i / W));
+        needy |= va && (a.inj_mask[i % W] & ~a.seen[v0 * W + i]) != 0;
+    }
+    if (!__syncthreads_or(needy)) {
+        for (uint32_t i = threadIdx.x; i < nv * W; i += kB) a.nx[v0 * W + i] = 0ull;
+        flush<kWaves>(acc, a.st);
+        return;
+    }
+    if (threadIdx.x == 0) acc.pulled = bn.s1 - bn.s0;  // slots scanned (byte accounting)
+    const unsigned long long upto = lane == 63 ? ~0ull : (2ull << lane) - 1;  // lanes 0..lane
+    if (bn.s1 > bn.s0) {
+        const uint64_t g_lo = bn.s0 >> 6, g_hi = ((bn.s1 - 1) >> 6) + 1;
+        for (uint64_t g0 = g_lo + wave; g0 < g_hi; g0 += (uint64_t)kWaves * kG) {
+            uint32_t d[kG], gr[kG];
+#pragma unroll
+            for (int j = 0; j < kG; ++j) {  // (bdst and ap_grp hold whole groups past the last slot)
+                const uint64_t g = min(g0 + (uint64_t)j * kWaves, g_hi - 1);
+                d[j] = b.bdst[g * 64 + lane];
+                gr[j] = b.ap_grp[g];
+            }
+            uint32_t off[kG];
+            bool ok[kG];
+#pragma unroll
+            for (int j = 0; j < kG; ++j) {
+                const uint64_t g = g0 + (uint64_t)j * kWaves;
+                const uint64_t q = g * 64 + lane;
+                ok[j] = g < g_hi && q >= bn.s0 && q < bn.s1;
+                const unsigned long long st = __ballot((d[j] & kRunStart) != 0);
+                // a slot of the bin lies in a run that starts at or before it: run >= 0
+                const uint32_t run = gr[j] + (uint32_t)__popcll(st & upto) - 1u;
+                off[j] = ok[j] ? b.ap_run[run] : 0u;
+            }
+            uint64_t x[kG][W];
+#pragma unroll
+            for (int j = 0; j < kG; ++j) {
+                const uint64_t q = (g0 + (uint64_t)j * kWaves) * 64 + lane;
+                const uint64_t p = ok[j] ? (uint64_t)((uint32_t)q - off[j]) : 0;  // the slot's cb position
+#pragma unroll
+                for (int w = 0; w < W; ++w) x[j][w] = b.val[p * W + w];
+            }
+#pragma unroll
+            for (int j = 0; j < kG; ++j) {
+                if (!ok[j]) continue;
+                const uint32_t dl = d[j] & (kRunStart - 1u);
+#pragma unroll
+                for (int w = 0; w < W; ++w)
+                    if (x[j][w]) atomicOr(&acc_s[dl * W + w], (unsigned long long)x[j][w]);  // ds_or_b64
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nv * W; i += kB) {
+        const uint64_t sv = a.seen[v0 * W + i];
+        const bool va = !a.dead_mode || bit_alive(a.alive, (uint32_t)(a.begin + v0 + i / W));  // dead: no receive
+        const uint64_t fr = va ? acc_s[i] & a.inj_mask[i % W] & ~sv : 0ull;
+        if (fr) {  // handleClient: new -> Message-List insert (peer.cpp:281-282)
+            a.seen[v0 * W + i] = sv | fr;
+            acc.fresh += (unsigned long long)__popcll(fr);
+            acc.activated++;
+        }
+        a.nx[v0 * W + i] = fr;  // heavy rows: 0 here, OR-ed by k_pull_heavy afterwards
+    }
+    flush<kWaves>(acc, a.st);
 }
 
 // ---------------------------------------------------------------------------
@@ -1588,6 +2213,14 @@ __global__ __launch_bounds__(kBlock) void k_apply_remote(RoundArgs a, const uint
             for (uint32_t p = 0; p < world; ++p) inc |= recv[((uint64_t)p * stride + v) * W + w];
             if (!inc) continue;
             const uint64_t cur = a.seen[v * W + w];
+            if (a.defer) {  // seen is folded in by k_commit_nx: this round's local receipts are in nx
+                const uint64_t nxc = a.nx[v * W + w];
+                const uint64_t fr = inc & ~cur & ~nxc;
+                if (!fr) continue;
+                a.nx[v * W + w] = nxc | fr;
+                acc.fresh += (unsigned long long)__popcll(fr);
+                continue;
+            }
             const uint64_t fr = inc & ~cur;
             if (!fr) continue;
             a.seen[v * W + w] = cur | fr;
@@ -1657,7 +2290,17 @@ __global__ __launch_bounds__(kBlock) void k_apply_records(RoundArgs a, const uin
         for (int w = 0; w < W; ++w) {
             const unsigned long long m = r[1 + w];
             if (!m || !(m & ~sp[w])) continue;
+            if (a.defer) {  // as deliver: the round-start seen, one atomic on nx
+                const unsigned long long u = m & ~sp[w];
+                const unsigned long long old = atomicOr(reinterpret_cast<unsigned long long*>(a.nx) + lv * W + w, u);
+                acc.atomics++;
+                const unsigned long long fr = u & ~old;
+                acc.activated += fr && old == 0;
+                acc.fresh += (unsigned long long)__popcll(fr);
+                continue;
+            }
             const unsigned long long fr = m & ~atomicOr(sp + w, m);
+            acc.atomics += fr ? 2 : 1;
             if (fr) {
                 const unsigned long long onx = atomicOr(reinterpret_cast<unsigned long long*>(a.nx) + lv * W + w, fr);
                 acc.activated += onx == 0;
@@ -1666,6 +2309,16 @@ __global__ __launch_bounds__(kBlock) void k_apply_records(RoundArgs a, const uin
         }
     }
     flush(acc, a.st);
+}
+
+// After a deferred push round: seen |= nx (nx holds exactly this round's
+// fresh bits).  16-B words, streamed; seen is written only where nx is set.
+__global__ __launch_bounds__(kBlock) void k_commit_nx(u64x2* seen, const u64x2* nx, uint64_t n2) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n2; i += (uint64_t)gridDim.x * kBlock) {
+        const u64x2 x = __builtin_nontemporal_load(nx + i);
+        if (!(x.x | x.y)) continue;
+        seen[i] |= x;
+    }
 }
 
 template <int W>
@@ -1782,7 +2435,9 @@ hipError_t launch_push_heavy(const RoundArgs& a, uint32_t W_, bool check_alive, 
 
 hipError_t launch_push_light(const RoundArgs& a, uint32_t W_, bool check_alive, bool remote, hipStream_t s) {
     const uint64_t tiles = (a.n_local + 63) / 64;
-    const unsigned g = grid_for(tiles, kWavesPerBlock);
+    // every wave resident at once (4 blocks per CU at <= 128 VGPRs): a sweep wave's packets carry its
+    // work, and a second partial wave of blocks would only stretch the tail
+    const unsigned g = std::min(grid_for(tiles, kWavesPerBlock), 1024u);
     const uint32_t wd = wd_of(W_);
     const bool cov = a.cov != nullptr;
 #define GOSSIP_LIGHT(CA, RM, COV) \
@@ -1820,12 +2475,34 @@ hipError_t launch_frontier_bits(const RoundArgs& a, uint32_t W_, hipStream_t s) 
     return hipGetLastError();
 }
 
+hipError_t launch_pull_diag(const RoundArgs& a, uint32_t W_, hipStream_t s) {
+    GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_pull_diag<W>, dim3(grid_for(a.n_local, kBlock)), dim3(kBlock),
+                                                   0, s, a));
+    return hipGetLastError();
+}
+
 hipError_t launch_pull_light(const RoundArgs& a, uint32_t W_, int unroll, hipStream_t s) {
     const uint64_t tiles = (a.n_local + 63) / 64;
     const unsigned g = grid_for(tiles, kWavesPerBlock);
     const uint32_t wd = wd_of(W_);
+    if (unroll & kPullRows) {  // row queue: every wave resident at once (its queue carries its work)
+        const unsigned gr = std::min(g, (unsigned)kMaxGrid);
+        const int rb = (unroll & ~(kPullRows | kPullNT)) >> 12;  // edges per step (GOSSIP_ROW_B), default 2
+#define GOSSIP_ROWS(COV, FR)                                                                                    \
+        do {                                                                                                    \
+            if (rb == 1) hipLaunchKernelGGL((k_pull_rows<W, COV, FR, 1>), dim3(gr), dim3(kBlock), 0, s, a, wd);  \
+            else if (rb == 4) hipLaunchKernelGGL((k_pull_rows<W, COV, FR, 4>), dim3(gr), dim3(kBlock), 0, s, a, wd); \
+            else hipLaunchKernelGGL((k_pull_rows<W, COV, FR, 2>), dim3(gr), dim3(kBlock), 0, s, a, wd);          \
+        } while (0)
+        GOSSIP_DISPATCH_W(wp_of(W_), {
+            if (a.cov) { if (a.front) GOSSIP_ROWS(true, true); else GOSSIP_ROWS(true, false); }
+            else { if (a.front) GOSSIP_ROWS(false, true); else GOSSIP_ROWS(false, false); }
+        });
+#undef GOSSIP_ROWS
+        return hipGetLastError();
+    }
     const bool nt = (unroll & kPullNT) != 0;
-    unroll &= ~kPullNT;
+    unroll &= 0xFF;  // batches in flight (the flags above it are handled)
 #define GOSSIP_PULL_U(COV, FR, U)                                                                               \
     do {                                                                                                        \
         if (nt) hipLaunchKernelGGL((k_pull_light<W, COV, FR, U, true>), dim3(g), dim3(kBlock), 0, s, a, wd);    \
@@ -1899,6 +2576,13 @@ static int scatter_pc() {
 
 hipError_t launch_bin_scatter(const RoundArgs& a, const BinArgs& b, uint32_t W_, hipStream_t s) {
     const uint32_t wd = wd_of(W_);
+    if (b.stream) {
+        GOSSIP_DISPATCH_W(wp_of(W_), {
+            if (a.cov) hipLaunchKernelGGL((k_bin_stream<W, true>), dim3(kScatterGrid), dim3(kScatterBlock), 0, s, a, b, wd);
+            else hipLaunchKernelGGL((k_bin_stream<W, false>), dim3(kScatterGrid), dim3(kScatterBlock), 0, s, a, b, wd);
+        });
+        return hipGetLastError();
+    }
     if (const int v = scatter_pc()) {
 #define GOSSIP_PC(P, G, R)                                                                                 \
         do {                                                                                               \
@@ -1927,6 +2611,16 @@ hipError_t launch_bin_scatter(const RoundArgs& a, const BinArgs& b, uint32_t W_,
 
 hipError_t launch_bin_apply(const RoundArgs& a, const BinArgs& b, uint32_t W_, hipStream_t s) {
     if (!b.n_bins) return hipSuccess;
+    if (b.stream) {
+        if (b.bin_words > kBinWords / 2) {
+            GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_apply_runs<W, kBinWords, 1024>),
+                                                           dim3((unsigned)b.n_bins), dim3(1024), 0, s, a, b));
+        } else {
+            GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_apply_runs<W, kBinWords / 2, kBlock>),
+                                                           dim3((unsigned)b.n_bins), dim3(kBlock), 0, s, a, b));
+        }
+        return hipGetLastError();
+    }
     if (b.bin_words > kBinWords / 2) {  // up to 144 KB accumulators: one 16-wave workgroup per CU
         GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_apply<W, kBinWords, 1024>), dim3((unsigned)b.n_bins),
                                                        dim3(1024), 0, s, a, b));
@@ -2007,6 +2701,13 @@ hipError_t launch_src_count(const RoundArgs& a, uint32_t W_, hipStream_t s) {
     const uint64_t tiles = (a.n_local + 63) / 64;
     GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_src_count<W>, dim3(grid_for(tiles, kWavesPerBlock)), dim3(kBlock),
                                                    0, s, a));
+    return hipGetLastError();
+}
+
+hipError_t launch_commit_nx(uint64_t* seen, const uint64_t* nx, uint64_t n_words, hipStream_t s) {
+    const uint64_t n2 = (n_words + 1) / 2;  // the word arrays are allocated in whole pairs
+    hipLaunchKernelGGL(k_commit_nx, dim3(grid_for(n2, kBlock)), dim3(kBlock), 0, s, reinterpret_cast<u64x2*>(seen),
+                       reinterpret_cast<const u64x2*>(nx), n2);
     return hipGetLastError();
 }
 

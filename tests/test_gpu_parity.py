@@ -303,3 +303,24 @@ def test_reload_overlay_with_kills(oracle, mode):
             e.inject(w.origins, w.inject_rounds)
             e.schedule_kills([k[0] for k in w.kills], [k[1] for k in w.kills])
             _compare(e, ref, w)
+
+
+@pytest.mark.parametrize("env", ["GOSSIP_DEFER_PM=1", "GOSSIP_BIN_STREAM=1", "GOSSIP_PULL_ROWS=0"])
+@pytest.mark.parametrize("idx,n,mode", [(2, 1 << 16, "auto"), (3, 1 << 18, "bin"), (5, 50_000, "auto"),
+                                        (5, 1 << 16, "push"), (3, 1 << 18, "pull")])
+def test_engine_variants_match_oracle(oracle, monkeypatch, env, idx, n, mode):
+    """The A/B variants the engine keeps behind environment switches (read at
+    gossip_create): the deferred seen update of wide push rounds, the streamed
+    binned layout and the tile-expansion pull give the oracle's results too."""
+    k, v = env.split("=")
+    monkeypatch.setenv(k, v)
+    w = config(idx, n, pick=oracle.pick_origins)
+    rp, col = oracle.gen_workload(w)
+    ref = oracle.simulate_workload(w, rp, col)
+    with _engine(w, mode=mode) as e:
+        e.build_graph()
+        e.inject(w.origins, w.inject_rounds)
+        if w.kills:
+            e.schedule_kills([k[0] for k in w.kills], [k[1] for k in w.kills])
+        e.reset()
+        _compare(e, ref, w)

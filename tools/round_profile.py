@@ -8,7 +8,7 @@ from gossip_hip import Engine  # noqa: E402
 from gossip_hip.workloads import config  # noqa: E402
 
 K = ("push_light", "push_heavy", "pull_light", "pull_heavy", "frontier_bits", "bin_scatter", "bin_apply", "inject",
-     "liveness", "churn", "kills", "src_count", "rebootstrap", "push_extra")
+     "liveness", "churn", "kills", "src_count", "rebootstrap", "push_extra", "commit")
 w = config(int(sys.argv[1]) if len(sys.argv) > 1 else 4)
 e = Engine(w.n, w.n_msgs, device=0, **w.engine_kwargs())
 e.build_graph()
@@ -16,12 +16,16 @@ e.inject(w.origins, w.inject_rounds)
 e.run()
 e.reset()
 e.enable_timing(True)
+C = ("#atomics", "#trav", "#heavy_trav", "#pulled", "#gathers", "#needy_rows", "#exit_gathers")
 prev = {k: e.kernel_time(k)[0] for k in K}
+prevc = {k: e.kernel_bytes(k) for k in C}
 while True:
     st, fin = e.step()
     cur = {k: e.kernel_time(k)[0] for k in K}
     d = {k: round(cur[k] - prev[k], 3) for k in K if cur[k] - prev[k] > 0}
-    print(st["round"], f"F={st['frontier'] / w.n:.4f}", d, flush=True)
-    prev = cur
+    curc = {k: e.kernel_bytes(k) for k in C}
+    dc = {k[1:]: int(curc[k] - prevc[k]) for k in C if curc[k] - prevc[k] > 0}
+    print(st["round"], f"F={st['frontier'] / w.n:.4f}", d, dc, flush=True)
+    prev, prevc = cur, curc
     if fin:
         break
