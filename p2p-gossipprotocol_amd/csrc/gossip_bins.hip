@@ -225,6 +225,7 @@ void free_bins(BinState* b) {
     hipFree(b->bdst);
     hipFree(b->val);
     hipFree(b->dummy);
+    hipFree(b->cb_slot);
     *b = BinState{};
 }
 
@@ -414,7 +415,8 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
             BCHECK(hipGetLastError());
         }
         BCHECK(hipStreamSynchronize(s));
-        hipFree(cb_slot);
+        if (const char* ks = std::getenv("GOSSIP_KEEP_SLOTS"); ks && std::atoi(ks)) st.cb_slot = cb_slot;  // measurement
+        else hipFree(cb_slot);
         cb_slot = nullptr;
         // (d) apply side of the streamed layout: runs sorted by first slot (keys_out / vals_out are free again)
         const uint64_t n_groups = (slots + 63) / 64 + 1;
@@ -480,6 +482,42 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
                 acc += units[i].p1 - units[i].p0;
                 while (x < 8 && acc * 8 >= upos * (uint64_t)x) xu[x++] = i + 1;
             }
+        } else if (const char* g = std::getenv("GOSSIP_BIN_ROWS"); g && std::atoi(g)) {
+            // global rows (A/B): hub chunks first, cut into units of about the mean and dealt
+            // round-robin over the XCDs; then rows of kScatterGrid consecutive chunks, XCD x taking
+            // chunks [32 x, 32 x + 32) of every row -- so the whole chip writes one contiguous region
+            // of every bin at about the same time
+            const uint64_t mean = std::max<uint64_t>(1024, upos / std::max<uint64_t>(1, n_chunks));
+            std::vector<std::vector<BinUnit>> per(8);
+            std::vector<uint32_t> reg;
+            uint64_t h = 0;
+            for (uint64_t c = 0; c < n_chunks; ++c) {
+                const uint64_t len = cbeg[c + 1] - cbeg[c];
+                if (len > kHubFactor * mean) {
+                    const uint64_t k = (len + mean - 1) / mean;
+                    for (uint64_t j = 0; j < k; ++j, ++h)
+                        per[h % 8].push_back(
+                            BinUnit{(uint32_t)c, j == 0 ? 1u : 0u, cbeg[c] + len * j / k, cbeg[c] + len * (j + 1) / k});
+                } else {
+                    reg.push_back((uint32_t)c);
+                }
+            }
+            for (auto& v : per)
+                while (v.size() % members) v.push_back(BinUnit{0u, 0u, 0, 0});
+            for (uint64_t r0 = 0; r0 < reg.size(); r0 += 8 * members)
+                for (int x = 0; x < 8; ++x)
+                    for (uint64_t j = 0; j < members; ++j) {
+                        const uint64_t i = r0 + x * members + j;
+                        if (i < reg.size())
+                            per[x].push_back(BinUnit{reg[i], 1u, cbeg[reg[i]], cbeg[reg[i] + 1]});
+                        else
+                            per[x].push_back(BinUnit{0u, 0u, 0, 0});
+                    }
+            for (int x = 0; x < 8; ++x) {
+                xu[x] = units.size();
+                units.insert(units.end(), per[x].begin(), per[x].end());
+            }
+            xu[8] = units.size();
         } else {
             const uint64_t mean = std::max<uint64_t>(1024, upos / std::max<uint64_t>(1, n_chunks));
             uint64_t c = 0, acc = 0;

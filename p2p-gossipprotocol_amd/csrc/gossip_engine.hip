@@ -75,6 +75,7 @@ struct gossip_ctx {
     uint64_t n_edges = 0;
     HeavyChunk* chunks = nullptr;
     uint64_t n_chunks = 0;
+    uint64_t* hacc = nullptr;  // k_pull_heavy's per-row found bits (n_chunks * Wp words)
     bool graph_ready = false;
 
     // dynamic state
@@ -115,6 +116,8 @@ struct gossip_ctx {
     bool symmetric = false;      // overlay is symmetric (pull rounds allowed)
     uint64_t n_started = 0;      // peers 0..n_started-1 start; the rest failed registration (list_cap, F10)
     bool nx_dirty = false;       // nx holds stale words (after a pull round)
+    bool bufs_zero = false;      // nw and nx are all zero: the last round was a single-partition push round
+                                 // that activated nobody (push_light clears the words it consumes)
     bool last_pull = false;      // mode of the round in flight
     bool last_front = false;     // pull round used the frontier bitmap
     bool in_round = false;       // between round_begin and round_compute
@@ -308,6 +311,7 @@ void free_graph(gossip_ctx* c) {
     hipFree(c->rp);
     hipFree(c->col);
     hipFree(c->chunks);
+    hipFree(c->hacc);
     // closed-form liveness state belongs to the overlay: round_begin rebuilds
     // all of it (rev included) for the next one
     hipFree(c->rev);
@@ -319,6 +323,7 @@ void free_graph(gossip_ctx* c) {
     c->rp = nullptr;
     c->col = nullptr;
     c->chunks = nullptr;
+    c->hacc = nullptr;
     c->rev = nullptr;
     c->n_edges = c->n_chunks = 0;
     c->graph_ready = false;
@@ -356,6 +361,7 @@ RoundArgs make_args(gossip_ctx* c) {
     a.cov = c->cov_hist ? c->cov_hist + (uint64_t)c->round * 64 * c->Wp : nullptr;
     a.chunks = c->chunks;
     a.n_chunks = c->n_chunks;
+    a.hacc = c->hacc;
     a.n_local = c->n_local;
     a.begin = c->begin;
     a.end = c->end;
@@ -396,6 +402,7 @@ gossip_status install_graph(gossip_ctx* c, uint64_t* d_rp, uint32_t* d_col, uint
     c->n_chunks = nch;
     if (nch) {
         HIPCHK(hipMalloc((void**)&c->chunks, nch * sizeof(HeavyChunk)));
+        HIPCHK(hipMalloc((void**)&c->hacc, nch * c->Wp * sizeof(uint64_t)));
         HIPCHK(launch_heavy_fill(c->rp, c->n_local, c->heavy, c->chunks, d_cnt + 1, c->stream));
     }
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -560,6 +567,7 @@ gossip_status rebootstrap_round(gossip_ctx* c, const RoundArgs& a) {
 // from global stats so every rank agrees; an ineligible pull falls back to
 // push, and eligibility is itself global state, so ranks still agree).
 gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) {
+    c->bufs_zero = false;  // any round may write nw / nx
     if (!c->graph_ready) return fail(GOSSIP_ESTATE, "no overlay: call gossip_build_graph or gossip_load_csr");
     if (!c->has_schedule) return fail(GOSSIP_ESTATE, "no schedule: call gossip_inject");
     if (c->finished) return fail(GOSSIP_ESTATE, "run finished: call gossip_reset");
@@ -735,7 +743,7 @@ gossip_status round_compute(gossip_ctx* c) {
                   c->bins.n_binned, c->bins.chunk_begin, c->bins.n_chunks, c->bins.chunk,    c->bins.units,
                   c->bins.xcd_units, c->bins.bdst,     c->bins.val,     c->bins.bin_words, c->bins.dummy,   c->bin_noskip || c->bins_first,
                   c->scatter_probe,  c->bins.n_runs ? c->bins.n_runs - 1 : 0, c->bins.ap_run, c->bins.ap_grp,
-                  c->bin_stream ? 1u : 0u};
+                  c->bin_stream ? 1u : 0u, c->bins.cb_slot};
         HIPCHK(timed(c, "bin_scatter", [&] { return launch_bin_scatter(a, b, pw, c->stream); }));
         HIPCHK(timed(c, "bin_apply", [&] { return launch_bin_apply(a, b, pw, c->stream); }));
         c->bins_first = false;
@@ -854,6 +862,10 @@ gossip_status advance(gossip_ctx* c, uint64_t fresh_global) {
         c->cur_defer = false;
     }
     std::swap(c->nw, c->nx);  // push: nw was cleared by push_light; pull: the old nw is stale
+    // a push round clears every word it consumes; if nobody was activated nx stayed zero too
+    // (only when this round's stats were read: frontier_est / last_fresh are then this round's)
+    c->bufs_zero = c->world <= 1 && !c->last_pull && c->last_st_round == c->round && c->frontier_est == 0 &&
+                   c->last_fresh == 0;
     c->tcur ^= 1;             // push with marks: every activation marked its tile; otherwise no marks
     c->tact_ok = !c->last_pull && c->tact_marked;
     c->nx_dirty = c->last_pull;
@@ -919,7 +931,6 @@ gossip_status gossip_create(const gossip_config* cfg, gossip_ctx** out) {
     if (const char* u = std::getenv("GOSSIP_PULL_UNROLL")) c->pull_unroll = std::atoi(u);
     if (const char* u = std::getenv("GOSSIP_PULL_NT"); u && std::atoi(u)) c->pull_unroll |= kPullNT;
     if (const char* u = std::getenv("GOSSIP_PULL_ROWS"); !u || std::atoi(u)) c->pull_unroll |= kPullRows;
-    if (const char* u = std::getenv("GOSSIP_ROW_B")) c->pull_unroll |= (std::atoi(u) & 7) << 12;
     if (const char* h = std::getenv("GOSSIP_HEAVY_DEGREE")) c->heavy = (uint32_t)std::max(1, std::atoi(h));
     if (const char* u = std::getenv("GOSSIP_BIN_NOSKIP"); u && std::atoi(u)) c->bin_noskip = true;
     if (const char* u = std::getenv("GOSSIP_SCATTER_PROBE")) c->scatter_probe = (uint32_t)std::atoi(u);
@@ -1201,9 +1212,12 @@ gossip_status gossip_reset(gossip_ctx* c) {
     hipStream_t s = c->stream;
     const uint64_t words = c->n_local * c->Wp;
     const uint64_t bitwords = (c->n + 31) / 32;
-    HIPCHK(hipMemsetAsync(c->seen, 0, words * 8, s));
-    HIPCHK(hipMemsetAsync(c->nw, 0, words * 8, s));
-    HIPCHK(hipMemsetAsync(c->nx, 0, words * 8, s));
+    HIPCHK(launch_zero_words(c->seen, words, s));
+    if (!c->bufs_zero) {  // (a run that ended normally left both zero)
+        HIPCHK(launch_zero_words(c->nw, words, s));
+        HIPCHK(launch_zero_words(c->nx, words, s));
+        c->bufs_zero = true;
+    }
     for (int k = 0; k < 2; ++k) HIPCHK(hipMemsetAsync(c->tact[k], 0, tact_bytes(c), s));
     c->tact_ok = true;  // no new words anywhere
     c->tact_marked = false;

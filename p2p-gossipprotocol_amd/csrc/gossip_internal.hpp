@@ -30,8 +30,8 @@ constexpr int kStatFields = 20;
 static_assert(sizeof(DevStats) == kStatFields * 8, "DevStats layout");
 
 struct HeavyChunk {
-    uint32_t v;    // local row
-    uint32_t pad;
+    uint32_t v;      // local row
+    uint32_t first;  // index of the row's first chunk (the row's word in RoundArgs.hacc)
     uint64_t e0, e1;
 };
 
@@ -83,6 +83,7 @@ struct BinArgs {
     const uint32_t* ap_run;       // per run, in slot order: slot - cb position (as cb_run)
     const uint32_t* ap_grp;       // per 64-slot group: runs that start before the group
     uint32_t stream;              // 1: streamed layout, 0: val in slot order (k_bin_scatter_*)
+    const uint32_t* cb_slot;      // measurement only (GOSSIP_KEEP_SLOTS=1): the slot of every cb entry
 };
 
 struct BinState {
@@ -102,6 +103,7 @@ struct BinState {
     uint16_t* bdst = nullptr;
     uint64_t* val = nullptr;
     uint64_t* dummy = nullptr;
+    uint32_t* cb_slot = nullptr;  // GOSSIP_KEEP_SLOTS=1 only (k_bin_scatter_flat)
     uint32_t bin_words = kBinWords;
     uint64_t n_slots = 0;   // padded
     uint64_t n_binned = 0;  // edges with a slot (light destinations)
@@ -158,6 +160,9 @@ struct RoundArgs {
     uint32_t* dgone;               // n_local: out-edges whose target has died (masked or not)
     uint32_t* dmask;               // n_local: out-edges masked by liveness
     uint32_t* rev;                 // n_edges: rev[e] for e = (v -> u) is the position of v in u's row
+    // k_pull_heavy: per heavy row (at its first chunk) the bits its chunks have found so far this
+    // round, n_chunks * Wp words cleared per launch; a chunk stops once they cover the row's need
+    uint64_t* hacc;
 };
 
 // Re-bootstrap draw (handleDeadPeer peer.cpp:398-404 -> selectAndConnectPeers
@@ -213,6 +218,7 @@ hipError_t launch_rejoin(const RoundArgs& a, uint32_t W, uint32_t seed, uint32_t
 hipError_t launch_rejoin_select(const RoundArgs& a, const RebootArgs& r, const uint32_t* list,
                                 const unsigned long long* n_list, uint64_t max_list, hipStream_t s);
 hipError_t launch_commit_nx(uint64_t* seen, const uint64_t* nx, uint64_t n_words, hipStream_t s);
+hipError_t launch_zero_words(uint64_t* words, uint64_t n_words, hipStream_t s);
 hipError_t launch_coverage(const uint64_t* words, uint64_t n_local, uint32_t W, unsigned long long* counts,
                            hipStream_t s);
 hipError_t launch_heavy_count(const uint64_t* rp, uint64_t n_local, uint32_t heavy, unsigned long long* n_chunks,

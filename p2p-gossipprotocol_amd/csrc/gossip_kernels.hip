@@ -775,26 +775,42 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
     const uint64_t n_tiles = (a.n_local + 63) >> 6;
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
     uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
-    auto sweep_tile = [&](uint64_t tt) {
+    // the sweep is a chain of two round trips per tile (the peer words, then the
+    // row bounds of the rows that matter); each wave keeps the next tile's
+    // words and row bounds in flight while it sweeps the current one
+    // (unconditional loads, clamped past the end)
+    struct TileIn {
+        uint64_t m[W], sv[W], r0, r1;
+        uint32_t al;
+    };
+    auto load_tile = [&](uint64_t tt, TileIn& d) {
+        const uint64_t v = min((tt << 6) + lane, a.n_local - 1);
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            d.m[w] = a.nw[v * W + w];
+            d.sv[w] = a.seen[v * W + w];
+        }
+        d.r0 = a.rp[v];
+        d.r1 = a.rp[v + 1];
+        d.al = a.dead_mode ? a.alive[(uint32_t)(a.begin + v) >> 5] : ~0u;
+    };
+    auto sweep_tile = [&](uint64_t tt, const TileIn& d) {
         const uint64_t v = (tt << 6) + lane;
         const bool vv = v < a.n_local;
         uint64_t m[W], nd[W];
         bool act = false, needy = false;
-        const bool va = vv && (!a.dead_mode || bit_alive(a.alive, (uint32_t)(a.begin + v)));  // dead: no receive
+        const bool va = vv && (!a.dead_mode || ((d.al >> ((uint32_t)(a.begin + v) & 31)) & 1u));  // dead: no receive
 #pragma unroll
         for (int w = 0; w < W; ++w) {
-            m[w] = vv ? a.nw[v * W + w] : 0ull;
-            const uint64_t sv = vv ? a.seen[v * W + w] : ~0ull;
+            m[w] = vv ? d.m[w] : 0ull;
+            const uint64_t sv = vv ? d.sv[w] : ~0ull;
             nd[w] = va ? a.inj_mask[w] & ~sv : 0ull;
             act |= m[w] != 0;
             needy |= nd[w] != 0;
             if (vv) a.nx[v * W + w] = 0ull;  // nx is written whole in a pull round; rows that learn rewrite it
         }
-        uint64_t rb = 0, d = 0;
-        if (act || needy) {
-            rb = a.rp[v];
-            d = a.rp[v + 1] - rb;
-        }
+        const uint64_t rb = d.r0, d_ = d.r1 - d.r0;
+        const uint64_t dg = (act || needy) ? d_ : 0ull;
         if (act) {  // source side of this peer's pushes (broadcastMessage, peer.cpp:310-316)
             uint32_t pc = 0;
 #pragma unroll
@@ -807,33 +823,37 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
             acc.frontier++;
             acc.covered += pc;
             if (!a.dead_mode) {  // every edge alive and unmasked
-                acc.trav += d;
-                acc.deliv += (unsigned long long)pc * d;
+                acc.trav += dg;
+                acc.deliv += (unsigned long long)pc * dg;
             } else if (a.dgone) {  // from the per-source counters; else k_src_count books them
                 const uint32_t g = a.dgone[v], k = a.dmask[v];
-                acc.trav += d - k;
-                acc.deliv += (unsigned long long)pc * (d - g);
+                acc.trav += dg - k;
+                acc.deliv += (unsigned long long)pc * (dg - g);
                 acc.undeliv += (unsigned long long)pc * (g - k);
             }
         }
-        const bool enq = needy && d > 0 && d <= a.heavy;  // heavy rows: k_pull_heavy
+        const bool enq = needy && dg > 0 && dg <= a.heavy;  // heavy rows: k_pull_heavy
         const unsigned long long bal = __ballot(enq);
         if (enq) {
             const uint32_t pos = (q_tail + (uint32_t)__builtin_amdgcn_mbcnt_hi(
                                                (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))) %
                                  kRowQ;
             qv[pos] = (uint32_t)v;
-            qd[pos] = (uint32_t)d;
+            qd[pos] = (uint32_t)dg;
             qrb[pos] = rb;
 #pragma unroll
             for (int w = 0; w < W; ++w) qneed[pos * W + w] = nd[w];
         }
         q_tail += (uint32_t)__popcll(bal);
     };
+    TileIn nxt;
+    if (t < n_tiles) load_tile(t, nxt);
     while (true) {
         // refill the queue while it has room for a whole tile
         while (t < n_tiles && q_tail - q_head <= (uint32_t)(kRowQ - 64)) {
-            sweep_tile(t);
+            const TileIn cur = nxt;
+            if (t + nwaves < n_tiles) load_tile(t + nwaves, nxt);
+            sweep_tile(t, cur);
             t += nwaves;
         }
         // idle lanes take queued rows
@@ -929,10 +949,11 @@ __global__ __launch_bounds__(kBlock) void k_pull_heavy(RoundArgs a) {
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
     for (uint64_t ci = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); ci < a.n_chunks; ci += nwaves) {
         const HeavyChunk ch = a.chunks[ci];
-        uint64_t need[W], part[W];
+        uint64_t need[W], part[W], pub[W];  // pub: bits this chunk has published in hacc
         bool any = false;
 #pragma unroll
         for (int w = 0; w < W; ++w) {
+            pub[w] = 0;
             // one lane reads, every lane uses the same value: the branch below stays wave-uniform
             const uint64_t s0 = __shfl(a.seen[(uint64_t)ch.v * W + w], 0);
             need[w] = a.inj_mask[w] & ~s0;
@@ -965,6 +986,19 @@ __global__ __launch_bounds__(kBlock) void k_pull_heavy(RoundArgs a) {
                     uint64_t x = part[w];
 #pragma unroll
                     for (int off = 32; off > 0; off >>= 1) x |= __shfl_xor(x, off);
+                    // what the row's other chunks found: publish ours (it is committed to seen at
+                    // this chunk's end, so every published bit reaches seen) and read theirs
+                    if (a.hacc) {
+                        unsigned long long* hw =
+                            reinterpret_cast<unsigned long long*>(a.hacc) + (uint64_t)ch.first * W + w;
+                        unsigned long long o = 0;
+                        if (lane == 0)
+                            o = (x & need[w] & ~pub[w]) ? atomicOr(hw, (unsigned long long)(x & need[w]))
+                                                        : __hip_atomic_load(hw, __ATOMIC_RELAXED,
+                                                                            __HIP_MEMORY_SCOPE_AGENT);
+                        pub[w] |= x & need[w];
+                        x |= __shfl(o, 0);
+                    }
                     done &= (x & need[w]) == need[w];
                 }
                 if (done) break;  // wave-uniform (x is the wave's OR)
@@ -1381,6 +1415,50 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_pc(RoundArgs a, B
         for (int i = threadIdx.x; i < 64 * W; i += kScatterBlock)
             if (cov_s[i]) atomicAdd(&a.cov[i], (unsigned long long)cov_s[i]);
     }
+}
+
+// Measurement only (GOSSIP_SCATTER_PC=9 with GOSSIP_KEEP_SLOTS=1): the slot of
+// every cb entry read from a kept u32 array, kD 64-entry groups per wave in
+// flight, stores by the same wave -- the store pattern of the binned scatter
+// with the least load-side work in front of it.
+template <int W, int kD>
+__global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_flat(RoundArgs a, BinArgs b, uint32_t wd) {
+    constexpr int kWaves = kScatterBlock / 64;
+    __shared__ unsigned long long slice[kBinChunkWords];
+    __shared__ unsigned long long live_s[kBinChunkWords / 64 / W];
+    Acc acc;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t nb = (uint32_t)b.n_binned;
+    scatter_rows(b, [&](const uint64_t ui) {
+        const BinUnit un = b.units[ui];
+        if (un.p0 >= un.p1 && !un.first) return;
+        scatter_stage<W, false>(a, b, un, wd, slice, live_s, nullptr, acc);
+        __syncthreads();
+        if (un.p0 >= un.p1 || b.probe == 1) return;
+        const uint32_t p0 = (uint32_t)un.p0, p1 = (uint32_t)un.p1;
+        const uint32_t g_hi = ((p1 - 1) >> 6) + 1;
+        for (uint32_t g = (p0 >> 6) + wave; g < g_hi; g += kWaves * kD) {
+            uint32_t sl[kD], sv[kD];
+#pragma unroll
+            for (int j = 0; j < kD; ++j) {
+                const uint32_t q = min((g + kWaves * j) * 64 + lane, nb - 1);
+                sl[j] = b.cb_slot[q];
+                sv[j] = b.cb_src[q];
+            }
+#pragma unroll
+            for (int j = 0; j < kD; ++j) {
+                const uint32_t q = (g + kWaves * j) * 64 + lane;
+                const uint32_t u = sv[j] & (kRunStart - 1u);
+                const bool live = (live_s[u >> 6] >> (u & 63)) & 1ull;
+                if (q >= p0 && q < p1 && live) {
+#pragma unroll
+                    for (int w = 0; w < W; ++w) b.val[(uint64_t)sl[j] * W + w] = slice[u * W + w];
+                    acc.gathered++;
+                }
+            }
+        }
+    });
+    flush<kWaves>(acc, a.st);
 }
 
 // Phase 2: one workgroup per bin folds the bin's slots into an LDS
@@ -2321,6 +2399,13 @@ __global__ __launch_bounds__(kBlock) void k_commit_nx(u64x2* seen, const u64x2* 
     }
 }
 
+// reset: zero a word array with 16-B stores (hipMemsetAsync's fill kernel
+// reached ~2.6 TB/s on the 2 GB arrays of config 4)
+__global__ __launch_bounds__(kBlock) void k_zero2(u64x2* p, uint64_t n2) {
+    const u64x2 z = {0ull, 0ull};
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n2; i += (uint64_t)gridDim.x * kBlock) p[i] = z;
+}
+
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_coverage(const uint64_t* words, uint64_t n, unsigned long long* counts) {
     __shared__ unsigned int cnt[64 * W];
@@ -2355,7 +2440,7 @@ __global__ void k_heavy_fill(const uint64_t* rp, uint64_t n, uint32_t heavy, Hea
         const unsigned long long at = atomicAdd(cursor, (unsigned long long)nc);
         for (uint64_t k = 0; k < nc; ++k) {
             const uint64_t e0 = b + k * kHeavyChunk;
-            chunks[at + k] = HeavyChunk{(uint32_t)v, 0u, e0, e0 + kHeavyChunk < e ? e0 + kHeavyChunk : e};
+            chunks[at + k] = HeavyChunk{(uint32_t)v, (uint32_t)at, e0, e0 + kHeavyChunk < e ? e0 + kHeavyChunk : e};
         }
     }
 }
@@ -2487,12 +2572,9 @@ hipError_t launch_pull_light(const RoundArgs& a, uint32_t W_, int unroll, hipStr
     const uint32_t wd = wd_of(W_);
     if (unroll & kPullRows) {  // row queue: every wave resident at once (its queue carries its work)
         const unsigned gr = std::min(g, (unsigned)kMaxGrid);
-        const int rb = (unroll & ~(kPullRows | kPullNT)) >> 12;  // edges per step (GOSSIP_ROW_B), default 2
 #define GOSSIP_ROWS(COV, FR)                                                                                    \
         do {                                                                                                    \
-            if (rb == 1) hipLaunchKernelGGL((k_pull_rows<W, COV, FR, 1>), dim3(gr), dim3(kBlock), 0, s, a, wd);  \
-            else if (rb == 4) hipLaunchKernelGGL((k_pull_rows<W, COV, FR, 4>), dim3(gr), dim3(kBlock), 0, s, a, wd); \
-            else hipLaunchKernelGGL((k_pull_rows<W, COV, FR, 2>), dim3(gr), dim3(kBlock), 0, s, a, wd);          \
+            hipLaunchKernelGGL((k_pull_rows<W, COV, FR, 2>), dim3(gr), dim3(kBlock), 0, s, a, wd);               \
         } while (0)
         GOSSIP_DISPATCH_W(wp_of(W_), {
             if (a.cov) { if (a.front) GOSSIP_ROWS(true, true); else GOSSIP_ROWS(true, false); }
@@ -2525,6 +2607,10 @@ hipError_t launch_pull_light(const RoundArgs& a, uint32_t W_, int unroll, hipStr
 
 hipError_t launch_pull_heavy(const RoundArgs& a, uint32_t W_, hipStream_t s) {
     if (!a.n_chunks) return hipSuccess;
+    if (a.hacc) {
+        const hipError_t e = hipMemsetAsync(a.hacc, 0, a.n_chunks * wp_of(W_) * sizeof(uint64_t), s);
+        if (e != hipSuccess) return e;
+    }
     GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_pull_heavy<W>, dim3(grid_for(a.n_chunks, kWavesPerBlock)),
                                                    dim3(kBlock), 0, s, a));
     return hipGetLastError();
@@ -2581,6 +2667,11 @@ hipError_t launch_bin_scatter(const RoundArgs& a, const BinArgs& b, uint32_t W_,
             if (a.cov) hipLaunchKernelGGL((k_bin_stream<W, true>), dim3(kScatterGrid), dim3(kScatterBlock), 0, s, a, b, wd);
             else hipLaunchKernelGGL((k_bin_stream<W, false>), dim3(kScatterGrid), dim3(kScatterBlock), 0, s, a, b, wd);
         });
+        return hipGetLastError();
+    }
+    if (scatter_pc() == 9 && b.cb_slot) {
+        GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_scatter_flat<W, 8>), dim3(kScatterGrid),
+                                                       dim3(kScatterBlock), 0, s, a, b, wd));
         return hipGetLastError();
     }
     if (const int v = scatter_pc()) {
@@ -2708,6 +2799,13 @@ hipError_t launch_commit_nx(uint64_t* seen, const uint64_t* nx, uint64_t n_words
     const uint64_t n2 = (n_words + 1) / 2;  // the word arrays are allocated in whole pairs
     hipLaunchKernelGGL(k_commit_nx, dim3(grid_for(n2, kBlock)), dim3(kBlock), 0, s, reinterpret_cast<u64x2*>(seen),
                        reinterpret_cast<const u64x2*>(nx), n2);
+    return hipGetLastError();
+}
+
+hipError_t launch_zero_words(uint64_t* words, uint64_t n_words, hipStream_t s) {
+    const uint64_t n2 = (n_words + 1) / 2;  // the word arrays are allocated in whole pairs
+    if (!n2) return hipSuccess;
+    hipLaunchKernelGGL(k_zero2, dim3(grid_for(n2, kBlock)), dim3(kBlock), 0, s, reinterpret_cast<u64x2*>(words), n2);
     return hipGetLastError();
 }
 
