@@ -61,6 +61,8 @@ struct TimerRec {
 
 }  // namespace
 
+constexpr uint32_t kDeferAuto = 0xFFFFFFFFu;  // defer_pm: chosen per round (round_begin)
+
 struct gossip_ctx {
     gossip_config cfg{};
     int device = 0;
@@ -154,8 +156,10 @@ struct gossip_ctx {
     bool heavy_exit = true;       // k_pull_heavy early exit (GOSSIP_HEAVY_EXIT=0: off, A/B)
     bool bin_stream = false;      // streamed binned layout (GOSSIP_BIN_STREAM=1; A/B: 1-1.5 ms per binned
                                   // round slower at config 4)
-    uint32_t defer_pm = 0;        // push rounds with a frontier of >= this per-mille defer the seen update
-                                  // (GOSSIP_DEFER_PM; 0: never -- measured slower at config 4, A/B only)
+    uint32_t defer_pm = kDeferAuto;  // push rounds with a frontier of >= this per-mille defer the seen update
+                                     // (GOSSIP_DEFER_PM; 0: never; auto: 10 where the fold can be fused)
+    bool fold_pending = false;    // a deferred round's receipts (now nw) are not yet in seen: the next
+                                  // binned round's apply folds them in, anything else commits first
     bool pull_diag = false;       // GOSSIP_PULL_DIAG: count the gathers of an early-exit row scan (measurement)
     bool cur_defer = false;       // this round defers: advance() folds nx into seen
     bool full_liveness = false;  // GOSSIP_FULL_LIVENESS: ping every edge each ping round (A/B against closed form)
@@ -190,6 +194,7 @@ struct gossip_ctx {
 
 namespace gossip {
 hipStream_t ctx_stream(gossip_ctx* c) { return c->stream; }
+
 int ctx_device(gossip_ctx* c) { return c->device; }
 const gossip_config& ctx_config(gossip_ctx* c) { return c->cfg; }
 void ctx_range(gossip_ctx* c, uint64_t* begin, uint64_t* end) {
@@ -513,6 +518,14 @@ gossip_status prepare_bins(gossip_ctx* c) {
     return GOSSIP_OK;
 }
 
+// seen |= nw for a deferred round whose fold was left to the next binned round
+gossip_status settle_fold(gossip_ctx* c) {
+    if (!c->fold_pending) return GOSSIP_OK;
+    c->fold_pending = false;
+    HIPCHK(timed(c, "commit", [&] { return launch_commit_nx(c->seen, c->nw, c->n_local * c->Wp, c->stream); }));
+    return GOSSIP_OK;
+}
+
 uint32_t kills_in_round(const gossip_ctx* c, uint32_t r, uint32_t* first) {
     auto lo = std::lower_bound(c->kill_round_sorted.begin(), c->kill_round_sorted.end(), r);
     auto hi = std::upper_bound(c->kill_round_sorted.begin(), c->kill_round_sorted.end(), r);
@@ -584,6 +597,11 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
             RoundArgs r0 = make_args(c);
             HIPCHK(launch_reverse_edges(r0, c->stream));
         }
+    }
+    if (c->fold_pending) {  // kills and churn book a dying peer's words: seen must hold them first
+        uint32_t kf = 0;
+        if (c->cfg.rejoin_threshold || c->cfg.churn_threshold || kills_in_round(c, c->round, &kf))
+            if (gossip_status fs = settle_fold(c)) return fs;
     }
     RoundArgs a = make_args(c);
     const uint32_t pw = pack_w(c);
@@ -681,8 +699,21 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
     // a wide push round (the explosion before the dense rounds) is bound by memory-side atomics, two per
     // fresh delivery (seen, then nx); deferring the seen update halves them for one streamed pass
     // (k_commit_nx).  A per-rank choice: results do not depend on it.
-    c->cur_defer = !pull && c->defer_pm && (c->frontier_est + cnt) * 1000 >= c->n_local * (uint64_t)c->defer_pm;
+    // Auto: only where the fold can ride on the next binned round's apply (one partition, the
+    // slot layout, no churn); config 4 round 3: push 5.6 -> 4.1 ms, the 1.3 ms fold pass removed.
+    const bool fusable = c->world <= 1 && !remote && c->bins_ready && !c->bin_stream && !c->cfg.churn_threshold &&
+                         !c->cfg.rejoin_threshold && requested == GOSSIP_MODE_AUTO;
+    const uint32_t dpm = c->defer_pm == kDeferAuto ? (fusable ? 10u : 0u) : c->defer_pm;
+    c->cur_defer = !pull && dpm && (c->frontier_est + cnt) * 1000 >= c->n_local * (uint64_t)dpm;
     a.defer = c->cur_defer ? 1u : 0u;
+    if (c->fold_pending) {  // the previous round deferred: its receipts are this round's nw
+        if (bin && !c->bin_stream && c->world <= 1 && !remote) {
+            a.fold = 1;  // k_bin_apply folds them (before k_pull_heavy reads seen)
+            c->fold_pending = false;
+        } else if (gossip_status fs = settle_fold(c)) {
+            return fs;
+        }
+    }
     c->last_pull = pull;
     c->last_bin = bin;
     c->last_front = false;
@@ -857,11 +888,16 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
 }
 
 gossip_status advance(gossip_ctx* c, uint64_t fresh_global) {
+    bool pend = false;
     if (c->cur_defer) {  // every delivery of the round is in nx (remote applies included): fold it into seen
-        HIPCHK(timed(c, "commit", [&] { return launch_commit_nx(c->seen, c->nx, c->n_local * c->Wp, c->stream); }));
+        if (c->world <= 1 && c->bins_ready && !c->bin_stream)
+            pend = true;  // after the swap, in nw: the next round folds it (settle_fold / k_bin_apply)
+        else
+            HIPCHK(timed(c, "commit", [&] { return launch_commit_nx(c->seen, c->nx, c->n_local * c->Wp, c->stream); }));
         c->cur_defer = false;
     }
-    std::swap(c->nw, c->nx);  // push: nw was cleared by push_light; pull: the old nw is stale
+    std::swap(c->nw, c->nx);
+    c->fold_pending = pend;  // push: nw was cleared by push_light; pull: the old nw is stale
     // a push round clears every word it consumes; if nobody was activated nx stayed zero too
     // (only when this round's stats were read: frontier_est / last_fresh are then this round's)
     c->bufs_zero = c->world <= 1 && !c->last_pull && c->last_st_round == c->round && c->frontier_est == 0 &&
@@ -1212,6 +1248,7 @@ gossip_status gossip_reset(gossip_ctx* c) {
     hipStream_t s = c->stream;
     const uint64_t words = c->n_local * c->Wp;
     const uint64_t bitwords = (c->n + 31) / 32;
+    c->fold_pending = false;  // seen is cleared
     HIPCHK(launch_zero_words(c->seen, words, s));
     if (!c->bufs_zero) {  // (a run that ended normally left both zero)
         HIPCHK(launch_zero_words(c->nw, words, s));
@@ -1414,6 +1451,7 @@ gossip_status gossip_round_commit(gossip_ctx* c, uint64_t global_new_receipts, i
 gossip_status gossip_read_seen(gossip_ctx* c, uint64_t* out) {
     if (!c || !out) return fail(GOSSIP_EINVAL, "null argument");
     if (set_dev(c)) return GOSSIP_EHIP;
+    if (gossip_status fs = settle_fold(c)) return fs;
     HIPCHK(hipStreamSynchronize(c->stream));
     if (c->W == c->Wp) {
         HIPCHK(hipMemcpy(out, c->seen, c->n_local * c->W * 8, hipMemcpyDeviceToHost));
@@ -1429,6 +1467,7 @@ gossip_status gossip_read_seen(gossip_ctx* c, uint64_t* out) {
 gossip_status gossip_read_coverage(gossip_ctx* c, uint64_t* counts) {
     if (!c || !counts) return fail(GOSSIP_EINVAL, "null argument");
     if (set_dev(c)) return GOSSIP_EHIP;
+    if (gossip_status fs = settle_fold(c)) return fs;
     unsigned long long* d = nullptr;
     HIPCHK(hipMalloc((void**)&d, 64 * c->Wp * 8));
     HIPCHK(hipMemsetAsync(d, 0, 64 * c->Wp * 8, c->stream));

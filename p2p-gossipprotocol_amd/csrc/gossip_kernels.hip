@@ -1309,15 +1309,9 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_pc(RoundArgs a, B
     auto ld_prod = [&](int p) { return __hip_atomic_load(&prod_cnt[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
     auto ld_cons = [&] { return __hip_atomic_load(&cons_cnt[pair], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
     const unsigned long long below = (lane == 63 ? ~0ull : ((2ull << lane) - 1)) & ~1ull;  // lanes 1..lane
-    auto scatter_unit = [&](const uint64_t ui) {
-        const BinUnit un = b.units[ui];
-        if (un.p0 >= un.p1 && !un.first) return;  // padding of a row (block-uniform)
-        scatter_stage<W, COV>(a, b, un, wd, slice, live_s, cov_s, acc);
-        if (threadIdx.x < kPcProd) prod_cnt[threadIdx.x] = cons_cnt[threadIdx.x] = 0;
-        __syncthreads();
-        if (b.probe == 1) return;
+    auto run = [&](const uint64_t p0_, const uint64_t p1_) {
         // positions fit 32 bits (build_bins: fewer than kNoSlot edges)
-        const uint32_t p0 = (uint32_t)un.p0, p1 = (uint32_t)un.p1, nb = (uint32_t)b.n_binned;
+        const uint32_t p0 = (uint32_t)p0_, p1 = (uint32_t)p1_, nb = (uint32_t)b.n_binned;
         if (p0 >= p1) return;  // block-uniform; nb >= 1 below
         const uint32_t g0 = p0 >> 6, n_groups = ((p1 - 1) >> 6) - g0 + 1;
         // producer p's groups: g0 + p + kPcProd * i, i < items(p)
@@ -1412,6 +1406,15 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_pc(RoundArgs a, B
             }
         }
     };
+    auto scatter_unit = [&](const uint64_t ui) {
+        const BinUnit un = b.units[ui];
+        if (un.p0 >= un.p1 && !un.first) return;  // padding of a row (block-uniform)
+        scatter_stage<W, COV>(a, b, un, wd, slice, live_s, cov_s, acc);
+        if (threadIdx.x < kPcProd) prod_cnt[threadIdx.x] = cons_cnt[threadIdx.x] = 0;
+        __syncthreads();
+        if (b.probe == 1) return;
+        run(un.p0, un.p1);
+    };
     scatter_rows(b, scatter_unit);
     static_assert(sizeof(ring_slot) >= kWaves * kStatFields * 8, "stat scratch fits the ring");
     __syncthreads();  // the ring is idle
@@ -1478,14 +1481,20 @@ __global__ __launch_bounds__(kB) void k_bin_apply(RoundArgs a, BinArgs b) {
     const Bin bn = b.bins[blockIdx.x];
     const uint32_t nv = bn.v1 - bn.v0;
     const uint64_t v0 = bn.v0;
+    // a.fold: the previous (deferred) push round's receipts are this round's new words and not yet
+    // in seen; every peer of the bin (heavy rows included) gets seen |= nw here, before k_pull_heavy
+    auto pend = [&](uint32_t i) { return a.fold ? a.nw[v0 * W + i] : 0ull; };
     bool needy = false;
     for (uint32_t i = threadIdx.x; i < nv * W; i += kB) {
         acc_s[i] = 0ull;
         const bool va = !a.dead_mode || bit_alive(a.alive, (uint32_t)(a.begin + v0 + i / W));
-        needy |= va && (a.inj_mask[i % W] & ~a.seen[v0 * W + i]) != 0;
+        needy |= va && (a.inj_mask[i % W] & ~(a.seen[v0 * W + i] | pend(i))) != 0;
     }
     if (!__syncthreads_or(needy)) {
-        for (uint32_t i = threadIdx.x; i < nv * W; i += kB) a.nx[v0 * W + i] = 0ull;
+        for (uint32_t i = threadIdx.x; i < nv * W; i += kB) {
+            a.nx[v0 * W + i] = 0ull;
+            if (const uint64_t p = pend(i)) a.seen[v0 * W + i] |= p;
+        }
         flush<kB / 64>(acc, a.st);
         return;
     }
@@ -1512,14 +1521,15 @@ __global__ __launch_bounds__(kB) void k_bin_apply(RoundArgs a, BinArgs b) {
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < nv * W; i += kB) {
-        const uint64_t sv = a.seen[v0 * W + i];
+        const uint64_t p = pend(i);
+        const uint64_t sv = a.seen[v0 * W + i] | p;
         const bool va = !a.dead_mode || bit_alive(a.alive, (uint32_t)(a.begin + v0 + i / W));  // dead: no receive
         const uint64_t fr = va ? acc_s[i] & a.inj_mask[i % W] & ~sv : 0ull;
         if (fr) {  // handleClient: new -> Message-List insert (peer.cpp:281-282)
-            a.seen[v0 * W + i] = sv | fr;
             acc.fresh += (unsigned long long)__popcll(fr);
             acc.activated++;
         }
+        if (fr | p) a.seen[v0 * W + i] = sv | fr;
         a.nx[v0 * W + i] = fr;  // heavy rows: 0 here, OR-ed by k_pull_heavy afterwards
     }
     flush<kB / 64>(acc, a.st);

@@ -324,3 +324,28 @@ def test_engine_variants_match_oracle(oracle, monkeypatch, env, idx, n, mode):
             e.schedule_kills([k[0] for k in w.kills], [k[1] for k in w.kills])
         e.reset()
         _compare(e, ref, w)
+
+
+@pytest.mark.parametrize("env", [None, "GOSSIP_DEFER_PM=10"])
+@pytest.mark.parametrize("stop", [3, 4, 5])
+def test_deferred_round_fold(oracle, monkeypatch, env, stop):
+    """Auto mode defers the seen update of the wide push round before the binned
+    rounds (config 3 shape: round 2 here) and leaves the fold to the next
+    binned round's apply.  A run stopped by max_rounds right after the deferred
+    round, or after the fused fold, must still read the oracle's seen set and
+    coverage; the explicit switch forces the same deferral (committed when the
+    fold cannot be fused)."""
+    if env:
+        k, v = env.split("=")
+        monkeypatch.setenv(k, v)
+    w = config(3, 1 << 18, pick=oracle.pick_origins)
+    rp, col = oracle.gen_workload(w)
+    ref = oracle.simulate_workload(w, rp, col, max_rounds=stop)
+    with Engine(w.n, w.n_msgs, max_rounds=stop, **w.engine_kwargs()) as e:
+        e.build_graph()
+        e.inject(w.origins, w.inject_rounds)
+        e.reset()
+        got = e.run()
+        assert got == ref["stats"]
+        assert np.array_equal(e.read_seen(), ref["seen"])
+        assert np.array_equal(e.coverage(), ref["coverage"])
