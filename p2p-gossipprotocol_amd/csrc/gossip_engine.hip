@@ -152,7 +152,8 @@ struct gossip_ctx {
     bool bins_first = false;             // no binned round since the last reset: rewrite every slot
     bool bin_noskip = false;     // GOSSIP_BIN_NOSKIP: rewrite every slot each binned round (A/B measurement)
     uint32_t scatter_probe = 0;  // GOSSIP_SCATTER_PROBE: partial scatter for timing breakdowns (wrong results)
-    uint32_t bin_front_pm = 100;  // binned rounds need a frontier of >= this per-mille (GOSSIP_BIN_FRONT_PM)
+    uint32_t bin_front_pm = 0;    // binned rounds need a frontier of >= this per-mille (GOSSIP_BIN_FRONT_PM;
+                                  // 0: 100, or 20 from 2^25 owned peers on -- see round_begin)
     bool heavy_exit = true;       // k_pull_heavy early exit (GOSSIP_HEAVY_EXIT=0: off, A/B)
     bool bin_stream = false;      // streamed binned layout (GOSSIP_BIN_STREAM=1; A/B: 1-1.5 ms per binned
                                   // round slower at config 4)
@@ -680,19 +681,27 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
     // mode while many (peer, message) pairs are still missing -- then nearly
     // every edge has to be looked at and streaming beats gathering.
     bool bin = pull && c->bins_ready && requested == GOSSIP_MODE_BIN;  // driver-chosen (partitioned runs)
+    // (peer, message) pairs still missing at push start (P = 1: the own counters are global)
+    uint64_t missing = 0;
+    {
+        uint64_t injected = 0;
+        for (int w = 0; w < kMaxWords; ++w) injected += (uint64_t)__builtin_popcountll(a.inj_mask[w]);
+        const uint64_t have = c->cum_covered + c->last_fresh + cnt;
+        const uint64_t total = injected * c->n_local;
+        missing = total > have ? total - have : 0;
+    }
     if (!remote && pull_ok && c->bins_ready && requested == GOSSIP_MODE_AUTO) {
         if (c->cfg.flags & GOSSIP_FLAG_FORCE_BIN) {
             pull = bin = true;
         } else if (pull && !(c->cfg.flags & GOSSIP_FLAG_FORCE_PULL)) {
-            uint64_t injected = 0;
-            for (int w = 0; w < kMaxWords; ++w) injected += (uint64_t)__builtin_popcountll(a.inj_mask[w]);
-            const uint64_t have = c->cum_covered + c->last_fresh + cnt;
-            const uint64_t total = injected * c->n_local;
-            const uint64_t missing = total > have ? total - have : 0;
             const uint32_t bpm = c->cfg.bin_permille ? c->cfg.bin_permille : 4000;
+            // a narrow frontier is cheaper to gather from while the frontier bitmap (n bits) stays in an
+            // XCD's 4 MB L2; beyond 2^25 peers its probes go to the MALL: config 5 (2^26, round 3 at an 8 %
+            // frontier) pull 8.6 ms against 4.0 binned; config 2 (2^20, a 5 % round) pull 0.18 against 0.33
+            const uint32_t front_pm = c->bin_front_pm ? c->bin_front_pm : c->n_local >= (1ull << 25) ? 20u : 100u;
             // and only on a wide frontier: a narrow one is cheaper to gather from (frontier bitmap)
             bin = missing * 1000 >= c->n_local * (uint64_t)bpm &&
-                  (c->frontier_est + cnt) * 1000 >= c->n_local * (uint64_t)c->bin_front_pm;
+                  (c->frontier_est + cnt) * 1000 >= c->n_local * (uint64_t)front_pm;
         }
     }
     c->cur_sparse = !pull && remote && requested == GOSSIP_MODE_PUSH_SPARSE && c->seg != nullptr;
@@ -731,9 +740,12 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
             a.nw_src = c->gather;
             a.n_src = c->n;
         }
-        // frontier bitmap only when enough neighbours are outside the frontier to pay for the probe
+        // frontier bitmap only when enough neighbours are outside the frontier to pay for the probe, and
+        // enough rows are still needy to pay for building it (a pass over every new word): config 4
+        // round 8 built it (0.45 ms) to save 2.7 K of 1.78 M gathers
         const uint32_t fpm = c->cfg.front_permille ? c->cfg.front_permille : 400;
-        if (!bin && requested == GOSSIP_MODE_AUTO && (c->frontier_est + cnt) * 1000 < c->n_local * (uint64_t)fpm) {
+        if (!bin && requested == GOSSIP_MODE_AUTO && (c->frontier_est + cnt) * 1000 < c->n_local * (uint64_t)fpm &&
+            (remote || c->cfg.front_permille || missing * 16 >= c->n_local)) {
             a.front = c->front;
             c->last_front = true;
         } else {

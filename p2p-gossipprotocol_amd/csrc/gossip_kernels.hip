@@ -1283,8 +1283,15 @@ __device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)"
 
 // kPcProd producer waves, the other 16 - kPcProd consume; consumer c serves the
 // producers p = c (mod consumers) in turn.  kPcG: groups a producer resolves per
-// pipeline stage; kPcRing: ring slots (64 entries each) per producer.
-template <int W, bool COV, int kPcProd, int kPcG, int kPcRing>
+// pipeline stage; kPcRing: ring slots (64 entries each) per producer; kPcSets:
+// register sets a producer rotates through -- a stage's cb entries are loaded
+// kPcSets - 1 stages before its hand-over and its slots resolved (cb_run
+// loads issued) (kPcSets - 1) / 2 stages before it.  Deeper rotations were
+// measured and dropped (config 4, per launch, one box: 3 sets 9.2-9.4 ms, 5
+// sets 9.6, 7 sets 16.0, 9 sets of one group 11.6): the 1024-thread block
+// caps a wave at 128 VGPRs, and the extra sets spill (scratch 52 -> 104-208
+// bytes per lane).
+template <int W, bool COV, int kPcProd, int kPcG, int kPcRing, int kPcSets>
 __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_pc(RoundArgs a, BinArgs b, uint32_t wd) {
     constexpr int kWaves = kScatterBlock / 64;
     constexpr int kPcCons = kWaves - kPcProd;
@@ -1309,7 +1316,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_pc(RoundArgs a, B
     auto ld_prod = [&](int p) { return __hip_atomic_load(&prod_cnt[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
     auto ld_cons = [&] { return __hip_atomic_load(&cons_cnt[pair], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
     const unsigned long long below = (lane == 63 ? ~0ull : ((2ull << lane) - 1)) & ~1ull;  // lanes 1..lane
-    auto run = [&](const uint64_t p0_, const uint64_t p1_) {
+    auto run = [&](const uint64_t p0_, const uint64_t p1_, const uint32_t un_c) {
         // positions fit 32 bits (build_bins: fewer than kNoSlot edges)
         const uint32_t p0 = (uint32_t)p0_, p1 = (uint32_t)p1_, nb = (uint32_t)b.n_binned;
         if (p0 >= p1) return;  // block-uniform; nb >= 1 below
@@ -1319,14 +1326,21 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_pc(RoundArgs a, B
         const uint32_t n_items = items(pair);
         if (producer) {
             const uint32_t n_grp = (nb + 63) >> 6;
-            // three register sets: loads of stage j+2 | run resolution of j+1 | hand-over of j
-            uint32_t sv[3][kPcG], gr[3][kPcG], rv[3][kPcG], uu[3][kPcG];
+            // register sets: loads of stage j+N-1 | run resolution of j+L | hand-over of j
+            constexpr int N = kPcSets, L = (kPcSets - 1) / 2;
+            static_assert(N >= 3, "load, resolve and hand-over each need a set");
+            uint32_t sv[N][kPcG], gr[N][kPcG], rv[N][kPcG], uu[N][kPcG];
             auto load = [&](int set, uint32_t j) {  // stage j = items j*kPcG .. j*kPcG + kPcG - 1
 #pragma unroll
                 for (int t = 0; t < kPcG; ++t) {
                     const uint32_t i = j * kPcG + t;
                     const uint32_t g = min(g0 + pair + kPcProd * i, n_grp - 1);  // clamped past the end
                     const uint32_t q = g * 64 + lane;
+                    if (b.probe == 4) {  // measurement: no loads (synthetic slots in resolve)
+                        sv[set][t] = q & 0x3FFFu;  // a source inside the chunk
+                        gr[set][t] = 0;
+                        continue;
+                    }
                     sv[set][t] = (uint32_t)__builtin_nontemporal_load(b.cb_src + min(q, nb - 1));
                     gr[set][t] = b.cb_grp[g];
                 }
@@ -1344,6 +1358,12 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_pc(RoundArgs a, B
                     uu[set][t] = u | (act << 15);
                     const unsigned long long starts = __ballot((v & kRunStart) != 0);
                     const uint32_t run = gr[set][t] + (uint32_t)__popcll(starts & below);
+                    if (b.probe == 4) {  // runs of 9 slots: chunk c's run in bin k at k * 9 * n_chunks + 9 c
+                        const uint32_t k = (q - p0) / 9u % (uint32_t)b.n_bins;
+                        rv[set][t] = min((uint64_t)k * 9 * b.n_chunks + 9ull * un_c + (q - p0) % 9u, b.n_binned - 1);
+                        uu[set][t] = (uu[set][t] & 0x7FFFu) | ((uint32_t)(i < n_items && q >= p0 && q < p1) << 15);
+                        continue;
+                    }
                     rv[set][t] = q + b.cb_run[min(run, (uint32_t)b.n_runs_m1)];  // the slot
                 }
             };
@@ -1364,22 +1384,20 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_pc(RoundArgs a, B
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
             };
             const uint32_t n_stages = (n_items + kPcG - 1) / kPcG;
-            load(0, 0);
-            load(1, 1);
-            resolve(0, 0);
-            for (uint32_t j = 0; j < n_stages; j += 3) {  // sets rotate 0,1,2 with no register copies
-                load(2, j + 2);
-                resolve(1, j + 1);
-                hand_over(0, j);
-                if (j + 1 >= n_stages) break;
-                load(0, j + 3);
-                resolve(2, j + 2);
-                hand_over(1, j + 1);
-                if (j + 2 >= n_stages) break;
-                load(1, j + 4);
-                resolve(0, j + 3);
-                hand_over(2, j + 2);
+#pragma unroll
+            for (int k = 0; k < N - 1; ++k) load(k, k);
+#pragma unroll
+            for (int k = 0; k < L; ++k) resolve(k, k);
+            for (uint32_t j = 0;; j += N) {  // sets rotate with no register copies (unrolled: constant indices)
+#pragma unroll
+                for (int k = 0; k < N; ++k) {
+                    load((k + N - 1) % N, j + k + N - 1);
+                    resolve((k + L) % N, j + k + L);
+                    hand_over(k, j + k);
+                    if (j + k + 1 >= n_stages) goto produced;
+                }
             }
+        produced:;
         } else {
             const uint32_t n_max = items(pair);  // the first producer served has the most items
             for (uint32_t i = 0; i < n_max; ++i) {
@@ -1413,7 +1431,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_pc(RoundArgs a, B
         if (threadIdx.x < kPcProd) prod_cnt[threadIdx.x] = cons_cnt[threadIdx.x] = 0;
         __syncthreads();
         if (b.probe == 1) return;
-        run(un.p0, un.p1);
+        run(un.p0, un.p1, un.c);
     };
     scatter_rows(b, scatter_unit);
     static_assert(sizeof(ring_slot) >= kWaves * kStatFields * 8, "stat scratch fits the ring");
@@ -2691,17 +2709,17 @@ hipError_t launch_bin_scatter(const RoundArgs& a, const BinArgs& b, uint32_t W_,
         return hipGetLastError();
     }
     if (const int v = scatter_pc()) {
-#define GOSSIP_PC(P, G, R)                                                                                 \
+#define GOSSIP_PC(P, G, R, N)                                                                              \
         do {                                                                                               \
-            if (a.cov) hipLaunchKernelGGL((k_bin_scatter_pc<W, true, P, G, R>), dim3(kScatterGrid),          \
+            if (a.cov) hipLaunchKernelGGL((k_bin_scatter_pc<W, true, P, G, R, N>), dim3(kScatterGrid),       \
                                           dim3(kScatterBlock), 0, s, a, b, wd);                            \
-            else hipLaunchKernelGGL((k_bin_scatter_pc<W, false, P, G, R>), dim3(kScatterGrid),               \
+            else hipLaunchKernelGGL((k_bin_scatter_pc<W, false, P, G, R, N>), dim3(kScatterGrid),            \
                                     dim3(kScatterBlock), 0, s, a, b, wd);                                  \
         } while (0)
         GOSSIP_DISPATCH_W(wp_of(W_), {
-            if (v == 2) GOSSIP_PC(12, 2, 2);
-            else if (v == 4) GOSSIP_PC(8, 4, 4);
-            else GOSSIP_PC(8, 2, 4);
+            if (v == 2) GOSSIP_PC(12, 2, 2, 3);
+            else if (v == 4) GOSSIP_PC(8, 4, 4, 3);
+            else GOSSIP_PC(8, 2, 4, 3);
         });
 #undef GOSSIP_PC
         return hipGetLastError();
