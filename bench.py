@@ -54,8 +54,9 @@ def parse():
 
 
 # kernel timer name -> rocprofv3 kernel-name prefix in the PMC summary
-PMC_KERNELS = {"bin_scatter": "k_bin_scatter_pc", "bin_apply": "k_bin_apply", "pull_light": "k_pull_light",
-               "push_light": "k_push_light", "push_heavy": "k_push_heavy", "pull_heavy": "k_pull_heavy"}
+PMC_KERNELS = {"bin_scatter": ("k_bin_scatter_pc",), "bin_apply": ("k_bin_apply",),
+               "pull_light": ("k_pull_rows", "k_pull_light"),  # the row-queue pull is the default
+               "push_light": ("k_push_light",), "push_heavy": ("k_push_heavy",), "pull_heavy": ("k_pull_heavy",)}
 
 
 def pmc_traffic(workload: str, kernel: str, alg_bytes_per_launch: float, n_local: int):
@@ -76,7 +77,7 @@ def pmc_traffic(workload: str, kernel: str, alg_bytes_per_launch: float, n_local
     if path is None:
         return None, None
     prof = json.loads(path.read_text())
-    keys = [k for k in prof["kernels"] if k.startswith(PMC_KERNELS[kernel] + "<") or k == PMC_KERNELS[kernel]]
+    keys = [k for k in prof["kernels"] if any(k.startswith(p + "<") or k == p for p in PMC_KERNELS[kernel])]
     keys = [k for k in keys if "fetch_bytes_per_launch_counted" in prof["kernels"][k]]
     if not keys:
         return None, None

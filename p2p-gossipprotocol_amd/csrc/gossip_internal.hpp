@@ -76,8 +76,7 @@ struct BinArgs {
     uint64_t* dummy;              // kScatterGrid * kScatterBlock * Wp words: stores of lanes with no slot
     uint32_t noskip;              // every slot is rewritten: first binned round after a reset (or GOSSIP_BIN_NOSKIP)
     uint32_t probe;               // measurement only (GOSSIP_SCATTER_PROBE=1: staging only, 2: slot stores to the
-                                  // sink, 3: stores in cb order, 4: no cb loads, synthetic 9-slot runs in the
-                                  // layout's geometry; results are then wrong)
+                                  // sink, 3: stores in cb order; results are then wrong)
     uint64_t n_runs_m1;           // cb_run entries - 1 (clamp for the run index of past-the-end lanes)
     // streamed layout (the default): val is in cb order, written front to back by k_bin_stream; the
     // apply walks its bin's slots and finds each value through the run of the slot

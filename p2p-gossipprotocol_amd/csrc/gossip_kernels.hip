@@ -1316,7 +1316,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_pc(RoundArgs a, B
     auto ld_prod = [&](int p) { return __hip_atomic_load(&prod_cnt[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
     auto ld_cons = [&] { return __hip_atomic_load(&cons_cnt[pair], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
     const unsigned long long below = (lane == 63 ? ~0ull : ((2ull << lane) - 1)) & ~1ull;  // lanes 1..lane
-    auto run = [&](const uint64_t p0_, const uint64_t p1_, const uint32_t un_c) {
+    auto run = [&](const uint64_t p0_, const uint64_t p1_) {
         // positions fit 32 bits (build_bins: fewer than kNoSlot edges)
         const uint32_t p0 = (uint32_t)p0_, p1 = (uint32_t)p1_, nb = (uint32_t)b.n_binned;
         if (p0 >= p1) return;  // block-uniform; nb >= 1 below
@@ -1336,11 +1336,6 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_pc(RoundArgs a, B
                     const uint32_t i = j * kPcG + t;
                     const uint32_t g = min(g0 + pair + kPcProd * i, n_grp - 1);  // clamped past the end
                     const uint32_t q = g * 64 + lane;
-                    if (b.probe == 4) {  // measurement: no loads (synthetic slots in resolve)
-                        sv[set][t] = q & 0x3FFFu;  // a source inside the chunk
-                        gr[set][t] = 0;
-                        continue;
-                    }
                     sv[set][t] = (uint32_t)__builtin_nontemporal_load(b.cb_src + min(q, nb - 1));
                     gr[set][t] = b.cb_grp[g];
                 }
@@ -1358,12 +1353,6 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_pc(RoundArgs a, B
                     uu[set][t] = u | (act << 15);
                     const unsigned long long starts = __ballot((v & kRunStart) != 0);
                     const uint32_t run = gr[set][t] + (uint32_t)__popcll(starts & below);
-                    if (b.probe == 4) {  // runs of 9 slots: chunk c's run in bin k at k * 9 * n_chunks + 9 c
-                        const uint32_t k = (q - p0) / 9u % (uint32_t)b.n_bins;
-                        rv[set][t] = min((uint64_t)k * 9 * b.n_chunks + 9ull * un_c + (q - p0) % 9u, b.n_binned - 1);
-                        uu[set][t] = (uu[set][t] & 0x7FFFu) | ((uint32_t)(i < n_items && q >= p0 && q < p1) << 15);
-                        continue;
-                    }
                     rv[set][t] = q + b.cb_run[min(run, (uint32_t)b.n_runs_m1)];  // the slot
                 }
             };
@@ -1431,7 +1420,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_pc(RoundArgs a, B
         if (threadIdx.x < kPcProd) prod_cnt[threadIdx.x] = cons_cnt[threadIdx.x] = 0;
         __syncthreads();
         if (b.probe == 1) return;
-        run(un.p0, un.p1, un.c);
+        run(un.p0, un.p1);
     };
     scatter_rows(b, scatter_unit);
     static_assert(sizeof(ring_slot) >= kWaves * kStatFields * 8, "stat scratch fits the ring");

@@ -4,7 +4,8 @@
 //   seq      : wave instruction = 512 contiguous bytes, grid-stride sweep
 //   seq16    : 16 B per lane (dwordx4), 1 KiB per instruction
 //   run L    : 64/L runs of L consecutive words per instruction, each run at a
-//              random word offset (L = 1 .. 64); "run L a64": runs 64-B aligned
+//              random word offset (L = 1 .. 64); "run L a64": runs 64-B aligned,
+//              "run L a32": 32-B aligned (is the memory's write atom 32 or 64 B?)
 //   rw       : seq stores with a 1/3-size coalesced read stream interleaved
 // Build: hipcc -O3 --offload-arch=gfx950 -o tools/calib_store tools/calib_store.hip
 #include <hip/hip_runtime.h>
@@ -23,7 +24,7 @@ __global__ void k_seq16(uint4* p, uint64_t n) {
         p[i] = make_uint4((unsigned)i, 1u, 2u, 3u);
 }
 
-template <int L, bool A64>
+template <int L, int A>  // A: run alignment in words (1, 4 or 8)
 __global__ void k_run(uint64_t* p, uint64_t n_words, uint64_t iters) {
     const int lane = threadIdx.x & 63;
     uint64_t h = ((uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63) + 1) * 0x9E3779B97F4A7C15ull;
@@ -35,7 +36,7 @@ __global__ void k_run(uint64_t* p, uint64_t n_words, uint64_t iters) {
         g ^= g >> 32;
         g *= 0x9E3779B97F4A7C15ull;
         uint64_t base = (g >> 20) % (n_words - 64);
-        if (A64) base &= ~7ull;
+        base &= ~(uint64_t)(A - 1);
         p[base + (lane % L)] = h;
     }
 }
@@ -85,8 +86,9 @@ int main() {
         const uint64_t iters = words / ((uint64_t)grid * 256);
         const double wb = (double)iters * grid * 256 * 8;
 #define RUN(L)                                                                                                 \
-        timeit("run " #L, wb, [&] { hipLaunchKernelGGL((k_run<L, false>), dim3(grid), dim3(256), 0, 0, p, words, iters); }); \
-        timeit("run " #L " a64", wb, [&] { hipLaunchKernelGGL((k_run<L, true>), dim3(grid), dim3(256), 0, 0, p, words, iters); });
+        timeit("run " #L, wb, [&] { hipLaunchKernelGGL((k_run<L, 1>), dim3(grid), dim3(256), 0, 0, p, words, iters); }); \
+        timeit("run " #L " a32", wb, [&] { hipLaunchKernelGGL((k_run<L, 4>), dim3(grid), dim3(256), 0, 0, p, words, iters); }); \
+        timeit("run " #L " a64", wb, [&] { hipLaunchKernelGGL((k_run<L, 8>), dim3(grid), dim3(256), 0, 0, p, words, iters); });
         RUN(1) RUN(4) RUN(8) RUN(16) RUN(32) RUN(64)
     }
     hipFree(p);
