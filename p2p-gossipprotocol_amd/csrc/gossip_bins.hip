@@ -238,8 +238,13 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
     uint32_t bin_words = kBinWords;
     if (const char* bw = std::getenv("GOSSIP_BIN_WORDS"))
         bin_words = std::max<uint32_t>(512, std::min<uint32_t>(kBinWords, (uint32_t)std::atoi(bw) / 512 * 512));
-    const uint32_t max_peers = bin_words / Wp;  // a multiple of 64 for Wp <= 8
-    const uint64_t slot_cap = kBinSlotCap * bin_words / kBinWords;
+    // split: a bin of up to `split` accumulator-sized parts (destination ids stay below 2^16 in bdst);
+    // the streamed layout keeps one part (its bdst bit 15 flags runs)
+    uint32_t split = 1;
+    if (const char* e = std::getenv("GOSSIP_BIN_SPLIT"); e && !stream)
+        split = std::max<uint32_t>(1, std::min<uint32_t>(65535u / (bin_words / Wp), (uint32_t)std::atoi(e)));
+    const uint32_t max_peers = split * (bin_words / Wp);  // a multiple of 64 for Wp <= 8
+    const uint64_t slot_cap = split * (kBinSlotCap * bin_words / kBinWords);
     uint32_t* tile_slots = nullptr;
     unsigned long long* light_bits = nullptr;
     uint32_t* bin_of_tile = nullptr;
@@ -341,6 +346,7 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
 
     st.n_bins = h_bins.size();
     st.bin_words = bin_words;
+    st.split = split;
     st.n_slots = slots;
     st.n_binned = upos;
     st.n_chunks = n_chunks;

@@ -786,7 +786,7 @@ gossip_status round_compute(gossip_ctx* c) {
                   c->bins.n_binned, c->bins.chunk_begin, c->bins.n_chunks, c->bins.chunk,    c->bins.units,
                   c->bins.xcd_units, c->bins.bdst,     c->bins.val,     c->bins.bin_words, c->bins.dummy,   c->bin_noskip || c->bins_first,
                   c->scatter_probe,  c->bins.n_runs ? c->bins.n_runs - 1 : 0, c->bins.ap_run, c->bins.ap_grp,
-                  c->bin_stream ? 1u : 0u, c->bins.cb_slot};
+                  c->bin_stream ? 1u : 0u, c->bins.cb_slot, c->bins.split};
         HIPCHK(timed(c, "bin_scatter", [&] { return launch_bin_scatter(a, b, pw, c->stream); }));
         HIPCHK(timed(c, "bin_apply", [&] { return launch_bin_apply(a, b, pw, c->stream); }));
         c->bins_first = false;

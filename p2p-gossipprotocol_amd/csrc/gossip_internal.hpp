@@ -84,6 +84,9 @@ struct BinArgs {
     const uint32_t* ap_grp;       // per 64-slot group: runs that start before the group
     uint32_t stream;              // 1: streamed layout, 0: val in slot order (k_bin_scatter_*)
     const uint32_t* cb_slot;      // measurement only (GOSSIP_KEEP_SLOTS=1): the slot of every cb entry
+    uint32_t split;               // a bin holds `split` parts of bin_words / Wp peers; its slots (in source
+                                  // order over the whole bin, so the scatter's runs are `split` times longer)
+                                  // are applied by `split` workgroups, each keeping its own part's slots
 };
 
 struct BinState {
@@ -105,6 +108,7 @@ struct BinState {
     uint64_t* dummy = nullptr;
     uint32_t* cb_slot = nullptr;  // GOSSIP_KEEP_SLOTS=1 only (k_bin_scatter_flat)
     uint32_t bin_words = kBinWords;
+    uint32_t split = 1;     // parts per bin (GOSSIP_BIN_SPLIT)
     uint64_t n_slots = 0;   // padded
     uint64_t n_binned = 0;  // edges with a slot (light destinations)
 };

@@ -1485,9 +1485,21 @@ template <int W, int kWords, int kB>  // kWords: LDS accumulator words; kB: thre
 __global__ __launch_bounds__(kB) void k_bin_apply(RoundArgs a, BinArgs b) {
     __shared__ unsigned long long acc_s[kWords];
     Acc acc;
-    const Bin bn = b.bins[blockIdx.x];
-    const uint32_t nv = bn.v1 - bn.v0;
-    const uint64_t v0 = bn.v0;
+    // workgroup -> (bin, part): a bin of b.split parts is applied by b.split workgroups, each keeping
+    // the slots of its own part's peers; the parts of a bin go to one XCD (block ids 8 apart, which the
+    // dispatcher deals to the same XCD) so that their reads of the bin's slots meet in its L2
+    uint32_t bi = blockIdx.x, part = 0;
+    if (b.split > 1) {
+        const uint32_t r = blockIdx.x >> 3;
+        part = r % b.split;
+        bi = r / b.split * 8 + (blockIdx.x & 7);
+    }
+    if (bi >= b.n_bins) return;  // (whole workgroup, before any barrier)
+    const Bin bn = b.bins[bi];
+    const uint32_t part_peers = b.bin_words / W, lo = part * part_peers;
+    if (lo >= bn.v1 - bn.v0) return;
+    const uint32_t nv = min(bn.v1 - bn.v0 - lo, part_peers);
+    const uint64_t v0 = bn.v0 + lo;
     // a.fold: the previous (deferred) push round's receipts are this round's new words and not yet
     // in seen; every peer of the bin (heavy rows included) gets seen |= nw here, before k_pull_heavy
     auto pend = [&](uint32_t i) { return a.fold ? a.nw[v0 * W + i] : 0ull; };
@@ -1505,7 +1517,7 @@ __global__ __launch_bounds__(kB) void k_bin_apply(RoundArgs a, BinArgs b) {
         flush<kB / 64>(acc, a.st);
         return;
     }
-    if (threadIdx.x == 0) acc.pulled = bn.s1 - bn.s0;  // slots scanned (byte accounting)
+    if (threadIdx.x == 0 && part == 0) acc.pulled = bn.s1 - bn.s0;  // slots scanned (byte accounting)
     // 8 slots per lane per step: 16 B of bdst, 64*W B of val
     for (uint64_t i = bn.s0 + (uint64_t)threadIdx.x * 8; i < bn.s1; i += (uint64_t)kB * 8) {
         const uint4 dd = *reinterpret_cast<const uint4*>(b.bdst + i);
@@ -1520,7 +1532,8 @@ __global__ __launch_bounds__(kB) void k_bin_apply(RoundArgs a, BinArgs b) {
         const uint32_t dw[4] = {dd.x, dd.y, dd.z, dd.w};
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const uint32_t dl = (dw[k >> 1] >> ((k & 1) * 16)) & (kRunStart - 1u);  // (bit 15: run start)
+            const uint32_t dl = ((dw[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu) - lo;  // destination in this part
+            if (dl >= nv) continue;  // another part's slot (padding slots hold zero words)
 #pragma unroll
             for (int w = 0; w < W; ++w)
                 if (x[k * W + w]) atomicOr(&acc_s[dl * W + w], (unsigned long long)x[k * W + w]);
@@ -2735,11 +2748,13 @@ hipError_t launch_bin_apply(const RoundArgs& a, const BinArgs& b, uint32_t W_, h
         }
         return hipGetLastError();
     }
+    // split bins: the parts of bin i at block ids 8 (i / 8 * split + part) + i % 8
+    const unsigned grid = (unsigned)(b.split > 1 ? (b.n_bins + 7) / 8 * 8 * b.split : b.n_bins);
     if (b.bin_words > kBinWords / 2) {  // up to 144 KB accumulators: one 16-wave workgroup per CU
-        GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_apply<W, kBinWords, 1024>), dim3((unsigned)b.n_bins),
-                                                       dim3(1024), 0, s, a, b));
+        GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_apply<W, kBinWords, 1024>), dim3(grid), dim3(1024), 0,
+                                                       s, a, b));
     } else {  // 64 KB accumulators: two 4-wave workgroups per CU
-        GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_apply<W, kBinWords / 2, kBlock>), dim3((unsigned)b.n_bins),
+        GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_apply<W, kBinWords / 2, kBlock>), dim3(grid),
                                                        dim3(kBlock), 0, s, a, b));
     }
     return hipGetLastError();
