@@ -741,11 +741,12 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
             a.n_src = c->n;
         }
         // frontier bitmap only when enough neighbours are outside the frontier to pay for the probe, and
-        // enough rows are still needy to pay for building it (a pass over every new word): config 4
-        // round 8 built it (0.45 ms) to save 2.7 K of 1.78 M gathers
+        // enough pairs are still missing to pay for building it (a pass over every new word): config 4
+        // round 8 (under 0.1 missing pairs per peer) built it (0.45 ms) to save 2.7 K of 1.78 M gathers --
+        // its few needy rows stop after a gather or two, at hubs that are in the frontier anyway
         const uint32_t fpm = c->cfg.front_permille ? c->cfg.front_permille : 400;
         if (!bin && requested == GOSSIP_MODE_AUTO && (c->frontier_est + cnt) * 1000 < c->n_local * (uint64_t)fpm &&
-            (remote || c->cfg.front_permille || missing * 16 >= c->n_local)) {
+            (remote || c->cfg.front_permille || missing * 4 >= c->n_local)) {
             a.front = c->front;
             c->last_front = true;
         } else {
