@@ -252,11 +252,8 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
     uint32_t *keys_in = nullptr, *vals_in = nullptr, *keys_out = nullptr, *vals_out = nullptr;
     uint32_t* row = nullptr;
     uint32_t* cb_slot = nullptr;  // per cb entry, until the run encoding is built
-    uint64_t chunk_words = kBinChunkWords;
-    if (const char* c = std::getenv("GOSSIP_BIN_CHUNK"))
-        chunk_words = std::max<uint64_t>(512, std::min<uint64_t>(kBinChunkWords, std::strtoull(c, nullptr, 0) / 512 * 512));
-    const uint64_t chunk = std::max<uint64_t>(64, chunk_words / Wp);
-    const uint64_t n_chunks = (n_global + chunk - 1) / chunk;
+    // source chunk (chosen once the bins are known, below)
+    uint64_t chunk_words = kBinChunkWords, chunk = 0, n_chunks = 0;
     void* temp = nullptr;
     size_t temp_bytes = 0;
     BinState st;
@@ -298,6 +295,20 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
         h_bins.push_back(b);
     }
     while ((1ull << (end_bit - 32)) <= h_bins.size()) ++end_bit;
+    // Source chunk: the whole LDS slice, unless a quarter of it or less still gives runs of about 32
+    // entries (run ≈ binned edges · |chunk| · |bin| / (n_local · n_global)); then that (a multiple of
+    // 512 words, at least 1024), so the scatter has several units per CU.  Config 2 (2^20): 57 whole
+    // chunks left 199 of the 256 CUs idle (scatter 10.6 -> 3.5-3.7 ms per step with 1024-word chunks);
+    // config 3 (2^24): 2.95-2.99 -> 2.54-2.57 ms with 4096; config 5 (2^26, runs of ≈ 35 at the whole
+    // slice) measured 12.5 against 14.4 ms with 16896-word chunks, so near-full chunks stay whole.
+    if (upos) {
+        const double want = 32.0 * (double)n_global * (double)n_local / ((double)upos * (double)(bin_words / Wp)) * Wp;
+        if (want * 4 <= (double)kBinChunkWords) chunk_words = std::max<uint64_t>(1024, ((uint64_t)want + 511) / 512 * 512);
+    }
+    if (const char* c = std::getenv("GOSSIP_BIN_CHUNK"))
+        chunk_words = std::max<uint64_t>(512, std::min<uint64_t>(kBinChunkWords, std::strtoull(c, nullptr, 0) / 512 * 512));
+    chunk = std::max<uint64_t>(64, chunk_words / Wp);
+    n_chunks = (n_global + chunk - 1) / chunk;
     if (n_chunks * h_bins.size() >= kNoSlot) {
         if (err) *err = "too many (chunk, bin) pairs for 32-bit keys";
         rc = hipErrorInvalidValue;
