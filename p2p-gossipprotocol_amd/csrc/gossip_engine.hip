@@ -160,7 +160,11 @@ struct gossip_ctx {
     uint32_t defer_pm = kDeferAuto;  // push rounds with a frontier of >= this per-mille defer the seen update
                                      // (GOSSIP_DEFER_PM; 0: never; auto: 10 where the fold can be fused)
     bool fold_pending = false;    // a deferred round's receipts (now nw) are not yet in seen: the next
-                                  // binned round's apply folds them in, anything else commits first
+                                  // binned round's apply or row-pull sweep folds them in, anything else
+                                  // commits first
+    bool cur_pdefer = false;      // this (wide) pull round stores only nx for the rows that learn
+    bool pdefer_ok = false;       // GOSSIP_PULL_DEFER=1: defer wide pull rounds (A/B: config 4 round 7 -0.3 to
+                                  // -0.75 ms, round 8's fold +0.5 to +0.7 ms, so off by default)
     bool pull_diag = false;       // GOSSIP_PULL_DIAG: count the gathers of an early-exit row scan (measurement)
     bool cur_defer = false;       // this round defers: advance() folds nx into seen
     bool full_liveness = false;  // GOSSIP_FULL_LIVENESS: ping every edge each ping round (A/B against closed form)
@@ -715,14 +719,22 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
     const uint32_t dpm = c->defer_pm == kDeferAuto ? (fusable ? 10u : 0u) : c->defer_pm;
     c->cur_defer = !pull && dpm && (c->frontier_est + cnt) * 1000 >= c->n_local * (uint64_t)dpm;
     a.defer = c->cur_defer ? 1u : 0u;
+    const bool rows_pull = pull && !bin && (c->pull_unroll & kPullRows) && !c->pull_diag;  // k_pull_rows
     if (c->fold_pending) {  // the previous round deferred: its receipts are this round's nw
-        if (bin && !c->bin_stream && c->world <= 1 && !remote) {
-            a.fold = 1;  // k_bin_apply folds them (before k_pull_heavy reads seen)
+        if (((bin && !c->bin_stream) || rows_pull) && c->world <= 1 && !remote) {
+            a.fold = 1;  // k_bin_apply / k_pull_rows's sweep folds them (before k_pull_heavy reads seen)
             c->fold_pending = false;
         } else if (gossip_status fs = settle_fold(c)) {
             return fs;
         }
     }
+    // a wide pull round whose rows learn a lot (config 4 round 7: 90 M rows) stores each learning row's
+    // seen word at random; deferred (GOSSIP_PULL_DEFER=1), the next round (dense: pull or binned) folds
+    // nx into seen in its sweep or apply.  Only while the frontier is wide (>= 40 %) and >= 1 pair per
+    // 4 peers is still missing.  Measured even (the fold's stores cost what the row stores did).
+    c->cur_pdefer = rows_pull && c->world <= 1 && !remote && !c->any_dead && requested == GOSSIP_MODE_AUTO &&
+                    c->pdefer_ok && (c->frontier_est + cnt) * 1000 >= c->n_local * 400ull && missing * 4 >= c->n_local;
+    a.pdefer = c->cur_pdefer ? 1u : 0u;
     c->last_pull = pull;
     c->last_bin = bin;
     c->last_front = false;
@@ -901,7 +913,8 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
 }
 
 gossip_status advance(gossip_ctx* c, uint64_t fresh_global) {
-    bool pend = false;
+    bool pend = c->cur_pdefer;  // a deferred pull round: nx, swapped into nw below, is not yet in seen
+    c->cur_pdefer = false;
     if (c->cur_defer) {  // every delivery of the round is in nx (remote applies included): fold it into seen
         if (c->world <= 1 && c->bins_ready && !c->bin_stream)
             pend = true;  // after the swap, in nw: the next round folds it (settle_fold / k_bin_apply)
@@ -986,6 +999,7 @@ gossip_status gossip_create(const gossip_config* cfg, gossip_ctx** out) {
     if (const char* u = std::getenv("GOSSIP_BIN_FRONT_PM")) c->bin_front_pm = (uint32_t)std::atoi(u);
     if (const char* u = std::getenv("GOSSIP_HEAVY_EXIT")) c->heavy_exit = std::atoi(u) != 0;
     if (const char* u = std::getenv("GOSSIP_DEFER_PM")) c->defer_pm = (uint32_t)std::atoi(u);
+    if (const char* u = std::getenv("GOSSIP_PULL_DEFER")) c->pdefer_ok = std::atoi(u) != 0;
     if (const char* u = std::getenv("GOSSIP_BIN_STREAM")) c->bin_stream = std::atoi(u) != 0;
     if (const char* u = std::getenv("GOSSIP_PULL_DIAG")) c->pull_diag = std::atoi(u) != 0;
     if (const char* u = std::getenv("GOSSIP_FULL_LIVENESS"); u && std::atoi(u)) c->full_liveness = true;
@@ -1314,7 +1328,7 @@ gossip_status gossip_reset(gossip_ctx* c) {
     c->nx_dirty = false;
     c->last_pull = false;
     c->last_bin = false;
-    c->cur_defer = false;
+    c->cur_defer = c->cur_pdefer = false;
     c->last_fresh = 0;
     c->frontier_est = c->prev_frontier_est = 0;
     c->round = 0;

@@ -149,8 +149,11 @@ struct RoundArgs {
     uint32_t defer;                // push round with a deferred seen update: deliveries test against the
                                    // round-start seen and OR the unseen bits into nx only (one atomic per
                                    // delivery); k_commit_nx folds nx into seen after the round
-    uint32_t fold;                 // binned round after a deferred push round: seen lacks this round's new
-                                   // words (nw); the apply folds them in (seen | nw) for every owned peer
+    uint32_t fold;                 // round after a deferred round: seen lacks this round's new words (nw);
+                                   // k_bin_apply, or k_pull_rows's sweep, folds them in (seen | nw) for
+                                   // every owned peer before anything else of the round reads seen
+    uint32_t pdefer;               // wide pull round (k_pull_rows): a row that learns stores only its nx
+                                   // word; its seen word is folded in by the next round (a.fold)
     uint64_t* front;               // pull rounds: 1 bit per source peer, set iff its new words are nonzero
     const uint64_t* nw_src;        // pull rounds: new words of every source, indexed by (global) peer id
     uint64_t n_src;                // peers covered by nw_src / front

@@ -806,7 +806,11 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
 #pragma unroll
         for (int w = 0; w < W; ++w) {
             m[w] = vv ? d.m[w] : 0ull;
-            const uint64_t sv = vv ? d.sv[w] : ~0ull;
+            // a.fold: the previous round's receipts (this round's new words) are not yet in seen; the
+            // sweep folds them in (the peers with new words of the tile) -- before the tile's rows are
+            // queued, so their own later stores come after it
+            const uint64_t sv = vv ? (a.fold ? d.sv[w] | m[w] : d.sv[w]) : ~0ull;
+            if (a.fold && vv && m[w]) a.seen[v * W + w] = sv;
             nd[w] = va ? a.inj_mask[w] & ~sv : 0ull;
             act |= m[w] != 0;
             needy |= nd[w] != 0;
@@ -930,7 +934,8 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
             for (int w = 0; w < W; ++w) {
                 const uint64_t fr = got[w];  // subset of need: bits this peer had not seen
                 if (fr) {
-                    a.seen[(uint64_t)rv * W + w] = (a.inj_mask[w] & ~need[w]) | fr;  // seen is within inj_mask
+                    // a.pdefer: the next round folds nx into seen (a random 8-B store saved per row)
+                    if (!a.pdefer) a.seen[(uint64_t)rv * W + w] = (a.inj_mask[w] & ~need[w]) | fr;  // within inj_mask
                     a.nx[(uint64_t)rv * W + w] = fr;
                     acc.fresh += (unsigned long long)__popcll(fr);
                     any = true;

@@ -306,7 +306,7 @@ def test_reload_overlay_with_kills(oracle, mode):
 
 
 @pytest.mark.parametrize("env", ["GOSSIP_DEFER_PM=1", "GOSSIP_BIN_STREAM=1", "GOSSIP_PULL_ROWS=0", "GOSSIP_BIN_SPLIT=2",
-                                 "GOSSIP_BIN_SPLIT=3"])
+                                 "GOSSIP_BIN_SPLIT=3", "GOSSIP_PULL_DEFER=1", "GOSSIP_BIN_PERMILLE=100000"])
 @pytest.mark.parametrize("idx,n,mode", [(2, 1 << 16, "auto"), (3, 1 << 18, "bin"), (5, 50_000, "auto"),
                                         (5, 1 << 16, "push"), (3, 1 << 18, "pull")])
 def test_engine_variants_match_oracle(oracle, monkeypatch, env, idx, n, mode):
@@ -327,17 +327,19 @@ def test_engine_variants_match_oracle(oracle, monkeypatch, env, idx, n, mode):
         _compare(e, ref, w)
 
 
-@pytest.mark.parametrize("env", [None, "GOSSIP_DEFER_PM=10"])
-@pytest.mark.parametrize("stop", [3, 4, 5])
+@pytest.mark.parametrize("env", [None, "GOSSIP_DEFER_PM=10", "GOSSIP_PULL_DEFER=1",
+                                 "GOSSIP_PULL_DEFER=1 GOSSIP_BIN_PERMILLE=100000"])
+@pytest.mark.parametrize("stop", [3, 4, 5, 6, 7, 8])
 def test_deferred_round_fold(oracle, monkeypatch, env, stop):
     """Auto mode defers the seen update of the wide push round before the binned
-    rounds (config 3 shape: round 2 here) and leaves the fold to the next
-    binned round's apply.  A run stopped by max_rounds right after the deferred
-    round, or after the fused fold, must still read the oracle's seen set and
-    coverage; the explicit switch forces the same deferral (committed when the
-    fold cannot be fused)."""
-    if env:
-        k, v = env.split("=")
+    rounds (config 3 shape: round 2 here) and of wide pull rounds, and leaves
+    the fold to the next round's apply or row-pull sweep.  A run stopped by
+    max_rounds right after a deferred round, or after the fused fold, must still
+    read the oracle's seen set and coverage; the explicit switches force the
+    deferrals (committed when the fold cannot be fused), and a huge binned
+    threshold turns the binned rounds into pulls (pull -> pull folds)."""
+    for kv in (env or "").split():
+        k, v = kv.split("=")
         monkeypatch.setenv(k, v)
     w = config(3, 1 << 18, pick=oracle.pick_origins)
     rp, col = oracle.gen_workload(w)
