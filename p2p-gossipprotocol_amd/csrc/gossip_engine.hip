@@ -78,6 +78,7 @@ struct gossip_ctx {
     HeavyChunk* chunks = nullptr;
     uint64_t n_chunks = 0;
     uint64_t* hacc = nullptr;  // k_pull_heavy's per-row found bits (n_chunks * Wp words)
+    uint64_t* inj_live = nullptr;  // kMaxWords: messages actually injected since the reset (k_inject)
     bool graph_ready = false;
 
     // dynamic state
@@ -290,6 +291,7 @@ void free_state(gossip_ctx* c) {
     hipFree(c->cov_hist);
     hipFree(c->reports);
     hipFree(c->n_reports);
+    hipFree(c->inj_live);
     hipFree(c->ex_col);
     hipFree(c->ex_cnt);
     hipFree(c->ex_miss);
@@ -313,6 +315,7 @@ void free_state(gossip_ctx* c) {
     c->cov_hist = nullptr;
     c->reports = nullptr;
     c->n_reports = nullptr;
+    c->inj_live = nullptr;
 }
 
 void free_graph(gossip_ctx* c) {
@@ -372,6 +375,7 @@ RoundArgs make_args(gossip_ctx* c) {
     a.chunks = c->chunks;
     a.n_chunks = c->n_chunks;
     a.hacc = c->hacc;
+    a.inj_live = c->world <= 1 && c->n_local == c->n ? c->inj_live : nullptr;  // a partition injects its own only
     a.n_local = c->n_local;
     a.begin = c->begin;
     a.end = c->end;
@@ -1037,6 +1041,7 @@ gossip_status gossip_create(const gossip_config* cfg, gossip_ctx** out) {
         return bail("stats", err);
     if ((err = hipHostMalloc((void**)&c->h_st, kStatLines * sizeof(DevStats))) != hipSuccess) return bail("pinned stats", err);
     if ((err = hipMalloc((void**)&c->n_reports, sizeof(unsigned long long))) != hipSuccess) return bail("nrep", err);
+    if ((err = hipMalloc((void**)&c->inj_live, kMaxWords * sizeof(uint64_t))) != hipSuccess) return bail("inj", err);
     if (c->cfg.extra_cap) {
         if (c->cfg.extra_cap > 64) {
             free_state(c);
@@ -1303,6 +1308,7 @@ gossip_status gossip_reset(gossip_ctx* c) {
     HIPCHK(hipMemsetAsync(c->st, 0, kStatLines * sizeof(DevStats), s));
     c->last_st_round = ~0u;
     HIPCHK(hipMemsetAsync(c->n_reports, 0, sizeof(unsigned long long), s));
+    HIPCHK(hipMemsetAsync(c->inj_live, 0, kMaxWords * sizeof(uint64_t), s));
     if (c->cov_hist) HIPCHK(hipMemsetAsync(c->cov_hist, 0, (uint64_t)c->cfg.max_rounds * 64 * c->Wp * 8, s));
     if (c->miss) HIPCHK(hipMemsetAsync(c->miss, 0, c->n_edges + 1, s));
     // slots still hold words of the last run: the first binned round of the next rewrites every slot

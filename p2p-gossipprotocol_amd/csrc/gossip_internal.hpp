@@ -141,7 +141,10 @@ struct RoundArgs {
     uint32_t heavy;                // light/heavy row threshold (rows > heavy are chunked)
     uint32_t dead_mode;            // some peers are dead: dense rounds skip dead destinations and the
                                    // traversal stats come from k_src_count (per-edge alive test)
-    uint64_t inj_mask[kMaxWords];  // messages injected so far (pull: bits a peer can still learn)
+    uint64_t inj_mask[kMaxWords];  // messages scheduled so far (pull: bits a peer can still learn)
+    uint64_t* inj_live;            // P = 1: messages actually injected so far (an origin dead at its round
+                                   // never injects; nobody can learn those bits); k_inject sets them.  A
+                                   // partition injects only its own origins, so P > 1 passes nullptr
     uint64_t* tcur;                // push rounds (P = 1): 1 bit per 64-peer tile, a superset of the tiles with
                                    // nonzero new words; cleared as consumed (nullptr: not kept)
     uint64_t* tnx;                 // the same bits for the next round's words, set at activation

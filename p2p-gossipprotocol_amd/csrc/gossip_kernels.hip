@@ -29,6 +29,12 @@ constexpr unsigned kMaxGrid = 2048;  // 256 CUs x 8 blocks of 256 threads
 
 __device__ __forceinline__ bool bit_alive(const uint32_t* bits, uint32_t v) { return (bits[v >> 5] >> (v & 31)) & 1u; }
 
+// the bits a peer can still learn: messages injected so far (at P = 1 the ones whose origin was alive to
+// inject them -- a never-injected message kept every row of config 5 scanning to its end)
+__device__ __forceinline__ uint64_t injm(const RoundArgs& a, int w) {
+    return a.inj_live ? a.inj_mask[w] & a.inj_live[w] : a.inj_mask[w];
+}
+
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
@@ -562,7 +568,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_diag(RoundArgs a) {
         bool needy = false;
 #pragma unroll
         for (int w = 0; w < W; ++w) {
-            need[w] = a.inj_mask[w] & ~a.seen[v * W + w];
+            need[w] = injm(a, w) & ~a.seen[v * W + w];
             got[w] = 0;
             needy |= need[w] != 0;
         }
@@ -612,7 +618,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_light(RoundArgs a, uint32_t wd)
         for (int w = 0; w < W; ++w) {
             m[w] = vv ? ld_s<NT>(a.nw + v * W + w) : 0ull;
             sv[w] = vv ? ld_s<NT>(a.seen + v * W + w) : ~0ull;
-            need[w] = va ? a.inj_mask[w] & ~sv[w] : 0ull;
+            need[w] = va ? injm(a, w) & ~sv[w] : 0ull;
             act |= m[w] != 0;
             needy |= need[w] != 0;
         }
@@ -811,7 +817,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
             // queued, so their own later stores come after it
             const uint64_t sv = vv ? (a.fold ? d.sv[w] | m[w] : d.sv[w]) : ~0ull;
             if (a.fold && vv && m[w]) a.seen[v * W + w] = sv;
-            nd[w] = va ? a.inj_mask[w] & ~sv : 0ull;
+            nd[w] = va ? injm(a, w) & ~sv : 0ull;
             act |= m[w] != 0;
             needy |= nd[w] != 0;
             if (vv) a.nx[v * W + w] = 0ull;  // nx is written whole in a pull round; rows that learn rewrite it
@@ -935,7 +941,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
                 const uint64_t fr = got[w];  // subset of need: bits this peer had not seen
                 if (fr) {
                     // a.pdefer: the next round folds nx into seen (a random 8-B store saved per row)
-                    if (!a.pdefer) a.seen[(uint64_t)rv * W + w] = (a.inj_mask[w] & ~need[w]) | fr;  // within inj_mask
+                    if (!a.pdefer) a.seen[(uint64_t)rv * W + w] = (injm(a, w) & ~need[w]) | fr;  // within inj_mask
                     a.nx[(uint64_t)rv * W + w] = fr;
                     acc.fresh += (unsigned long long)__popcll(fr);
                     any = true;
@@ -967,7 +973,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_heavy(RoundArgs a) {
             pub[w] = 0;
             // one lane reads, every lane uses the same value: the branch below stays wave-uniform
             const uint64_t s0 = __shfl(a.seen[(uint64_t)ch.v * W + w], 0);
-            need[w] = a.inj_mask[w] & ~s0;
+            need[w] = injm(a, w) & ~s0;
             if (a.dead_mode && !bit_alive(a.alive, (uint32_t)(a.begin + ch.v))) need[w] = 0;  // dead: no receive
             part[w] = 0;
             any |= need[w] != 0;
@@ -1512,7 +1518,7 @@ __global__ __launch_bounds__(kB) void k_bin_apply(RoundArgs a, BinArgs b) {
     for (uint32_t i = threadIdx.x; i < nv * W; i += kB) {
         acc_s[i] = 0ull;
         const bool va = !a.dead_mode || bit_alive(a.alive, (uint32_t)(a.begin + v0 + i / W));
-        needy |= va && (a.inj_mask[i % W] & ~(a.seen[v0 * W + i] | pend(i))) != 0;
+        needy |= va && (injm(a, i % W) & ~(a.seen[v0 * W + i] | pend(i))) != 0;
     }
     if (!__syncthreads_or(needy)) {
         for (uint32_t i = threadIdx.x; i < nv * W; i += kB) {
@@ -1549,7 +1555,7 @@ __global__ __launch_bounds__(kB) void k_bin_apply(RoundArgs a, BinArgs b) {
         const uint64_t p = pend(i);
         const uint64_t sv = a.seen[v0 * W + i] | p;
         const bool va = !a.dead_mode || bit_alive(a.alive, (uint32_t)(a.begin + v0 + i / W));  // dead: no receive
-        const uint64_t fr = va ? acc_s[i] & a.inj_mask[i % W] & ~sv : 0ull;
+        const uint64_t fr = va ? acc_s[i] & injm(a, i % W) & ~sv : 0ull;
         if (fr) {  // handleClient: new -> Message-List insert (peer.cpp:281-282)
             acc.fresh += (unsigned long long)__popcll(fr);
             acc.activated++;
@@ -1656,7 +1662,7 @@ __global__ __launch_bounds__(kB) void k_bin_apply_runs(RoundArgs a, BinArgs b) {
     for (uint32_t i = threadIdx.x; i < nv * W; i += kB) {
         acc_s[i] = 0ull;
         const bool va = !a.dead_mode || bit_alive(a.alive, (uint32_t)(a.begin + v0 + i / W));
-        needy |= va && (a.inj_mask[i % W] & ~a.seen[v0 * W + i]) != 0;
+        needy |= va && (injm(a, i % W) & ~a.seen[v0 * W + i]) != 0;
     }
     if (!__syncthreads_or(needy)) {
         for (uint32_t i = threadIdx.x; i < nv * W; i += kB) a.nx[v0 * W + i] = 0ull;
@@ -1709,7 +1715,7 @@ __global__ __launch_bounds__(kB) void k_bin_apply_runs(RoundArgs a, BinArgs b) {
     for (uint32_t i = threadIdx.x; i < nv * W; i += kB) {
         const uint64_t sv = a.seen[v0 * W + i];
         const bool va = !a.dead_mode || bit_alive(a.alive, (uint32_t)(a.begin + v0 + i / W));  // dead: no receive
-        const uint64_t fr = va ? acc_s[i] & a.inj_mask[i % W] & ~sv : 0ull;
+        const uint64_t fr = va ? acc_s[i] & injm(a, i % W) & ~sv : 0ull;
         if (fr) {  // handleClient: new -> Message-List insert (peer.cpp:281-282)
             a.seen[v0 * W + i] = sv | fr;
             acc.fresh += (unsigned long long)__popcll(fr);
@@ -2312,6 +2318,7 @@ __global__ __launch_bounds__(kBlock) void k_inject(RoundArgs a, const uint32_t* 
             const unsigned long long bit = 1ull << (m & 63);
             atomicOr(reinterpret_cast<unsigned long long*>(a.seen) + idx, bit);
             atomicOr(reinterpret_cast<unsigned long long*>(a.nw) + idx, bit);
+            if (a.inj_live) atomicOr(reinterpret_cast<unsigned long long*>(a.inj_live) + (m >> 6), bit);
             if (a.tcur) atomicOr(reinterpret_cast<unsigned long long*>(a.tcur) + ((o - a.begin) >> 12), 1ull << (((o - a.begin) >> 6) & 63));
             acc.injected++;
         }
