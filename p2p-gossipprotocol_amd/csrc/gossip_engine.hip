@@ -79,6 +79,7 @@ struct gossip_ctx {
     uint64_t n_chunks = 0;
     uint64_t* hacc = nullptr;  // k_pull_heavy's per-row found bits (n_chunks * Wp words)
     uint64_t* inj_live = nullptr;  // kMaxWords: messages actually injected since the reset (k_inject)
+    uint64_t* first2 = nullptr;    // per owned peer: its row's first two entries (k_pull_rows, RoundArgs.first2)
     bool graph_ready = false;
 
     // dynamic state
@@ -164,6 +165,7 @@ struct gossip_ctx {
                                   // binned round's apply or row-pull sweep folds them in, anything else
                                   // commits first
     bool cur_pdefer = false;      // this (wide) pull round stores only nx for the rows that learn
+    bool first_ok = true;         // GOSSIP_PULL_FIRST2=0: k_pull_rows loads every col entry (A/B)
     bool pdefer_ok = false;       // GOSSIP_PULL_DEFER=1: defer wide pull rounds (A/B: config 4 round 7 -0.3 to
                                   // -0.75 ms, round 8's fold +0.5 to +0.7 ms, so off by default)
     bool pull_diag = false;       // GOSSIP_PULL_DIAG: count the gathers of an early-exit row scan (measurement)
@@ -325,6 +327,8 @@ void free_graph(gossip_ctx* c) {
     hipFree(c->col);
     hipFree(c->chunks);
     hipFree(c->hacc);
+    hipFree(c->first2);
+    c->first2 = nullptr;
     // closed-form liveness state belongs to the overlay: round_begin rebuilds
     // all of it (rev included) for the next one
     hipFree(c->rev);
@@ -431,6 +435,8 @@ gossip_status install_graph(gossip_ctx* c, uint64_t* d_rp, uint32_t* d_col, uint
         HIPCHK(hipMalloc((void**)&c->miss, m + 1));
         HIPCHK(hipMemsetAsync(c->miss, 0, m + 1, c->stream));
     }
+    HIPCHK(hipMalloc((void**)&c->first2, (c->n_local + 1) * sizeof(uint64_t)));
+    HIPCHK(launch_first2(c->rp, c->col, c->n_local, c->first2, c->stream));
     c->graph_ready = true;
     return GOSSIP_OK;
 }
@@ -739,6 +745,9 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
     c->cur_pdefer = rows_pull && c->world <= 1 && !remote && !c->any_dead && requested == GOSSIP_MODE_AUTO &&
                     c->pdefer_ok && (c->frontier_est + cnt) * 1000 >= c->n_local * 400ull && missing * 4 >= c->n_local;
     a.pdefer = c->cur_pdefer ? 1u : 0u;
+    // a row's first step from its queue entry: worth the extra 8 B per swept peer while many rows are
+    // needy (config 4 round 7: 90 M rows, one random col line each); rows are unmasked (no liveness yet)
+    a.first2 = rows_pull && c->first_ok && !c->any_masked && missing * 4 >= c->n_local ? c->first2 : nullptr;
     c->last_pull = pull;
     c->last_bin = bin;
     c->last_front = false;
@@ -1004,6 +1013,7 @@ gossip_status gossip_create(const gossip_config* cfg, gossip_ctx** out) {
     if (const char* u = std::getenv("GOSSIP_HEAVY_EXIT")) c->heavy_exit = std::atoi(u) != 0;
     if (const char* u = std::getenv("GOSSIP_DEFER_PM")) c->defer_pm = (uint32_t)std::atoi(u);
     if (const char* u = std::getenv("GOSSIP_PULL_DEFER")) c->pdefer_ok = std::atoi(u) != 0;
+    if (const char* u = std::getenv("GOSSIP_PULL_FIRST2")) c->first_ok = std::atoi(u) != 0;
     if (const char* u = std::getenv("GOSSIP_BIN_STREAM")) c->bin_stream = std::atoi(u) != 0;
     if (const char* u = std::getenv("GOSSIP_PULL_DIAG")) c->pull_diag = std::atoi(u) != 0;
     if (const char* u = std::getenv("GOSSIP_FULL_LIVENESS"); u && std::atoi(u)) c->full_liveness = true;

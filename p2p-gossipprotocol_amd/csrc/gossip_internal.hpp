@@ -155,6 +155,10 @@ struct RoundArgs {
     uint32_t fold;                 // round after a deferred round: seen lacks this round's new words (nw);
                                    // k_bin_apply, or k_pull_rows's sweep, folds them in (seen | nw) for
                                    // every owned peer before anything else of the round reads seen
+    const uint64_t* first2;        // pull rounds with many needy rows (nullptr otherwise): per owned peer the
+                                   // first two entries of its row (col[rp[v]] | col[rp[v] + 1] << 32; no
+                                   // masked edges), read with the sweep so a row's first step needs no
+                                   // random col line
     uint32_t pdefer;               // wide pull round (k_pull_rows): a row that learns stores only its nx
                                    // word; its seen word is folded in by the next round (a.fold)
     uint64_t* front;               // pull rounds: 1 bit per source peer, set iff its new words are nonzero
@@ -230,6 +234,7 @@ hipError_t launch_rejoin(const RoundArgs& a, uint32_t W, uint32_t seed, uint32_t
 hipError_t launch_rejoin_select(const RoundArgs& a, const RebootArgs& r, const uint32_t* list,
                                 const unsigned long long* n_list, uint64_t max_list, hipStream_t s);
 hipError_t launch_commit_nx(uint64_t* seen, const uint64_t* nx, uint64_t n_words, hipStream_t s);
+hipError_t launch_first2(const uint64_t* rp, const uint32_t* col, uint64_t n, uint64_t* out, hipStream_t s);
 hipError_t launch_zero_words(uint64_t* words, uint64_t n_words, hipStream_t s);
 hipError_t launch_coverage(const uint64_t* words, uint64_t n_local, uint32_t W, unsigned long long* counts,
                            hipStream_t s);

@@ -758,6 +758,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
     __shared__ uint32_t q_v[kWavesPerBlock][kRowQ];
     __shared__ uint32_t q_d[kWavesPerBlock][kRowQ];
     __shared__ unsigned long long q_rb[kWavesPerBlock][kRowQ];
+    __shared__ unsigned long long q_f2[kWavesPerBlock][kRowQ];  // the row's first two entries (a.first2)
     __shared__ unsigned long long q_need[kWavesPerBlock][kRowQ * W];
     if (COV) {
         for (int i = threadIdx.x; i < 64 * W; i += kBlock) cov_s[i] = 0;
@@ -768,6 +769,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
     uint32_t* qv = q_v[wv];
     uint32_t* qd = q_d[wv];
     unsigned long long* qrb = q_rb[wv];
+    unsigned long long* qf2 = q_f2[wv];
     unsigned long long* qneed = q_need[wv];
     uint32_t q_head = 0, q_tail = 0;  // wave-uniform ring counters (q_tail - q_head <= kRowQ)
     auto wave_sync = [] {
@@ -778,7 +780,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
     // this lane's row
     bool has = false;
     uint32_t rv = 0, rd = 0, rk = 0;
-    uint64_t rrb = 0, need[W], got[W];
+    uint64_t rrb = 0, rf2 = 0, need[W], got[W];
 #pragma unroll
     for (int w = 0; w < W; ++w) need[w] = got[w] = 0;
     const uint64_t n_tiles = (a.n_local + 63) >> 6;
@@ -789,7 +791,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
     // words and row bounds in flight while it sweeps the current one
     // (unconditional loads, clamped past the end)
     struct TileIn {
-        uint64_t m[W], sv[W], r0, r1;
+        uint64_t m[W], sv[W], r0, r1, f2;
         uint32_t al;
     };
     auto load_tile = [&](uint64_t tt, TileIn& d) {
@@ -801,6 +803,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
         }
         d.r0 = a.rp[v];
         d.r1 = a.rp[v + 1];
+        d.f2 = a.first2 ? a.first2[v] : 0ull;
         d.al = a.dead_mode ? a.alive[(uint32_t)(a.begin + v) >> 5] : ~0u;
     };
     auto sweep_tile = [&](uint64_t tt, const TileIn& d) {
@@ -854,6 +857,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
             qv[pos] = (uint32_t)v;
             qd[pos] = (uint32_t)dg;
             qrb[pos] = rb;
+            qf2[pos] = d.f2;
 #pragma unroll
             for (int w = 0; w < W; ++w) qneed[pos * W + w] = nd[w];
         }
@@ -882,6 +886,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
                 rv = qv[pos];
                 rd = qd[pos];
                 rrb = qrb[pos];
+                rf2 = qf2[pos];
                 rk = 0;
 #pragma unroll
                 for (int w = 0; w < W; ++w) {
@@ -905,8 +910,10 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
             ok[j] = has && rk + j < rd;
             // rows are sorted, so the scan meets the hubs first: their words are cache-hot (scanning
             // from the row's end measured 192 M gathers and 8.0-9.2 ms against 180 M, 7.3-7.5 ms at
-            // config 4 round 7)
-            u[j] = a.col[ok[j] ? rrb + rk + j : 0];
+            // config 4 round 7).  A row's first two entries may come with its queue entry (a.first2).
+            const bool f2 = a.first2 && rk == 0 && j < 2;
+            const uint32_t uc = a.col[ok[j] && !f2 ? rrb + rk + j : 0];
+            u[j] = f2 ? (uint32_t)(rf2 >> (32 * j)) : uc;
         }
         acc.pulled += (has ? min(kRowB, (int)(rd - rk)) : 0);
 #pragma unroll
@@ -2469,6 +2476,16 @@ __global__ __launch_bounds__(kBlock) void k_coverage(const uint64_t* words, uint
         if (cnt[i]) atomicAdd(&counts[i], (unsigned long long)cnt[i]);
 }
 
+// first two entries of every row (a.first2); rows of one entry repeat it
+__global__ __launch_bounds__(kBlock) void k_first2(const uint64_t* rp, const uint32_t* col, uint64_t n,
+                                                   uint64_t* out) {
+    for (uint64_t v = (uint64_t)blockIdx.x * kBlock + threadIdx.x; v < n; v += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t b = rp[v], d = rp[v + 1] - b;
+        const uint64_t c0 = d ? col[b] : 0u, c1 = d > 1 ? col[b + 1] : c0;
+        out[v] = c0 | (c1 << 32);
+    }
+}
+
 __global__ void k_heavy_count(const uint64_t* rp, uint64_t n, uint32_t heavy, unsigned long long* n_chunks) {
     unsigned long long mine = 0;
     for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x) {
@@ -2842,6 +2859,12 @@ hipError_t launch_src_count(const RoundArgs& a, uint32_t W_, hipStream_t s) {
     const uint64_t tiles = (a.n_local + 63) / 64;
     GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_src_count<W>, dim3(grid_for(tiles, kWavesPerBlock)), dim3(kBlock),
                                                    0, s, a));
+    return hipGetLastError();
+}
+
+hipError_t launch_first2(const uint64_t* rp, const uint32_t* col, uint64_t n, uint64_t* out, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_first2, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, rp, col, n, out);
     return hipGetLastError();
 }
 
