@@ -165,6 +165,9 @@ struct gossip_ctx {
                                   // binned round's apply or row-pull sweep folds them in, anything else
                                   // commits first
     bool cur_pdefer = false;      // this (wide) pull round stores only nx for the rows that learn
+    bool defer_nr = false;        // GOSSIP_DEFER_NR=1: deferred push rounds issue no-return atomics and count
+                                  // the receipts from nx afterwards (A/B, config 4 round 3: push 4.29-4.37 +
+                                  // 0.40 ms count against 4.05-4.38 ms -- the atomics are memory-side bound)
     bool first_ok = true;         // GOSSIP_PULL_FIRST2=0: k_pull_rows loads every col entry (A/B)
     bool pdefer_ok = false;       // GOSSIP_PULL_DEFER=1: defer wide pull rounds (A/B: config 4 round 7 -0.3 to
                                   // -0.75 ms, round 8's fold +0.5 to +0.7 ms, so off by default)
@@ -728,7 +731,8 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
                          !c->cfg.rejoin_threshold && requested == GOSSIP_MODE_AUTO;
     const uint32_t dpm = c->defer_pm == kDeferAuto ? (fusable ? 10u : 0u) : c->defer_pm;
     c->cur_defer = !pull && dpm && (c->frontier_est + cnt) * 1000 >= c->n_local * (uint64_t)dpm;
-    a.defer = c->cur_defer ? 1u : 0u;
+    // no-return atomics (the receipts counted from nx after the round) unless tile marks need the old words
+    a.defer = c->cur_defer ? (c->defer_nr && !remote && c->world <= 1 && !a.tnx ? 2u : 1u) : 0u;
     const bool rows_pull = pull && !bin && (c->pull_unroll & kPullRows) && !c->pull_diag;  // k_pull_rows
     if (c->fold_pending) {  // the previous round deferred: its receipts are this round's nw
         if (((bin && !c->bin_stream) || rows_pull) && c->world <= 1 && !remote) {
@@ -833,6 +837,7 @@ gossip_status round_compute(gossip_ctx* c) {
     HIPCHK(timed(c, "push_heavy", [&] { return launch_push_heavy(a, pw, c->any_dead, remote, c->stream); }));
     if (a.tcur && !a.tsparse) HIPCHK(hipMemsetAsync(a.tcur, 0, tact_bytes(c), c->stream));  // unread marks go
     HIPCHK(timed(c, "push_light", [&] { return launch_push_light(a, pw, c->any_dead, remote, c->stream); }));
+    if (a.defer == 2) HIPCHK(timed(c, "count_nx", [&] { return launch_count_nx(a, pw, c->stream); }));
     if (c->cur_sparse) {
         HIPCHK(timed(c, "compact_send", [&] {
             return launch_compact_send(a, pw, c->part_begins[1], c->d_counts, c->seg, c->stream);
@@ -1014,6 +1019,7 @@ gossip_status gossip_create(const gossip_config* cfg, gossip_ctx** out) {
     if (const char* u = std::getenv("GOSSIP_DEFER_PM")) c->defer_pm = (uint32_t)std::atoi(u);
     if (const char* u = std::getenv("GOSSIP_PULL_DEFER")) c->pdefer_ok = std::atoi(u) != 0;
     if (const char* u = std::getenv("GOSSIP_PULL_FIRST2")) c->first_ok = std::atoi(u) != 0;
+    if (const char* u = std::getenv("GOSSIP_DEFER_NR")) c->defer_nr = std::atoi(u) != 0;
     if (const char* u = std::getenv("GOSSIP_BIN_STREAM")) c->bin_stream = std::atoi(u) != 0;
     if (const char* u = std::getenv("GOSSIP_PULL_DIAG")) c->pull_diag = std::atoi(u) != 0;
     if (const char* u = std::getenv("GOSSIP_FULL_LIVENESS"); u && std::atoi(u)) c->full_liveness = true;

@@ -151,7 +151,8 @@ struct RoundArgs {
     uint32_t tsparse;              // tcur is valid: push_light visits only its tiles
     uint32_t defer;                // push round with a deferred seen update: deliveries test against the
                                    // round-start seen and OR the unseen bits into nx only (one atomic per
-                                   // delivery); k_commit_nx folds nx into seen after the round
+                                   // delivery); k_commit_nx folds nx into seen after the round.  2: the
+                                   // atomics return nothing and k_count_nx counts the receipts from nx
     uint32_t fold;                 // round after a deferred round: seen lacks this round's new words (nw);
                                    // k_bin_apply, or k_pull_rows's sweep, folds them in (seen | nw) for
                                    // every owned peer before anything else of the round reads seen
@@ -235,6 +236,7 @@ hipError_t launch_rejoin_select(const RoundArgs& a, const RebootArgs& r, const u
                                 const unsigned long long* n_list, uint64_t max_list, hipStream_t s);
 hipError_t launch_commit_nx(uint64_t* seen, const uint64_t* nx, uint64_t n_words, hipStream_t s);
 hipError_t launch_first2(const uint64_t* rp, const uint32_t* col, uint64_t n, uint64_t* out, hipStream_t s);
+hipError_t launch_count_nx(const RoundArgs& a, uint32_t W_, hipStream_t s);
 hipError_t launch_zero_words(uint64_t* words, uint64_t n_words, hipStream_t s);
 hipError_t launch_coverage(const uint64_t* words, uint64_t n_local, uint32_t W, unsigned long long* counts,
                            hipStream_t s);

@@ -158,6 +158,11 @@ __device__ __forceinline__ void deliver_local(const RoundArgs& a, uint64_t lv, c
     for (int w = 0; w < W; ++w) {
         const unsigned long long u = m[w] & ~cur[w];
         if (!u) continue;  // all duplicates: dropped (peer.cpp:281)
+        if (a.defer == 2) {  // no-return atomic: the round's receipts are counted from nx (k_count_nx)
+            atomicOr(np + w, u);
+            acc.atomics++;
+            continue;
+        }
         if (a.defer) {     // seen is the round-start set all round: one atomic, on nx
             const unsigned long long old = atomicOr(np + w, u);
             acc.atomics++;
@@ -260,6 +265,18 @@ __device__ __forceinline__ void deliver_batch(const RoundArgs& a, const uint32_t
             const uint64_t x = a.seen[loc[j] ? (uint64_t)(c[j] - (uint32_t)a.begin) * W + w : 0];
             cur[j][w] = x | (loc[j] && m[j][w] ? 0ull : ~0ull);  // (a select would sink the load into a branch)
         }
+    if (a.defer == 2) {  // no-return atomics on nx; the round's receipts are counted from nx (k_count_nx)
+#pragma unroll
+        for (int j = 0; j < kU; ++j)
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                const uint64_t lv = (uint64_t)(c[j] - (uint32_t)a.begin);
+                const unsigned long long u = m[j][w] & ~cur[j][w];
+                if (u) atomicOr(reinterpret_cast<unsigned long long*>(a.nx) + lv * W + w, u);
+                acc.atomics += u != 0;
+            }
+        return;
+    }
     // the test-and-sets, every atomic of a phase issued before any result is used
     uint64_t old[kU][W];
 #pragma unroll
@@ -2456,6 +2473,25 @@ __global__ __launch_bounds__(kBlock) void k_commit_nx(u64x2* seen, const u64x2* 
 
 // reset: zero a word array with 16-B stores (hipMemsetAsync's fill kernel
 // reached ~2.6 TB/s on the 2 GB arrays of config 4)
+// After a no-return deferred push round (RoundArgs.defer == 2): nx holds exactly the round's receipts
+// (bits not in the round-start seen), so new receipts = its popcount and activations = peers with a
+// nonzero word.
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_count_nx(RoundArgs a) {
+    Acc acc;
+    for (uint64_t v = (uint64_t)blockIdx.x * kBlock + threadIdx.x; v < a.n_local; v += (uint64_t)gridDim.x * kBlock) {
+        bool any = false;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            const uint64_t x = a.nx[v * W + w];
+            any |= x != 0;
+            acc.fresh += (unsigned long long)__popcll(x);
+        }
+        acc.activated += any;
+    }
+    flush(acc, a.st);
+}
+
 __global__ __launch_bounds__(kBlock) void k_zero2(u64x2* p, uint64_t n2) {
     const u64x2 z = {0ull, 0ull};
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n2; i += (uint64_t)gridDim.x * kBlock) p[i] = z;
@@ -2859,6 +2895,12 @@ hipError_t launch_src_count(const RoundArgs& a, uint32_t W_, hipStream_t s) {
     const uint64_t tiles = (a.n_local + 63) / 64;
     GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_src_count<W>, dim3(grid_for(tiles, kWavesPerBlock)), dim3(kBlock),
                                                    0, s, a));
+    return hipGetLastError();
+}
+
+hipError_t launch_count_nx(const RoundArgs& a, uint32_t W_, hipStream_t s) {
+    GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_count_nx<W>, dim3(grid_for(a.n_local, kBlock)), dim3(kBlock), 0, s,
+                                                   a));
     return hipGetLastError();
 }
 

@@ -17,7 +17,7 @@ from ._abi import DeadReport, GossipConfig, RoundStats, check
 
 _GRAPHS = {"powerlaw": _abi.GRAPH_POWERLAW, "ref_bootstrap": _abi.GRAPH_REF_BOOTSTRAP}
 KERNELS = ("push_light", "push_heavy", "push_extra", "src_count", "frontier_bits", "pull_light", "pull_heavy", "bin_scatter",
-           "bin_apply", "liveness", "rebootstrap", "rejoin", "churn", "kills", "inject", "apply_remote")
+           "bin_apply", "liveness", "rebootstrap", "rejoin", "churn", "kills", "inject", "apply_remote", "commit", "count_nx")
 
 
 def _u32(a) -> np.ndarray:

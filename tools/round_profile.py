@@ -8,7 +8,7 @@ from gossip_hip import Engine  # noqa: E402
 from gossip_hip.workloads import config  # noqa: E402
 
 K = ("push_light", "push_heavy", "pull_light", "pull_heavy", "frontier_bits", "bin_scatter", "bin_apply", "inject",
-     "liveness", "churn", "kills", "src_count", "rebootstrap", "push_extra", "commit")
+     "liveness", "churn", "kills", "src_count", "rebootstrap", "push_extra", "commit", "count_nx")
 w = config(int(sys.argv[1]) if len(sys.argv) > 1 else 4)
 e = Engine(w.n, w.n_msgs, device=0, **w.engine_kwargs())
 e.build_graph()
