@@ -169,6 +169,9 @@ struct gossip_ctx {
                                   // the receipts from nx afterwards (A/B, config 4 round 3: push 4.29-4.37 +
                                   // 0.40 ms count against 4.05-4.38 ms -- the atomics are memory-side bound)
     bool first_ok = true;         // GOSSIP_PULL_FIRST2=0: k_pull_rows loads every col entry (A/B)
+    bool flight_ok = true;        // GOSSIP_FLIGHT=0: needy tests ignore which bits are in flight (A/B)
+    uint64_t flight[kMaxWords] = {};  // receipts of round flight_round (from its stats)
+    uint32_t flight_round = ~0u;
     bool pdefer_ok = false;       // GOSSIP_PULL_DEFER=1: defer wide pull rounds (A/B: config 4 round 7 -0.3 to
                                   // -0.75 ms, round 8's fold +0.5 to +0.7 ms, so off by default)
     bool pull_diag = false;       // GOSSIP_PULL_DIAG: count the gathers of an early-exit row scan (measurement)
@@ -678,6 +681,19 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
         uint32_t hi = (uint32_t)(std::upper_bound(c->inj_round_sorted.begin(), c->inj_round_sorted.end(), c->round) -
                                  c->inj_round_sorted.begin());
         for (int w = 0; w < kMaxWords; ++w) a.inj_mask[w] = hi ? c->inj_prefix[(uint64_t)(hi - 1) * kMaxWords + w] : 0;
+        // bits in flight this round (P = 1): the previous round's receipts (read with its stats) and this
+        // round's injections; nothing else is in a new word
+        const uint32_t lo = c->round ? (uint32_t)(std::upper_bound(c->inj_round_sorted.begin(), c->inj_round_sorted.end(),
+                                                                   c->round - 1) - c->inj_round_sorted.begin())
+                                     : 0u;
+        const bool known = c->round == 0 || c->flight_round == c->round - 1;
+        if (c->flight_ok && known && c->world <= 1 && c->n_local == c->n && !c->cfg.rejoin_threshold) {
+            a.use_flight = 1;
+            for (int w = 0; w < kMaxWords; ++w) {
+                const uint64_t before = lo ? c->inj_prefix[(uint64_t)(lo - 1) * kMaxWords + w] : 0;
+                a.in_flight[w] = (c->round ? c->flight[w] : 0) | (a.inj_mask[w] & ~before);
+            }
+        }
     }
     // dead peers are fine for pull / binned rounds (a live peer's in-edges from
     // live peers are never masked: only edges to dead peers are); re-bootstrap
@@ -856,9 +872,13 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
         const unsigned long long* src = reinterpret_cast<const unsigned long long*>(c->h_st);
         unsigned long long* dst = reinterpret_cast<unsigned long long*>(&sum);
         for (int l = 0; l < kStatLines; ++l)
-            for (int f = 0; f < kStatFields; ++f) dst[f] += src[l * kStatFields + f];
+            for (int f = 0; f < kStatFields; ++f)
+                dst[f] = f < kStatSums ? dst[f] + src[l * kStatFields + f] : dst[f] | src[l * kStatFields + f];
         c->last_st = sum;
         c->last_st_round = c->round;
+        // the bits of the round's receipts: the next round's new words (with its injections)
+        for (int w = 0; w < kMaxWords; ++w) c->flight[w] = sum.fresh_or[w];
+        c->flight_round = c->round;
     }
     const DevStats d = c->last_st;
     c->prev_frontier_est = c->frontier_est;
@@ -1020,6 +1040,7 @@ gossip_status gossip_create(const gossip_config* cfg, gossip_ctx** out) {
     if (const char* u = std::getenv("GOSSIP_PULL_DEFER")) c->pdefer_ok = std::atoi(u) != 0;
     if (const char* u = std::getenv("GOSSIP_PULL_FIRST2")) c->first_ok = std::atoi(u) != 0;
     if (const char* u = std::getenv("GOSSIP_DEFER_NR")) c->defer_nr = std::atoi(u) != 0;
+    if (const char* u = std::getenv("GOSSIP_FLIGHT")) c->flight_ok = std::atoi(u) != 0;
     if (const char* u = std::getenv("GOSSIP_BIN_STREAM")) c->bin_stream = std::atoi(u) != 0;
     if (const char* u = std::getenv("GOSSIP_PULL_DIAG")) c->pull_diag = std::atoi(u) != 0;
     if (const char* u = std::getenv("GOSSIP_FULL_LIVENESS"); u && std::atoi(u)) c->full_liveness = true;
@@ -1351,6 +1372,7 @@ gossip_status gossip_reset(gossip_ctx* c) {
     c->last_pull = false;
     c->last_bin = false;
     c->cur_defer = c->cur_pdefer = false;
+    c->flight_round = ~0u;
     c->last_fresh = 0;
     c->frontier_est = c->prev_frontier_est = 0;
     c->round = 0;

@@ -25,8 +25,10 @@ struct DevStats {
         seed_removals, digest, covered, heavy_traversals, live_checked, activated, pull_edges, pull_gathers,
         reconnects, rejoined, atomics,  // atomics: device-scope atomics issued on peer state (seen, nx, marks)
         diag;                           // measurement counters (GOSSIP_PULL_DIAG)
+    unsigned long long fresh_or[8];     // OR of the round's receipts (the next round's new words), word w
 };
-constexpr int kStatFields = 20;
+constexpr int kStatSums = 20;                 // fields summed; the kMaxWords after them are OR-ed
+constexpr int kStatFields = kStatSums + 8;
 static_assert(sizeof(DevStats) == kStatFields * 8, "DevStats layout");
 
 struct HeavyChunk {
@@ -142,6 +144,10 @@ struct RoundArgs {
     uint32_t dead_mode;            // some peers are dead: dense rounds skip dead destinations and the
                                    // traversal stats come from k_src_count (per-edge alive test)
     uint64_t inj_mask[kMaxWords];  // messages scheduled so far (pull: bits a peer can still learn)
+    uint64_t in_flight[kMaxWords]; // P = 1, use_flight: a superset of the bits in this round's new words (the
+                                   // previous round's receipts OR this round's injections); a bit outside it
+                                   // cannot be learned this round
+    uint32_t use_flight;
     uint64_t* inj_live;            // P = 1: messages actually injected so far (an origin dead at its round
                                    // never injects; nobody can learn those bits); k_inject sets them.  A
                                    // partition injects only its own origins, so P > 1 passes nullptr

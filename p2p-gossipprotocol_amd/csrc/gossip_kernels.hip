@@ -31,8 +31,14 @@ __device__ __forceinline__ bool bit_alive(const uint32_t* bits, uint32_t v) { re
 
 // the bits a peer can still learn: messages injected so far (at P = 1 the ones whose origin was alive to
 // inject them -- a never-injected message kept every row of config 5 scanning to its end)
-__device__ __forceinline__ uint64_t injm(const RoundArgs& a, int w) {
+__device__ __forceinline__ uint64_t injm_full(const RoundArgs& a, int w) {
     return a.inj_live ? a.inj_mask[w] & a.inj_live[w] : a.inj_mask[w];
+}
+// ... and of those, this round: only bits that are in some new word (P = 1: in_flight, the previous
+// round's receipts with this round's injections -- a bit outside it kept config 5's hubs and needy
+// rows scanning to their ends: a message injected at an isolated peer is never in flight)
+__device__ __forceinline__ uint64_t injm(const RoundArgs& a, int w) {
+    return injm_full(a, w) & (a.use_flight ? a.in_flight[w] : ~0ull);
 }
 
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
@@ -53,6 +59,7 @@ struct Acc {
                        reports = 0, removals = 0, injected = 0, htrav = 0, checked = 0,
                        activated = 0, pulled = 0, gathered = 0, reconnects = 0, rejoined = 0, atomics = 0,
                        diag = 0;
+    unsigned long long fresh_or[kMaxWords] = {};  // OR of the receipts (only the words a kernel touches stay)
 };
 
 // Block-level flush: wave sums -> LDS -> one atomic per nonzero field per
@@ -79,18 +86,31 @@ __device__ __forceinline__ void flush_into(Acc& acc, DevStats* st, unsigned long
     const unsigned long long v[kF] = {acc.frontier, acc.trav,     acc.deliv,   acc.undeliv, acc.fresh,  acc.injected,
                                       acc.died,     acc.reports,  acc.removals, acc.digest, acc.covered, acc.htrav,
                                       acc.checked,  acc.activated, acc.pulled,  acc.gathered, acc.reconnects,
-                                      acc.rejoined, acc.atomics, acc.diag};
+                                      acc.rejoined, acc.atomics, acc.diag,
+                                      acc.fresh_or[0], acc.fresh_or[1], acc.fresh_or[2], acc.fresh_or[3],
+                                      acc.fresh_or[4], acc.fresh_or[5], acc.fresh_or[6], acc.fresh_or[7]};
 #pragma unroll
     for (int f = 0; f < kF; ++f) {
-        const unsigned long long s_ = wave_sum(v[f]);
+        unsigned long long s_ = v[f];
+        if (f < kStatSums) {
+            s_ = wave_sum(s_);
+        } else {
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) s_ |= __shfl_xor(s_, off);
+        }
         if (lane == 0) red[wave][f] = s_;
     }
     __syncthreads();
     if (threadIdx.x < kF) {
         unsigned long long s_ = 0;
+        const bool sum = threadIdx.x < kStatSums;
 #pragma unroll
-        for (int w = 0; w < kWaves; ++w) s_ += red[w][threadIdx.x];
-        if (s_) atomicAdd(reinterpret_cast<unsigned long long*>(st + blockIdx.x % kStatLines) + threadIdx.x, s_);
+        for (int w = 0; w < kWaves; ++w) s_ = sum ? s_ + red[w][threadIdx.x] : s_ | red[w][threadIdx.x];
+        unsigned long long* f = reinterpret_cast<unsigned long long*>(st + blockIdx.x % kStatLines) + threadIdx.x;
+        if (s_) {
+            if (sum) atomicAdd(f, s_);
+            else atomicOr(f, s_);
+        }
     }
 }
 
@@ -161,12 +181,14 @@ __device__ __forceinline__ void deliver_local(const RoundArgs& a, uint64_t lv, c
         if (a.defer == 2) {  // no-return atomic: the round's receipts are counted from nx (k_count_nx)
             atomicOr(np + w, u);
             acc.atomics++;
+            acc.fresh_or[w] |= u;  // (a superset of the receipts)
             continue;
         }
         if (a.defer) {     // seen is the round-start set all round: one atomic, on nx
             const unsigned long long old = atomicOr(np + w, u);
             acc.atomics++;
             const unsigned long long fr = u & ~old;  // not yet received this round either
+            acc.fresh_or[w] |= fr;
             if (fr) {
                 acc.activated += old == 0;
                 if (a.tnx && old == 0) mark();
@@ -177,6 +199,7 @@ __device__ __forceinline__ void deliver_local(const RoundArgs& a, uint64_t lv, c
         const unsigned long long old = atomicOr(sp + w, (unsigned long long)m[w]);
         acc.atomics++;
         const unsigned long long fr = m[w] & ~old;
+        acc.fresh_or[w] |= fr;
         if (fr) {
             const unsigned long long onx = atomicOr(np + w, fr);
             acc.atomics++;
@@ -274,6 +297,7 @@ __device__ __forceinline__ void deliver_batch(const RoundArgs& a, const uint32_t
                 const unsigned long long u = m[j][w] & ~cur[j][w];
                 if (u) atomicOr(reinterpret_cast<unsigned long long*>(a.nx) + lv * W + w, u);
                 acc.atomics += u != 0;
+                acc.fresh_or[w] |= u;  // (a superset of the receipts)
             }
         return;
     }
@@ -307,6 +331,7 @@ __device__ __forceinline__ void deliver_batch(const RoundArgs& a, const uint32_t
     for (int j = 0; j < kU; ++j)
 #pragma unroll
         for (int w = 0; w < W; ++w) {
+            acc.fresh_or[w] |= fr[j][w];
             if (!fr[j][w]) continue;
             acc.fresh += (unsigned long long)__popcll(fr[j][w]);
             acc.activated += onx[j][w] == 0;
@@ -740,6 +765,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_light(RoundArgs a, uint32_t wd)
 #pragma unroll
             for (int w = 0; w < W; ++w) {
                 const uint64_t fr = light ? (my[lane * W + w] & need[w]) : 0ull;
+                acc.fresh_or[w] |= fr;
                 if (fr) {  // handleClient: new -> Message-List insert (peer.cpp:281-282)
                     st_s<NT>(a.seen + v * W + w, sv[w] | fr);
                     acc.fresh += (unsigned long long)__popcll(fr);
@@ -837,9 +863,11 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
             // queued, so their own later stores come after it
             const uint64_t sv = vv ? (a.fold ? d.sv[w] | m[w] : d.sv[w]) : ~0ull;
             if (a.fold && vv && m[w]) a.seen[v * W + w] = sv;
-            nd[w] = va ? injm(a, w) & ~sv : 0ull;
+            // nd: every bit the peer lacks (the row's final seen word is rebuilt from it); a row is queued
+            // only if one of them is in flight this round
+            nd[w] = va ? injm_full(a, w) & ~sv : 0ull;
             act |= m[w] != 0;
-            needy |= nd[w] != 0;
+            needy |= (nd[w] & injm(a, w)) != 0;
             if (vv) a.nx[v * W + w] = 0ull;  // nx is written whole in a pull round; rows that learn rewrite it
         }
         const uint64_t rb = d.r0, d_ = d.r1 - d.r0;
@@ -955,7 +983,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
         for (int w = 0; w < W; ++w) {
 #pragma unroll
             for (int j = 0; j < kRowB; ++j) got[w] |= x[j][w] & need[w];
-            done &= got[w] == need[w];
+            done &= got[w] == (need[w] & injm(a, w));  // every bit it can still learn this round
         }
         rk += kRowB;
         if (has && (done || rk >= rd)) {  // the row is finished: handleClient's test-and-set, owner stores
@@ -963,9 +991,10 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
 #pragma unroll
             for (int w = 0; w < W; ++w) {
                 const uint64_t fr = got[w];  // subset of need: bits this peer had not seen
+                acc.fresh_or[w] |= fr;
                 if (fr) {
                     // a.pdefer: the next round folds nx into seen (a random 8-B store saved per row)
-                    if (!a.pdefer) a.seen[(uint64_t)rv * W + w] = (injm(a, w) & ~need[w]) | fr;  // within inj_mask
+                    if (!a.pdefer) a.seen[(uint64_t)rv * W + w] = (injm_full(a, w) & ~need[w]) | fr;  // within inj_mask
                     a.nx[(uint64_t)rv * W + w] = fr;
                     acc.fresh += (unsigned long long)__popcll(fr);
                     any = true;
@@ -1057,6 +1086,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_heavy(RoundArgs a) {
                 unsigned long long* sp = reinterpret_cast<unsigned long long*>(a.seen) + (uint64_t)ch.v * W + w;
                 const unsigned long long fr = part[w] & ~atomicOr(sp, (unsigned long long)part[w]);
                 acc.atomics += fr ? 2 : 1;
+                acc.fresh_or[w] |= fr;
                 if (fr) {
                     const unsigned long long onx =
                         atomicOr(reinterpret_cast<unsigned long long*>(a.nx) + (uint64_t)ch.v * W + w, fr);
@@ -1580,6 +1610,9 @@ __global__ __launch_bounds__(kB) void k_bin_apply(RoundArgs a, BinArgs b) {
         const uint64_t sv = a.seen[v0 * W + i] | p;
         const bool va = !a.dead_mode || bit_alive(a.alive, (uint32_t)(a.begin + v0 + i / W));  // dead: no receive
         const uint64_t fr = va ? acc_s[i] & injm(a, i % W) & ~sv : 0ull;
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+            if (i % W == w) acc.fresh_or[w] |= fr;  // (constant register indices)
         if (fr) {  // handleClient: new -> Message-List insert (peer.cpp:281-282)
             acc.fresh += (unsigned long long)__popcll(fr);
             acc.activated++;
@@ -1740,6 +1773,9 @@ __global__ __launch_bounds__(kB) void k_bin_apply_runs(RoundArgs a, BinArgs b) {
         const uint64_t sv = a.seen[v0 * W + i];
         const bool va = !a.dead_mode || bit_alive(a.alive, (uint32_t)(a.begin + v0 + i / W));  // dead: no receive
         const uint64_t fr = va ? acc_s[i] & injm(a, i % W) & ~sv : 0ull;
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+            if (i % W == w) acc.fresh_or[w] |= fr;  // (constant register indices)
         if (fr) {  // handleClient: new -> Message-List insert (peer.cpp:281-282)
             a.seen[v0 * W + i] = sv | fr;
             acc.fresh += (unsigned long long)__popcll(fr);
@@ -2486,6 +2522,7 @@ __global__ __launch_bounds__(kBlock) void k_count_nx(RoundArgs a) {
             const uint64_t x = a.nx[v * W + w];
             any |= x != 0;
             acc.fresh += (unsigned long long)__popcll(x);
+            acc.fresh_or[w] |= x;
         }
         acc.activated += any;
     }

@@ -307,7 +307,7 @@ def test_reload_overlay_with_kills(oracle, mode):
 
 @pytest.mark.parametrize("env", ["GOSSIP_DEFER_PM=1", "GOSSIP_BIN_STREAM=1", "GOSSIP_PULL_ROWS=0", "GOSSIP_BIN_SPLIT=2",
                                  "GOSSIP_BIN_SPLIT=3", "GOSSIP_PULL_DEFER=1", "GOSSIP_BIN_PERMILLE=100000",
-                                 "GOSSIP_PULL_FIRST2=0", "GOSSIP_DEFER_NR=1"])
+                                 "GOSSIP_PULL_FIRST2=0", "GOSSIP_DEFER_NR=1", "GOSSIP_FLIGHT=0"])
 @pytest.mark.parametrize("idx,n,mode", [(2, 1 << 16, "auto"), (3, 1 << 18, "bin"), (5, 50_000, "auto"),
                                         (5, 1 << 16, "push"), (3, 1 << 18, "pull")])
 def test_engine_variants_match_oracle(oracle, monkeypatch, env, idx, n, mode):
