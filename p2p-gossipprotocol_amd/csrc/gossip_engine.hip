@@ -187,6 +187,7 @@ struct gossip_ctx {
     uint64_t frontier_est = 0;   // activated peers of the previous round
     std::vector<uint64_t> inj_prefix;  // per sorted injection: cumulative mask words
     uint64_t cum_digest = 0, cum_covered = 0;
+    uint64_t cum_dead_cov = 0, cum_died = 0, cum_injected = 0;  // P = 1: for the binned-round test
 
     // partitioned exchange
     uint64_t* send = nullptr;
@@ -719,8 +720,18 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
     {
         uint64_t injected = 0;
         for (int w = 0; w < kMaxWords; ++w) injected += (uint64_t)__builtin_popcountll(a.inj_mask[w]);
-        const uint64_t have = c->cum_covered + c->last_fresh + cnt;
-        const uint64_t total = injected * c->n_local;
+        uint64_t have = c->cum_covered + c->last_fresh + cnt, peers = c->n_local;
+        // P = 1 with every round's stats read: only the live peers can still learn, only messages that were
+        // injected exist, and the pairs the dead held leave the count (config 5 at round 7: ≈ 4 of the
+        // "missing" pairs per peer were dead peers' and never-injected messages', which kept it binned)
+        if (c->world <= 1 && c->n_local == c->n && !c->cfg.rejoin_threshold && c->flight_round + 1 == c->round &&
+            c->round > 0) {
+            const uint64_t sched = injected;
+            injected = std::min<uint64_t>(sched, c->cum_injected + cnt);
+            peers = c->n_started > c->cum_died ? c->n_started - c->cum_died : 0;
+            have = have > c->cum_dead_cov ? have - c->cum_dead_cov : 0;
+        }
+        const uint64_t total = injected * peers;
         missing = total > have ? total - have : 0;
     }
     if (!remote && pull_ok && c->bins_ready && requested == GOSSIP_MODE_AUTO) {
@@ -940,6 +951,9 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
     if (cumulative) {
         c->cum_digest += d.digest;
         c->cum_covered += d.covered;
+        c->cum_dead_cov += d.dead_covered;
+        c->cum_died += d.died;
+        c->cum_injected += d.injected;
         s.digest = c->cum_digest;
         s.covered = c->cum_covered;
     } else {
@@ -1379,6 +1393,7 @@ gossip_status gossip_reset(gossip_ctx* c) {
     c->finished = false;
     c->any_dead = c->n_started < c->n;
     c->cum_digest = c->cum_covered = 0;
+    c->cum_dead_cov = c->cum_died = c->cum_injected = 0;
     if (c->dist) gossip::dist_reset(c->dist);
     HIPCHK(hipStreamSynchronize(s));
     return GOSSIP_OK;

@@ -24,10 +24,11 @@ struct DevStats {
     unsigned long long frontier, traversals, deliveries, undelivered, new_receipts, injected, died, reports,
         seed_removals, digest, covered, heavy_traversals, live_checked, activated, pull_edges, pull_gathers,
         reconnects, rejoined, atomics,  // atomics: device-scope atomics issued on peer state (seen, nx, marks)
-        diag;                           // measurement counters (GOSSIP_PULL_DIAG)
+        diag,                           // measurement counters (GOSSIP_PULL_DIAG)
+        dead_covered;                   // (peer, message) pairs held by the peers that died this round
     unsigned long long fresh_or[8];     // OR of the round's receipts (the next round's new words), word w
 };
-constexpr int kStatSums = 20;                 // fields summed; the kMaxWords after them are OR-ed
+constexpr int kStatSums = 21;                 // fields summed; the kMaxWords after them are OR-ed
 constexpr int kStatFields = kStatSums + 8;
 static_assert(sizeof(DevStats) == kStatFields * 8, "DevStats layout");
 

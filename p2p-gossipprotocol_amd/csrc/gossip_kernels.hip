@@ -58,7 +58,7 @@ struct Acc {
     unsigned long long frontier = 0, trav = 0, deliv = 0, undeliv = 0, fresh = 0, digest = 0, covered = 0, died = 0,
                        reports = 0, removals = 0, injected = 0, htrav = 0, checked = 0,
                        activated = 0, pulled = 0, gathered = 0, reconnects = 0, rejoined = 0, atomics = 0,
-                       diag = 0;
+                       diag = 0, dead_cov = 0;
     unsigned long long fresh_or[kMaxWords] = {};  // OR of the receipts (only the words a kernel touches stay)
 };
 
@@ -86,7 +86,7 @@ __device__ __forceinline__ void flush_into(Acc& acc, DevStats* st, unsigned long
     const unsigned long long v[kF] = {acc.frontier, acc.trav,     acc.deliv,   acc.undeliv, acc.fresh,  acc.injected,
                                       acc.died,     acc.reports,  acc.removals, acc.digest, acc.covered, acc.htrav,
                                       acc.checked,  acc.activated, acc.pulled,  acc.gathered, acc.reconnects,
-                                      acc.rejoined, acc.atomics, acc.diag,
+                                      acc.rejoined, acc.atomics, acc.diag, acc.dead_cov,
                                       acc.fresh_or[0], acc.fresh_or[1], acc.fresh_or[2], acc.fresh_or[3],
                                       acc.fresh_or[4], acc.fresh_or[5], acc.fresh_or[6], acc.fresh_or[7]};
 #pragma unroll
@@ -2319,6 +2319,7 @@ __device__ __forceinline__ void retire_peer(const RoundArgs& a, uint32_t v, uint
 #pragma unroll
     for (int w = 0; w < W; ++w) {
         const uint64_t mm = a.nw[lv * W + w];
+        acc.dead_cov += (unsigned long long)__popcll(a.seen[lv * W + w] | mm);  // (a pending fold: mm not in seen)
         if (!mm) continue;
         if (w < (int)wd) acc.digest += digest_weight((uint64_t)v * wd + w) * mm;
         acc.covered += (unsigned long long)__popcll(mm);
