@@ -172,6 +172,7 @@ struct gossip_ctx {
     bool flight_ok = true;        // GOSSIP_FLIGHT=0: needy tests ignore which bits are in flight (A/B)
     uint64_t flight[kMaxWords] = {};  // receipts of round flight_round (from its stats)
     uint32_t flight_round = ~0u;
+    uint32_t dgone_next = 0;      // first round whose deaths dgone does not count yet
     bool pdefer_ok = false;       // GOSSIP_PULL_DEFER=1: defer wide pull rounds (A/B: config 4 round 7 -0.3 to
                                   // -0.75 ms, round 8's fold +0.5 to +0.7 ms, so off by default)
     bool pull_diag = false;       // GOSSIP_PULL_DIAG: count the gathers of an early-exit row scan (measurement)
@@ -644,8 +645,6 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
         c->any_dead = true;
         HIPCHK(timed(c, "churn", [&] { return launch_churn(a, pw, c->cfg.rng_seed, c->cfg.churn_threshold, c->stream); }));
     }
-    if (c->death_r && (cnt || c->cfg.churn_threshold))  // this round's deaths -> their in-neighbours' dgone
-        HIPCHK(timed(c, "churn", [&] { return launch_dead_edges(a, c->stream); }));
     if (c->cfg.rejoin_threshold && c->cfg.extra_cap)  // the restarted peers' new out-edges, after the deaths
         HIPCHK(timed(c, "rejoin", [&] {
             return launch_rejoin_select(a, c->reboot, c->rj_list, c->rj_n, c->n_local, c->stream);
@@ -779,6 +778,14 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
     // a row's first step from its queue entry: worth the extra 8 B per swept peer while many rows are
     // needy (config 4 round 7: 90 M rows, one random col line each); rows are unmasked (no liveness yet)
     a.first2 = rows_pull && c->first_ok && !c->any_masked && missing * 4 >= c->n_local ? c->first2 : nullptr;
+    // the deaths since the last dense round -> their in-neighbours' dgone, which only the source side of
+    // dense rounds reads (one walk over their rows instead of one per round; the deaths of the push rounds
+    // after the last dense round are never walked: config 5, rounds 9-11)
+    if (pull && c->death_r && c->dgone_next <= c->round) {
+        const uint32_t lo = c->dgone_next, hi = c->round;
+        HIPCHK(timed(c, "churn", [&] { return launch_dead_edges(a, lo, hi, c->stream); }));
+        c->dgone_next = c->round + 1;
+    }
     c->last_pull = pull;
     c->last_bin = bin;
     c->last_front = false;
@@ -1387,6 +1394,7 @@ gossip_status gossip_reset(gossip_ctx* c) {
     c->last_bin = false;
     c->cur_defer = c->cur_pdefer = false;
     c->flight_round = ~0u;
+    c->dgone_next = 0;
     c->last_fresh = 0;
     c->frontier_est = c->prev_frontier_est = 0;
     c->round = 0;

@@ -226,7 +226,7 @@ hipError_t launch_rebootstrap(const RoundArgs& a, const RebootArgs& r, const uns
 hipError_t launch_src_count(const RoundArgs& a, uint32_t W, hipStream_t s);
 // after the round's deaths: dgone[u]++ for every in-neighbour u of a peer
 // that died this round (its own row, the overlay being symmetric)
-hipError_t launch_dead_edges(const RoundArgs& a, hipStream_t s);
+hipError_t launch_dead_edges(const RoundArgs& a, uint32_t lo, uint32_t hi, hipStream_t s);  // deaths of rounds [lo, hi]
 // closed-form liveness of a ping round: the in-edges of peers that died in
 // death rounds [lo, hi] reach max_missed misses now; alive reporters mask them,
 // report and (dmask) count them

@@ -2921,7 +2921,9 @@ static hipError_t launch_rows(const RoundArgs& a, uint32_t lo, uint32_t hi, hipS
     return hipGetLastError();
 }
 
-hipError_t launch_dead_edges(const RoundArgs& a, hipStream_t s) { return launch_rows<kRowsDead>(a, a.round, a.round, s); }
+hipError_t launch_dead_edges(const RoundArgs& a, uint32_t lo, uint32_t hi, hipStream_t s) {
+    return launch_rows<kRowsDead>(a, lo, hi, s);
+}
 
 hipError_t launch_liveness_window(const RoundArgs& a, uint32_t lo, uint32_t hi, hipStream_t s) {
     return launch_rows<kRowsLive>(a, lo, hi, s);
