@@ -525,6 +525,68 @@ gossip_status upload_csr(gossip_ctx* c, const uint64_t* rp, const uint32_t* col,
     return install_graph(c, d_rp, d_col, m);
 }
 
+// The scatter's store rate depends on where the slot array's pages landed: the same library ran its
+// binned rounds' scatter at 9.2-9.4 ms in some processes and 10.7-11.8 in others, the apply (a
+// sequential read of the same array) at 5.0-5.8 in all, and a physically contiguous array at 14 ms.
+// Allocations in one process differ too (trial scatters of 9.3 / 10.3 / 8.8 ms), though some processes
+// get only slow ones.  On big layouts, time one full scatter (every slot rewritten) into each of four
+// allocations and keep the fastest (GOSSIP_VAL_TUNE=0: keep the first; 2: print the trials); config 4,
+// five processes each: scatter 9.3-11.3 (mean 9.9) against 9.7-11.7 (mean 10.4) ms.  The trial words
+// are garbage: the first binned round rewrites every slot.
+gossip_status tune_val(gossip_ctx* c) {
+    const char* env = std::getenv("GOSSIP_VAL_TUNE");
+    if ((env && !std::atoi(env)) || c->bin_stream || c->bins.n_slots < (1ull << 26)) return GOSSIP_OK;
+    const uint64_t bytes = (c->bins.n_slots + 64) * c->Wp * sizeof(uint64_t);
+    constexpr int kCand = 4;
+    uint64_t* cand[kCand] = {c->bins.val};
+    for (int k = 1; k < kCand; ++k)
+        if (hipMalloc((void**)&cand[k], bytes) != hipSuccess) {
+            hipGetLastError();
+            cand[k] = nullptr;
+        }
+    RoundArgs a = make_args(c);
+    a.dead_mode = 0;
+    a.cov = nullptr;
+    a.defer = 0;
+    a.fold = 0;
+    a.tcur = a.tnx = nullptr;
+    BinArgs b{c->bins.bins,     c->bins.n_bins,    c->bins.cb_src,  c->bins.cb_run,    c->bins.cb_grp,
+              c->bins.n_binned, c->bins.chunk_begin, c->bins.n_chunks, c->bins.chunk,    c->bins.units,
+              c->bins.xcd_units, c->bins.bdst,     c->bins.val,     c->bins.bin_words, c->bins.dummy,   1u,
+              0u,               c->bins.n_runs ? c->bins.n_runs - 1 : 0, c->bins.ap_run, c->bins.ap_grp,
+              0u,               c->bins.cb_slot,   c->bins.split};
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    float best = 0.f;
+    int bi = 0;
+    for (int k = 0; k < kCand; ++k) {
+        if (!cand[k]) continue;
+        b.val = cand[k];
+        float ms = 0.f;
+        for (int rep = 0; rep < 2; ++rep) {  // the second launch is timed
+            HIPCHK(hipEventRecord(e0, c->stream));
+            HIPCHK(launch_bin_scatter(a, b, pack_w(c), c->stream));
+            HIPCHK(hipEventRecord(e1, c->stream));
+            HIPCHK(hipEventSynchronize(e1));
+            HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+        }
+        if (env && std::atoi(env) == 2) fprintf(stderr, "tune_val: candidate %d %.3f ms\n", k, ms);
+        if (k == 0 || ms < best) {
+            best = ms;
+            bi = k;
+        }
+    }
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    for (int k = 0; k < kCand; ++k)
+        if (cand[k] && k != bi) hipFree(cand[k]);
+    c->bins.val = cand[bi];
+    HIPCHK(hipMemsetAsync(c->st, 0, kStatLines * sizeof(DevStats), c->stream));  // the trials' stats
+    c->bins_first = true;  // the trials left words in every slot
+    return GOSSIP_OK;
+}
+
 // Slot layout for binned dense rounds: only for a full, symmetric overlay
 // (pull-eligible); skipped, not failed, when it does not fit in HBM.
 gossip_status prepare_bins(gossip_ctx* c) {
@@ -538,7 +600,7 @@ gossip_status prepare_bins(gossip_ctx* c) {
     if (e == hipErrorOutOfMemory || e == hipErrorInvalidValue) return GOSSIP_OK;  // dense rounds gather instead
     if (e != hipSuccess) return fail(GOSSIP_EHIP, "bin layout: " + err);
     c->bins_ready = true;
-    return GOSSIP_OK;
+    return tune_val(c);
 }
 
 // seen |= nw for a deferred round whose fold was left to the next binned round
