@@ -421,7 +421,11 @@ gossip_status install_graph(gossip_ctx* c, uint64_t* d_rp, uint32_t* d_col, uint
     unsigned long long* d_cnt = nullptr;
     HIPCHK(hipMalloc((void**)&d_cnt, 2 * sizeof(unsigned long long)));
     HIPCHK(hipMemsetAsync(d_cnt, 0, 2 * sizeof(unsigned long long), c->stream));
-    HIPCHK(launch_heavy_count(c->rp, c->n_local, c->heavy, d_cnt, c->stream));
+    // heavy chunks: a wave each; on small overlays (cache-resident) a chunk's chain of 64-edge batches, not the
+    // number of chunks, sets k_pull_heavy's time -- shorter chunks there (GOSSIP_HEAVY_CHUNK overrides)
+    uint32_t clen = c->n_local < (1ull << 22) ? 256u : kHeavyChunk;
+    if (const char* e = std::getenv("GOSSIP_HEAVY_CHUNK")) clen = std::max(64, std::atoi(e)) / 64 * 64;
+    HIPCHK(launch_heavy_count(c->rp, c->n_local, c->heavy, clen, d_cnt, c->stream));
     unsigned long long nch = 0;
     HIPCHK(hipMemcpyAsync(&nch, d_cnt, sizeof(nch), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -429,7 +433,7 @@ gossip_status install_graph(gossip_ctx* c, uint64_t* d_rp, uint32_t* d_col, uint
     if (nch) {
         HIPCHK(hipMalloc((void**)&c->chunks, nch * sizeof(HeavyChunk)));
         HIPCHK(hipMalloc((void**)&c->hacc, nch * c->Wp * sizeof(uint64_t)));
-        HIPCHK(launch_heavy_fill(c->rp, c->n_local, c->heavy, c->chunks, d_cnt + 1, c->stream));
+        HIPCHK(launch_heavy_fill(c->rp, c->n_local, c->heavy, clen, c->chunks, d_cnt + 1, c->stream));
     }
     HIPCHK(hipStreamSynchronize(c->stream));
     hipFree(d_cnt);

@@ -11,7 +11,7 @@ namespace gossip {
 
 constexpr uint32_t kMaskedEdge = 0x80000000u;  // col[e] bit 31: edge dropped by liveness (peer.cpp:388)
 constexpr uint32_t kHeavyDegree = 256;         // default: rows longer than this go to the edge-chunked kernels
-constexpr uint32_t kHeavyChunk = 1024;         // edges per heavy chunk (one wave)
+constexpr uint32_t kHeavyChunk = 1024;         // edges per heavy chunk (one wave); 256 below 2^22 owned peers
 constexpr int kBlock = 256;                    // 4 waves of 64
 constexpr int kMaxWords = 8;                   // M <= 512 concurrent messages
 constexpr int kStatLines = 64;                 // striped DevStats lines per round (summed at read)
@@ -247,9 +247,9 @@ hipError_t launch_count_nx(const RoundArgs& a, uint32_t W_, hipStream_t s);
 hipError_t launch_zero_words(uint64_t* words, uint64_t n_words, hipStream_t s);
 hipError_t launch_coverage(const uint64_t* words, uint64_t n_local, uint32_t W, unsigned long long* counts,
                            hipStream_t s);
-hipError_t launch_heavy_count(const uint64_t* rp, uint64_t n_local, uint32_t heavy, unsigned long long* n_chunks,
-                              hipStream_t s);
-hipError_t launch_heavy_fill(const uint64_t* rp, uint64_t n_local, uint32_t heavy, HeavyChunk* chunks,
+hipError_t launch_heavy_count(const uint64_t* rp, uint64_t n_local, uint32_t heavy, uint32_t clen,
+                              unsigned long long* n_chunks, hipStream_t s);
+hipError_t launch_heavy_fill(const uint64_t* rp, uint64_t n_local, uint32_t heavy, uint32_t clen, HeavyChunk* chunks,
                              unsigned long long* cursor, hipStream_t s);
 
 // ---- overlay generator (gossip_graph.hip) ----

@@ -2560,26 +2560,26 @@ __global__ __launch_bounds__(kBlock) void k_first2(const uint64_t* rp, const uin
     }
 }
 
-__global__ void k_heavy_count(const uint64_t* rp, uint64_t n, uint32_t heavy, unsigned long long* n_chunks) {
+__global__ void k_heavy_count(const uint64_t* rp, uint64_t n, uint32_t heavy, uint32_t clen, unsigned long long* n_chunks) {
     unsigned long long mine = 0;
     for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t d = rp[v + 1] - rp[v];
-        if (d > heavy) mine += (d + kHeavyChunk - 1) / kHeavyChunk;
+        if (d > heavy) mine += (d + clen - 1) / clen;
     }
     mine = wave_sum(mine);
     if ((threadIdx.x & 63) == 0 && mine) atomicAdd(n_chunks, mine);
 }
 
-__global__ void k_heavy_fill(const uint64_t* rp, uint64_t n, uint32_t heavy, HeavyChunk* chunks,
+__global__ void k_heavy_fill(const uint64_t* rp, uint64_t n, uint32_t heavy, uint32_t clen, HeavyChunk* chunks,
                              unsigned long long* cursor) {
     for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t b = rp[v], e = rp[v + 1];
         if (e - b <= heavy) continue;
-        const uint64_t nc = (e - b + kHeavyChunk - 1) / kHeavyChunk;
+        const uint64_t nc = (e - b + clen - 1) / clen;
         const unsigned long long at = atomicAdd(cursor, (unsigned long long)nc);
         for (uint64_t k = 0; k < nc; ++k) {
-            const uint64_t e0 = b + k * kHeavyChunk;
-            chunks[at + k] = HeavyChunk{(uint32_t)v, (uint32_t)at, e0, e0 + kHeavyChunk < e ? e0 + kHeavyChunk : e};
+            const uint64_t e0 = b + k * clen;
+            chunks[at + k] = HeavyChunk{(uint32_t)v, (uint32_t)at, e0, e0 + clen < e ? e0 + clen : e};
         }
     }
 }
@@ -2972,16 +2972,17 @@ hipError_t launch_coverage(const uint64_t* words, uint64_t n_local, uint32_t W_,
     return hipGetLastError();
 }
 
-hipError_t launch_heavy_count(const uint64_t* rp, uint64_t n_local, uint32_t heavy, unsigned long long* n_chunks,
-                              hipStream_t s) {
-    hipLaunchKernelGGL(k_heavy_count, dim3(grid_for(n_local, kBlock)), dim3(kBlock), 0, s, rp, n_local, heavy, n_chunks);
+hipError_t launch_heavy_count(const uint64_t* rp, uint64_t n_local, uint32_t heavy, uint32_t clen,
+                              unsigned long long* n_chunks, hipStream_t s) {
+    hipLaunchKernelGGL(k_heavy_count, dim3(grid_for(n_local, kBlock)), dim3(kBlock), 0, s, rp, n_local, heavy, clen,
+                       n_chunks);
     return hipGetLastError();
 }
 
-hipError_t launch_heavy_fill(const uint64_t* rp, uint64_t n_local, uint32_t heavy, HeavyChunk* chunks,
+hipError_t launch_heavy_fill(const uint64_t* rp, uint64_t n_local, uint32_t heavy, uint32_t clen, HeavyChunk* chunks,
                              unsigned long long* cursor, hipStream_t s) {
-    hipLaunchKernelGGL(k_heavy_fill, dim3(grid_for(n_local, kBlock)), dim3(kBlock), 0, s, rp, n_local, heavy, chunks,
-                       cursor);
+    hipLaunchKernelGGL(k_heavy_fill, dim3(grid_for(n_local, kBlock)), dim3(kBlock), 0, s, rp, n_local, heavy, clen,
+                       chunks, cursor);
     return hipGetLastError();
 }
 
