@@ -155,7 +155,7 @@ struct gossip_ctx {
     bool bin_noskip = false;     // GOSSIP_BIN_NOSKIP: rewrite every slot each binned round (A/B measurement)
     uint32_t scatter_probe = 0;  // GOSSIP_SCATTER_PROBE: partial scatter for timing breakdowns (wrong results)
     uint32_t bin_front_pm = 0;    // binned rounds need a frontier of >= this per-mille (GOSSIP_BIN_FRONT_PM;
-                                  // 0: 100, or 20 from 2^25 owned peers on -- see round_begin)
+                                  // 0: 20 -- see round_begin)
     bool heavy_exit = true;       // k_pull_heavy early exit (GOSSIP_HEAVY_EXIT=0: off, A/B)
     bool bin_stream = false;      // streamed binned layout (GOSSIP_BIN_STREAM=1; A/B: 1-1.5 ms per binned
                                   // round slower at config 4)
@@ -804,10 +804,11 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
             pull = bin = true;
         } else if (pull && !(c->cfg.flags & GOSSIP_FLAG_FORCE_PULL)) {
             const uint32_t bpm = c->cfg.bin_permille ? c->cfg.bin_permille : 4000;
-            // a narrow frontier is cheaper to gather from while the frontier bitmap (n bits) stays in an
-            // XCD's 4 MB L2; beyond 2^25 peers its probes go to the MALL: config 5 (2^26, round 3 at an 8 %
-            // frontier) pull 8.6 ms against 4.0 binned; config 2 (2^20, a 5 % round) pull 0.18 against 0.33
-            const uint32_t front_pm = c->bin_front_pm ? c->bin_front_pm : c->n_local >= (1ull << 25) ? 20u : 100u;
+            // binned from a 2 % frontier: config 5 (2^26, round 3 at an 8 % frontier) pull 8.6 ms against
+            // 4.0 binned; config 2 (2^20, 5 % rounds) kernels 7.5-7.6 against 6.9-7.1 ms per step once its
+            // bins and chunks were sized for small overlays (with whole-slice bins pull had won, 0.18
+            // against 0.33 ms per round)
+            const uint32_t front_pm = c->bin_front_pm ? c->bin_front_pm : 20u;
             // and only on a wide frontier: a narrow one is cheaper to gather from (frontier bitmap)
             bin = missing * 1000 >= c->n_local * (uint64_t)bpm &&
                   (c->frontier_est + cnt) * 1000 >= c->n_local * (uint64_t)front_pm;
