@@ -909,12 +909,12 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
         q_tail += (uint32_t)__popcll(bal);
     };
     TileIn nxt;
-    if (t < n_tiles) load_tile(t, nxt);
+    load_tile(t, nxt);
     while (true) {
         // refill the queue while it has room for a whole tile
         while (t < n_tiles && q_tail - q_head <= (uint32_t)(kRowQ - 64)) {
             const TileIn cur = nxt;
-            if (t + nwaves < n_tiles) load_tile(t + nwaves, nxt);
+            load_tile(t + nwaves, nxt);  // unconditional (clamped): the wait before the sweep can then count it
             sweep_tile(t, cur);
             t += nwaves;
         }
