@@ -10,8 +10,14 @@ Default workload (N=1): BASELINE.json configs[3] -- 2^28 peers, power-law
 overlay, 64 concurrent messages from Philox-chosen origins, run to full
 coverage -- the largest configuration, and the one the metric's 1/2/4/8-GPU
 series is quoted on.  With --gpus N the same 2^28-peer overlay is
-vertex-partitioned over N ranks (strong scaling); libgossip_hip issues each
-round's RCCL collectives itself (gossip_comm_init).
+vertex-partitioned over N GPUs (strong scaling) and libgossip_hip issues
+each round's RCCL collectives itself:
+  * under a launcher (torchrun: WORLD_SIZE = N) one process per GPU joins the
+    communicator with gossip_comm_init;
+  * without one, this process drives GPUs 0..N-1 itself (gossip_group_create,
+    ncclCommInitAll) -- and exits non-zero if fewer GPUs are visible.
+--parts P (N = 1) runs the same partitioned driver as P parts on ONE GPU, the
+exchanges done by device copies: the single-GPU rehearsal of the N-GPU path.
 
 One JSON line on rank 0; see DESIGN.md section 7 for every field.
 """
@@ -28,6 +34,7 @@ REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO / "p2p-gossipprotocol_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+DENSE_KERNELS = ("bin_scatter", "bin_apply", "pull_heavy")  # the device work of a binned round
 
 
 def parse():
@@ -37,6 +44,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", type=int, default=4, help="BASELINE.json config index (1-5)")
     ap.add_argument("--n", type=int, default=0, help="override peer count")
+    ap.add_argument("--parts", type=int, default=0,
+                    help="N = 1 only: run the partitioned driver as this many parts on one GPU (device copies)")
     ap.add_argument("--cpu-sample-n", type=int, default=0, help="CPU baseline sample size, all threads (0: per config)")
     ap.add_argument("--cpu-sample-n1", type=int, default=0, help="CPU baseline sample size, 1 thread (0: per config)")
     ap.add_argument("--cpu-repeats", type=int, default=5)
@@ -54,47 +63,41 @@ def parse():
 
 
 # kernel timer name -> rocprofv3 kernel-name prefix in the PMC summary
-PMC_KERNELS = {"bin_scatter": ("k_bin_scatter_pc",), "bin_apply": ("k_bin_apply",),
+PMC_KERNELS = {"bin_scatter": ("k_bin_scatter_pc", "k_bin_stream"), "bin_apply": ("k_bin_apply",),
                "pull_light": ("k_pull_rows", "k_pull_light"),  # the row-queue pull is the default
                "push_light": ("k_push_light",), "push_heavy": ("k_push_heavy",), "pull_heavy": ("k_pull_heavy",)}
 
 
-def pmc_traffic(workload: str, kernel: str, alg_bytes_per_launch: float, n_local: int):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
-    (FETCH_SIZE and WRITE_SIZE, separate runs of this bench command on the same
-    config: tools/gpu_profile_r02.sh, newest round first) with the
-    gfx950 corrections measured by tools/calib_fetch.hip (profiles/r01/
-    calib_fetch_timing.log): FETCH_SIZE counts 1/2 of coalesced streamed bytes
-    and one 64-B line per random 8-B gather; WRITE_SIZE counts stores 1:1.
-    bin_scatter / bin_apply read only coalesced streams (traffic = 2 x fetch +
-    write); pull_light mixes streams with random gathers (only its streamed
-    reads are doubled)."""
-    if kernel not in PMC_KERNELS:
-        return None, None
+def pmc_traffic(workload: str, kernels, n_local: int):
+    """HBM bytes per launch of `kernels` (summed: one binned round runs each
+    once) from the committed rocprofv3 PMC passes (FETCH_SIZE and WRITE_SIZE,
+    separate runs of this bench command on the same config, newest round
+    first) with the gfx950 corrections measured by tools/calib_fetch.hip
+    (profiles/r01/calib_fetch_timing.log): FETCH_SIZE counts 1/2 of coalesced
+    streamed bytes and one 64-B line per random 8-B gather; WRITE_SIZE counts
+    stores 1:1.  The binned kernels read coalesced streams (traffic = 2 x
+    fetch + write); pull_heavy's gathers are counted 1:1."""
     cfg = workload.split("_")[0]  # "config4" ...
-    cands = [REPO / "profiles" / r / f"{cfg}_pmc_summary.json" for r in ("r02", "r01")]
+    cands = [REPO / "profiles" / r / f"{cfg}_pmc_summary.json" for r in ("r03", "r02", "r01")]
     path = next((p for p in cands if p.exists()), None)
     if path is None:
         return None, None
     prof = json.loads(path.read_text())
-    keys = [k for k in prof["kernels"] if any(k.startswith(p + "<") or k == p for p in PMC_KERNELS[kernel])]
-    keys = [k for k in keys if "fetch_bytes_per_launch_counted" in prof["kernels"][k]]
-    if not keys:
-        return None, None
-    launches = sum(prof["kernels"][k]["launches"] for k in keys)
-    fetch = sum(prof["kernels"][k]["fetch_bytes_per_launch_counted"] * prof["kernels"][k]["launches"] for k in keys)
-    write = sum(prof["kernels"][k].get("write_bytes_per_launch_counted", 0.0) * prof["kernels"][k]["launches"]
-                for k in keys)
-    fetch, write = fetch / launches, write / launches
-    if kernel in ("bin_scatter", "bin_apply"):
-        t = 2 * fetch + write
-    elif kernel == "pull_light":
-        scanned = max(alg_bytes_per_launch - 40.0 * n_local, 0.0) / 12.0
-        t = fetch + (24.0 * n_local + 4.0 * scanned) / 2 + write
-    else:
-        t = fetch + write
-    avg = sum(prof["kernels"][k]["avg_ms"] * prof["kernels"][k]["launches"] for k in keys) / launches
-    return round(t), f"{path.relative_to(REPO)} ({', '.join(keys)}: {launches} launches, avg {avg:.3f} ms)"
+    total, parts = 0.0, []
+    for kernel in kernels:
+        keys = [k for k in prof["kernels"] if any(k.startswith(p + "<") or k == p for p in PMC_KERNELS.get(kernel, ()))]
+        keys = [k for k in keys if "fetch_bytes_per_launch_counted" in prof["kernels"][k]]
+        if not keys:
+            return None, None
+        launches = sum(prof["kernels"][k]["launches"] for k in keys)
+        fetch = sum(prof["kernels"][k]["fetch_bytes_per_launch_counted"] * prof["kernels"][k]["launches"] for k in keys)
+        write = sum(prof["kernels"][k].get("write_bytes_per_launch_counted", 0.0) * prof["kernels"][k]["launches"]
+                    for k in keys)
+        fetch, write = fetch / launches, write / launches
+        total += (2 * fetch if kernel in ("bin_scatter", "bin_apply") else fetch) + write
+        avg = sum(prof["kernels"][k]["avg_ms"] * prof["kernels"][k]["launches"] for k in keys) / launches
+        parts.append(f"{', '.join(keys)}: {launches} launches, avg {avg:.3f} ms")
+    return round(total), f"{path.relative_to(REPO)} ({'; '.join(parts)})"
 
 
 def rounds_to_full(stats: list[dict]) -> int:
@@ -113,6 +116,14 @@ def _cpu_model() -> str:
     except OSError:
         pass
     return "unknown"
+
+
+def host_cores() -> int:
+    """CPUs this process may run on (its affinity mask: 16 of the box's 256 on a gpurun box)."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
 
 
 # CPU baseline samples per BASELINE.json config: (all-threads n, 1-thread n, literal-driver n or 0)
@@ -135,8 +146,8 @@ def cpu_baseline(args, cfg_idx: int) -> dict:
 
     so = REPO / "oracle" / "_build" / "libgossip_oracle.so"
     orc = oracle_ref.Oracle(so)
-    nproc = os.cpu_count() or 1
-    threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", 0) or nproc)
+    cores = host_cores()
+    threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", 0) or cores)
     n_all, n_one, n_lit = CPU_SAMPLES[cfg_idx]
     n_all = args.cpu_sample_n or n_all
     n_one = args.cpu_sample_n1 or n_one
@@ -159,10 +170,11 @@ def cpu_baseline(args, cfg_idx: int) -> dict:
            "traversal_gteps": round(a["traversal_gteps"], 4),
            "single_thread": {"value": round(o["gteps"], 4), "traversal_gteps": round(o["traversal_gteps"], 4),
                              "median_s": round(o["median_s"], 4), "runs_s": o["runs_s"], "sample": o["sample"]},
-           "nproc": nproc, "cpu_model": _cpu_model(), "median_s": round(a["median_s"], 4), "runs_s": a["runs_s"],
+           "host_cores": cores, "machine_cpus": os.cpu_count(), "cpu_model": _cpu_model(),
+           "median_s": round(a["median_s"], 4), "runs_s": a["runs_s"],
            "timed": "oracle_sim_run only (rounds); generation, allocation and read-backs excluded",
-           "sample": f"{a['sample']}, oracle fast driver, {threads} threads of {nproc} visible CPUs, "
-                     f"median of {args.cpu_repeats}"}
+           "sample": f"{a['sample']}, oracle fast driver, {threads} threads ({cores} CPUs in this process's affinity "
+                     f"mask), median of {args.cpu_repeats}"}
     if "literal" in out:
         lt = out["literal"]
         res["literal_driver"] = {"value": round(lt["gteps"], 6), "median_s": round(lt["median_s"], 4),
@@ -170,23 +182,148 @@ def cpu_baseline(args, cfg_idx: int) -> dict:
     return res
 
 
-def per_round_profile(eng) -> list[dict]:
-    """One run, stepped round by round with per-kernel timing (untimed pass)."""
-    from gossip_hip.engine import KERNELS
-    eng.reset()
-    eng.enable_timing(True)
-    prev = {k: eng.kernel_time(k)[0] for k in KERNELS}
+# ---- the three ways of running the workload --------------------------------------------------
+class Single:
+    """One ctx owns every peer (gossip_step / gossip_run)."""
+
+    def __init__(self, w, dev, tune):
+        from gossip_hip import Engine
+        self.eng = Engine(w.n, w.n_msgs, device=dev, **tune, **w.engine_kwargs())
+        self.eng.build_graph()
+        self.eng.inject(w.origins, w.inject_rounds)
+        if w.kills:
+            self.eng.schedule_kills([k[0] for k in w.kills], [k[1] for k in w.kills])
+        self.parts, self.n_gpus = 1, 1
+        sh = self.eng.shape()
+        self.n_edges, self.n_local = sh["n_edges"], [sh["n_local"]]
+
+    def step(self):
+        self.eng.reset()
+        return self.eng.run()
+
+    def sync(self):
+        import torch
+        torch.cuda.synchronize()
+
+    def timing(self, on):
+        self.eng.enable_timing(on)
+
+    def ktime(self, p, k):
+        return self.eng.kernel_time(k)
+
+    def kbytes(self, p, k):
+        return self.eng.kernel_bytes(k)
+
+    def round_step(self):
+        return self.eng.step()
+
+    def reset(self):
+        self.eng.reset()
+
+    def close(self):
+        self.eng.close()
+
+
+class Grouped(Single):
+    """One process drives P parts (gossip_group_*): on P GPUs (RCCL from
+    ncclCommInitAll) or, emulated, all on one GPU (device copies)."""
+
+    def __init__(self, w, devices, tune):
+        from gossip_hip import Group
+        self.g = Group(w.n, w.n_msgs, devices, **tune, **w.engine_kwargs())
+        self.g.build_graph()
+        self.g.inject(w.origins, w.inject_rounds)
+        if w.kills:
+            self.g.schedule_kills([k[0] for k in w.kills], [k[1] for k in w.kills])
+        self.devices = devices
+        self.parts, self.n_gpus = len(devices), len(set(devices))
+        shapes = [self.g.shape(p) for p in range(self.parts)]
+        self.n_edges = sum(s["n_edges"] for s in shapes)
+        self.n_local = [s["n_local"] for s in shapes]
+
+    def step(self):
+        self.g.reset()
+        return self.g.run()
+
+    def sync(self):
+        import torch
+        for d in sorted(set(self.devices)):
+            torch.cuda.synchronize(d)
+
+    def timing(self, on):
+        self.g.enable_timing(on)
+
+    def ktime(self, p, k):
+        return self.g.kernel_time(p, k)
+
+    def kbytes(self, p, k):
+        return self.g.kernel_bytes(p, k)
+
+    def round_step(self):
+        return self.g.step()
+
+    def reset(self):
+        self.g.reset()
+
+    def close(self):
+        self.g.close()
+
+
+class Ranked(Single):
+    """One process per GPU under a launcher: this rank's block, gossip_comm_init."""
+
+    def __init__(self, w, dev, tune, world, rank):
+        import torch.distributed as dist
+
+        from gossip_hip import Engine, comm_unique_id, partition
+        self.dist, self.world, self.rank = dist, world, rank
+        part = partition(w.n, world)
+        self.eng = Engine(w.n, w.n_msgs, device=dev, part=(part[rank], part[rank + 1]), **tune, **w.engine_kwargs())
+        self.eng.build_graph()
+        self.eng.inject(w.origins, w.inject_rounds)
+        if w.kills:
+            self.eng.schedule_kills([k[0] for k in w.kills], [k[1] for k in w.kills])
+        uid = [comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        self.eng.comm_init(uid[0], world, rank)
+        self.parts, self.n_gpus = 1, world
+        sh = self.eng.shape()
+        import torch
+        t = torch.tensor([sh["n_edges"]], dtype=torch.int64)
+        dist.all_reduce(t)
+        self.n_edges, self.n_local = int(t.item()), [sh["n_local"]]
+
+    def sync(self):
+        import torch
+        torch.cuda.synchronize()
+        self.dist.barrier()
+
+
+def per_round_profile(run, n_peers: int) -> list[dict]:
+    """One run, stepped round by round with per-kernel timing (untimed pass):
+    each round's mode, SURVEY 8(d)'s algorithmic bytes B_r = 32 F_r + 20 T_r
+    and the device time of its kernels (max over the parts of a partitioned
+    run) and exchanges."""
+    from gossip_hip.engine import EXCHANGES, KERNELS
+    names = KERNELS + EXCHANGES
+    run.reset()
+    run.timing(True)
+    prev = [{k: run.ktime(p, k)[0] for k in names} for p in range(run.parts)]
     rows = []
     while True:
-        st, fin = eng.step()
-        cur = {k: eng.kernel_time(k)[0] for k in KERNELS}
-        d = {k: cur[k] - prev[k] for k in KERNELS if cur[k] - prev[k] > 0}
+        st, fin = run.round_step()
+        cur = [{k: run.ktime(p, k)[0] for k in names} for p in range(run.parts)]
+        d = [{k: c[k] - q[k] for k in names if c[k] - q[k] > 0} for c, q in zip(cur, prev)]
         prev = cur
-        mode = "bin" if "bin_scatter" in d else "pull" if "pull_light" in d else "push"
-        rows.append({"round": st["round"], "mode": mode, "frontier_frac": round(st["frontier"] / eng.n_peers, 4),
+        mode = "bin" if any("bin_scatter" in x for x in d) else "pull" if any("pull_light" in x for x in d) else "push"
+        kms = max(sum(v for k, v in x.items() if k in KERNELS) for x in d)
+        xms = max(sum(v for k, v in x.items() if k in EXCHANGES) for x in d)
+        dense = max(sum(x.get(k, 0.0) for k in DENSE_KERNELS) for x in d)
+        rows.append({"round": st["round"], "mode": mode, "frontier_frac": round(st["frontier"] / n_peers, 4),
                      "traversals": st["traversals"], "alg_bytes": 32 * st["frontier"] + 20 * st["traversals"],
-                     "kernel_ms": round(sum(d.values()), 3)})
+                     "kernel_ms": round(kms, 3), "exchange_ms": round(xms, 3), "dense_ms": round(dense, 3)})
         if fin:
+            run.timing(False)
             return rows
 
 
@@ -197,76 +334,50 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and world > 1:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-
-    from gossip_hip import Engine
+    if world > 1 and args.gpus != world:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}: {world} ranks run", file=sys.stderr)
+    from gossip_hip import device_count
     from gossip_hip.workloads import config
 
     w = config(args.config, args.n or None, rebootstrap=args.rebootstrap)
     tune = dict(pull_permille=args.pull_permille, front_permille=args.front_permille, mode=args.mode)
-    partitioned = world > 1 or args.force_partitioned
-    if partitioned:
+    dist = None
+    if world > 1 or args.force_partitioned:
         # one process per GPU; libgossip_hip drives every round's RCCL collectives
         # itself (gossip_comm_init); torch.distributed (gloo, host side) only hands
         # out the RCCL unique id and keeps the barrier and max-over-ranks timing
         import torch.distributed as dist
-
-        from gossip_hip import comm_unique_id, partition
-
         for k, v in (("RANK", "0"), ("WORLD_SIZE", "1"), ("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29511")):
             os.environ.setdefault(k, v)  # --force-partitioned run without a launcher
+        torch.cuda.set_device(local)
         dist.init_process_group("gloo")
-        part = partition(w.n, world)
-        eng = Engine(w.n, w.n_msgs, device=local, part=(part[rank], part[rank + 1]), **tune, **w.engine_kwargs())
-        eng.build_graph()
-        eng.inject(w.origins, w.inject_rounds)
-        if w.kills:
-            eng.schedule_kills([k[0] for k in w.kills], [k[1] for k in w.kills])
-        uid = [comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        eng.comm_init(uid[0], world, rank)
-
-        def one_step():
-            eng.reset()
-            return eng.run()
-
-        def barrier():
-            torch.cuda.synchronize()
-            dist.barrier()
+        run = Ranked(w, local, tune, world, rank)
+    elif args.gpus > 1:
+        have = device_count()
+        if have < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs, this process sees {have} "
+                  f"(one process drives GPUs 0..{args.gpus - 1} through gossip_group_create; or launch "
+                  f"{args.gpus} ranks with torchrun)", file=sys.stderr)
+            sys.exit(2)
+        run = Grouped(w, list(range(args.gpus)), tune)
+    elif args.parts > 1:
+        torch.cuda.set_device(local)
+        run = Grouped(w, [local] * args.parts, tune)
     else:
-        eng = Engine(w.n, w.n_msgs, device=local, **tune, **w.engine_kwargs())
-        eng.build_graph()
-        eng.inject(w.origins, w.inject_rounds)
-        if w.kills:
-            eng.schedule_kills([k[0] for k in w.kills], [k[1] for k in w.kills])
+        torch.cuda.set_device(local)
+        run = Single(w, local, tune)
 
-        def one_step():
-            eng.reset()
-            return eng.run()
-
-        def barrier():
-            torch.cuda.synchronize()
-
-    shape = eng.shape()
-    n_edges = shape["n_edges"]
-    if partitioned:
-        t = torch.tensor([n_edges], dtype=torch.int64)
-        dist.all_reduce(t)
-        n_edges = int(t.item())
     for _ in range(args.warmup):
-        one_step()
+        run.step()
     # the headline: K steps with per-kernel timing off (no events in the timed loop)
-    barrier()
+    run.sync()
     t0 = time.perf_counter()
     stats = None
     for _ in range(args.steps):
-        stats = one_step()
-    barrier()
+        stats = run.step()
+    run.sync()
     dt = time.perf_counter() - t0
-    if partitioned:
+    if dist is not None:
         t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
@@ -274,63 +385,77 @@ def main():
     deliveries = sum(s["deliveries"] for s in stats)
     value = args.steps * deliveries / dt / 1e9
     roofline = None
-    timed_steps = 0
+    rounds_prof = None
     if not args.no_timing:
-        # per-kernel device times from HIP events on the ctx stream, in a separate pass of the same steps
-        from gossip_hip.engine import KERNELS
+        from gossip_hip.engine import EXCHANGES, KERNELS
+        # per-kernel device times from HIP events on each part's stream, in a separate pass of the same steps
         timed_steps = min(args.steps, 5)
-        eng.enable_timing(True)
-        barrier()
+        run.timing(True)
+        run.sync()
         t1 = time.perf_counter()
         for _ in range(timed_steps):
-            one_step()
-        barrier()
+            run.step()
+        run.sync()
         dt_timed = time.perf_counter() - t1
-        k_ms = {k: eng.kernel_time(k) for k in KERNELS}
-        k_b = {k: eng.kernel_bytes(k) for k in KERNELS}
-        dom = max(k_ms, key=lambda k: k_ms[k][0])
-        ms, launches = k_ms[dom]
-        if ms > 0 and launches:
-            per_launch_bytes = k_b[dom] / launches
-            avg_s = ms / launches / 1e3
-            ach = per_launch_bytes / avg_s / 1e9
-            traffic, tsrc = pmc_traffic(w.name, dom, per_launch_bytes, shape["n_local"])
-            roofline = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
-                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-                        "traffic_source": tsrc,
-                        "avg_launch_ms": round(ms / launches, 4), "launches": launches,
-                        "alg_bytes_per_launch": round(per_launch_bytes),
-                        "timed_steps": timed_steps,
-                        "ms_per_step_with_events": round(dt_timed / timed_steps * 1e3, 3),
-                        "kernel_ms_per_step": {k: round(v[0] / timed_steps, 3) for k, v in k_ms.items() if v[1]},
-                        "kernel_frac": {k: round(k_b[k] / (v[0] / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
-                                        for k, v in k_ms.items() if v[0] > 0 and k_b[k] > 0}}
-
-    # per-round pass (untimed, P = 1): one step round by round with per-kernel
-    # deltas -- which rounds ran binned / pull / push, and SURVEY 8(d)'s
-    # algorithmic bytes B_r = 32 F_r + 20 T_r against the kernels' device time
-    rounds_prof = None
-    if not partitioned and not args.no_timing:
-        rounds_prof = per_round_profile(eng)
-        traversals = sum(s["traversals"] for s in stats)
-        alg = sum(r["alg_bytes"] for r in rounds_prof)
+        k_ms = [{k: run.ktime(p, k) for k in KERNELS + EXCHANGES} for p in range(run.parts)]
+        k_b = [{k: run.kbytes(p, k) for k in KERNELS + EXCHANGES} for p in range(run.parts)]
+        run.timing(False)
+        # the per-round pass: which rounds ran binned / pull / push, their 8(d) bytes and device time
+        rounds_prof = per_round_profile(run, w.n)
         dense = [r for r in rounds_prof if r["mode"] == "bin"]
-        if roofline is not None:
-            roofline["step_frac"] = round(alg / (dt / args.steps) / 1e9 / HBM_PEAK_GBS, 4)
-            if dense:
-                d_b = sum(r["alg_bytes"] for r in dense)
-                d_ms = sum(r["kernel_ms"] for r in dense)
-                roofline["dense_round"] = {"rounds": [r["round"] for r in dense], "alg_bytes": d_b,
-                                           "kernel_ms": round(d_ms, 3),
-                                           "frac": round(d_b / (d_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                                           "kernels": "bin_scatter + bin_apply + pull_heavy"}
+        alg = sum(r["alg_bytes"] for r in rounds_prof)
+        # the dominant kernel by device time (part 0's; every part runs the same schedule)
+        dom = max((k for k in KERNELS), key=lambda k: k_ms[0][k][0])
+        ms, launches = k_ms[0][dom]
+        roofline = {"bound": "hbm", "peak": HBM_PEAK_GBS * run.n_gpus, "unit": "GB/s",
+                    "step_frac": round(alg / (dt / args.steps) / 1e9 / (HBM_PEAK_GBS * run.n_gpus), 4),
+                    "timed_steps": timed_steps,
+                    "ms_per_step_with_events": round(dt_timed / timed_steps * 1e3, 3),
+                    "kernel_ms_per_step": {k: round(max(x[k][0] for x in k_ms) / timed_steps, 3)
+                                           for k in KERNELS if k_ms[0][k][1]},
+                    "exchange_ms_per_step": {k: round(max(x[k][0] for x in k_ms) / timed_steps, 3)
+                                             for k in EXCHANGES if k_ms[0][k][1]},
+                    "exchange_gb_per_step": {k: round(sum(x[k] for x in k_b) / timed_steps / 1e9, 3)
+                                             for k in EXCHANGES if k_ms[0][k][1]}}
+        if dense:
+            # SURVEY 8(d)'s bytes of the binned rounds over the device time of their kernels
+            # (bin_scatter + bin_apply + pull_heavy; max over parts): the honest dense-round fraction
+            d_b = sum(r["alg_bytes"] for r in dense)
+            d_ms = sum(r["dense_ms"] for r in dense)
+            ach = d_b / (d_ms / 1e3) / 1e9
+            traffic, tsrc = pmc_traffic(w.name, DENSE_KERNELS, run.n_local[0]) if run.parts == 1 else (None, None)
+            roofline.update({"kernel": "binned round: " + " + ".join(DENSE_KERNELS),
+                             "achieved": round(ach, 2), "frac": round(ach / roofline["peak"], 4),
+                             "alg_bytes_per_launch": round(d_b / len(dense)),
+                             "avg_launch_ms": round(d_ms / len(dense), 4), "launches": len(dense),
+                             "unit_of_work": "one binned round (SURVEY 8(d): 32 B per frontier peer + 20 B per "
+                                             "edge traversal)",
+                             "traffic": traffic, "traffic_source": tsrc,
+                             "dense_rounds": [r["round"] for r in dense]})
+        if ms > 0 and launches:
+            # the dominant kernel's own design bytes per launch over its HIP-event time
+            per_launch = sum(x[dom] for x in k_b) / run.parts / launches
+            ach_k = per_launch / (ms / launches / 1e3) / 1e9
+            roofline.update({"dominant_kernel": dom, "dominant_avg_launch_ms": round(ms / launches, 4),
+                             "dominant_launches": launches, "dominant_design_bytes_per_launch": round(per_launch),
+                             "dominant_design_frac": round(ach_k / HBM_PEAK_GBS, 4)})
+            if "kernel" not in roofline:  # no binned round: the dominant kernel is the roofline line
+                traffic, tsrc = pmc_traffic(w.name, (dom,), run.n_local[0]) if run.parts == 1 else (None, None)
+                roofline.update({"kernel": dom, "achieved": round(ach_k * run.n_gpus, 2),
+                                 "frac": round(ach_k / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": round(per_launch),
+                                 "avg_launch_ms": round(ms / launches, 4), "launches": launches,
+                                 "traffic": traffic, "traffic_source": tsrc})
 
     if rank == 0:
+        para = (f"vertex-partition x{run.n_gpus}" if run.parts == run.n_gpus else
+                f"vertex-partition x{run.parts} on one GPU (device-copy exchange)")
+        launcher = "torchrun (gossip_comm_init)" if dist is not None else \
+            "one process, gossip_group (ncclCommInitAll)" if run.n_gpus > 1 else "one process"
         line = {
             "metric": "gossip edge-deliveries/sec (GTEPS) + rounds-to-full-coverage",
             "value": round(value, 3),
             "unit": "GTEPS",
-            "n_gpus": world,
+            "n_gpus": run.n_gpus,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 3),
@@ -339,27 +464,30 @@ def main():
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic (Philox-generated power-law overlay and origins)",
-            "config": {"workload": w.name, "peers": w.n, "edges": n_edges,
+            "config": {"workload": w.name, "peers": w.n, "edges": run.n_edges,
                        "messages": w.n_msgs, "rounds": len(stats),
                        "rounds_to_full_coverage": rounds_to_full(stats),
                        "deliveries_per_step": deliveries,
                        "traversals_per_step": sum(s["traversals"] for s in stats),
-                       "parallelism": f"vertex-partition x{world}"},
+                       "parallelism": para, "launch": launcher},
             "traversal_gteps": round(args.steps * sum(s["traversals"] for s in stats) / dt / 1e9, 3),
         }
         if rounds_prof:
-            line["rounds"] = [{k: r[k] for k in ("round", "mode", "frontier_frac", "traversals", "kernel_ms")}
+            line["rounds"] = [{k: r[k] for k in ("round", "mode", "frontier_frac", "traversals", "kernel_ms")} |
+                              ({"exchange_ms": r["exchange_ms"]} if run.parts > 1 or dist is not None else {})
                               for r in rounds_prof]
         if roofline:
             line["roofline"] = roofline
-        if world == 1 and not args.no_cpu_baseline:
+        if run.n_gpus == 1 and run.parts == 1 and dist is None and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args, args.config)
         print(json.dumps(line), flush=True)
-    if partitioned:
-        reps = eng.comm_finalize(stats)
+    if isinstance(run, Ranked):
+        reps = run.eng.comm_finalize(stats)
         if rank == 0 and args.force_partitioned:
-            print(json.dumps({"partitioned_check": {"modes": eng.comm_modes(), "reports": int(len(reps))}}), flush=True)
-        eng.close()
+            print(json.dumps({"partitioned_check": {"modes": run.eng.comm_modes(), "reports": int(len(reps))}}),
+                  flush=True)
+    run.close()
+    if dist is not None:
         dist.destroy_process_group()
 
 

@@ -156,6 +156,8 @@ gossip_status gossip_schedule_kills(gossip_ctx* ctx, const uint32_t* kill_peer, 
                                     uint32_t n_kills);
 /* Philox-chosen distinct origins (host helper; same draw on every rank). */
 gossip_status gossip_pick_origins(uint64_t n_peers, uint32_t rng_seed, uint32_t count, uint32_t* out);
+/* HIP devices visible to this process (the GPUs a gossip_group can spread over). */
+gossip_status gossip_device_count(int32_t* count);
 
 /* ---- rounds (single partition) ------------------------------------------ */
 /* Clears all dynamic state (seen/new, alive, edge masks, miss counters,

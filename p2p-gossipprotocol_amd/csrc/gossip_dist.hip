@@ -180,9 +180,33 @@ int choose_mode(const DistDriver* d) {
 
 // ---- collectives (RCCL, or device copies when emulating on one GPU) ----
 
+// Times one exchange on every local rank's stream (gossip_kernel_time(name)
+// of each part while timing is on) and books its bytes received per rank.
+struct ExchTimer {
+    DistDriver* d;
+    const char* name;
+    std::vector<void*> tok;
+    TraceRange tr;
+    ExchTimer(DistDriver* d_, const char* n) : d(d_), name(n), tok(d_->ranks.size(), nullptr), tr("%s", n) {
+        for (size_t i = 0; i < d->ranks.size(); ++i) {
+            hipSetDevice(d->ranks[i].device);
+            ctx_timer_start(d->ranks[i].ctx, name, &tok[i]);
+        }
+    }
+    void bytes(size_t i, double b) { ctx_add_bytes(d->ranks[i].ctx, name, b); }
+    ~ExchTimer() {
+        for (size_t i = 0; i < d->ranks.size(); ++i) {
+            hipSetDevice(d->ranks[i].device);
+            ctx_timer_stop(d->ranks[i].ctx, name, tok[i]);
+        }
+    }
+};
+
 // every block's new words (published at gather + rank * chunk * X) to every rank
 gossip_status all_gather(DistDriver* d) {
     const uint64_t words = d->chunk * d->X;
+    ExchTimer t(d, "all_gather");
+    for (size_t i = 0; i < d->ranks.size(); ++i) t.bytes(i, 8.0 * words * (d->world - 1));
     if (d->emulate) {
         for (auto& q : d->ranks)
             for (auto& p : d->ranks)
@@ -204,6 +228,8 @@ gossip_status all_gather(DistDriver* d) {
 // received at recv + p * n_local(q) * X
 gossip_status all_to_all(DistDriver* d) {
     const uint64_t X = d->X;
+    ExchTimer t(d, "all_to_all");
+    for (size_t i = 0; i < d->ranks.size(); ++i) t.bytes(i, 8.0 * X * d->ranks[i].n_local * (d->world - 1));
     if (d->emulate) {
         for (auto& q : d->ranks)
             for (auto& p : d->ranks)
@@ -261,6 +287,12 @@ gossip_status exchange_records(DistDriver* d, std::vector<uint64_t>& total_in) {
         }
     }
     total_in.assign(d->ranks.size(), 0);
+    ExchTimer t(d, "records");
+    for (size_t i = 0; i < d->ranks.size(); ++i) {
+        uint64_t c = 0;
+        for (uint32_t q = 0; q < W; ++q) c += q == d->ranks[i].rank ? 0 : d->ranks[i].counts_in[q];
+        t.bytes(i, 8.0 * R * c);
+    }
     if (d->emulate) {
         for (size_t i = 0; i < d->ranks.size(); ++i) {
             DistRank& q = d->ranks[i];
@@ -333,6 +365,7 @@ gossip_status all_reduce_stats(DistDriver* d, uint64_t* g) {
 // One round on every local rank, lockstep phases.
 gossip_status dist_step(DistDriver* d, gossip_round_stats* out) {
     if (d->finished) return set_error(GOSSIP_ESTATE, "run finished: call gossip_reset");
+    TraceRange tr("gossip round %zu (%u parts)", d->modes.size(), (unsigned)d->ranks.size());
     const int want = choose_mode(d);
     int mode = -1;
     for (auto& r : d->ranks) {
@@ -563,7 +596,10 @@ gossip_status gossip_comm_init(gossip_ctx* ctx, const uint8_t* id, uint32_t worl
         if (nr != ncclSuccess) s = set_error(GOSSIP_ECOMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(nr));
     }
     if (s) {
-        gossip_set_stream(ctx, nullptr);  // back to the null stream before ours goes
+        // the ctx must not keep pointers into the buffers dist_free releases: it stays a
+        // single-partition ctx on the null stream, usable with gossip_step
+        ctx_clear_exchange(ctx);
+        gossip_set_stream(ctx, nullptr);
         dist_free(d);
         return s;
     }

@@ -222,6 +222,15 @@ void ctx_attach_dist(gossip_ctx* c, DistDriver* d, bool owned) {
     c->dist_owned = owned;
 }
 DistDriver* ctx_dist(gossip_ctx* c) { return c->dist; }
+bool ctx_timing(gossip_ctx* c) { return c->timing; }
+void ctx_clear_exchange(gossip_ctx* c) {
+    c->send = nullptr;
+    c->recv = nullptr;
+    c->gather = nullptr;
+    c->seg = nullptr;
+    c->world = 1;
+    c->part_begins.clear();
+}
 }  // namespace gossip
 
 namespace {
@@ -263,6 +272,32 @@ hipError_t timed(gossip_ctx* c, const char* name, F&& launch) {
     c->timers[name].pending.emplace_back(a, b);
     return e;
 }
+
+}  // namespace
+
+namespace gossip {
+// Device work the dist driver issues on the ctx's stream (collectives, device
+// copies) timed like a kernel: events recorded on the stream around it.
+void ctx_timer_start(gossip_ctx* c, const char* name, void** token) {
+    *token = nullptr;
+    if (!c->timing) return;
+    hipEvent_t a = take_event(c);
+    hipEventRecord(a, c->stream);
+    *token = a;
+    (void)name;
+}
+void ctx_timer_stop(gossip_ctx* c, const char* name, void* token) {
+    if (!c->timing || !token) return;
+    hipEvent_t b = take_event(c);
+    hipEventRecord(b, c->stream);
+    c->timers[name].pending.emplace_back(static_cast<hipEvent_t>(token), b);
+}
+void ctx_add_bytes(gossip_ctx* c, const char* name, double bytes) {
+    if (c->timing) c->kbytes[name] += bytes;
+}
+}  // namespace gossip
+
+namespace {
 
 void drain_timers(gossip_ctx* c) {
     for (auto& kv : c->timers) {
@@ -559,35 +594,42 @@ gossip_status tune_val(gossip_ctx* c) {
               c->bins.xcd_units, c->bins.bdst,     c->bins.val,     c->bins.bin_words, c->bins.dummy,   1u,
               0u,               c->bins.n_runs ? c->bins.n_runs - 1 : 0, c->bins.ap_run, c->bins.ap_grp,
               0u,               c->bins.cb_slot,   c->bins.split};
-    hipEvent_t e0, e1;
-    HIPCHK(hipEventCreate(&e0));
-    HIPCHK(hipEventCreate(&e1));
+    hipEvent_t e0 = nullptr, e1 = nullptr;
     float best = 0.f;
     int bi = 0;
-    for (int k = 0; k < kCand; ++k) {
+    // every exit frees the candidates not kept (only the first one, the layout's own, on an error)
+    auto finish = [&](hipError_t err) {
+        if (e0) hipEventDestroy(e0);
+        if (e1) hipEventDestroy(e1);
+        if (err != hipSuccess) bi = 0;
+        for (int k = 0; k < kCand; ++k)
+            if (cand[k] && k != bi) hipFree(cand[k]);
+        c->bins.val = cand[bi];
+        return err;
+    };
+    hipError_t err = hipEventCreate(&e0);
+    if (err == hipSuccess) err = hipEventCreate(&e1);
+    for (int k = 0; k < kCand && err == hipSuccess; ++k) {
         if (!cand[k]) continue;
         b.val = cand[k];
         float ms = 0.f;
-        for (int rep = 0; rep < 2; ++rep) {  // the second launch is timed
-            HIPCHK(hipEventRecord(e0, c->stream));
-            HIPCHK(launch_bin_scatter(a, b, pack_w(c), c->stream));
-            HIPCHK(hipEventRecord(e1, c->stream));
-            HIPCHK(hipEventSynchronize(e1));
-            HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+        for (int rep = 0; rep < 2 && err == hipSuccess; ++rep) {  // the second launch is timed
+            err = hipEventRecord(e0, c->stream);
+            if (err == hipSuccess) err = launch_bin_scatter(a, b, pack_w(c), c->stream);
+            if (err == hipSuccess) err = hipEventRecord(e1, c->stream);
+            if (err == hipSuccess) err = hipEventSynchronize(e1);
+            if (err == hipSuccess) err = hipEventElapsedTime(&ms, e0, e1);
         }
+        if (err != hipSuccess) break;
         if (env && std::atoi(env) == 2) fprintf(stderr, "tune_val: candidate %d %.3f ms\n", k, ms);
         if (k == 0 || ms < best) {
             best = ms;
             bi = k;
         }
     }
-    hipEventDestroy(e0);
-    hipEventDestroy(e1);
-    for (int k = 0; k < kCand; ++k)
-        if (cand[k] && k != bi) hipFree(cand[k]);
-    c->bins.val = cand[bi];
-    HIPCHK(hipMemsetAsync(c->st, 0, kStatLines * sizeof(DevStats), c->stream));  // the trials' stats
     c->bins_first = true;  // the trials left words in every slot
+    HIPCHK(finish(err));
+    HIPCHK(hipMemsetAsync(c->st, 0, kStatLines * sizeof(DevStats), c->stream));  // the trials' stats
     return GOSSIP_OK;
 }
 
@@ -910,6 +952,7 @@ gossip_status round_compute(gossip_ctx* c) {
     RoundArgs a = c->cur;
     const uint32_t pw = pack_w(c);
     c->in_round = false;
+    TraceRange tr("%s", c->last_bin ? "binned" : c->last_pull ? "pull" : c->cur_sparse ? "push (sparse exchange)" : "push");
     if (c->last_pull && a.dead_mode && !a.dgone)  // else the per-source counters give the source side
         HIPCHK(timed(c, "src_count", [&] { return launch_src_count(a, pw, c->stream); }));
     if (c->last_bin) {
@@ -1382,6 +1425,16 @@ gossip_status gossip_schedule_kills(gossip_ctx* c, const uint32_t* peer, const u
     return GOSSIP_OK;
 }
 
+gossip_status gossip_device_count(int32_t* count) {
+    if (!count) return fail(GOSSIP_EINVAL, "null argument");
+    int n = 0;
+    const hipError_t e = hipGetDeviceCount(&n);
+    if (e == hipErrorNoDevice) n = 0;
+    else if (e != hipSuccess) return fail(GOSSIP_EHIP, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+    *count = n;
+    return GOSSIP_OK;
+}
+
 gossip_status gossip_pick_origins(uint64_t n, uint32_t seed, uint32_t count, uint32_t* out) {
     if (!out || n == 0) return fail(GOSSIP_EINVAL, "bad argument");
     for (uint32_t k = 0; k < count; ++k) {
@@ -1479,6 +1532,7 @@ gossip_status gossip_step(gossip_ctx* c, gossip_round_stats* out) {
     if (set_dev(c)) return GOSSIP_EHIP;
     if (c->dist) return gossip::dist_step_ctx(c, out);  // the library's own collectives (gossip_comm_init)
     if (c->world > 1) return fail(GOSSIP_ESTATE, "partitioned ctx: use gossip_comm_init or gossip_round_*");
+    TraceRange tr("gossip round %u", c->round);
     gossip_status s = round_begin(c, false, GOSSIP_MODE_AUTO, nullptr);
     if (!s) s = round_compute(c);
     if (s) return s;

@@ -3,11 +3,28 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
+#include <cstdio>
 #include <string>
 
 #include "../../include/gossip/gossip.h"
 
 namespace gossip {
+
+// roctx range around a round or one of its phases (rocprofv3 --marker-trace shows them per round;
+// without a profiler attached a push/pop is a call into an empty dispatch table)
+struct TraceRange {
+    template <class... A>
+    explicit TraceRange(const char* fmt, A... args) {
+        char buf[64];
+        std::snprintf(buf, sizeof(buf), fmt, args...);
+        roctxRangePushA(buf);
+    }
+    ~TraceRange() { roctxRangePop(); }
+    TraceRange(const TraceRange&) = delete;
+    TraceRange& operator=(const TraceRange&) = delete;
+};
 
 constexpr uint32_t kMaskedEdge = 0x80000000u;  // col[e] bit 31: edge dropped by liveness (peer.cpp:388)
 constexpr uint32_t kHeavyDegree = 256;         // default: rows longer than this go to the edge-chunked kernels
@@ -276,6 +293,13 @@ const gossip_config& ctx_config(gossip_ctx* c);
 void ctx_range(gossip_ctx* c, uint64_t* begin, uint64_t* end);
 void ctx_attach_dist(gossip_ctx* c, DistDriver* d, bool owned);
 DistDriver* ctx_dist(gossip_ctx* c);
+bool ctx_timing(gossip_ctx* c);
+// forget the exchange buffers registered by gossip_set_exchange / _gather / _sparse (they are being freed)
+void ctx_clear_exchange(gossip_ctx* c);
+// time device work issued on the ctx's stream under `name` (gossip_kernel_time) while timing is on
+void ctx_timer_start(gossip_ctx* c, const char* name, void** token);
+void ctx_timer_stop(gossip_ctx* c, const char* name, void* token);
+void ctx_add_bytes(gossip_ctx* c, const char* name, double bytes);  // gossip_kernel_bytes
 gossip_status dist_step_ctx(gossip_ctx* c, gossip_round_stats* out);
 void dist_reset(DistDriver* d);
 void dist_free(DistDriver* d);

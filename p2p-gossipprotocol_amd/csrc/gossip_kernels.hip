@@ -1712,7 +1712,12 @@ __global__ __launch_bounds__(kB) void k_bin_apply_runs(RoundArgs a, BinArgs b) {
     __shared__ unsigned long long acc_s[kWords];
     Acc acc;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const Bin bn = b.bins[blockIdx.x];
+    // XCD-contiguous bins: the blocks that share an XCD (blockIdx % 8) take consecutive bins, so the
+    // ~32 bins in flight on an XCD read neighbouring runs of every chunk and share their partial
+    // sectors in that XCD's L2
+    const uint32_t bi = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    if (bi >= b.n_bins) return;  // (whole workgroup, before any barrier)
+    const Bin bn = b.bins[bi];
     const uint32_t nv = bn.v1 - bn.v0;
     const uint64_t v0 = bn.v0;
     bool needy = false;
@@ -2842,12 +2847,13 @@ hipError_t launch_bin_scatter(const RoundArgs& a, const BinArgs& b, uint32_t W_,
 hipError_t launch_bin_apply(const RoundArgs& a, const BinArgs& b, uint32_t W_, hipStream_t s) {
     if (!b.n_bins) return hipSuccess;
     if (b.stream) {
+        const unsigned sgrid = (unsigned)((b.n_bins + 7) / 8 * 8);  // whole groups of 8 (XCD-contiguous bins)
         if (b.bin_words > kBinWords / 2) {
             GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_apply_runs<W, kBinWords, 1024>),
-                                                           dim3((unsigned)b.n_bins), dim3(1024), 0, s, a, b));
+                                                           dim3(sgrid), dim3(1024), 0, s, a, b));
         } else {
             GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_apply_runs<W, kBinWords / 2, kBlock>),
-                                                           dim3((unsigned)b.n_bins), dim3(kBlock), 0, s, a, b));
+                                                           dim3(sgrid), dim3(kBlock), 0, s, a, b));
         }
         return hipGetLastError();
     }

@@ -114,6 +114,7 @@ def lib() -> C.CDLL:
         "gossip_inject": (i32, [P, pu32, pu32, u32]),
         "gossip_schedule_kills": (i32, [P, pu32, pu32, u32]),
         "gossip_pick_origins": (i32, [u64, u32, u32, pu32]),
+        "gossip_device_count": (i32, [C.POINTER(C.c_int32)]),
         "gossip_reset": (i32, [P]),
         "gossip_step": (i32, [P, C.POINTER(RoundStats)]),
         "gossip_run": (i32, [P, C.POINTER(RoundStats), u32, pu32]),

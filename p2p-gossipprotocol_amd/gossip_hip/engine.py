@@ -17,7 +17,10 @@ from ._abi import DeadReport, GossipConfig, RoundStats, check
 
 _GRAPHS = {"powerlaw": _abi.GRAPH_POWERLAW, "ref_bootstrap": _abi.GRAPH_REF_BOOTSTRAP}
 KERNELS = ("push_light", "push_heavy", "push_extra", "src_count", "frontier_bits", "pull_light", "pull_heavy", "bin_scatter",
-           "bin_apply", "liveness", "rebootstrap", "rejoin", "churn", "kills", "inject", "apply_remote", "commit", "count_nx")
+           "bin_apply", "liveness", "rebootstrap", "rejoin", "churn", "kills", "inject", "apply_remote", "commit", "count_nx",
+           "compact_send")
+# exchange steps of partitioned rounds, timed on each part's stream (gossip_dist.hip; bytes = received per part)
+EXCHANGES = ("all_gather", "all_to_all", "records")
 
 
 def _u32(a) -> np.ndarray:
@@ -40,6 +43,13 @@ def partition(n_peers: int, world: int) -> list[int]:
     out = np.zeros(world + 1, dtype=np.uint64)
     check(_abi.lib().gossip_partition(n_peers, world, _ptr(out, C.c_uint64)), "gossip_partition")
     return [int(x) for x in out]
+
+
+def device_count() -> int:
+    """HIP devices visible to this process (gossip_device_count)."""
+    n = C.c_int32()
+    check(_abi.lib().gossip_device_count(C.byref(n)), "gossip_device_count")
+    return n.value
 
 
 def pick_origins(n_peers: int, rng_seed: int, count: int) -> np.ndarray:
@@ -387,3 +397,50 @@ class Group:
         ctx = C.c_void_p()
         check(self._L.gossip_group_part(self._g, p, C.byref(ctx)), "gossip_group_part")
         return ctx
+
+    # per-part measurement (each part's ctx times the kernels and exchanges issued on its stream)
+    def enable_timing(self, on: bool = True) -> None:
+        for p in range(self.n_parts):
+            check(self._L.gossip_enable_timing(self.part_ctx(p), 1 if on else 0), "gossip_enable_timing")
+
+    def kernel_time(self, p: int, name: str) -> tuple[float, int]:
+        ms, n = C.c_double(), C.c_uint64()
+        check(self._L.gossip_kernel_time(self.part_ctx(p), name.encode(), C.byref(ms), C.byref(n)),
+              "gossip_kernel_time")
+        return ms.value, n.value
+
+    def kernel_bytes(self, p: int, name: str) -> float:
+        b = C.c_double()
+        check(self._L.gossip_kernel_bytes(self.part_ctx(p), name.encode(), C.byref(b)), "gossip_kernel_bytes")
+        return b.value
+
+    def coverage(self) -> np.ndarray:
+        """Per-message coverage over all peers (the parts' counts summed)."""
+        tot = np.zeros(self.n_msgs, dtype=np.uint64)
+        for p in range(self.n_parts):
+            out = np.zeros(self.n_msgs, dtype=np.uint64)
+            check(self._L.gossip_read_coverage(self.part_ctx(p), _ptr(out, C.c_uint64)), "gossip_read_coverage")
+            tot += out
+        return tot
+
+    def alive(self) -> np.ndarray:
+        """Alive flags of all peers (every part keeps the same global bitset: churn is drawn redundantly)."""
+        out = np.zeros(self.n_peers, dtype=np.uint8)
+        check(self._L.gossip_read_alive(self.part_ctx(0), _ptr(out, C.c_uint8)), "gossip_read_alive")
+        return out
+
+    def registered(self) -> np.ndarray:
+        """Seed-registry membership: a peer is gone once any part's reporter has reported it
+        (each part clears the registry bits of its own reports)."""
+        reg = None
+        for p in range(self.n_parts):
+            out = np.zeros(self.n_peers, dtype=np.uint8)
+            check(self._L.gossip_read_registered(self.part_ctx(p), _ptr(out, C.c_uint8)), "gossip_read_registered")
+            reg = out if reg is None else reg & out
+        return reg
+
+    def shape(self, p: int) -> dict:
+        w, x, nl, ne = C.c_uint32(), C.c_uint32(), C.c_uint64(), C.c_uint64()
+        check(self._L.gossip_get_shape(self.part_ctx(p), C.byref(w), C.byref(x), C.byref(nl), C.byref(ne)),
+              "get_shape")
+        return {"words": w.value, "exchange_words": x.value, "n_local": nl.value, "n_edges": ne.value}

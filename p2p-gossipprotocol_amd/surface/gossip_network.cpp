@@ -119,13 +119,16 @@ bool GossipNetwork::start() {
     const uint32_t parts = trace_ ? 1u : std::max<uint32_t>(1, opt_.n_gpus);
     gossip_status st = GOSSIP_OK;
     if (parts > 1) {
+        // parts on GPUs device, device+1, ...; with fewer GPUs visible than that, every part on
+        // `device`, exchanging by device copies (the single-GPU rehearsal of the partitioned path).
+        // Any other failure (RCCL, memory) is reported, not papered over.
+        int32_t ndev = 0;
+        st = gossip_device_count(&ndev);
+        const int32_t base = std::max(opt_.device, 0);
+        const bool distinct = (int64_t)ndev >= (int64_t)base + parts;
         std::vector<int32_t> devs(parts);
-        for (uint32_t p = 0; p < parts; ++p) devs[p] = (int32_t)p;
-        st = gossip_group_create(&cfg, parts, devs.data(), &group_);
-        if (st != GOSSIP_OK) {  // fewer GPUs than parts: all parts on one device, exchanged by device copies
-            std::fill(devs.begin(), devs.end(), (int32_t)std::max(opt_.device, 0));
-            st = gossip_group_create(&cfg, parts, devs.data(), &group_);
-        }
+        for (uint32_t p = 0; p < parts; ++p) devs[p] = distinct ? base + (int32_t)p : base;
+        if (st == GOSSIP_OK) st = gossip_group_create(&cfg, parts, devs.data(), &group_);
         if (st == GOSSIP_OK) st = gossip_group_build_graph(group_);
     } else {
         st = gossip_create(&cfg, &ctx_);
@@ -241,7 +244,12 @@ int GossipNetwork::step() {
     }
     rounds_.push_back(st);
     if (trace_) captureRound(st.round);
-    if (rc == 1) finished_ = true;
+    if (rc == 1) {
+        finished_ = true;
+        // a partitioned run's seed removals come from the merged reports once it ends
+        // (single-partition stats carry them every round)
+        if (group_) seedRemovalsFromReports();
+    }
     return rc;
 }
 
@@ -250,7 +258,6 @@ bool GossipNetwork::run() {
     while (!finished_ && !stop_) {
         if (step() < 0) return false;
     }
-    if (finished_ && group_) seedRemovalsFromReports();
     if (finished_ && !opt_.log_dir.empty() && trace_) writeLogs(opt_.log_dir);
     return true;
 }
