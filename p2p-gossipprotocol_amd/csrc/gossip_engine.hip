@@ -177,6 +177,7 @@ struct gossip_ctx {
                                   // -0.75 ms, round 8's fold +0.5 to +0.7 ms, so off by default)
     bool pull_diag = false;       // GOSSIP_PULL_DIAG: count the gathers of an early-exit row scan (measurement)
     bool cur_defer = false;       // this round defers: advance() folds nx into seen
+    bool overlap_probe = false;  // GOSSIP_OVERLAP_PROBE: measurement only (overlap_probe)
     bool full_liveness = false;  // GOSSIP_FULL_LIVENESS: ping every edge each ping round (A/B against closed form)
     uint64_t* seg = nullptr;     // sparse push: per-destination record segments (world x chunk records)
     unsigned long long* d_counts = nullptr;  // records per destination rank
@@ -574,7 +575,10 @@ gossip_status upload_csr(gossip_ctx* c, const uint64_t* rp, const uint32_t* col,
 // are garbage: the first binned round rewrites every slot.
 gossip_status tune_val(gossip_ctx* c) {
     const char* env = std::getenv("GOSSIP_VAL_TUNE");
-    if ((env && !std::atoi(env)) || c->bin_stream || c->bins.n_slots < (1ull << 26)) return GOSSIP_OK;
+    // single partition only: a vertex block's scatter stages global source chunks from the all-gathered
+    // words, which do not exist at bootstrap (the trial launch read past the block's own words)
+    if ((env && !std::atoi(env)) || c->bin_stream || c->bins.n_slots < (1ull << 26) || c->n_local != c->n)
+        return GOSSIP_OK;
     const uint64_t bytes = (c->bins.n_slots + 64) * c->Wp * sizeof(uint64_t);
     constexpr int kCand = 4;
     uint64_t* cand[kCand] = {c->bins.val};
@@ -945,6 +949,59 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
     return GOSSIP_OK;
 }
 
+// Measurement only (GOSSIP_OVERLAP_PROBE=1): can one binned round's slot stores share HBM with the slot
+// reads of another?  On copies of seen / nx / the stats, times the scatter on all CUs, the apply, the
+// scatter on half the CUs, and that half scatter concurrently with the apply on a second stream (the
+// apply then reads slots being rewritten: timing only).  Prints the four times (ms) to stderr.
+gossip_status overlap_probe(gossip_ctx* c, RoundArgs a, const BinArgs& b, uint32_t pw) {
+    static hipStream_t s2 = nullptr;
+    static uint64_t *seen2 = nullptr, *nx2 = nullptr;
+    static DevStats* st2 = nullptr;
+    static hipEvent_t ev[9];
+    const size_t words = c->n_local * c->Wp * sizeof(uint64_t);
+    if (!s2) {
+        HIPCHK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+        HIPCHK(hipMalloc((void**)&seen2, words));
+        HIPCHK(hipMalloc((void**)&nx2, words));
+        HIPCHK(hipMalloc((void**)&st2, kStatLines * sizeof(DevStats)));
+        for (auto& e : ev) HIPCHK(hipEventCreate(&e));
+    }
+    a.st = st2;
+    a.cov = nullptr;
+    a.seen = seen2;
+    a.nx = nx2;
+    hipStream_t s = c->stream;
+    HIPCHK(hipEventRecord(ev[0], s));
+    HIPCHK(launch_bin_scatter(a, b, pw, s));
+    HIPCHK(hipEventRecord(ev[1], s));
+    HIPCHK(hipMemcpyAsync(seen2, c->seen, words, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipEventRecord(ev[2], s));
+    HIPCHK(launch_bin_apply(a, b, pw, s));
+    HIPCHK(hipEventRecord(ev[3], s));
+    g_scatter_grid_probe = 128;
+    HIPCHK(hipEventRecord(ev[4], s));
+    HIPCHK(launch_bin_scatter(a, b, pw, s));
+    HIPCHK(hipEventRecord(ev[5], s));
+    HIPCHK(hipMemcpyAsync(seen2, c->seen, words, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipEventRecord(ev[6], s));
+    HIPCHK(hipStreamWaitEvent(s2, ev[6], 0));
+    HIPCHK(launch_bin_scatter(a, b, pw, s));
+    HIPCHK(launch_bin_apply(a, b, pw, s2));
+    HIPCHK(hipEventRecord(ev[8], s2));
+    HIPCHK(hipStreamWaitEvent(s, ev[8], 0));
+    HIPCHK(hipEventRecord(ev[7], s));
+    g_scatter_grid_probe = 0;
+    HIPCHK(hipEventSynchronize(ev[7]));
+    float t[4];
+    HIPCHK(hipEventElapsedTime(&t[0], ev[0], ev[1]));
+    HIPCHK(hipEventElapsedTime(&t[1], ev[2], ev[3]));
+    HIPCHK(hipEventElapsedTime(&t[2], ev[4], ev[5]));
+    HIPCHK(hipEventElapsedTime(&t[3], ev[6], ev[7]));
+    fprintf(stderr, "overlap_probe round %u: scatter %.3f apply %.3f | half scatter %.3f | half scatter || apply %.3f ms\n",
+            c->round, t[0], t[1], t[2], t[3]);
+    return GOSSIP_OK;
+}
+
 // Round phase 2: the push or pull kernels (after the caller's all-gather in a
 // partitioned pull round).
 gossip_status round_compute(gossip_ctx* c) {
@@ -961,6 +1018,10 @@ gossip_status round_compute(gossip_ctx* c) {
                   c->bins.xcd_units, c->bins.bdst,     c->bins.val,     c->bins.bin_words, c->bins.dummy,   c->bin_noskip || c->bins_first,
                   c->scatter_probe,  c->bins.n_runs ? c->bins.n_runs - 1 : 0, c->bins.ap_run, c->bins.ap_grp,
                   c->bin_stream ? 1u : 0u, c->bins.cb_slot, c->bins.split};
+        if (c->overlap_probe) {
+            gossip_status ps = overlap_probe(c, a, b, pw);
+            if (ps) return ps;
+        }
         HIPCHK(timed(c, "bin_scatter", [&] { return launch_bin_scatter(a, b, pw, c->stream); }));
         HIPCHK(timed(c, "bin_apply", [&] { return launch_bin_apply(a, b, pw, c->stream); }));
         c->bins_first = false;
@@ -1175,6 +1236,7 @@ gossip_status gossip_create(const gossip_config* cfg, gossip_ctx** out) {
     if (const char* u = std::getenv("GOSSIP_BIN_STREAM")) c->bin_stream = std::atoi(u) != 0;
     if (const char* u = std::getenv("GOSSIP_PULL_DIAG")) c->pull_diag = std::atoi(u) != 0;
     if (const char* u = std::getenv("GOSSIP_FULL_LIVENESS"); u && std::atoi(u)) c->full_liveness = true;
+    if (const char* u = std::getenv("GOSSIP_OVERLAP_PROBE"); u && std::atoi(u)) c->overlap_probe = true;
     if (const char* b = std::getenv("GOSSIP_BIN_PERMILLE"); b && !cfg->bin_permille) c->cfg.bin_permille = (uint32_t)std::atoi(b);
     c->n = cfg->n_peers;
     c->begin = b;

@@ -232,6 +232,7 @@ hipError_t launch_compact_send(const RoundArgs& a, uint32_t W, uint64_t chunk, u
                                uint64_t* seg, hipStream_t s);
 hipError_t launch_apply_records(const RoundArgs& a, uint32_t W, const uint64_t* rec, uint64_t n_rec, hipStream_t s);
 hipError_t launch_bin_scatter(const RoundArgs& a, const BinArgs& b, uint32_t W, hipStream_t s);
+extern int g_scatter_grid_probe;  // measurement only
 hipError_t launch_bin_apply(const RoundArgs& a, const BinArgs& b, uint32_t W, hipStream_t s);
 hipError_t launch_liveness_extra(const RoundArgs& a, hipStream_t s);
 hipError_t launch_push_extra(const RoundArgs& a, uint32_t W, bool check_alive, bool remote, hipStream_t s);

@@ -2804,8 +2804,11 @@ static int scatter_pc() {
     return pc;
 }
 
+int g_scatter_grid_probe = 0;  // measurement only (overlap probe): scatter workgroups, 0 = kScatterGrid
+
 hipError_t launch_bin_scatter(const RoundArgs& a, const BinArgs& b, uint32_t W_, hipStream_t s) {
     const uint32_t wd = wd_of(W_);
+    const int kScatterGrid = g_scatter_grid_probe ? g_scatter_grid_probe : gossip::kScatterGrid;
     if (b.stream) {
         GOSSIP_DISPATCH_W(wp_of(W_), {
             if (a.cov) hipLaunchKernelGGL((k_bin_stream<W, true>), dim3(kScatterGrid), dim3(kScatterBlock), 0, s, a, b, wd);
