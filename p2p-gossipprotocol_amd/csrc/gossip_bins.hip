@@ -83,6 +83,11 @@ __global__ void k_tile_slots(const uint64_t* rp, uint64_t n, uint32_t heavy, uin
     }
 }
 
+__global__ void k_degree(const uint64_t* rp, uint64_t n, uint32_t* deg) {
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x)
+        deg[v] = (uint32_t)(rp[v + 1] - rp[v]);
+}
+
 __global__ void k_edge_rows(const uint64_t* rp, uint64_t n, uint32_t* row) {
     for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x)
         for (uint64_t e = rp[v]; e < rp[v + 1]; ++e) row[e] = (uint32_t)v;
@@ -226,6 +231,7 @@ void free_bins(BinState* b) {
     hipFree(b->val);
     hipFree(b->dummy);
     hipFree(b->cb_slot);
+    hipFree(b->deg);
     *b = BinState{};
 }
 
@@ -371,6 +377,9 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
     BCHECK(hipMemsetAsync(st.bdst, 0, (slots + 64) * sizeof(uint16_t), s));
     BCHECK(hipMemsetAsync(st.val, 0, (slots + 64) * Wp * sizeof(uint64_t), s));
     BCHECK(hipMalloc((void**)&st.dummy, (uint64_t)kScatterGrid * kScatterBlock * Wp * sizeof(uint64_t)));
+    BCHECK(hipMalloc((void**)&st.deg, (n_local + 1) * sizeof(uint32_t)));
+    hipLaunchKernelGGL(k_degree, dim3(gridn(n_local)), dim3(256), 0, s, rp, n_local, st.deg);
+    BCHECK(hipGetLastError());
     hipLaunchKernelGGL(k_bin_assign, dim3(gridn(m)), dim3(256), 0, s, keys64_out, vals_out, m, st.bins,
                        (uint32_t)st.n_bins, row, st.bdst);
     BCHECK(hipGetLastError());

@@ -203,6 +203,15 @@ struct gossip_ctx {
     std::map<std::string, double> kbytes;
     std::vector<hipEvent_t> event_pool;
 
+    // small overlays: a whole run in one launch (gossip_tiny.hip)
+    bool tiny_off = false;                 // GOSSIP_TINY=0: round by round (A/B, tests)
+    uint32_t* tiny_erow = nullptr;         // per edge: its row
+    gossip_round_stats* tiny_out = nullptr;  // device, tiny_cap rounds
+    uint32_t tiny_cap = 0;
+    uint32_t* tiny_result = nullptr;       // device [rounds, buffers swapped]
+    uint32_t* d_inj_round = nullptr;       // the sorted schedule rounds on the device
+    uint32_t* d_kill_round = nullptr;
+
     // library-driven multi-GPU rounds (gossip_dist.hip): the driver that issues
     // this ctx's collectives; owned here for gossip_comm_init, by the group otherwise
     gossip::DistDriver* dist = nullptr;
@@ -365,6 +374,8 @@ void free_state(gossip_ctx* c) {
 }
 
 void free_graph(gossip_ctx* c) {
+    hipFree(c->tiny_erow);
+    c->tiny_erow = nullptr;
     free_bins(&c->bins);
     c->bins_ready = false;
     hipFree(c->rp);
@@ -597,7 +608,7 @@ gossip_status tune_val(gossip_ctx* c) {
               c->bins.n_binned, c->bins.chunk_begin, c->bins.n_chunks, c->bins.chunk,    c->bins.units,
               c->bins.xcd_units, c->bins.bdst,     c->bins.val,     c->bins.bin_words, c->bins.dummy,   1u,
               0u,               c->bins.n_runs ? c->bins.n_runs - 1 : 0, c->bins.ap_run, c->bins.ap_grp,
-              0u,               c->bins.cb_slot,   c->bins.split};
+              0u,               c->bins.cb_slot,   c->bins.split, c->bins.deg, 1u};
     hipEvent_t e0 = nullptr, e1 = nullptr;
     float best = 0.f;
     int bi = 0;
@@ -866,7 +877,7 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
     // (k_commit_nx).  A per-rank choice: results do not depend on it.
     // Auto: only where the fold can ride on the next binned round's apply (one partition, the
     // slot layout, no churn); config 4 round 3: push 5.6 -> 4.1 ms, the 1.3 ms fold pass removed.
-    const bool fusable = c->world <= 1 && !remote && c->bins_ready && !c->bin_stream && !c->cfg.churn_threshold &&
+    const bool fusable = c->world <= 1 && !remote && c->bins_ready && !c->cfg.churn_threshold &&
                          !c->cfg.rejoin_threshold && requested == GOSSIP_MODE_AUTO;
     const uint32_t dpm = c->defer_pm == kDeferAuto ? (fusable ? 10u : 0u) : c->defer_pm;
     c->cur_defer = !pull && dpm && (c->frontier_est + cnt) * 1000 >= c->n_local * (uint64_t)dpm;
@@ -874,7 +885,7 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
     a.defer = c->cur_defer ? (c->defer_nr && !remote && c->world <= 1 && !a.tnx ? 2u : 1u) : 0u;
     const bool rows_pull = pull && !bin && (c->pull_unroll & kPullRows) && !c->pull_diag;  // k_pull_rows
     if (c->fold_pending) {  // the previous round deferred: its receipts are this round's nw
-        if (((bin && !c->bin_stream) || rows_pull) && c->world <= 1 && !remote) {
+        if ((bin || rows_pull) && c->world <= 1 && !remote) {
             a.fold = 1;  // k_bin_apply / k_pull_rows's sweep folds them (before k_pull_heavy reads seen)
             c->fold_pending = false;
         } else if (gossip_status fs = settle_fold(c)) {
@@ -1002,6 +1013,113 @@ gossip_status overlap_probe(gossip_ctx* c, RoundArgs a, const BinArgs& b, uint32
     return GOSSIP_OK;
 }
 
+// Small overlays run whole in one launch (gossip_tiny.hip) unless they use a feature only the round-by-round
+// engine has (re-bootstrap, join churn, coverage history) or are partitioned.
+bool tiny_ok(const gossip_ctx* c) {
+    return !c->tiny_off && c->graph_ready && c->n_local == c->n && c->world <= 1 && !c->dist && !c->gather &&
+           c->n <= kTinyPeers && c->n_edges <= kTinyEdges && !c->cfg.extra_cap && !c->cfg.rejoin_threshold &&
+           !c->cov_hist && !c->in_round;
+}
+
+TinyArgs tiny_args(gossip_ctx* c) {
+    TinyArgs t{};
+    t.erow = c->tiny_erow;
+    t.col = c->col;
+    t.alive = c->alive;
+    t.registered = c->registered;
+    t.seen = c->seen;
+    t.nw = c->nw;
+    t.nx = c->nx;
+    t.miss = c->miss;
+    t.reports = c->reports;
+    t.n_reports = c->n_reports;
+    t.report_cap = c->report_cap;
+    t.inj_live = c->inj_live;
+    t.inj_origin = c->d_inj_origin;
+    t.inj_msg = c->d_inj_msg;
+    t.inj_round = c->d_inj_round;
+    t.n_inj = c->has_schedule ? (uint32_t)c->inj_round_sorted.size() : 0u;
+    t.kill_peer = c->d_kill_peer;
+    t.kill_round = c->d_kill_round;
+    t.n_kill = (uint32_t)c->kill_round_sorted.size();
+    t.n = (uint32_t)c->n;
+    t.n_edges = (uint32_t)c->n_edges;
+    t.wd = c->W;
+    t.seed = c->cfg.rng_seed;
+    t.churn = c->cfg.churn_threshold;
+    t.ping_every = c->cfg.ping_every;
+    t.max_missed = c->cfg.max_missed;
+    t.start = c->round;
+    t.min_rounds = c->cfg.min_rounds;
+    t.max_rounds = c->cfg.max_rounds;
+    t.last_inject_round = c->last_inject_round;
+    t.has_schedule = c->has_schedule ? 1u : 0u;
+    t.out = c->tiny_out;
+    t.out_cap = c->tiny_cap;
+    t.result = c->tiny_result;
+    return t;
+}
+
+// A whole run (from round 0) in one launch; the host reads every round's stats once.
+gossip_status tiny_run(gossip_ctx* c, gossip_round_stats* per_round, uint32_t cap, uint32_t* rounds) {
+    if (!c->tiny_erow) {
+        HIPCHK(hipMalloc((void**)&c->tiny_erow, (c->n_edges + 1) * sizeof(uint32_t)));
+        HIPCHK(launch_tiny_erow(c->rp, (uint32_t)c->n, c->tiny_erow, c->stream));
+    }
+    // the kernel writes the stats straight into pinned host memory: after it, one stream sync and no copies
+    if (!c->tiny_out || c->tiny_cap < c->cfg.max_rounds) {
+        if (c->tiny_out) hipHostFree(c->tiny_out);
+        c->tiny_out = nullptr;
+        HIPCHK(hipHostMalloc((void**)&c->tiny_out, (uint64_t)c->cfg.max_rounds * sizeof(gossip_round_stats)));
+        c->tiny_cap = c->cfg.max_rounds;
+    }
+    if (!c->tiny_result) HIPCHK(hipHostMalloc((void**)&c->tiny_result, 4 * sizeof(uint32_t)));
+    if (!c->d_kill_round) {  // no kills scheduled: an empty list
+        const uint32_t none = 0xFFFFFFFFu;
+        HIPCHK(hipMalloc((void**)&c->d_kill_round, sizeof(uint32_t)));
+        HIPCHK(hipMemcpy(c->d_kill_round, &none, sizeof(uint32_t), hipMemcpyHostToDevice));
+    }
+    const TinyArgs t = tiny_args(c);
+    HIPCHK(timed(c, "tiny", [&] { return launch_tiny_run(t, c->Wp, c->stream); }));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const uint32_t k = std::min(c->tiny_result[0], c->tiny_cap);
+    const std::vector<gossip_round_stats> st(c->tiny_out, c->tiny_out + k);
+    if (c->tiny_result[1]) std::swap(c->nw, c->nx);
+    uint64_t died = 0, reps = 0;
+    for (const auto& x : st) {
+        died += x.died;
+        reps += x.reports;
+        if (c->timing) c->kbytes["tiny"] += 32.0 * (double)x.frontier + 20.0 * (double)x.traversals;
+    }
+    c->round += k;
+    c->finished = true;
+    c->any_dead |= died > 0;
+    c->any_masked |= reps > 0;
+    if (k) {
+        c->last_fresh = st.back().new_receipts;
+        c->cum_digest = st.back().digest;
+        c->cum_covered = st.back().covered;
+    }
+    c->bufs_zero = c->last_fresh == 0;  // the last round consumed every new word and produced none
+    c->nx_dirty = !c->bufs_zero;
+    c->last_pull = c->last_bin = false;
+    c->last_st_round = ~0u;
+    c->flight_round = ~0u;
+    if (per_round) std::copy(st.begin(), st.begin() + std::min<size_t>(cap, st.size()), per_round);
+    if (rounds) *rounds = k;
+    return GOSSIP_OK;
+}
+
+// Who books the source side of a binned round: the scatter's staging (slot layout) or the apply
+// (streamed layout; GOSSIP_SRC_STATS=0/1 overrides, A/B)
+uint32_t src_stats(const gossip_ctx* c) {
+    static const int env = [] {
+        const char* e = std::getenv("GOSSIP_SRC_STATS");
+        return e ? std::atoi(e) : -1;
+    }();
+    return env >= 0 ? (uint32_t)(env != 0) : (c->bin_stream ? 0u : 1u);
+}
+
 // Round phase 2: the push or pull kernels (after the caller's all-gather in a
 // partitioned pull round).
 gossip_status round_compute(gossip_ctx* c) {
@@ -1017,7 +1135,7 @@ gossip_status round_compute(gossip_ctx* c) {
                   c->bins.n_binned, c->bins.chunk_begin, c->bins.n_chunks, c->bins.chunk,    c->bins.units,
                   c->bins.xcd_units, c->bins.bdst,     c->bins.val,     c->bins.bin_words, c->bins.dummy,   c->bin_noskip || c->bins_first,
                   c->scatter_probe,  c->bins.n_runs ? c->bins.n_runs - 1 : 0, c->bins.ap_run, c->bins.ap_grp,
-                  c->bin_stream ? 1u : 0u, c->bins.cb_slot, c->bins.split};
+                  c->bin_stream ? 1u : 0u, c->bins.cb_slot, c->bins.split, c->bins.deg, src_stats(c)};
         if (c->overlap_probe) {
             gossip_status ps = overlap_probe(c, a, b, pw);
             if (ps) return ps;
@@ -1083,9 +1201,10 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
             // the apply's when streamed
             const double runs = 4.0 * c->bins.n_runs + 4.0 * ((c->bins.n_binned + 63) / 64);
             const double cb = 2.0 * c->bins.n_binned + (c->bin_stream ? 0.0 : runs);
-            c->kbytes["bin_scatter"] += wb * n_src + 16.0 * d.frontier + cb + wb * (double)d.pull_gathers;
+            const bool ss = src_stats(c) != 0;  // source side: row bounds in the scatter, or nw + deg in the apply
+            c->kbytes["bin_scatter"] += wb * n_src + (ss ? 16.0 * d.frontier : 0.0) + cb + wb * (double)d.pull_gathers;
             c->kbytes["bin_apply"] += (2.0 + wb) * (double)d.pull_edges + 2.0 * wb * c->n_local +
-                                      (c->bin_stream && d.pull_edges ? runs : 0.0);
+                                      (c->bin_stream && d.pull_edges ? runs : 0.0) + (ss ? 0.0 : (wb + 4.0) * c->n_local);
             c->kbytes["pull_heavy"] += 12.0 * (double)d.heavy_traversals;
         }
         if (c->last_pull && c->cur.dead_mode) c->kbytes["src_count"] += 32.0 * d.frontier + 4.125 * (double)d.traversals;
@@ -1146,7 +1265,7 @@ gossip_status advance(gossip_ctx* c, uint64_t fresh_global) {
     bool pend = c->cur_pdefer;  // a deferred pull round: nx, swapped into nw below, is not yet in seen
     c->cur_pdefer = false;
     if (c->cur_defer) {  // every delivery of the round is in nx (remote applies included): fold it into seen
-        if (c->world <= 1 && c->bins_ready && !c->bin_stream)
+        if (c->world <= 1 && c->bins_ready)
             pend = true;  // after the swap, in nw: the next round folds it (settle_fold / k_bin_apply)
         else
             HIPCHK(timed(c, "commit", [&] { return launch_commit_nx(c->seen, c->nx, c->n_local * c->Wp, c->stream); }));
@@ -1237,6 +1356,7 @@ gossip_status gossip_create(const gossip_config* cfg, gossip_ctx** out) {
     if (const char* u = std::getenv("GOSSIP_PULL_DIAG")) c->pull_diag = std::atoi(u) != 0;
     if (const char* u = std::getenv("GOSSIP_FULL_LIVENESS"); u && std::atoi(u)) c->full_liveness = true;
     if (const char* u = std::getenv("GOSSIP_OVERLAP_PROBE"); u && std::atoi(u)) c->overlap_probe = true;
+    if (const char* u = std::getenv("GOSSIP_TINY"); u && !std::atoi(u)) c->tiny_off = true;
     if (const char* b = std::getenv("GOSSIP_BIN_PERMILLE"); b && !cfg->bin_permille) c->cfg.bin_permille = (uint32_t)std::atoi(b);
     c->n = cfg->n_peers;
     c->begin = b;
@@ -1318,6 +1438,10 @@ void gossip_destroy(gossip_ctx* c) {
     hipFree(c->d_inj_origin);
     hipFree(c->d_inj_msg);
     hipFree(c->d_kill_peer);
+    hipFree(c->d_inj_round);
+    hipFree(c->d_kill_round);
+    if (c->tiny_out) hipHostFree(c->tiny_out);
+    if (c->tiny_result) hipHostFree(c->tiny_result);
     hipFree(c->d_counts);
     if (c->h_counts) hipHostFree(c->h_counts);
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
@@ -1461,6 +1585,10 @@ gossip_status gossip_inject(gossip_ctx* c, const uint32_t* origin, const uint32_
     HIPCHK(hipMalloc((void**)&c->d_inj_msg, n_msgs * sizeof(uint32_t)));
     HIPCHK(hipMemcpy(c->d_inj_origin, o.data(), n_msgs * sizeof(uint32_t), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c->d_inj_msg, mid.data(), n_msgs * sizeof(uint32_t), hipMemcpyHostToDevice));
+    hipFree(c->d_inj_round);
+    c->d_inj_round = nullptr;
+    HIPCHK(hipMalloc((void**)&c->d_inj_round, n_msgs * sizeof(uint32_t)));
+    HIPCHK(hipMemcpy(c->d_inj_round, c->inj_round_sorted.data(), n_msgs * sizeof(uint32_t), hipMemcpyHostToDevice));
     c->has_schedule = true;
     return GOSSIP_OK;
 }
@@ -1484,6 +1612,12 @@ gossip_status gossip_schedule_kills(gossip_ctx* c, const uint32_t* peer, const u
     c->d_kill_peer = nullptr;
     HIPCHK(hipMalloc((void**)&c->d_kill_peer, (n + 1) * sizeof(uint32_t)));
     HIPCHK(hipMemcpy(c->d_kill_peer, p.data(), (n + 1) * sizeof(uint32_t), hipMemcpyHostToDevice));
+    hipFree(c->d_kill_round);
+    c->d_kill_round = nullptr;
+    std::vector<uint32_t> kr(c->kill_round_sorted);
+    kr.push_back(0xFFFFFFFFu);
+    HIPCHK(hipMalloc((void**)&c->d_kill_round, kr.size() * sizeof(uint32_t)));
+    HIPCHK(hipMemcpy(c->d_kill_round, kr.data(), kr.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     return GOSSIP_OK;
 }
 
@@ -1521,42 +1655,49 @@ gossip_status gossip_reset(gossip_ctx* c) {
     const uint64_t words = c->n_local * c->Wp;
     const uint64_t bitwords = (c->n + 31) / 32;
     c->fold_pending = false;  // seen is cleared
-    HIPCHK(launch_zero_words(c->seen, words, s));
-    if (!c->bufs_zero) {  // (a run that ended normally left both zero)
-        HIPCHK(launch_zero_words(c->nw, words, s));
-        HIPCHK(launch_zero_words(c->nx, words, s));
-        c->bufs_zero = true;
-    }
-    for (int k = 0; k < 2; ++k) HIPCHK(hipMemsetAsync(c->tact[k], 0, tact_bytes(c), s));
-    c->tact_ok = true;  // no new words anywhere
+    c->tact_ok = true;        // no new words anywhere
     c->tact_marked = false;
-    HIPCHK(hipMemsetAsync(c->alive, 0xFF, bitwords * 4, s));
-    HIPCHK(hipMemsetAsync(c->registered, 0xFF, bitwords * 4, s));
-    if (c->n % 32) {
-        static thread_local uint32_t tail;
-        tail = (1u << (c->n % 32)) - 1u;
-        HIPCHK(hipMemcpyAsync(c->alive + bitwords - 1, &tail, 4, hipMemcpyHostToDevice, s));
-        HIPCHK(hipMemcpyAsync(c->registered + bitwords - 1, &tail, 4, hipMemcpyHostToDevice, s));
-        HIPCHK(hipStreamSynchronize(s));
-    }
-    if (c->n_started < c->n) {  // failed registration (list_cap): registered, never alive
-        std::vector<uint32_t> bits(bitwords, 0u);
-        for (uint64_t v = 0; v < c->n_started; ++v) bits[v >> 5] |= 1u << (v & 31);
-        HIPCHK(hipMemcpyAsync(c->alive, bits.data(), bitwords * 4, hipMemcpyHostToDevice, s));
-        HIPCHK(hipStreamSynchronize(s));
-    }
-    HIPCHK(hipMemsetAsync(c->st, 0, kStatLines * sizeof(DevStats), s));
     c->last_st_round = ~0u;
-    HIPCHK(hipMemsetAsync(c->n_reports, 0, sizeof(unsigned long long), s));
-    HIPCHK(hipMemsetAsync(c->inj_live, 0, kMaxWords * sizeof(uint64_t), s));
+    const bool tiny = tiny_ok(c);
+    if (tiny) {  // small overlays: every clear below in one launch
+        HIPCHK(launch_tiny_reset(tiny_args(c), words, (uint32_t)c->n_started, c->any_masked, tact_bytes(c) / 8,
+                                 c->tact[0], c->tact[1], c->st, s));
+        c->bufs_zero = true;
+    } else {
+        HIPCHK(launch_zero_words(c->seen, words, s));
+        if (!c->bufs_zero) {  // (a run that ended normally left both zero)
+            HIPCHK(launch_zero_words(c->nw, words, s));
+            HIPCHK(launch_zero_words(c->nx, words, s));
+            c->bufs_zero = true;
+        }
+        for (int k = 0; k < 2; ++k) HIPCHK(hipMemsetAsync(c->tact[k], 0, tact_bytes(c), s));
+        HIPCHK(hipMemsetAsync(c->alive, 0xFF, bitwords * 4, s));
+        HIPCHK(hipMemsetAsync(c->registered, 0xFF, bitwords * 4, s));
+        if (c->n % 32) {
+            static thread_local uint32_t tail;
+            tail = (1u << (c->n % 32)) - 1u;
+            HIPCHK(hipMemcpyAsync(c->alive + bitwords - 1, &tail, 4, hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(c->registered + bitwords - 1, &tail, 4, hipMemcpyHostToDevice, s));
+            HIPCHK(hipStreamSynchronize(s));
+        }
+        if (c->n_started < c->n) {  // failed registration (list_cap): registered, never alive
+            std::vector<uint32_t> bits(bitwords, 0u);
+            for (uint64_t v = 0; v < c->n_started; ++v) bits[v >> 5] |= 1u << (v & 31);
+            HIPCHK(hipMemcpyAsync(c->alive, bits.data(), bitwords * 4, hipMemcpyHostToDevice, s));
+            HIPCHK(hipStreamSynchronize(s));
+        }
+        HIPCHK(hipMemsetAsync(c->st, 0, kStatLines * sizeof(DevStats), s));
+        HIPCHK(hipMemsetAsync(c->n_reports, 0, sizeof(unsigned long long), s));
+        HIPCHK(hipMemsetAsync(c->inj_live, 0, kMaxWords * sizeof(uint64_t), s));
+        if (c->miss) HIPCHK(hipMemsetAsync(c->miss, 0, c->n_edges + 1, s));
+        if (c->any_masked && c->col && c->n_edges) {
+            hipLaunchKernelGGL(k_unmask, dim3(2048), dim3(256), 0, s, c->col, c->n_edges);
+            HIPCHK(hipGetLastError());
+        }
+    }
     if (c->cov_hist) HIPCHK(hipMemsetAsync(c->cov_hist, 0, (uint64_t)c->cfg.max_rounds * 64 * c->Wp * 8, s));
-    if (c->miss) HIPCHK(hipMemsetAsync(c->miss, 0, c->n_edges + 1, s));
     // slots still hold words of the last run: the first binned round of the next rewrites every slot
     c->bins_first = true;
-    if (c->any_masked && c->col && c->n_edges) {
-        hipLaunchKernelGGL(k_unmask, dim3(2048), dim3(256), 0, s, c->col, c->n_edges);
-        HIPCHK(hipGetLastError());
-    }
     if (c->cfg.extra_cap) {
         HIPCHK(hipMemsetAsync(c->ex_cnt, 0, c->n_local * 4 + 4, s));
         HIPCHK(hipMemsetAsync(c->ex_miss, 0, c->n_local * c->cfg.extra_cap + 1, s));
@@ -1585,7 +1726,7 @@ gossip_status gossip_reset(gossip_ctx* c) {
     c->cum_digest = c->cum_covered = 0;
     c->cum_dead_cov = c->cum_died = c->cum_injected = 0;
     if (c->dist) gossip::dist_reset(c->dist);
-    HIPCHK(hipStreamSynchronize(s));
+    if (!tiny) HIPCHK(hipStreamSynchronize(s));  // (every read of device state synchronises the stream first)
     return GOSSIP_OK;
 }
 
@@ -1607,6 +1748,10 @@ gossip_status gossip_step(gossip_ctx* c, gossip_round_stats* out) {
 
 gossip_status gossip_run(gossip_ctx* c, gossip_round_stats* per_round, uint32_t cap, uint32_t* rounds) {
     if (!c) return fail(GOSSIP_EINVAL, "null ctx");
+    if (c->round == 0 && !c->finished && tiny_ok(c)) {
+        if (set_dev(c)) return GOSSIP_EHIP;
+        return tiny_run(c, per_round, cap, rounds);
+    }
     uint32_t k = 0;
     while (!c->finished) {
         gossip_round_stats st;

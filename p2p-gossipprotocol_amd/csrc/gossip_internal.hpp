@@ -107,6 +107,11 @@ struct BinArgs {
     uint32_t split;               // a bin holds `split` parts of bin_words / Wp peers; its slots (in source
                                   // order over the whole bin, so the scatter's runs are `split` times longer)
                                   // are applied by `split` workgroups, each keeping its own part's slots
+    const uint32_t* deg;          // per owned peer: its row length (source-side stats booked by the apply)
+    uint32_t src_stats;           // 1: the scatter books the source side of the round's pushes (its first
+                                  // unit of each chunk, row bounds loaded after the slice); 0: the apply
+                                  // does, for its bin's peers (bin_src_stats), and the scatter's staging is
+                                  // one round trip
 };
 
 struct BinState {
@@ -127,6 +132,7 @@ struct BinState {
     uint64_t* val = nullptr;
     uint64_t* dummy = nullptr;
     uint32_t* cb_slot = nullptr;  // GOSSIP_KEEP_SLOTS=1 only (k_bin_scatter_flat)
+    uint32_t* deg = nullptr;      // n_local row lengths (BinArgs.deg)
     uint32_t bin_words = kBinWords;
     uint32_t split = 1;     // parts per bin (GOSSIP_BIN_SPLIT)
     uint64_t n_slots = 0;   // padded
@@ -214,6 +220,28 @@ struct RebootArgs {
     uint32_t seed;
 };
 
+// A whole run of a small overlay in one launch (gossip_tiny.hip): everything one workgroup needs.
+struct TinyArgs {
+    const uint32_t* erow;                  // per edge: its row (source)
+    uint32_t* col;                         // bit 31 = masked
+    uint32_t *alive, *registered;          // global bitsets
+    uint64_t *seen, *nw, *nx;              // n * Wp words
+    uint8_t* miss;                         // per edge (null: no liveness)
+    DeadReport* reports;
+    unsigned long long* n_reports;
+    uint64_t report_cap;
+    uint64_t* inj_live;                    // kMaxWords: messages injected since the reset
+    const uint32_t *inj_origin, *inj_msg, *inj_round;  // the schedule, sorted by round
+    const uint32_t *kill_peer, *kill_round;
+    uint32_t n_inj, n_kill;
+    uint32_t n, n_edges, wd;               // peers, edges, words per peer (unpadded)
+    uint32_t seed, churn, ping_every, max_missed;
+    uint32_t start, min_rounds, max_rounds, last_inject_round, has_schedule;
+    gossip_round_stats* out;               // one entry per round run
+    uint32_t out_cap;
+    uint32_t* result;                      // [rounds run, new words in the nx buffer]
+};
+
 // ---- launchers (gossip_kernels.hip) ----
 hipError_t launch_churn(const RoundArgs& a, uint32_t W, uint32_t seed, uint32_t threshold, hipStream_t s);
 hipError_t launch_kills(const RoundArgs& a, uint32_t W, const uint32_t* kill_peers, uint32_t n, hipStream_t s);
@@ -269,6 +297,14 @@ hipError_t launch_heavy_count(const uint64_t* rp, uint64_t n_local, uint32_t hea
                               unsigned long long* n_chunks, hipStream_t s);
 hipError_t launch_heavy_fill(const uint64_t* rp, uint64_t n_local, uint32_t heavy, uint32_t clen, HeavyChunk* chunks,
                              unsigned long long* cursor, hipStream_t s);
+
+// ---- small overlays (gossip_tiny.hip) ----
+hipError_t launch_tiny_erow(const uint64_t* rp, uint32_t n, uint32_t* erow, hipStream_t s);
+hipError_t launch_tiny_reset(const TinyArgs& t, uint64_t words, uint32_t n_started, bool unmask, uint64_t tact_words,
+                             uint64_t* tact0, uint64_t* tact1, DevStats* st, hipStream_t s);
+hipError_t launch_tiny_run(const TinyArgs& t, uint32_t Wp, hipStream_t s);
+constexpr uint32_t kTinyPeers = 65536;  // overlays up to this many peers and edges run whole in one launch
+constexpr uint32_t kTinyEdges = 65536;
 
 // ---- overlay generator (gossip_graph.hip) ----
 // Builds the owned rows of the powerlaw overlay on the device.  On success

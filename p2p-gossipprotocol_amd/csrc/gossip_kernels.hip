@@ -1118,7 +1118,10 @@ __global__ __launch_bounds__(kBlock) void k_pull_heavy(RoundArgs a) {
 // Staging of one scatter unit's source chunk (every thread of the block):
 // the chunk's new words into the LDS slice, the live bits of its sources and,
 // in the chunk's first unit, the source side of its pushes (broadcastMessage,
-// peer.cpp:310-316).  Ends before the block barrier that publishes the slice.
+// peer.cpp:310-316) unless the apply books them (BinArgs.src_stats = 0: the
+// staging is then one round trip instead of a chain of dependent row-bound
+// loads, ~40 us per unit).  Ends before the block barrier that publishes the
+// slice.
 template <int W, bool COV>
 __device__ __forceinline__ void scatter_stage(const RoundArgs& a, const BinArgs& b, const BinUnit& un, uint32_t wd,
                                               unsigned long long* slice, unsigned long long* live_s,
@@ -1158,7 +1161,7 @@ __device__ __forceinline__ void scatter_stage(const RoundArgs& a, const BinArgs&
             if (k0 + kk >= kSrcIt || j >= ((n_src + 63) & ~63ull)) continue;  // wave-uniform
             const uint64_t v = vb + j;
             const bool vv = j < n_src;
-            const bool own = vv && un.first && v >= a.begin && v < a.end;
+            const bool own = vv && b.src_stats && un.first && v >= a.begin && v < a.end;
             bool nz = false;
 #pragma unroll
             for (int w = 0; w < W; ++w) {
@@ -1542,13 +1545,49 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_flat(RoundArgs a,
     flush<kWaves>(acc, a.st);
 }
 
+// The source side of a binned round for a bin's peers (their pushes,
+// broadcastMessage peer.cpp:310-316) when the scatter leaves it to the apply
+// (BinArgs.src_stats = 0): per peer with new words, frontier, traversals,
+// deliveries and undelivered sends from its row length (and dead-edge
+// counters), digest, covered and coverage of the words -- the same sums
+// scatter_stage books, read as three sequential streams (nw, deg, dgone/dmask).
+template <int W, int kB>
+__device__ __forceinline__ void bin_src_stats(const RoundArgs& a, const BinArgs& b, uint64_t v0, uint32_t nv,
+                                              uint32_t wd, unsigned int* cov_s, Acc& acc) {
+    const bool cnt = a.dead_mode && a.dgone;
+    for (uint32_t i = threadIdx.x; i < nv; i += kB) {
+        const uint64_t lv = v0 + i, v = a.begin + lv;
+        uint32_t pc = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            const uint64_t m = a.nw[lv * W + w];
+            if (!m) continue;
+            pc += (uint32_t)__popcll(m);
+            if (w < (int)wd) acc.digest += digest_weight(v * wd + w) * m;
+            if (a.cov)
+                for (uint64_t x = m; x; x &= x - 1) atomicAdd(&cov_s[w * 64 + __builtin_ctzll(x)], 1u);
+        }
+        if (!pc) continue;
+        acc.frontier++;
+        acc.covered += pc;
+        const uint64_t d = b.deg[lv];
+        const uint32_t dg = cnt ? a.dgone[lv] : 0u, dk = cnt ? a.dmask[lv] : 0u;
+        if (!a.dead_mode || cnt) {
+            acc.trav += d - dk;
+            acc.deliv += (unsigned long long)pc * (d - dg);
+            acc.undeliv += (unsigned long long)pc * (dg - dk);
+        }
+    }
+}
+
 // Phase 2: one workgroup per bin folds the bin's slots into an LDS
 // accumulator (ds_or_b64), then applies handleClient's test-and-set to the
 // bin's peers with plain stores.  A bin none of whose peers can still learn
 // anything skips its slots.
 template <int W, int kWords, int kB>  // kWords: LDS accumulator words; kB: threads
-__global__ __launch_bounds__(kB) void k_bin_apply(RoundArgs a, BinArgs b) {
+__global__ __launch_bounds__(kB) void k_bin_apply(RoundArgs a, BinArgs b, uint32_t wd) {
     __shared__ unsigned long long acc_s[kWords];
+    __shared__ unsigned int cov_s[64 * W];
     Acc acc;
     // workgroup -> (bin, part): a bin of b.split parts is applied by b.split workgroups, each keeping
     // the slots of its own part's peers; the parts of a bin go to one XCD (block ids 8 apart, which the
@@ -1565,6 +1604,12 @@ __global__ __launch_bounds__(kB) void k_bin_apply(RoundArgs a, BinArgs b) {
     if (lo >= bn.v1 - bn.v0) return;
     const uint32_t nv = min(bn.v1 - bn.v0 - lo, part_peers);
     const uint64_t v0 = bn.v0 + lo;
+    if (!b.src_stats) {
+        if (a.cov)
+            for (uint32_t i = threadIdx.x; i < 64 * W; i += kB) cov_s[i] = 0;
+        __syncthreads();
+        bin_src_stats<W, kB>(a, b, v0, nv, wd, cov_s, acc);
+    }
     // a.fold: the previous (deferred) push round's receipts are this round's new words and not yet
     // in seen; every peer of the bin (heavy rows included) gets seen |= nw here, before k_pull_heavy
     auto pend = [&](uint32_t i) { return a.fold ? a.nw[v0 * W + i] : 0ull; };
@@ -1574,12 +1619,19 @@ __global__ __launch_bounds__(kB) void k_bin_apply(RoundArgs a, BinArgs b) {
         const bool va = !a.dead_mode || bit_alive(a.alive, (uint32_t)(a.begin + v0 + i / W));
         needy |= va && (injm(a, i % W) & ~(a.seen[v0 * W + i] | pend(i))) != 0;
     }
+    auto cov_out = [&] {
+        if (b.src_stats || !a.cov) return;
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < 64 * W; i += kB)
+            if (cov_s[i]) atomicAdd(&a.cov[i], (unsigned long long)cov_s[i]);
+    };
     if (!__syncthreads_or(needy)) {
         for (uint32_t i = threadIdx.x; i < nv * W; i += kB) {
             a.nx[v0 * W + i] = 0ull;
             if (const uint64_t p = pend(i)) a.seen[v0 * W + i] |= p;
         }
         flush<kB / 64>(acc, a.st);
+        cov_out();
         return;
     }
     if (threadIdx.x == 0 && part == 0) acc.pulled = bn.s1 - bn.s0;  // slots scanned (byte accounting)
@@ -1621,6 +1673,7 @@ __global__ __launch_bounds__(kB) void k_bin_apply(RoundArgs a, BinArgs b) {
         a.nx[v0 * W + i] = fr;  // heavy rows: 0 here, OR-ed by k_pull_heavy afterwards
     }
     flush<kB / 64>(acc, a.st);
+    cov_out();
 }
 
 // ---------------------------------------------------------------------------
@@ -1629,14 +1682,19 @@ __global__ __launch_bounds__(kB) void k_bin_apply(RoundArgs a, BinArgs b) {
 // access moves to the apply, as reads of slot runs (a read of a short run
 // costs no read-modify-write of a partly written line).
 // ---------------------------------------------------------------------------
-// Phase 1: stage each unit's source chunk in LDS (scatter_stage: also the
-// chunk's source-side stats), then val[p] = slice[cb_src[p]] for the unit's cb
-// entries, consecutive lanes on consecutive entries.  Every entry is written
-// every binned round.
+// Phase 1: stage each unit's source chunk in LDS (scatter_stage), then
+// val[p] = slice[cb_src[p]] for the unit's cb entries, written front to back
+// in 16-B pieces with consecutive lanes on consecutive pieces, so every store
+// instruction covers 1 KB of whole lines (W = 1: a piece holds two entries;
+// W >= 2: an entry is W / 2 pieces).  An earlier mapping -- 8 entries per lane
+// as four 16-B stores 64 B apart -- sent every lane's store to L2 as a request
+// of its own (config 4: 9.7e8 write requests per launch, the TA ~92 % busy).
+// Every entry is written every binned round.
 template <int W, bool COV>
 __global__ __launch_bounds__(kScatterBlock) void k_bin_stream(RoundArgs a, BinArgs b, uint32_t wd) {
     constexpr int kWaves = kScatterBlock / 64;
-    constexpr int kU = W <= 2 ? 2 : 1;  // 8-entry blocks in flight per lane
+    constexpr int kPW = W == 1 ? 1 : W / 2;  // pieces per entry (W >= 2)
+    constexpr int kU = 4;                    // pieces per lane in flight
     __shared__ unsigned long long slice[kBinChunkWords];
     __shared__ unsigned long long live_s[kBinChunkWords / 64 / W];
     __shared__ unsigned int cov_s[COV ? 64 * W : 1];
@@ -1648,45 +1706,54 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_stream(RoundArgs a, BinAr
         const BinUnit un = b.units[ui];
         if (un.p0 >= un.p1 && !un.first) return;  // padding of a row (block-uniform)
         scatter_stage<W, COV>(a, b, un, wd, slice, live_s, cov_s, acc);
-        // aligned blocks of 8 entries per lane: one 16-B load of cb_src, 8 * W words stored as 16-B pairs
-        const uint64_t k0 = un.p0 >> 3, k1 = (un.p1 + 7) >> 3;
-        for (uint64_t kb = k0 + threadIdx.x; kb < k1; kb += (uint64_t)kScatterBlock * kU) {
-            v4u32 sv[kU];
+        __syncthreads();
+        if (un.p0 >= un.p1) return;
+        acc.gathered += threadIdx.x == 0 ? un.p1 - un.p0 : 0;  // slots written (byte accounting)
+        if (W == 1) {
+            // piece k = entries 2k, 2k + 1 (cb_src read as one u32: 4-B aligned)
+            const uint64_t k0 = un.p0 >> 1, k1 = (un.p1 + 1) >> 1;
+            const uint32_t* cb2 = reinterpret_cast<const uint32_t*>(b.cb_src);
+            for (uint64_t kb = k0 + threadIdx.x; kb < k1; kb += (uint64_t)kScatterBlock * kU) {
+                uint32_t sv[kU];
 #pragma unroll
-            for (int j = 0; j < kU; ++j) {
-                const uint64_t k = kb + (uint64_t)j * kScatterBlock;
-                sv[j] = __builtin_nontemporal_load(reinterpret_cast<const v4u32*>(b.cb_src) + min(k, k1 - 1));
-            }
+                for (int j = 0; j < kU; ++j)
+                    sv[j] = __builtin_nontemporal_load(cb2 + min(kb + (uint64_t)j * kScatterBlock, k1 - 1));
 #pragma unroll
-            for (int j = 0; j < kU; ++j) {
-                const uint64_t k = kb + (uint64_t)j * kScatterBlock;
-                if (k >= k1) continue;
-                const uint32_t sw[4] = {sv[j].x, sv[j].y, sv[j].z, sv[j].w};
-                uint64_t x[8 * W];
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const uint32_t u = (sw[e >> 1] >> ((e & 1) * 16)) & (kRunStart - 1u);
-#pragma unroll
-                    for (int w = 0; w < W; ++w) x[e * W + w] = slice[u * W + w];
-                }
-                const uint64_t p = k * 8;
-                if (p >= un.p0 && p + 8 <= un.p1) {  // whole block: 16-B stores
-                    u64x2* dst = reinterpret_cast<u64x2*>(b.val + p * W);
-#pragma unroll
-                    for (int i = 0; i < 4 * W; ++i) {
+                for (int j = 0; j < kU; ++j) {
+                    const uint64_t k = kb + (uint64_t)j * kScatterBlock;
+                    if (k >= k1) break;
+                    const uint64_t x0 = slice[sv[j] & (kRunStart - 1u)];
+                    const uint64_t x1 = slice[(sv[j] >> 16) & (kRunStart - 1u)];
+                    const uint64_t e = 2 * k;
+                    if (e >= un.p0 && e + 2 <= un.p1) {
                         u64x2 y;
-                        y.x = x[2 * i];
-                        y.y = x[2 * i + 1];
-                        dst[i] = y;
+                        y.x = x0;
+                        y.y = x1;
+                        reinterpret_cast<u64x2*>(b.val)[k] = y;
+                    } else {  // a piece cut by the unit's ends
+                        if (e >= un.p0 && e < un.p1) b.val[e] = x0;
+                        if (e + 1 >= un.p0 && e + 1 < un.p1) b.val[e + 1] = x1;
                     }
-                } else {  // the unit's ragged ends
-#pragma unroll
-                    for (int e = 0; e < 8; ++e)
-                        if (p + e >= un.p0 && p + e < un.p1)
-#pragma unroll
-                            for (int w = 0; w < W; ++w) b.val[(p + e) * W + w] = x[e * W + w];
                 }
-                acc.gathered += (unsigned)(min(p + 8, un.p1) - max(p, un.p0));
+            }
+        } else {
+            const uint64_t k0 = un.p0 * kPW, k1 = un.p1 * kPW;
+            for (uint64_t kb = k0 + threadIdx.x; kb < k1; kb += (uint64_t)kScatterBlock * kU) {
+                uint32_t sv[kU];
+#pragma unroll
+                for (int j = 0; j < kU; ++j)
+                    sv[j] = b.cb_src[min(kb + (uint64_t)j * kScatterBlock, k1 - 1) / kPW];
+#pragma unroll
+                for (int j = 0; j < kU; ++j) {
+                    const uint64_t k = kb + (uint64_t)j * kScatterBlock;
+                    if (k >= k1) break;
+                    const uint32_t u = sv[j] & (kRunStart - 1u);
+                    const uint32_t w0 = (uint32_t)(k % kPW) * 2;
+                    u64x2 y;
+                    y.x = slice[(uint64_t)u * W + w0];
+                    y.y = slice[(uint64_t)u * W + w0 + 1];
+                    reinterpret_cast<u64x2*>(b.val)[k] = y;  // entry k / kPW, words w0, w0 + 1
+                }
             }
         }
     };
@@ -1699,96 +1766,152 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_stream(RoundArgs a, BinAr
     }
 }
 
-// Phase 2: one workgroup per bin.  Each wave takes 64-slot groups of the bin
-// (kG at once): bdst (destination, bit 15 = a run starts here), the run of
-// each slot from the group's count of earlier runs plus a ballot of the
-// flags, the run's offset, then the value at q - ap_run[run] -- a read from
-// the run's stretch of cb order -- OR-ed into the LDS accumulator.  The end
-// is k_bin_apply's: test-and-set of the bin's peers with plain stores.
+// Phase 2 (streamed layout): the bin's slots, each folded into the LDS
+// accumulator of its destination.  A slot's value sits at its cb position
+// q - ap_run[run], so each 64-slot group is a chain of three dependent loads:
+// bdst (destination, bit 15 = a run starts here) with the group's count of
+// earlier runs (ap_grp) -> the run's offset (ap_run, the run from a ballot of
+// the flags) -> the value.  Unpipelined that chain made the apply latency-bound
+// (config 4: 12.3 ms per launch for ~20 GB).  Here every wave keeps kS stages
+// of kG groups in flight: in iteration i it issues the first loads of stage
+// i+3, the offsets of i+2, the values of i+1 and folds the values of i into
+// the LDS accumulator (ds_or_b64), rotating kS register sets without copies
+// (loop unrolled by kS) so each wait is for loads issued an iteration earlier.
+// Lanes past the bin or its groups load clamped addresses and fold nothing.
+// The blocks that share an XCD (blockIdx % 8) apply consecutive bins, which read neighbouring runs of every
+// chunk.  (Measured at config 4: a persistent launch with rows of consecutive bins per XCD and a bounded
+// per-row sync, so that neighbouring bins walk their chunks together, was slower: 10.3-11.5 against
+// 9.6-9.8 ms per launch.)  The end of each bin is k_bin_apply's: test-and-set of its peers with plain
+// stores (and the fold of a deferred push round's words, a.fold).
 template <int W, int kWords, int kB>
-__global__ __launch_bounds__(kB) void k_bin_apply_runs(RoundArgs a, BinArgs b) {
+__global__ __launch_bounds__(kB) void k_bin_apply_runs(RoundArgs a, BinArgs b, uint32_t wd) {
     constexpr int kWaves = kB / 64;
-    constexpr int kG = W <= 2 ? 4 : 2;  // groups in flight per wave
+    constexpr int kG = W == 1 ? 4 : W == 2 ? 2 : 1;  // groups per stage
+    constexpr int kS = 4;                             // stages in flight
     __shared__ unsigned long long acc_s[kWords];
+    __shared__ unsigned int cov_s[64 * W];
     Acc acc;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    // XCD-contiguous bins: the blocks that share an XCD (blockIdx % 8) take consecutive bins, so the
-    // ~32 bins in flight on an XCD read neighbouring runs of every chunk and share their partial
-    // sectors in that XCD's L2
-    const uint32_t bi = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
-    if (bi >= b.n_bins) return;  // (whole workgroup, before any barrier)
-    const Bin bn = b.bins[bi];
-    const uint32_t nv = bn.v1 - bn.v0;
-    const uint64_t v0 = bn.v0;
-    bool needy = false;
-    for (uint32_t i = threadIdx.x; i < nv * W; i += kB) {
-        acc_s[i] = 0ull;
-        const bool va = !a.dead_mode || bit_alive(a.alive, (uint32_t)(a.begin + v0 + i / W));
-        needy |= va && (injm(a, i % W) & ~a.seen[v0 * W + i]) != 0;
-    }
-    if (!__syncthreads_or(needy)) {
-        for (uint32_t i = threadIdx.x; i < nv * W; i += kB) a.nx[v0 * W + i] = 0ull;
-        flush<kWaves>(acc, a.st);
-        return;
-    }
-    if (threadIdx.x == 0) acc.pulled = bn.s1 - bn.s0;  // slots scanned (byte accounting)
+    if (!b.src_stats && a.cov)
+        for (uint32_t i = threadIdx.x; i < 64 * W; i += kB) cov_s[i] = 0;
     const unsigned long long upto = lane == 63 ? ~0ull : (2ull << lane) - 1;  // lanes 0..lane
-    if (bn.s1 > bn.s0) {
-        const uint64_t g_lo = bn.s0 >> 6, g_hi = ((bn.s1 - 1) >> 6) + 1;
-        for (uint64_t g0 = g_lo + wave; g0 < g_hi; g0 += (uint64_t)kWaves * kG) {
-            uint32_t d[kG], gr[kG];
-#pragma unroll
-            for (int j = 0; j < kG; ++j) {  // (bdst and ap_grp hold whole groups past the last slot)
-                const uint64_t g = min(g0 + (uint64_t)j * kWaves, g_hi - 1);
-                d[j] = b.bdst[g * 64 + lane];
-                gr[j] = b.ap_grp[g];
+    const uint32_t run_max = (uint32_t)b.n_runs_m1;
+    auto apply_bin = [&](const uint32_t bi) {
+        const Bin bn = b.bins[bi];
+        const uint32_t nv = bn.v1 - bn.v0;
+        const uint64_t v0 = bn.v0;
+        __syncthreads();  // the previous bin is done with acc_s (and cov_s is initialised)
+        if (!b.src_stats) bin_src_stats<W, kB>(a, b, v0, nv, wd, cov_s, acc);
+        auto pend = [&](uint32_t i) { return a.fold ? a.nw[v0 * W + i] : 0ull; };
+        bool needy = false;
+        for (uint32_t i = threadIdx.x; i < nv * W; i += kB) {
+            acc_s[i] = 0ull;
+            const bool va = !a.dead_mode || bit_alive(a.alive, (uint32_t)(a.begin + v0 + i / W));
+            needy |= va && (injm(a, i % W) & ~(a.seen[v0 * W + i] | pend(i))) != 0;
+        }
+        if (!__syncthreads_or(needy)) {
+            for (uint32_t i = threadIdx.x; i < nv * W; i += kB) {
+                a.nx[v0 * W + i] = 0ull;
+                if (const uint64_t p = pend(i)) a.seen[v0 * W + i] |= p;
             }
-            uint32_t off[kG];
-            bool ok[kG];
+            return;
+        }
+        if (threadIdx.x == 0) acc.pulled += bn.s1 - bn.s0;  // slots scanned (byte accounting)
+        if (bn.s1 > bn.s0) {
+            const uint64_t g_lo = bn.s0 >> 6, g_hi = ((bn.s1 - 1) >> 6) + 1;
+            // this wave's groups: g_lo + wave + kWaves * t, t < n_t
+            const uint32_t n_t =
+                g_hi - g_lo > (uint64_t)wave ? (uint32_t)((g_hi - g_lo - wave + kWaves - 1) / kWaves) : 0u;
+            const uint32_t n_it = (n_t + kG - 1) / kG;
+            uint32_t d[kS][kG], gr[kS][kG], off[kS][kG];
+            uint64_t x[kS][kG][W];
+            auto grp = [&](uint32_t i, int j) { return g_lo + wave + (uint64_t)kWaves * (i * kG + j); };
+            auto valid = [&](uint32_t i, int j) {  // lane's slot belongs to the bin (and to this wave's groups)
+                const uint64_t g = grp(i, j), q = g * 64 + lane;
+                return i * kG + j < n_t && q >= bn.s0 && q < bn.s1;
+            };
+            auto ld_a = [&](int st, uint32_t i) {  // bdst and the group's earlier runs (ap_grp holds whole groups)
 #pragma unroll
-            for (int j = 0; j < kG; ++j) {
-                const uint64_t g = g0 + (uint64_t)j * kWaves;
-                const uint64_t q = g * 64 + lane;
-                ok[j] = g < g_hi && q >= bn.s0 && q < bn.s1;
-                const unsigned long long st = __ballot((d[j] & kRunStart) != 0);
-                // a slot of the bin lies in a run that starts at or before it: run >= 0
-                const uint32_t run = gr[j] + (uint32_t)__popcll(st & upto) - 1u;
-                off[j] = ok[j] ? b.ap_run[run] : 0u;
-            }
-            uint64_t x[kG][W];
+                for (int j = 0; j < kG; ++j) {
+                    const uint64_t g = min(grp(i, j), g_hi - 1);
+                    d[st][j] = b.bdst[g * 64 + lane];
+                    gr[st][j] = b.ap_grp[g];
+                }
+            };
+            auto ld_b = [&](int st, uint32_t i) {  // the run of each slot -> its offset
 #pragma unroll
-            for (int j = 0; j < kG; ++j) {
-                const uint64_t q = (g0 + (uint64_t)j * kWaves) * 64 + lane;
-                const uint64_t p = ok[j] ? (uint64_t)((uint32_t)q - off[j]) : 0;  // the slot's cb position
+                for (int j = 0; j < kG; ++j) {
+                    const unsigned long long fl = __ballot((d[st][j] & kRunStart) != 0);
+                    // a slot of the bin lies in a run that starts at or before it (run >= 0); others clamp
+                    const uint32_t run = min(gr[st][j] + (uint32_t)__popcll(fl & upto) - 1u, run_max);
+                    off[st][j] = b.ap_run[run];
+                }
+            };
+            auto ld_c = [&](int st, uint32_t i) {  // the values
 #pragma unroll
-                for (int w = 0; w < W; ++w) x[j][w] = b.val[p * W + w];
-            }
+                for (int j = 0; j < kG; ++j) {
+                    const uint64_t q = grp(i, j) * 64 + lane;
+                    const uint64_t p = valid(i, j) ? (uint64_t)((uint32_t)q - off[st][j]) : 0;  // the slot's cb position
 #pragma unroll
-            for (int j = 0; j < kG; ++j) {
-                if (!ok[j]) continue;
-                const uint32_t dl = d[j] & (kRunStart - 1u);
+                    for (int w = 0; w < W; ++w) x[st][j][w] = b.val[p * W + w];
+                }
+            };
+            auto fold = [&](int st, uint32_t i) {
 #pragma unroll
-                for (int w = 0; w < W; ++w)
-                    if (x[j][w]) atomicOr(&acc_s[dl * W + w], (unsigned long long)x[j][w]);  // ds_or_b64
+                for (int j = 0; j < kG; ++j) {
+                    if (!valid(i, j)) continue;
+                    const uint32_t dl = d[st][j] & (kRunStart - 1u);
+#pragma unroll
+                    for (int w = 0; w < W; ++w)
+                        if (x[st][j][w]) atomicOr(&acc_s[dl * W + w], (unsigned long long)x[st][j][w]);  // ds_or_b64
+                }
+            };
+            // prologue: stages 0..2 partly issued
+            ld_a(0, 0);
+            ld_a(1, 1);
+            ld_b(0, 0);
+            ld_a(2, 2);
+            ld_b(1, 1);
+            ld_c(0, 0);
+            for (uint32_t i0 = 0; i0 < n_it; i0 += kS) {
+#pragma unroll
+                for (int k = 0; k < kS; ++k) {
+                    const uint32_t i = i0 + k;
+                    if (i >= n_it) break;  // wave-uniform
+                    ld_a((k + 3) % kS, i + 3);
+                    ld_b((k + 2) % kS, i + 2);
+                    ld_c((k + 1) % kS, i + 1);
+                    fold(k, i);
+                }
             }
         }
-    }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < nv * W; i += kB) {
-        const uint64_t sv = a.seen[v0 * W + i];
-        const bool va = !a.dead_mode || bit_alive(a.alive, (uint32_t)(a.begin + v0 + i / W));  // dead: no receive
-        const uint64_t fr = va ? acc_s[i] & injm(a, i % W) & ~sv : 0ull;
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < nv * W; i += kB) {
+            const uint64_t p = pend(i);
+            const uint64_t sv = a.seen[v0 * W + i] | p;
+            const bool va = !a.dead_mode || bit_alive(a.alive, (uint32_t)(a.begin + v0 + i / W));  // dead: no receive
+            const uint64_t fr = va ? acc_s[i] & injm(a, i % W) & ~sv : 0ull;
 #pragma unroll
-        for (int w = 0; w < W; ++w)
-            if (i % W == w) acc.fresh_or[w] |= fr;  // (constant register indices)
-        if (fr) {  // handleClient: new -> Message-List insert (peer.cpp:281-282)
-            a.seen[v0 * W + i] = sv | fr;
-            acc.fresh += (unsigned long long)__popcll(fr);
-            acc.activated++;
+            for (int w = 0; w < W; ++w)
+                if (i % W == w) acc.fresh_or[w] |= fr;  // (constant register indices)
+            if (fr) {  // handleClient: new -> Message-List insert (peer.cpp:281-282)
+                acc.fresh += (unsigned long long)__popcll(fr);
+                acc.activated++;
+            }
+            if (fr | p) a.seen[v0 * W + i] = sv | fr;
+            a.nx[v0 * W + i] = fr;  // heavy rows: 0 here, OR-ed by k_pull_heavy afterwards
         }
-        a.nx[v0 * W + i] = fr;  // heavy rows: 0 here, OR-ed by k_pull_heavy afterwards
-    }
+    };
+    // bins of XCD group x: [x * per, (x + 1) * per), block x + 8 j applying bin j of it (the blocks in flight
+    // on an XCD apply consecutive bins)
+    const uint32_t xg = blockIdx.x & 7, member = blockIdx.x >> 3, per = (uint32_t)((b.n_bins + 7) / 8);
+    if (member < per && xg * per + member < b.n_bins) apply_bin(xg * per + member);
     flush<kWaves>(acc, a.st);
+    if (!b.src_stats && a.cov) {
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < 64 * W; i += kB)
+            if (cov_s[i]) atomicAdd(&a.cov[i], (unsigned long long)cov_s[i]);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -2849,14 +2972,15 @@ hipError_t launch_bin_scatter(const RoundArgs& a, const BinArgs& b, uint32_t W_,
 
 hipError_t launch_bin_apply(const RoundArgs& a, const BinArgs& b, uint32_t W_, hipStream_t s) {
     if (!b.n_bins) return hipSuccess;
+    const uint32_t wd = wd_of(W_);
     if (b.stream) {
         const unsigned sgrid = (unsigned)((b.n_bins + 7) / 8 * 8);  // whole groups of 8 (XCD-contiguous bins)
         if (b.bin_words > kBinWords / 2) {
             GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_apply_runs<W, kBinWords, 1024>),
-                                                           dim3(sgrid), dim3(1024), 0, s, a, b));
+                                                           dim3(sgrid), dim3(1024), 0, s, a, b, wd));
         } else {
             GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_apply_runs<W, kBinWords / 2, kBlock>),
-                                                           dim3(sgrid), dim3(kBlock), 0, s, a, b));
+                                                           dim3(sgrid), dim3(kBlock), 0, s, a, b, wd));
         }
         return hipGetLastError();
     }
@@ -2864,10 +2988,10 @@ hipError_t launch_bin_apply(const RoundArgs& a, const BinArgs& b, uint32_t W_, h
     const unsigned grid = (unsigned)(b.split > 1 ? (b.n_bins + 7) / 8 * 8 * b.split : b.n_bins);
     if (b.bin_words > kBinWords / 2) {  // up to 144 KB accumulators: one 16-wave workgroup per CU
         GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_apply<W, kBinWords, 1024>), dim3(grid), dim3(1024), 0,
-                                                       s, a, b));
+                                                       s, a, b, wd));
     } else {  // 64 KB accumulators: two 4-wave workgroups per CU
         GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_apply<W, kBinWords / 2, kBlock>), dim3(grid),
-                                                       dim3(kBlock), 0, s, a, b));
+                                                       dim3(kBlock), 0, s, a, b, wd));
     }
     return hipGetLastError();
 }

@@ -353,3 +353,28 @@ def test_deferred_round_fold(oracle, monkeypatch, env, stop):
         assert got == ref["stats"]
         assert np.array_equal(e.read_seen(), ref["seen"])
         assert np.array_equal(e.coverage(), ref["coverage"])
+
+
+@pytest.mark.parametrize("tiny", ["1", "0"])
+@pytest.mark.parametrize("idx,n,max_rounds", [(1, None, 0), (1, 40, 0), (1, 40, 20), (2, 4096, 0), (3, 2048, 0),
+                                               (5, 4096, 0), (5, 6000, 7), (5, 6000, 0)])
+def test_small_overlay_one_launch_matches_oracle(oracle, monkeypatch, tiny, idx, n, max_rounds):
+    """Small overlays (<= 65,536 peers and edges) run whole in one launch
+    (gossip_tiny.hip: kills, churn, liveness with reports and registry,
+    injection, push, stats and termination on the device); GOSSIP_TINY=0 runs
+    them round by round.  Both give the oracle's every round, seen set,
+    coverage, reports, alive flags and registry, also when max_rounds cuts the
+    run short; a second run from reset repeats the first."""
+    monkeypatch.setenv("GOSSIP_TINY", tiny)
+    w = config(idx, n, pick=oracle.pick_origins)
+    kw = {"max_rounds": max_rounds} if max_rounds else {}
+    rp, col = oracle.gen_workload(w)
+    ref = oracle.simulate_workload(w, rp, col, **kw)
+    with _engine(w, **kw) as e:
+        e.build_graph()
+        e.inject(w.origins, w.inject_rounds)
+        if w.kills:
+            e.schedule_kills([k[0] for k in w.kills], [k[1] for k in w.kills])
+        for _ in range(2):
+            e.reset()
+            _compare(e, ref, w)
