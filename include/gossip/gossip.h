@@ -67,7 +67,7 @@ typedef struct gossip_config {
     int32_t device;           /* HIP device ordinal; -1 = current */
     uint32_t flags;           /* GOSSIP_FLAG_* */
     uint64_t report_capacity; /* dead-node report buffer entries (0 = default) */
-    uint32_t pull_permille;   /* pull when the frontier estimate >= this per-mille of the owned peers (0 = 50) */
+    uint32_t pull_permille;   /* pull when the frontier estimate >= this per-mille of the owned peers (0 = 60) */
     uint32_t front_permille;  /* pull rounds probe a frontier bitmap below this per-mille (0 = 400; 1000 = always) */
     uint32_t bin_permille;    /* a dense round runs binned while the (peer, message) pairs still missing are
                                  >= this per-mille of the owned peers (0 = default) */

@@ -69,7 +69,7 @@ struct DistDriver {
     std::vector<uint64_t> part;
     uint64_t n = 0, chunk = 0;
     uint32_t X = 1, R = 2;
-    uint32_t pull_pm = 50, sparse_pm = 250, bin_pm = 4000, bin_front_pm = 100;
+    uint32_t pull_pm = kPullPermille, sparse_pm = 250, bin_pm = 4000, bin_front_pm = 100;
     // schedule state, from global stats (identical on every rank)
     uint64_t prev_new = 0, injected = 0, cum_digest = 0, cum_covered = 0;
     bool finished = false;

@@ -157,8 +157,8 @@ struct gossip_ctx {
     uint32_t bin_front_pm = 0;    // binned rounds need a frontier of >= this per-mille (GOSSIP_BIN_FRONT_PM;
                                   // 0: 20 -- see round_begin)
     bool heavy_exit = true;       // k_pull_heavy early exit (GOSSIP_HEAVY_EXIT=0: off, A/B)
-    bool bin_stream = false;      // streamed binned layout (GOSSIP_BIN_STREAM=1; A/B: 1-1.5 ms per binned
-                                  // round slower at config 4)
+    bool bin_stream = false;      // streamed binned layout (chosen in prepare_bins)
+    int bin_stream_req = -1;      // GOSSIP_BIN_STREAM=0/1 forces the layout (A/B); -1: by slot-array size
     uint32_t defer_pm = kDeferAuto;  // push rounds with a frontier of >= this per-mille defer the seen update
                                      // (GOSSIP_DEFER_PM; 0: never; auto: 10 where the fold can be fused)
     bool fold_pending = false;    // a deferred round's receipts (now nw) are not yet in seen: the next
@@ -655,6 +655,11 @@ gossip_status prepare_bins(gossip_ctx* c) {
     free_bins(&c->bins);
     c->bins_ready = false;
     if (!c->symmetric || (c->cfg.flags & GOSSIP_FLAG_NO_BIN) || !c->n_edges) return GOSSIP_OK;
+    // streamed layout while the slot array fits the 256 MB MALL with room to spare: its runs are then
+    // re-read from MALL, not HBM (config 2: 6.59 vs 7.04 ms per step); beyond that the slot layout's
+    // sequential apply wins (config 4: 62.6 vs 64.5 ms, config 3: 6.03 vs 6.88 ms)
+    c->bin_stream = c->bin_stream_req >= 0 ? c->bin_stream_req != 0
+                                           : (uint64_t)c->n_edges * 8ull * c->Wp <= kStreamSlotBytes;
     std::string err;
     const hipError_t e =
         build_bins(c->rp, c->col, c->n_local, c->n, c->n_edges, c->heavy, c->Wp, c->bin_stream, c->stream, &c->bins, &err);
@@ -827,7 +832,7 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
     a.dead_mode = c->any_dead ? 1u : 0u;
     bool pull;
     if (requested == GOSSIP_MODE_AUTO) {
-        const uint32_t permille = c->cfg.pull_permille ? c->cfg.pull_permille : 50;
+        const uint32_t permille = c->cfg.pull_permille ? c->cfg.pull_permille : kPullPermille;
         pull = !remote && pull_ok &&
                ((c->cfg.flags & GOSSIP_FLAG_FORCE_PULL) || (c->frontier_est + cnt) * 1000 >= c->n_local * (uint64_t)permille);
     } else {
@@ -1352,7 +1357,7 @@ gossip_status gossip_create(const gossip_config* cfg, gossip_ctx** out) {
     if (const char* u = std::getenv("GOSSIP_PULL_FIRST2")) c->first_ok = std::atoi(u) != 0;
     if (const char* u = std::getenv("GOSSIP_DEFER_NR")) c->defer_nr = std::atoi(u) != 0;
     if (const char* u = std::getenv("GOSSIP_FLIGHT")) c->flight_ok = std::atoi(u) != 0;
-    if (const char* u = std::getenv("GOSSIP_BIN_STREAM")) c->bin_stream = std::atoi(u) != 0;
+    if (const char* u = std::getenv("GOSSIP_BIN_STREAM")) c->bin_stream_req = std::atoi(u) != 0;
     if (const char* u = std::getenv("GOSSIP_PULL_DIAG")) c->pull_diag = std::atoi(u) != 0;
     if (const char* u = std::getenv("GOSSIP_FULL_LIVENESS"); u && std::atoi(u)) c->full_liveness = true;
     if (const char* u = std::getenv("GOSSIP_OVERLAP_PROBE"); u && std::atoi(u)) c->overlap_probe = true;

@@ -305,6 +305,12 @@ hipError_t launch_tiny_reset(const TinyArgs& t, uint64_t words, uint32_t n_start
 hipError_t launch_tiny_run(const TinyArgs& t, uint32_t Wp, hipStream_t s);
 constexpr uint32_t kTinyPeers = 65536;  // overlays up to this many peers and edges run whole in one launch
 constexpr uint32_t kTinyEdges = 65536;
+// a round pulls (gathers or runs binned) once the frontier reaches this per-mille of the owned peers:
+// a push touches deg x frontier edges with atomics, a binned round streams all of them; measured
+// crossover 6-9 % (config 2: 5.05 %-frontier rounds cost 0.03 ms pushed, 0.13 ms binned)
+constexpr uint32_t kPullPermille = 60;
+// the streamed bin layout is chosen while the slot array (8 B x edges x padded words) is at most this
+constexpr uint64_t kStreamSlotBytes = 128ull << 20;
 
 // ---- overlay generator (gossip_graph.hip) ----
 // Builds the owned rows of the powerlaw overlay on the device.  On success

@@ -61,7 +61,7 @@ def partition(n: int, world: int) -> list[int]:
 
 class PartitionedRun:
     def __init__(self, engine, n: int, rank: int, world: int, device: torch.device, group=None,
-                 pull_permille: int = 50, pull: bool = True, sparse: bool = True, sparse_permille: int = 250,
+                 pull_permille: int = 60, pull: bool = True, sparse: bool = True, sparse_permille: int = 250,
                  bin_permille: int = 4000, bin_front_permille: int = 100):
         self.engine = engine
         self.n, self.rank, self.world = n, rank, world
