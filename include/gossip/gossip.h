@@ -45,6 +45,9 @@ typedef int gossip_status;
 #define GOSSIP_FLAG_FORCE_PULL 4u       /* pull every eligible round (symmetric overlay, nobody dead, P = 1) */
 #define GOSSIP_FLAG_NO_BIN 8u           /* do not lay out the binned edge slots (saves ~(4 + 2 + 8W) B per edge) */
 #define GOSSIP_FLAG_FORCE_BIN 16u       /* every pull-eligible round runs binned (needs the slot layout) */
+#define GOSSIP_FLAG_NO_BLOCKED 32u      /* no propagation-blocked push rounds (saves ~22 B per edge of records) */
+#define GOSSIP_FLAG_FORCE_BLOCKED 64u   /* every push or binned round runs propagation-blocked where it can
+                                           (single partition, one word per peer, slot layout) */
 
 /*
  * Replaces: NetworkConfig's parsed values (config.cpp:31-42,93-96) plus the
@@ -81,6 +84,9 @@ typedef struct gossip_config {
                                   r restarts in r iff philox({seed,v},{7,r,0,0}).x < threshold -- re-registered,
                                   empty Message-List, old connections gone, fresh out-edges from one seed response
                                   into its overflow row (extra_cap > 0).  0 = never.  Single partition only */
+    uint32_t blocked_permille; /* propagation-blocked push (single partition, M <= 64): a push round from a 0.2 %
+                                  frontier estimate, or a binned round below this per-mille, runs blocked
+                                  (0 = 300) */
 } gossip_config;
 
 /*
@@ -190,6 +196,7 @@ gossip_status gossip_run(gossip_ctx* ctx, gossip_round_stats* per_round, uint32_
 #define GOSSIP_MODE_PULL 1
 #define GOSSIP_MODE_PUSH_SPARSE 2 /* push; only touched peers are exchanged (needs gossip_set_sparse) */
 #define GOSSIP_MODE_BIN 3         /* pull semantics (same all-gather), run binned when the slot layout exists */
+#define GOSSIP_MODE_BLOCKED 4     /* push semantics, propagation-blocked (single partition; chosen by the engine) */
 gossip_status gossip_set_exchange(gossip_ctx* ctx, void* send_dev, void* recv_dev, uint32_t world,
                                   const uint64_t* part_begins /* world+1 */);
 gossip_status gossip_set_gather(gossip_ctx* ctx, void* gather_dev);
@@ -282,7 +289,7 @@ gossip_status gossip_read_registered(gossip_ctx* ctx, uint8_t* out);
 /* ---- measurement ----------------------------------------------------------- */
 /* Per-kernel device time (ms) accumulated since timing was last enabled, by kernel name
  * ("push_light", "push_heavy", "pull_light", "pull_heavy", "frontier_bits", "bin_scatter", "bin_apply",
- * "liveness", "churn", "kills", "inject", "apply_remote"),
+ * "pb_scatter", "pb_split", "pb_apply", "liveness", "churn", "kills", "inject", "apply_remote"),
  * measured with HIP events on the ctx stream.  enable != 0 turns timing on. */
 gossip_status gossip_enable_timing(gossip_ctx* ctx, int enable);
 gossip_status gossip_kernel_time(gossip_ctx* ctx, const char* kernel, double* ms, uint64_t* launches);
@@ -294,8 +301,22 @@ gossip_status gossip_kernel_time(gossip_ctx* ctx, const char* kernel, double* ms
  * ("pull_heavy"), 8.125 B per owned peer ("frontier_bits"); binned rounds:
  * 8·Wp B per source word staged + 16 B per frontier peer + 6 B per binned edge
  * + 8·Wp B per slot written ("bin_scatter"), (2 + 8·Wp) B per slot scanned +
- * 16·Wp B per owned peer ("bin_apply"). */
+ * 16·Wp B per owned peer ("bin_apply"); propagation-blocked rounds: 8 B per owned
+ * peer + 24 B per frontier peer + 16 B per traversal ("pb_scatter"), 22 B per
+ * traversal ("pb_split"), 10 B per traversal + 24 B per activated peer
+ * ("pb_apply"). */
 gossip_status gossip_kernel_bytes(gossip_ctx* ctx, const char* kernel, double* bytes);
+
+/* ---- engineering options ---------------------------------------------------- */
+/* Parity-tested A/B variants and layout sizes of one ctx (never read from the
+ * environment; results are identical under every setting).  Keys: "tiny" (0:
+ * small overlays run round by round), "full_liveness" (ping every edge instead
+ * of the closed form), "defer_permille" (-1 auto), "bin_stream" (-1 by size,
+ * 0/1 forced), "pull_first2", "in_flight", "heavy_exit", "heavy_degree",
+ * "heavy_chunk", "bin_front_permille", "bin_words", "bin_chunk", "val_tune"
+ * (-1 auto, 0, 1, 2 = print), "src_stats" (-1 auto, 0/1).  Layout keys apply at
+ * the next gossip_build_graph / gossip_load_csr.  GOSSIP_EINVAL: unknown key. */
+gossip_status gossip_set_tuning(gossip_ctx* ctx, const char* key, int64_t value);
 
 #ifdef __cplusplus
 }

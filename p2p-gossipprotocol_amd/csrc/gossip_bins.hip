@@ -230,13 +230,13 @@ void free_bins(BinState* b) {
     hipFree(b->bdst);
     hipFree(b->val);
     hipFree(b->dummy);
-    hipFree(b->cb_slot);
     hipFree(b->deg);
     *b = BinState{};
 }
 
 hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local, uint64_t n_global, uint64_t m,
-                      uint32_t heavy, uint32_t Wp, bool stream, hipStream_t s, BinState* out, std::string* err) {
+                      uint32_t heavy, uint32_t Wp, bool stream, uint32_t bin_words_req, uint32_t chunk_words_req,
+                      hipStream_t s, BinState* out, std::string* err) {
     hipError_t rc = hipSuccess;
     const uint64_t n_tiles = (n_local + 63) / 64;
     // bigger bins -> longer slot runs per (source chunk, bin) in the scatter
@@ -245,15 +245,9 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
     // idle in the apply; 256 bins of 4 K: kernels 9.2-9.3 -> 7.9 ms per step; config 3 keeps whole bins:
     // 4 K bins cost it 0.5 ms)
     uint32_t bin_words = (uint32_t)std::min<uint64_t>(kBinWords, std::max<uint64_t>(2048, n_local * Wp / 256 / 512 * 512));
-    if (const char* bw = std::getenv("GOSSIP_BIN_WORDS"))
-        bin_words = std::max<uint32_t>(512, std::min<uint32_t>(kBinWords, (uint32_t)std::atoi(bw) / 512 * 512));
-    // split: a bin of up to `split` accumulator-sized parts (destination ids stay below 2^16 in bdst);
-    // the streamed layout keeps one part (its bdst bit 15 flags runs)
-    uint32_t split = 1;
-    if (const char* e = std::getenv("GOSSIP_BIN_SPLIT"); e && !stream)
-        split = std::max<uint32_t>(1, std::min<uint32_t>(65535u / (bin_words / Wp), (uint32_t)std::atoi(e)));
-    const uint32_t max_peers = split * (bin_words / Wp);  // a multiple of 64 for Wp <= 8
-    const uint64_t slot_cap = split * (kBinSlotCap * bin_words / kBinWords);
+    if (bin_words_req) bin_words = std::max<uint32_t>(512, std::min<uint32_t>(kBinWords, bin_words_req / 512 * 512));
+    const uint32_t max_peers = bin_words / Wp;  // a multiple of 64 for Wp <= 8
+    const uint64_t slot_cap = kBinSlotCap * bin_words / kBinWords;
     uint32_t* tile_slots = nullptr;
     unsigned long long* light_bits = nullptr;
     uint32_t* bin_of_tile = nullptr;
@@ -314,8 +308,8 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
         const double want = 32.0 * (double)n_global * (double)n_local / ((double)upos * (double)(bin_words / Wp)) * Wp;
         if (want * 4 <= (double)kBinChunkWords) chunk_words = std::max<uint64_t>(1024, ((uint64_t)want + 511) / 512 * 512);
     }
-    if (const char* c = std::getenv("GOSSIP_BIN_CHUNK"))
-        chunk_words = std::max<uint64_t>(512, std::min<uint64_t>(kBinChunkWords, std::strtoull(c, nullptr, 0) / 512 * 512));
+    if (chunk_words_req)
+        chunk_words = std::max<uint64_t>(512, std::min<uint64_t>(kBinChunkWords, chunk_words_req / 512 * 512));
     chunk = std::max<uint64_t>(64, chunk_words / Wp);
     n_chunks = (n_global + chunk - 1) / chunk;
     if (n_chunks * h_bins.size() >= kNoSlot) {
@@ -366,7 +360,6 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
 
     st.n_bins = h_bins.size();
     st.bin_words = bin_words;
-    st.split = split;
     st.n_slots = slots;
     st.n_binned = upos;
     st.n_chunks = n_chunks;
@@ -444,8 +437,7 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
             BCHECK(hipGetLastError());
         }
         BCHECK(hipStreamSynchronize(s));
-        if (const char* ks = std::getenv("GOSSIP_KEEP_SLOTS"); ks && std::atoi(ks)) st.cb_slot = cb_slot;  // measurement
-        else hipFree(cb_slot);
+        hipFree(cb_slot);
         cb_slot = nullptr;
         // (d) apply side of the streamed layout: runs sorted by first slot (keys_out / vals_out are free again)
         const uint64_t n_groups = (slots + 63) / 64 + 1;
@@ -485,69 +477,15 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
     // row stage consecutive chunks and write adjacent slot runs in every bin
     // at about the same time (adjacent runs can merge in the XCD's L2; with
     // the single-role scatter 36.0 against 39.2 ms per step for capped units
-    // dealt round-robin).  GOSSIP_BIN_UNIT = cap
-    // restores capped units dealt round-robin with no padding (the round-1
-    // layout, A/B only).
+    // dealt round-robin; global rows over all XCDs
+    // measured no better).
     {
         std::vector<uint64_t> cbeg(n_chunks + 1);
         BCHECK(hipMemcpy(cbeg.data(), st.chunk_begin, (n_chunks + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost));
         std::vector<BinUnit> units;
         std::vector<uint64_t> xu(9, 0);
         const uint64_t members = kScatterGrid / 8;
-        if (const char* e = std::getenv("GOSSIP_BIN_UNIT")) {
-            const uint64_t cap = std::max<uint64_t>(1024, std::strtoull(e, nullptr, 0));
-            for (uint64_t c = 0; c < n_chunks; ++c) {
-                const uint64_t len = cbeg[c + 1] - cbeg[c];
-                const uint64_t k = std::max<uint64_t>(1, (len + cap - 1) / cap);
-                for (uint64_t j = 0; j < k; ++j)
-                    units.push_back(
-                        BinUnit{(uint32_t)c, j == 0 ? 1u : 0u, cbeg[c] + len * j / k, cbeg[c] + len * (j + 1) / k});
-            }
-            xu.assign(9, units.size());
-            xu[0] = 0;
-            uint64_t acc = 0;
-            int x = 1;
-            for (uint64_t i = 0; i < units.size() && x < 8; ++i) {
-                acc += units[i].p1 - units[i].p0;
-                while (x < 8 && acc * 8 >= upos * (uint64_t)x) xu[x++] = i + 1;
-            }
-        } else if (const char* g = std::getenv("GOSSIP_BIN_ROWS"); g && std::atoi(g)) {
-            // global rows (A/B): hub chunks first, cut into units of about the mean and dealt
-            // round-robin over the XCDs; then rows of kScatterGrid consecutive chunks, XCD x taking
-            // chunks [32 x, 32 x + 32) of every row -- so the whole chip writes one contiguous region
-            // of every bin at about the same time
-            const uint64_t mean = std::max<uint64_t>(1024, upos / std::max<uint64_t>(1, n_chunks));
-            std::vector<std::vector<BinUnit>> per(8);
-            std::vector<uint32_t> reg;
-            uint64_t h = 0;
-            for (uint64_t c = 0; c < n_chunks; ++c) {
-                const uint64_t len = cbeg[c + 1] - cbeg[c];
-                if (len > kHubFactor * mean) {
-                    const uint64_t k = (len + mean - 1) / mean;
-                    for (uint64_t j = 0; j < k; ++j, ++h)
-                        per[h % 8].push_back(
-                            BinUnit{(uint32_t)c, j == 0 ? 1u : 0u, cbeg[c] + len * j / k, cbeg[c] + len * (j + 1) / k});
-                } else {
-                    reg.push_back((uint32_t)c);
-                }
-            }
-            for (auto& v : per)
-                while (v.size() % members) v.push_back(BinUnit{0u, 0u, 0, 0});
-            for (uint64_t r0 = 0; r0 < reg.size(); r0 += 8 * members)
-                for (int x = 0; x < 8; ++x)
-                    for (uint64_t j = 0; j < members; ++j) {
-                        const uint64_t i = r0 + x * members + j;
-                        if (i < reg.size())
-                            per[x].push_back(BinUnit{reg[i], 1u, cbeg[reg[i]], cbeg[reg[i] + 1]});
-                        else
-                            per[x].push_back(BinUnit{0u, 0u, 0, 0});
-                    }
-            for (int x = 0; x < 8; ++x) {
-                xu[x] = units.size();
-                units.insert(units.end(), per[x].begin(), per[x].end());
-            }
-            xu[8] = units.size();
-        } else {
+        {
             const uint64_t mean = std::max<uint64_t>(1024, upos / std::max<uint64_t>(1, n_chunks));
             uint64_t c = 0, acc = 0;
             for (int x = 0; x < 8; ++x) {

@@ -1,0 +1,122 @@
+// gossip_device.hpp -- device helpers shared by the round kernels of libgossip_hip
+// (gossip_kernels.hip, gossip_blocked.hip): stat accumulation and its block flush,
+// the bits a peer can still learn, wave reductions.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "gossip_internal.hpp"
+
+namespace gossip {
+namespace {
+
+constexpr int kWavesPerBlock = kBlock / 64;
+constexpr unsigned kMaxGrid = 2048;  // 256 CUs x 8 blocks of 256 threads
+
+__device__ __forceinline__ bool bit_alive(const uint32_t* bits, uint32_t v) { return (bits[v >> 5] >> (v & 31)) & 1u; }
+
+// the bits a peer can still learn: messages injected so far (at P = 1 the ones whose origin was alive to
+// inject them -- a never-injected message kept every row of config 5 scanning to its end)
+__device__ __forceinline__ uint64_t injm_full(const RoundArgs& a, int w) {
+    return a.inj_live ? a.inj_mask[w] & a.inj_live[w] : a.inj_mask[w];
+}
+// ... and of those, this round: only bits that are in some new word (P = 1: in_flight, the previous
+// round's receipts with this round's injections -- a bit outside it kept config 5's hubs and needy
+// rows scanning to their ends: a message injected at an isolated peer is never in flight)
+__device__ __forceinline__ uint64_t injm(const RoundArgs& a, int w) {
+    return injm_full(a, w) & (a.use_flight ? a.in_flight[w] : ~0ull);
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+    return x;
+}
+
+__device__ __forceinline__ uint32_t lane_rank(unsigned long long mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
+
+struct Acc {
+    unsigned long long frontier = 0, trav = 0, deliv = 0, undeliv = 0, fresh = 0, digest = 0, covered = 0, died = 0,
+                       reports = 0, removals = 0, injected = 0, htrav = 0, checked = 0,
+                       activated = 0, pulled = 0, gathered = 0, reconnects = 0, rejoined = 0, atomics = 0,
+                       diag = 0, dead_cov = 0;
+    unsigned long long fresh_or[kMaxWords] = {};  // OR of the receipts (only the words a kernel touches stay)
+};
+
+// Block-level flush: wave sums -> LDS -> one atomic per nonzero field per
+// block, into stat line blockIdx % kStatLines of the round.  Same-line device
+// atomics serialise (~9 ns each measured); one line per round hit by every
+// wave cost ~0.65 ms per pull round at 2^20 peers.  Must be reached by every
+// wave of the block (it holds a barrier).
+// flush_into: the same with caller-provided LDS scratch (kWaves * kStatFields words).
+template <int kWaves>
+__device__ __forceinline__ void flush_into(Acc& acc, DevStats* st, unsigned long long (*red)[kStatFields]);
+
+template <int kWaves = kWavesPerBlock>
+__device__ __forceinline__ void flush(Acc& acc, DevStats* st) {
+    __shared__ unsigned long long red[kWaves][kStatFields];
+    flush_into<kWaves>(acc, st, red);
+}
+
+template <int kWaves>
+__device__ __forceinline__ void flush_into(Acc& acc, DevStats* st, unsigned long long (*red)[kStatFields]) {
+    constexpr int kF = kStatFields;
+    static_assert(sizeof(DevStats) == kF * 8, "one u64 per stat field");
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // DevStats field order
+    const unsigned long long v[kF] = {acc.frontier, acc.trav,     acc.deliv,   acc.undeliv, acc.fresh,  acc.injected,
+                                      acc.died,     acc.reports,  acc.removals, acc.digest, acc.covered, acc.htrav,
+                                      acc.checked,  acc.activated, acc.pulled,  acc.gathered, acc.reconnects,
+                                      acc.rejoined, acc.atomics, acc.diag, acc.dead_cov,
+                                      acc.fresh_or[0], acc.fresh_or[1], acc.fresh_or[2], acc.fresh_or[3],
+                                      acc.fresh_or[4], acc.fresh_or[5], acc.fresh_or[6], acc.fresh_or[7]};
+#pragma unroll
+    for (int f = 0; f < kF; ++f) {
+        unsigned long long s_ = v[f];
+        if (f < kStatSums) {
+            s_ = wave_sum(s_);
+        } else {
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) s_ |= __shfl_xor(s_, off);
+        }
+        if (lane == 0) red[wave][f] = s_;
+    }
+    __syncthreads();
+    if (threadIdx.x < kF) {
+        unsigned long long s_ = 0;
+        const bool sum = threadIdx.x < kStatSums;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) s_ = sum ? s_ + red[w][threadIdx.x] : s_ | red[w][threadIdx.x];
+        unsigned long long* f = reinterpret_cast<unsigned long long*>(st + blockIdx.x % kStatLines) + threadIdx.x;
+        if (s_) {
+            if (sum) atomicAdd(f, s_);
+            else atomicOr(f, s_);
+        }
+    }
+}
+
+// Source lane of edge position p within a tile: the number of rows whose
+// inclusive end is <= p (incl = in-wave inclusive scan of row lengths).
+__device__ __forceinline__ int src_lane(uint32_t incl, uint32_t p) {
+    int s = 0;
+#pragma unroll
+    for (int step = 32; step > 0; step >>= 1) {
+        const uint32_t val = __shfl(incl, s + step - 1);
+        if (val <= p) s += step;
+    }
+    return s;
+}
+
+unsigned grid_for(uint64_t items, uint64_t per_block) {
+    uint64_t g = (items + per_block - 1) / per_block;
+    if (g < 1) g = 1;
+    if (g > kMaxGrid) g = kMaxGrid;
+    return (unsigned)g;
+}
+
+}  // namespace
+}  // namespace gossip

@@ -149,43 +149,42 @@ struct gossip_ctx {
     unsigned long long* rj_n = nullptr;   // their count
     BinState bins;               // binned dense rounds: slot layout (gossip_bins.hip)
     bool bins_ready = false;
+    PbState pb;                  // propagation-blocked push rounds: record regions (gossip_blocked.hip)
+    bool pb_ready = false;
+    bool cur_pb = false;         // the round in flight runs propagation-blocked
     bool last_bin = false;       // the pull round in flight runs binned
     uint64_t last_fresh = 0;     // new receipts of the previous round
     bool bins_first = false;             // no binned round since the last reset: rewrite every slot
-    bool bin_noskip = false;     // GOSSIP_BIN_NOSKIP: rewrite every slot each binned round (A/B measurement)
-    uint32_t scatter_probe = 0;  // GOSSIP_SCATTER_PROBE: partial scatter for timing breakdowns (wrong results)
-    uint32_t bin_front_pm = 0;    // binned rounds need a frontier of >= this per-mille (GOSSIP_BIN_FRONT_PM;
-                                  // 0: 20 -- see round_begin)
-    bool heavy_exit = true;       // k_pull_heavy early exit (GOSSIP_HEAVY_EXIT=0: off, A/B)
+    // engineering options (gossip_set_tuning; A/B variants that are parity-tested, and layout sizes)
+    uint32_t bin_front_pm = 0;    // "bin_front_permille": binned rounds need a frontier of >= this per-mille
+                                  // (0: 20 -- see round_begin)
+    bool heavy_exit = true;       // "heavy_exit": k_pull_heavy's early exit
+    uint32_t heavy_chunk = 0;     // "heavy_chunk": edges per heavy chunk (0: by overlay size)
+    uint32_t bin_words_req = 0;   // "bin_words" / "bin_chunk": LDS words of a bin / a source chunk (0: by size)
+    uint32_t bin_chunk_req = 0;
+    int val_tune = -1;            // "val_tune": pick the slot array's allocation by trial scatters (-1: by size,
+                                  // 0: never, 1: always, 2: and print the trials)
+    int src_stats_req = -1;       // "src_stats": who books a binned round's source side (-1: by layout)
     bool bin_stream = false;      // streamed binned layout (chosen in prepare_bins)
-    int bin_stream_req = -1;      // GOSSIP_BIN_STREAM=0/1 forces the layout (A/B); -1: by slot-array size
-    uint32_t defer_pm = kDeferAuto;  // push rounds with a frontier of >= this per-mille defer the seen update
-                                     // (GOSSIP_DEFER_PM; 0: never; auto: 10 where the fold can be fused)
+    int bin_stream_req = -1;      // "bin_stream": 0/1 forces the layout; -1: by slot-array size
+    uint32_t defer_pm = kDeferAuto;  // "defer_permille": push rounds with a frontier of >= this per-mille defer
+                                     // the seen update (0: never; auto: 10 where the fold can be fused)
     bool fold_pending = false;    // a deferred round's receipts (now nw) are not yet in seen: the next
                                   // binned round's apply or row-pull sweep folds them in, anything else
                                   // commits first
-    bool cur_pdefer = false;      // this (wide) pull round stores only nx for the rows that learn
-    bool defer_nr = false;        // GOSSIP_DEFER_NR=1: deferred push rounds issue no-return atomics and count
-                                  // the receipts from nx afterwards (A/B, config 4 round 3: push 4.29-4.37 +
-                                  // 0.40 ms count against 4.05-4.38 ms -- the atomics are memory-side bound)
-    bool first_ok = true;         // GOSSIP_PULL_FIRST2=0: k_pull_rows loads every col entry (A/B)
-    bool flight_ok = true;        // GOSSIP_FLIGHT=0: needy tests ignore which bits are in flight (A/B)
+    bool first_ok = true;         // "pull_first2": k_pull_rows carries a row's first two entries
+    bool flight_ok = true;        // "in_flight": needy tests wait only for bits that are in flight
     uint64_t flight[kMaxWords] = {};  // receipts of round flight_round (from its stats)
     uint32_t flight_round = ~0u;
     uint32_t dgone_next = 0;      // first round whose deaths dgone does not count yet
-    bool pdefer_ok = false;       // GOSSIP_PULL_DEFER=1: defer wide pull rounds (A/B: config 4 round 7 -0.3 to
-                                  // -0.75 ms, round 8's fold +0.5 to +0.7 ms, so off by default)
-    bool pull_diag = false;       // GOSSIP_PULL_DIAG: count the gathers of an early-exit row scan (measurement)
     bool cur_defer = false;       // this round defers: advance() folds nx into seen
-    bool overlap_probe = false;  // GOSSIP_OVERLAP_PROBE: measurement only (overlap_probe)
-    bool full_liveness = false;  // GOSSIP_FULL_LIVENESS: ping every edge each ping round (A/B against closed form)
+    bool full_liveness = false;  // "full_liveness": ping every edge each ping round (A/B against closed form)
     uint64_t* seg = nullptr;     // sparse push: per-destination record segments (world x chunk records)
     unsigned long long* d_counts = nullptr;  // records per destination rank
     uint64_t* h_counts = nullptr;            // pinned copy
     bool cur_sparse = false;
     bool send_dirty = false;     // the dense staging buffer holds a dense push round's masks
-    int pull_unroll = 2;         // 64-edge batches in flight per wave in pull_light (GOSSIP_PULL_UNROLL)
-    uint32_t heavy = kHeavyDegree;  // light/heavy row threshold (GOSSIP_HEAVY_DEGREE)
+    uint32_t heavy = kHeavyDegree;  // "heavy_degree": light/heavy row threshold
     uint64_t frontier_est = 0;   // activated peers of the previous round
     std::vector<uint64_t> inj_prefix;  // per sorted injection: cumulative mask words
     uint64_t cum_digest = 0, cum_covered = 0;
@@ -204,7 +203,7 @@ struct gossip_ctx {
     std::vector<hipEvent_t> event_pool;
 
     // small overlays: a whole run in one launch (gossip_tiny.hip)
-    bool tiny_off = false;                 // GOSSIP_TINY=0: round by round (A/B, tests)
+    bool tiny_off = false;                 // "tiny" = 0: round by round (A/B, tests)
     uint32_t* tiny_erow = nullptr;         // per edge: its row
     gossip_round_stats* tiny_out = nullptr;  // device, tiny_cap rounds
     uint32_t tiny_cap = 0;
@@ -378,6 +377,8 @@ void free_graph(gossip_ctx* c) {
     c->tiny_erow = nullptr;
     free_bins(&c->bins);
     c->bins_ready = false;
+    free_pb(&c->pb);
+    c->pb_ready = false;
     hipFree(c->rp);
     hipFree(c->col);
     hipFree(c->chunks);
@@ -469,9 +470,9 @@ gossip_status install_graph(gossip_ctx* c, uint64_t* d_rp, uint32_t* d_col, uint
     HIPCHK(hipMalloc((void**)&d_cnt, 2 * sizeof(unsigned long long)));
     HIPCHK(hipMemsetAsync(d_cnt, 0, 2 * sizeof(unsigned long long), c->stream));
     // heavy chunks: a wave each; on small overlays (cache-resident) a chunk's chain of 64-edge batches, not the
-    // number of chunks, sets k_pull_heavy's time -- shorter chunks there (GOSSIP_HEAVY_CHUNK overrides)
+    // number of chunks, sets k_pull_heavy's time -- shorter chunks there ("heavy_chunk" overrides)
     uint32_t clen = c->n_local < (1ull << 22) ? 256u : kHeavyChunk;
-    if (const char* e = std::getenv("GOSSIP_HEAVY_CHUNK")) clen = std::max(64, std::atoi(e)) / 64 * 64;
+    if (c->heavy_chunk) clen = std::max<uint32_t>(64, c->heavy_chunk) / 64 * 64;
     HIPCHK(launch_heavy_count(c->rp, c->n_local, c->heavy, clen, d_cnt, c->stream));
     unsigned long long nch = 0;
     HIPCHK(hipMemcpyAsync(&nch, d_cnt, sizeof(nch), hipMemcpyDeviceToHost, c->stream));
@@ -481,6 +482,16 @@ gossip_status install_graph(gossip_ctx* c, uint64_t* d_rp, uint32_t* d_col, uint
         HIPCHK(hipMalloc((void**)&c->chunks, nch * sizeof(HeavyChunk)));
         HIPCHK(hipMalloc((void**)&c->hacc, nch * c->Wp * sizeof(uint64_t)));
         HIPCHK(launch_heavy_fill(c->rp, c->n_local, c->heavy, clen, c->chunks, d_cnt + 1, c->stream));
+        // in row order (the fill appends rows in any order): a vertex range's chunks are then contiguous
+        // (blocked push rounds give each workgroup the chunks of its rows); first = the row's first chunk
+        std::vector<HeavyChunk> h(nch);
+        HIPCHK(hipMemcpyAsync(h.data(), c->chunks, nch * sizeof(HeavyChunk), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        std::sort(h.begin(), h.end(), [](const HeavyChunk& x, const HeavyChunk& y) {
+            return x.v != y.v ? x.v < y.v : x.e0 < y.e0;
+        });
+        for (uint64_t i = 0; i < nch; ++i) h[i].first = i && h[i - 1].v == h[i].v ? h[i - 1].first : (uint32_t)i;
+        HIPCHK(hipMemcpyAsync(c->chunks, h.data(), nch * sizeof(HeavyChunk), hipMemcpyHostToDevice, c->stream));
     }
     HIPCHK(hipStreamSynchronize(c->stream));
     hipFree(d_cnt);
@@ -581,14 +592,21 @@ gossip_status upload_csr(gossip_ctx* c, const uint64_t* rp, const uint32_t* col,
 // sequential read of the same array) at 5.0-5.8 in all, and a physically contiguous array at 14 ms.
 // Allocations in one process differ too (trial scatters of 9.3 / 10.3 / 8.8 ms), though some processes
 // get only slow ones.  On big layouts, time one full scatter (every slot rewritten) into each of four
-// allocations and keep the fastest (GOSSIP_VAL_TUNE=0: keep the first; 2: print the trials); config 4,
+// allocations and keep the fastest ("val_tune" 0: keep the first; 2: print the trials); config 4,
 // five processes each: scatter 9.3-11.3 (mean 9.9) against 9.7-11.7 (mean 10.4) ms.  The trial words
 // are garbage: the first binned round rewrites every slot.
+BinArgs bin_args(const gossip_ctx* c, bool noskip, uint32_t src_side) {
+    const BinState& s = c->bins;
+    return BinArgs{s.bins,      s.n_bins,   s.cb_src,    s.cb_run,   s.cb_grp,   s.n_binned, s.chunk_begin,
+                   s.n_chunks,  s.chunk,    s.units,     s.xcd_units, s.bdst,    s.val,      s.bin_words,
+                   s.dummy,     noskip ? 1u : 0u, s.n_runs ? s.n_runs - 1 : 0, s.ap_run, s.ap_grp,
+                   c->bin_stream ? 1u : 0u, s.deg, src_side};
+}
+
 gossip_status tune_val(gossip_ctx* c) {
-    const char* env = std::getenv("GOSSIP_VAL_TUNE");
     // single partition only: a vertex block's scatter stages global source chunks from the all-gathered
     // words, which do not exist at bootstrap (the trial launch read past the block's own words)
-    if ((env && !std::atoi(env)) || c->bin_stream || c->bins.n_slots < (1ull << 26) || c->n_local != c->n)
+    if (c->val_tune == 0 || c->bin_stream || c->n_local != c->n || (c->val_tune < 0 && c->bins.n_slots < (1ull << 26)))
         return GOSSIP_OK;
     const uint64_t bytes = (c->bins.n_slots + 64) * c->Wp * sizeof(uint64_t);
     constexpr int kCand = 4;
@@ -604,11 +622,7 @@ gossip_status tune_val(gossip_ctx* c) {
     a.defer = 0;
     a.fold = 0;
     a.tcur = a.tnx = nullptr;
-    BinArgs b{c->bins.bins,     c->bins.n_bins,    c->bins.cb_src,  c->bins.cb_run,    c->bins.cb_grp,
-              c->bins.n_binned, c->bins.chunk_begin, c->bins.n_chunks, c->bins.chunk,    c->bins.units,
-              c->bins.xcd_units, c->bins.bdst,     c->bins.val,     c->bins.bin_words, c->bins.dummy,   1u,
-              0u,               c->bins.n_runs ? c->bins.n_runs - 1 : 0, c->bins.ap_run, c->bins.ap_grp,
-              0u,               c->bins.cb_slot,   c->bins.split, c->bins.deg, 1u};
+    BinArgs b = bin_args(c, true, 1u);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     float best = 0.f;
     int bi = 0;
@@ -636,7 +650,7 @@ gossip_status tune_val(gossip_ctx* c) {
             if (err == hipSuccess) err = hipEventElapsedTime(&ms, e0, e1);
         }
         if (err != hipSuccess) break;
-        if (env && std::atoi(env) == 2) fprintf(stderr, "tune_val: candidate %d %.3f ms\n", k, ms);
+        if (c->val_tune == 2) fprintf(stderr, "tune_val: candidate %d %.3f ms\n", k, ms);
         if (k == 0 || ms < best) {
             best = ms;
             bi = k;
@@ -648,25 +662,47 @@ gossip_status tune_val(gossip_ctx* c) {
     return GOSSIP_OK;
 }
 
+// Record segments of propagation-blocked push rounds: one partition, one word per peer, no overflow rows
+// (re-bootstrap and rejoin edges are not in the CSR the segments are counted from); skipped, not failed,
+// when they do not fit.
+gossip_status prepare_pb(gossip_ctx* c) {
+    if (c->Wp != 1 || c->n_local != c->n || (c->cfg.flags & GOSSIP_FLAG_NO_BLOCKED) || c->cfg.extra_cap ||
+        c->cfg.rejoin_threshold || !c->n_edges)
+        return GOSSIP_OK;
+    std::string err;
+    const hipError_t e = build_pb(c->rp, c->col, c->n_local, c->n_edges, c->heavy, c->chunks, c->n_chunks,
+                                  c->stream, &c->pb, &err);
+    if (e == hipErrorOutOfMemory || e == hipErrorInvalidValue) return GOSSIP_OK;  // push rounds stay atomic
+    if (e != hipSuccess) return fail(GOSSIP_EHIP, "blocked-push regions: " + err);
+    c->pb_ready = true;
+    return GOSSIP_OK;
+}
+
 // Slot layout for binned dense rounds: only for a full, symmetric overlay
 // (pull-eligible); skipped, not failed, when it does not fit in HBM.
 gossip_status prepare_bins(gossip_ctx* c) {
     c->bins_first = false;  // a fresh layout holds zeros
     free_bins(&c->bins);
     c->bins_ready = false;
-    if (!c->symmetric || (c->cfg.flags & GOSSIP_FLAG_NO_BIN) || !c->n_edges) return GOSSIP_OK;
-    // streamed layout while the slot array fits the 256 MB MALL with room to spare: its runs are then
-    // re-read from MALL, not HBM (config 2: 6.59 vs 7.04 ms per step); beyond that the slot layout's
-    // sequential apply wins (config 4: 62.6 vs 64.5 ms, config 3: 6.03 vs 6.88 ms)
-    c->bin_stream = c->bin_stream_req >= 0 ? c->bin_stream_req != 0
-                                           : (uint64_t)c->n_edges * 8ull * c->Wp <= kStreamSlotBytes;
-    std::string err;
-    const hipError_t e =
-        build_bins(c->rp, c->col, c->n_local, c->n, c->n_edges, c->heavy, c->Wp, c->bin_stream, c->stream, &c->bins, &err);
-    if (e == hipErrorOutOfMemory || e == hipErrorInvalidValue) return GOSSIP_OK;  // dense rounds gather instead
-    if (e != hipSuccess) return fail(GOSSIP_EHIP, "bin layout: " + err);
-    c->bins_ready = true;
-    return tune_val(c);
+    free_pb(&c->pb);
+    c->pb_ready = false;
+    if (c->symmetric && !(c->cfg.flags & GOSSIP_FLAG_NO_BIN) && c->n_edges) {
+        // streamed layout while the slot array fits the 256 MB MALL with room to spare: its runs are then
+        // re-read from MALL, not HBM (config 2: 6.59 vs 7.04 ms per step); beyond that the slot layout's
+        // sequential apply wins (config 4: 62.6 vs 64.5 ms, config 3: 6.03 vs 6.88 ms)
+        c->bin_stream = c->bin_stream_req >= 0 ? c->bin_stream_req != 0
+                                               : (uint64_t)c->n_edges * 8ull * c->Wp <= kStreamSlotBytes;
+        std::string err;
+        const hipError_t e = build_bins(c->rp, c->col, c->n_local, c->n, c->n_edges, c->heavy, c->Wp, c->bin_stream,
+                                        c->bin_words_req, c->bin_chunk_req, c->stream, &c->bins, &err);
+        if (e == hipSuccess) {
+            c->bins_ready = true;
+            if (gossip_status ts = tune_val(c)) return ts;
+        } else if (e != hipErrorOutOfMemory && e != hipErrorInvalidValue) {  // else dense rounds gather instead
+            return fail(GOSSIP_EHIP, "bin layout: " + err);
+        }
+    }
+    return prepare_pb(c);
 }
 
 // seen |= nw for a deferred round whose fold was left to the next binned round
@@ -876,6 +912,22 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
                   (c->frontier_est + cnt) * 1000 >= c->n_local * (uint64_t)front_pm;
         }
     }
+    // propagation-blocked push (gossip_blocked.hip; one partition, one word per peer): a push round from a
+    // 0.2 % frontier estimate -- below it the atomic push's few deliveries cost less than the blocked
+    // round's sweeps -- and a binned round below blocked_permille (every edge streamed for a minority of
+    // active sources) write one record per delivery instead
+    c->cur_pb = false;
+    if (c->pb_ready && !remote && c->world <= 1 && requested == GOSSIP_MODE_AUTO &&
+        !(c->cfg.flags & (GOSSIP_FLAG_FORCE_PUSH | GOSSIP_FLAG_FORCE_PULL | GOSSIP_FLAG_FORCE_BIN))) {
+        const uint64_t front = c->frontier_est + cnt;
+        const uint32_t hi = c->cfg.blocked_permille ? c->cfg.blocked_permille : kPbHiPermille;
+        if (c->cfg.flags & GOSSIP_FLAG_FORCE_BLOCKED)
+            c->cur_pb = !pull || bin;
+        else
+            c->cur_pb = (!pull && front * 1000 >= c->n_local * (uint64_t)kPbLoPermille) ||
+                        (bin && front * 1000 < c->n_local * (uint64_t)hi);
+        if (c->cur_pb) pull = bin = false;
+    }
     c->cur_sparse = !pull && remote && requested == GOSSIP_MODE_PUSH_SPARSE && c->seg != nullptr;
     // a wide push round (the explosion before the dense rounds) is bound by memory-side atomics, two per
     // fresh delivery (seen, then nx); deferring the seen update halves them for one streamed pass
@@ -885,10 +937,10 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
     const bool fusable = c->world <= 1 && !remote && c->bins_ready && !c->cfg.churn_threshold &&
                          !c->cfg.rejoin_threshold && requested == GOSSIP_MODE_AUTO;
     const uint32_t dpm = c->defer_pm == kDeferAuto ? (fusable ? 10u : 0u) : c->defer_pm;
-    c->cur_defer = !pull && dpm && (c->frontier_est + cnt) * 1000 >= c->n_local * (uint64_t)dpm;
+    c->cur_defer = !pull && !c->cur_pb && dpm && (c->frontier_est + cnt) * 1000 >= c->n_local * (uint64_t)dpm;
     // no-return atomics (the receipts counted from nx after the round) unless tile marks need the old words
-    a.defer = c->cur_defer ? (c->defer_nr && !remote && c->world <= 1 && !a.tnx ? 2u : 1u) : 0u;
-    const bool rows_pull = pull && !bin && (c->pull_unroll & kPullRows) && !c->pull_diag;  // k_pull_rows
+    a.defer = c->cur_defer ? 1u : 0u;
+    const bool rows_pull = pull && !bin;  // k_pull_rows
     if (c->fold_pending) {  // the previous round deferred: its receipts are this round's nw
         if ((bin || rows_pull) && c->world <= 1 && !remote) {
             a.fold = 1;  // k_bin_apply / k_pull_rows's sweep folds them (before k_pull_heavy reads seen)
@@ -897,13 +949,6 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
             return fs;
         }
     }
-    // a wide pull round whose rows learn a lot (config 4 round 7: 90 M rows) stores each learning row's
-    // seen word at random; deferred (GOSSIP_PULL_DEFER=1), the next round (dense: pull or binned) folds
-    // nx into seen in its sweep or apply.  Only while the frontier is wide (>= 40 %) and >= 1 pair per
-    // 4 peers is still missing.  Measured even (the fold's stores cost what the row stores did).
-    c->cur_pdefer = rows_pull && c->world <= 1 && !remote && !c->any_dead && requested == GOSSIP_MODE_AUTO &&
-                    c->pdefer_ok && (c->frontier_est + cnt) * 1000 >= c->n_local * 400ull && missing * 4 >= c->n_local;
-    a.pdefer = c->cur_pdefer ? 1u : 0u;
     // a row's first step from its queue entry: worth the extra 8 B per swept peer while many rows are
     // needy (config 4 round 7: 90 M rows, one random col line each); rows are unmasked (no liveness yet)
     a.first2 = rows_pull && c->first_ok && !c->any_masked && missing * 4 >= c->n_local ? c->first2 : nullptr;
@@ -958,63 +1003,16 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
         if (remote && !c->cur_sparse) c->send_dirty = true;
         if (c->cur_sparse) HIPCHK(hipMemsetAsync(c->d_counts, 0, c->world * sizeof(unsigned long long), c->stream));
     }
+    if (c->cur_pb) a.tsparse = 0;  // the blocked round sweeps every tile (round_compute clears the marks)
     c->cur = a;
     c->cur_remote = remote;
     c->in_round = true;
-    if (mode) *mode = bin ? GOSSIP_MODE_BIN : pull ? GOSSIP_MODE_PULL : c->cur_sparse ? GOSSIP_MODE_PUSH_SPARSE : GOSSIP_MODE_PUSH;
-    return GOSSIP_OK;
-}
-
-// Measurement only (GOSSIP_OVERLAP_PROBE=1): can one binned round's slot stores share HBM with the slot
-// reads of another?  On copies of seen / nx / the stats, times the scatter on all CUs, the apply, the
-// scatter on half the CUs, and that half scatter concurrently with the apply on a second stream (the
-// apply then reads slots being rewritten: timing only).  Prints the four times (ms) to stderr.
-gossip_status overlap_probe(gossip_ctx* c, RoundArgs a, const BinArgs& b, uint32_t pw) {
-    static hipStream_t s2 = nullptr;
-    static uint64_t *seen2 = nullptr, *nx2 = nullptr;
-    static DevStats* st2 = nullptr;
-    static hipEvent_t ev[9];
-    const size_t words = c->n_local * c->Wp * sizeof(uint64_t);
-    if (!s2) {
-        HIPCHK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
-        HIPCHK(hipMalloc((void**)&seen2, words));
-        HIPCHK(hipMalloc((void**)&nx2, words));
-        HIPCHK(hipMalloc((void**)&st2, kStatLines * sizeof(DevStats)));
-        for (auto& e : ev) HIPCHK(hipEventCreate(&e));
-    }
-    a.st = st2;
-    a.cov = nullptr;
-    a.seen = seen2;
-    a.nx = nx2;
-    hipStream_t s = c->stream;
-    HIPCHK(hipEventRecord(ev[0], s));
-    HIPCHK(launch_bin_scatter(a, b, pw, s));
-    HIPCHK(hipEventRecord(ev[1], s));
-    HIPCHK(hipMemcpyAsync(seen2, c->seen, words, hipMemcpyDeviceToDevice, s));
-    HIPCHK(hipEventRecord(ev[2], s));
-    HIPCHK(launch_bin_apply(a, b, pw, s));
-    HIPCHK(hipEventRecord(ev[3], s));
-    g_scatter_grid_probe = 128;
-    HIPCHK(hipEventRecord(ev[4], s));
-    HIPCHK(launch_bin_scatter(a, b, pw, s));
-    HIPCHK(hipEventRecord(ev[5], s));
-    HIPCHK(hipMemcpyAsync(seen2, c->seen, words, hipMemcpyDeviceToDevice, s));
-    HIPCHK(hipEventRecord(ev[6], s));
-    HIPCHK(hipStreamWaitEvent(s2, ev[6], 0));
-    HIPCHK(launch_bin_scatter(a, b, pw, s));
-    HIPCHK(launch_bin_apply(a, b, pw, s2));
-    HIPCHK(hipEventRecord(ev[8], s2));
-    HIPCHK(hipStreamWaitEvent(s, ev[8], 0));
-    HIPCHK(hipEventRecord(ev[7], s));
-    g_scatter_grid_probe = 0;
-    HIPCHK(hipEventSynchronize(ev[7]));
-    float t[4];
-    HIPCHK(hipEventElapsedTime(&t[0], ev[0], ev[1]));
-    HIPCHK(hipEventElapsedTime(&t[1], ev[2], ev[3]));
-    HIPCHK(hipEventElapsedTime(&t[2], ev[4], ev[5]));
-    HIPCHK(hipEventElapsedTime(&t[3], ev[6], ev[7]));
-    fprintf(stderr, "overlap_probe round %u: scatter %.3f apply %.3f | half scatter %.3f | half scatter || apply %.3f ms\n",
-            c->round, t[0], t[1], t[2], t[3]);
+    if (mode)
+        *mode = bin ? GOSSIP_MODE_BIN
+                : pull ? GOSSIP_MODE_PULL
+                : c->cur_pb ? GOSSIP_MODE_BLOCKED
+                : c->cur_sparse ? GOSSIP_MODE_PUSH_SPARSE
+                : GOSSIP_MODE_PUSH;
     return GOSSIP_OK;
 }
 
@@ -1116,13 +1114,9 @@ gossip_status tiny_run(gossip_ctx* c, gossip_round_stats* per_round, uint32_t ca
 }
 
 // Who books the source side of a binned round: the scatter's staging (slot layout) or the apply
-// (streamed layout; GOSSIP_SRC_STATS=0/1 overrides, A/B)
+// (streamed layout; "src_stats" 0/1 overrides)
 uint32_t src_stats(const gossip_ctx* c) {
-    static const int env = [] {
-        const char* e = std::getenv("GOSSIP_SRC_STATS");
-        return e ? std::atoi(e) : -1;
-    }();
-    return env >= 0 ? (uint32_t)(env != 0) : (c->bin_stream ? 0u : 1u);
+    return c->src_stats_req >= 0 ? (uint32_t)(c->src_stats_req != 0) : (c->bin_stream ? 0u : 1u);
 }
 
 // Round phase 2: the push or pull kernels (after the caller's all-gather in a
@@ -1132,19 +1126,22 @@ gossip_status round_compute(gossip_ctx* c) {
     RoundArgs a = c->cur;
     const uint32_t pw = pack_w(c);
     c->in_round = false;
-    TraceRange tr("%s", c->last_bin ? "binned" : c->last_pull ? "pull" : c->cur_sparse ? "push (sparse exchange)" : "push");
+    TraceRange tr("%s", c->last_bin ? "binned" : c->last_pull ? "pull" : c->cur_pb ? "push (blocked)" : c->cur_sparse ? "push (sparse exchange)" : "push");
+    if (c->cur_pb) {
+        PbArgs p = pb_args(c->pb);
+        p.chunks = c->chunks;
+        p.n_chunks = c->n_chunks;
+        p.nw = reinterpret_cast<unsigned long long*>(c->nw);
+        if (a.tcur) HIPCHK(hipMemsetAsync(a.tcur, 0, tact_bytes(c), c->stream));  // unread marks go
+        HIPCHK(timed(c, "pb_scatter", [&] { return launch_pb_scatter(a, p, c->any_dead, c->W, c->stream); }));
+        HIPCHK(timed(c, "pb_split", [&] { return launch_pb_split(p, c->stream); }));
+        HIPCHK(timed(c, "pb_apply", [&] { return launch_pb_apply(a, p, c->stream); }));
+        return GOSSIP_OK;
+    }
     if (c->last_pull && a.dead_mode && !a.dgone)  // else the per-source counters give the source side
         HIPCHK(timed(c, "src_count", [&] { return launch_src_count(a, pw, c->stream); }));
     if (c->last_bin) {
-        BinArgs b{c->bins.bins,     c->bins.n_bins,    c->bins.cb_src,  c->bins.cb_run,    c->bins.cb_grp,
-                  c->bins.n_binned, c->bins.chunk_begin, c->bins.n_chunks, c->bins.chunk,    c->bins.units,
-                  c->bins.xcd_units, c->bins.bdst,     c->bins.val,     c->bins.bin_words, c->bins.dummy,   c->bin_noskip || c->bins_first,
-                  c->scatter_probe,  c->bins.n_runs ? c->bins.n_runs - 1 : 0, c->bins.ap_run, c->bins.ap_grp,
-                  c->bin_stream ? 1u : 0u, c->bins.cb_slot, c->bins.split, c->bins.deg, src_stats(c)};
-        if (c->overlap_probe) {
-            gossip_status ps = overlap_probe(c, a, b, pw);
-            if (ps) return ps;
-        }
+        const BinArgs b = bin_args(c, c->bins_first, src_stats(c));
         HIPCHK(timed(c, "bin_scatter", [&] { return launch_bin_scatter(a, b, pw, c->stream); }));
         HIPCHK(timed(c, "bin_apply", [&] { return launch_bin_apply(a, b, pw, c->stream); }));
         c->bins_first = false;
@@ -1153,9 +1150,8 @@ gossip_status round_compute(gossip_ctx* c) {
     }
     if (c->last_pull) {
         if (a.front) HIPCHK(timed(c, "frontier_bits", [&] { return launch_frontier_bits(a, pw, c->stream); }));
-        if (c->pull_diag) HIPCHK(launch_pull_diag(a, pw, c->stream));
-        // nx is written whole by pull_light; heavy rows are OR-ed in afterwards
-        HIPCHK(timed(c, "pull_light", [&] { return launch_pull_light(a, pw, c->pull_unroll, c->stream); }));
+        // nx is written whole by the light rows' pull; heavy rows are OR-ed in afterwards
+        HIPCHK(timed(c, "pull_light", [&] { return launch_pull_rows(a, pw, c->stream); }));
         HIPCHK(timed(c, "pull_heavy", [&] { return launch_pull_heavy(a, pw, c->stream); }));
         return GOSSIP_OK;
     }
@@ -1165,7 +1161,6 @@ gossip_status round_compute(gossip_ctx* c) {
     HIPCHK(timed(c, "push_heavy", [&] { return launch_push_heavy(a, pw, c->any_dead, remote, c->stream); }));
     if (a.tcur && !a.tsparse) HIPCHK(hipMemsetAsync(a.tcur, 0, tact_bytes(c), c->stream));  // unread marks go
     HIPCHK(timed(c, "push_light", [&] { return launch_push_light(a, pw, c->any_dead, remote, c->stream); }));
-    if (a.defer == 2) HIPCHK(timed(c, "count_nx", [&] { return launch_count_nx(a, pw, c->stream); }));
     if (c->cur_sparse) {
         HIPCHK(timed(c, "compact_send", [&] {
             return launch_compact_send(a, pw, c->part_begins[1], c->d_counts, c->seg, c->stream);
@@ -1180,6 +1175,11 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
         HIPCHK(hipMemcpyAsync(c->h_st, c->st, kStatLines * sizeof(DevStats), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         HIPCHK(hipMemsetAsync(c->st, 0, kStatLines * sizeof(DevStats), c->stream));
+        if (c->cur_pb) {  // a record region that would have overflowed (cannot happen: capacities are in-degrees)
+            uint32_t e = 0;
+            HIPCHK(hipMemcpy(&e, c->pb.err, sizeof(e), hipMemcpyDeviceToHost));
+            if (e) return fail(GOSSIP_EOVERFLOW, "blocked push: a record region overflowed");
+        }
         DevStats sum{};
         const unsigned long long* src = reinterpret_cast<const unsigned long long*>(c->h_st);
         unsigned long long* dst = reinterpret_cast<unsigned long long*>(&sum);
@@ -1213,13 +1213,22 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
             c->kbytes["pull_heavy"] += 12.0 * (double)d.heavy_traversals;
         }
         if (c->last_pull && c->cur.dead_mode) c->kbytes["src_count"] += 32.0 * d.frontier + 4.125 * (double)d.traversals;
+        if (c->cur_pb) {
+            // level 1: the new words swept, the frontier's rows and cleared words, 4 B of col and a 12-B record
+            // per traversal (an upper bound with dead targets); level 2: 12 B read + 10 B written per record;
+            // apply: 10 B per record + the seen read and seen / nx writes of the activated peers
+            const double t = (double)d.traversals;
+            c->kbytes["pb_scatter"] += 8.0 * c->n_local + 24.0 * d.frontier + 16.0 * t;
+            c->kbytes["pb_split"] += 22.0 * t;
+            c->kbytes["pb_apply"] += 10.0 * t + 24.0 * (double)d.activated;
+        }
         if (c->last_bin) {
             // booked above
         } else if (c->last_pull) {
             if (c->last_front) c->kbytes["frontier_bits"] += 8.125 * (c->gather ? c->n : c->n_local);
             c->kbytes["pull_light"] += 40.0 * c->n_local + 4.0 * (double)d.pull_edges + 8.0 * (double)d.pull_gathers;
             c->kbytes["pull_heavy"] += 12.0 * (double)d.heavy_traversals;
-        } else {
+        } else if (!c->cur_pb) {
             c->kbytes["push_light"] += 32.0 * d.frontier + 20.0 * (double)(d.traversals - d.heavy_traversals);
             c->kbytes["push_heavy"] += 20.0 * (double)d.heavy_traversals;
         }
@@ -1267,8 +1276,7 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
 }
 
 gossip_status advance(gossip_ctx* c, uint64_t fresh_global) {
-    bool pend = c->cur_pdefer;  // a deferred pull round: nx, swapped into nw below, is not yet in seen
-    c->cur_pdefer = false;
+    bool pend = false;
     if (c->cur_defer) {  // every delivery of the round is in nx (remote applies included): fold it into seen
         if (c->world <= 1 && c->bins_ready)
             pend = true;  // after the swap, in nw: the next round folds it (settle_fold / k_bin_apply)
@@ -1344,25 +1352,6 @@ gossip_status gossip_create(const gossip_config* cfg, gossip_ctx** out) {
     if (!c->cfg.n_seeds) c->cfg.n_seeds = 20;
     if (!c->cfg.graph_model) c->cfg.graph_model = GOSSIP_GRAPH_POWERLAW;
     c->device = dev;
-    if (const char* u = std::getenv("GOSSIP_PULL_UNROLL")) c->pull_unroll = std::atoi(u);
-    if (const char* u = std::getenv("GOSSIP_PULL_NT"); u && std::atoi(u)) c->pull_unroll |= kPullNT;
-    if (const char* u = std::getenv("GOSSIP_PULL_ROWS"); !u || std::atoi(u)) c->pull_unroll |= kPullRows;
-    if (const char* h = std::getenv("GOSSIP_HEAVY_DEGREE")) c->heavy = (uint32_t)std::max(1, std::atoi(h));
-    if (const char* u = std::getenv("GOSSIP_BIN_NOSKIP"); u && std::atoi(u)) c->bin_noskip = true;
-    if (const char* u = std::getenv("GOSSIP_SCATTER_PROBE")) c->scatter_probe = (uint32_t)std::atoi(u);
-    if (const char* u = std::getenv("GOSSIP_BIN_FRONT_PM")) c->bin_front_pm = (uint32_t)std::atoi(u);
-    if (const char* u = std::getenv("GOSSIP_HEAVY_EXIT")) c->heavy_exit = std::atoi(u) != 0;
-    if (const char* u = std::getenv("GOSSIP_DEFER_PM")) c->defer_pm = (uint32_t)std::atoi(u);
-    if (const char* u = std::getenv("GOSSIP_PULL_DEFER")) c->pdefer_ok = std::atoi(u) != 0;
-    if (const char* u = std::getenv("GOSSIP_PULL_FIRST2")) c->first_ok = std::atoi(u) != 0;
-    if (const char* u = std::getenv("GOSSIP_DEFER_NR")) c->defer_nr = std::atoi(u) != 0;
-    if (const char* u = std::getenv("GOSSIP_FLIGHT")) c->flight_ok = std::atoi(u) != 0;
-    if (const char* u = std::getenv("GOSSIP_BIN_STREAM")) c->bin_stream_req = std::atoi(u) != 0;
-    if (const char* u = std::getenv("GOSSIP_PULL_DIAG")) c->pull_diag = std::atoi(u) != 0;
-    if (const char* u = std::getenv("GOSSIP_FULL_LIVENESS"); u && std::atoi(u)) c->full_liveness = true;
-    if (const char* u = std::getenv("GOSSIP_OVERLAP_PROBE"); u && std::atoi(u)) c->overlap_probe = true;
-    if (const char* u = std::getenv("GOSSIP_TINY"); u && !std::atoi(u)) c->tiny_off = true;
-    if (const char* b = std::getenv("GOSSIP_BIN_PERMILLE"); b && !cfg->bin_permille) c->cfg.bin_permille = (uint32_t)std::atoi(b);
     c->n = cfg->n_peers;
     c->begin = b;
     c->end = e;
@@ -1429,6 +1418,30 @@ gossip_status gossip_create(const gossip_config* cfg, gossip_ctx** out) {
         return fail(rs, m);
     }
     *out = c;
+    return GOSSIP_OK;
+}
+
+// Engineering options (parity-tested A/B variants and layout sizes): explicit per ctx, never read from
+// the environment.  Layout options take effect at the next gossip_build_graph / gossip_load_csr.
+gossip_status gossip_set_tuning(gossip_ctx* c, const char* key, int64_t value) {
+    if (!c || !key) return fail(GOSSIP_EINVAL, "null argument");
+    const std::string k(key);
+    const uint32_t u = value < 0 ? 0u : (uint32_t)std::min<int64_t>(value, 0xFFFFFFFFll);
+    if (k == "tiny") c->tiny_off = value == 0;
+    else if (k == "full_liveness") c->full_liveness = value != 0;
+    else if (k == "defer_permille") c->defer_pm = value < 0 ? kDeferAuto : u;
+    else if (k == "bin_stream") c->bin_stream_req = value < 0 ? -1 : (value != 0);
+    else if (k == "pull_first2") c->first_ok = value != 0;
+    else if (k == "in_flight") c->flight_ok = value != 0;
+    else if (k == "heavy_exit") c->heavy_exit = value != 0;
+    else if (k == "heavy_degree") c->heavy = std::max<uint32_t>(1u, u);
+    else if (k == "heavy_chunk") c->heavy_chunk = u;
+    else if (k == "bin_front_permille") c->bin_front_pm = u;
+    else if (k == "bin_words") c->bin_words_req = u;
+    else if (k == "bin_chunk") c->bin_chunk_req = u;
+    else if (k == "val_tune") c->val_tune = value < 0 ? -1 : (int)std::min<int64_t>(value, 2);
+    else if (k == "src_stats") c->src_stats_req = value < 0 ? -1 : (value != 0);
+    else return fail(GOSSIP_EINVAL, "unknown tuning option: " + k);
     return GOSSIP_OK;
 }
 
@@ -1720,7 +1733,7 @@ gossip_status gossip_reset(gossip_ctx* c) {
     c->nx_dirty = false;
     c->last_pull = false;
     c->last_bin = false;
-    c->cur_defer = c->cur_pdefer = false;
+    c->cur_defer = false;
     c->flight_round = ~0u;
     c->dgone_next = 0;
     c->last_fresh = 0;

@@ -32,8 +32,6 @@ constexpr uint32_t kHeavyChunk = 1024;         // edges per heavy chunk (one wav
 constexpr int kBlock = 256;                    // 4 waves of 64
 constexpr int kMaxWords = 8;                   // M <= 512 concurrent messages
 constexpr int kStatLines = 64;                 // striped DevStats lines per round (summed at read)
-constexpr int kPullNT = 0x100;                 // launch_pull_light unroll flag: non-temporal streamed accesses
-constexpr int kPullRows = 0x200;               // launch_pull_light flag: the row-queue kernel (k_pull_rows)
 constexpr uint32_t kHeavyExitEvery = 4;        // k_pull_heavy checks its early exit every 4 batches of 64 edges
 
 // Per-round device counters (all integer; order-independent sums).
@@ -56,7 +54,7 @@ struct HeavyChunk {
 };
 
 // Binned dense rounds (layout in gossip_bins.hip).
-constexpr uint32_t kBinWords = 18432;       // LDS accumulator words per bin (144 KB; GOSSIP_BIN_WORDS: fewer)
+constexpr uint32_t kBinWords = 18432;       // LDS accumulator words per bin (144 KB; "bin_words": fewer)
 constexpr uint32_t kBinSlotPad = 8;         // bin slot ranges padded to 8 slots (16-B loads)
 constexpr uint64_t kBinSlotCap = 1u << 18;  // slots per bin (load balance between bins)
 constexpr uint32_t kBinChunkWords = 18432;     // source chunk: its new words (144 KB) are staged in LDS
@@ -94,19 +92,13 @@ struct BinArgs {
     uint64_t* val;                // per slot: Wp words, the source's new words of this round
     uint32_t bin_words;           // LDS accumulator words of a bin (kBinWords or kBinWords / 2)
     uint64_t* dummy;              // kScatterGrid * kScatterBlock * Wp words: stores of lanes with no slot
-    uint32_t noskip;              // every slot is rewritten: first binned round after a reset (or GOSSIP_BIN_NOSKIP)
-    uint32_t probe;               // measurement only (GOSSIP_SCATTER_PROBE=1: staging only, 2: slot stores to the
-                                  // sink, 3: stores in cb order; results are then wrong)
+    uint32_t noskip;              // every slot is rewritten: the first binned round after a reset
     uint64_t n_runs_m1;           // cb_run entries - 1 (clamp for the run index of past-the-end lanes)
     // streamed layout (the default): val is in cb order, written front to back by k_bin_stream; the
     // apply walks its bin's slots and finds each value through the run of the slot
     const uint32_t* ap_run;       // per run, in slot order: slot - cb position (as cb_run)
     const uint32_t* ap_grp;       // per 64-slot group: runs that start before the group
     uint32_t stream;              // 1: streamed layout, 0: val in slot order (k_bin_scatter_*)
-    const uint32_t* cb_slot;      // measurement only (GOSSIP_KEEP_SLOTS=1): the slot of every cb entry
-    uint32_t split;               // a bin holds `split` parts of bin_words / Wp peers; its slots (in source
-                                  // order over the whole bin, so the scatter's runs are `split` times longer)
-                                  // are applied by `split` workgroups, each keeping its own part's slots
     const uint32_t* deg;          // per owned peer: its row length (source-side stats booked by the apply)
     uint32_t src_stats;           // 1: the scatter books the source side of the round's pushes (its first
                                   // unit of each chunk, row bounds loaded after the slice); 0: the apply
@@ -131,12 +123,74 @@ struct BinState {
     uint16_t* bdst = nullptr;
     uint64_t* val = nullptr;
     uint64_t* dummy = nullptr;
-    uint32_t* cb_slot = nullptr;  // GOSSIP_KEEP_SLOTS=1 only (k_bin_scatter_flat)
     uint32_t* deg = nullptr;      // n_local row lengths (BinArgs.deg)
     uint32_t bin_words = kBinWords;
-    uint32_t split = 1;     // parts per bin (GOSSIP_BIN_SPLIT)
     uint64_t n_slots = 0;   // padded
     uint64_t n_binned = 0;  // edges with a slot (light destinations)
+};
+
+// Propagation-blocked push rounds (gossip_blocked.hip; P = 1, one word per peer).  A push round
+// whose frontier is too wide for per-delivery atomics and too narrow for a binned round (which streams
+// every edge) writes one record {destination, new word} per delivery instead, in two binning passes:
+// level 1 into kPbCoarse coarse bins, level 2 into the fine bins of the slot layout; the apply folds
+// each fine bin's records into an LDS accumulator and test-and-sets its peers with plain stores.
+// Every (producer, bin) pair owns a segment of the record arrays sized at bootstrap by the overlay's
+// edge counts (its worst case: every source active), so records are written without global atomics:
+// a level-1 workgroup owns every kPbGrid-th tile and heavy chunk, a level-2 slice the segments of
+// kPbGrid / kPbSlices of them.
+constexpr uint32_t kPbCoarse = 256;    // level-1 bins (a power of two: the LDS search is branch-free)
+constexpr uint32_t kPbFineMax = 96;    // fine bins per coarse bin (level-2 LDS staging)
+constexpr uint32_t kPbFineIn = 1u << 18;  // a fine bin: whole tiles, <= kBinWords peers and <= this in-degree
+                                          // (unless one tile has more): no hot bin in level 2
+constexpr uint32_t kPbB1 = 32;         // level-1 records per flush: 128 B of destinations, 256 B of words
+constexpr uint32_t kPbB2 = 64;         // level-2 records per flush: 128 B of destinations, 512 B of words
+constexpr uint32_t kPbSlices = 4;      // level-2 workgroups per coarse bin
+constexpr int kPbBlock = 1024;         // 16 waves per workgroup, one workgroup per CU (level 1)
+constexpr int kPbGrid = 256;           // level-1 workgroups (row ranges)
+constexpr uint32_t kPbPad = 0xFFFFFFFFu;  // level-1 padding record (level 2: 0xFFFF)
+constexpr uint32_t kPbMap = 4096;         // level 1's id buckets (coarse bin lookup)
+constexpr uint32_t kPbLoPermille = 20;    // push rounds from this frontier run blocked ...
+constexpr uint32_t kPbHiPermille = 300;   // ... and dense rounds below this one (gossip_config.blocked_permille)
+
+struct PbArgs {
+    uint32_t n_coarse;
+    uint64_t n_fine;
+    const uint32_t* c_lo;     // n_coarse + 1: first owned peer of each coarse bin (whole fine bins)
+    const uint32_t* c_fine;   // n_coarse + 1: first fine bin of each coarse bin
+    const uint32_t* f_lo;     // n_fine + 1: first owned peer of each fine bin
+                              // level-1 workgroup w: tiles and heavy chunks w (mod kPbGrid)
+    const uint64_t* s1_base;  // [w][k] (kPbGrid x n_coarse): level-1 segment of workgroup w, coarse bin k
+    const uint32_t* s1_cap;   //   its capacity (records; a multiple of kPbB1)
+    uint32_t* s1_len;         //   records written this round (whole flushes)
+    const uint64_t* s2_base;  // [s][f] (kPbSlices x n_fine): level-2 segment of slice s, fine bin f
+    const uint32_t* s2_cap;
+    uint32_t* s2_len;
+    uint32_t* r1_dst;         // level-1 records: destination (global id; kPbPad: padding) ...
+    unsigned long long* r1_w;  // ... and the source's new word
+    uint16_t* r2_dst;         // level-2 records: destination - fine bin's first peer (0xFFFF: padding) ...
+    unsigned long long* r2_w;
+    uint32_t* err;            // set if a segment would overflow (cannot happen: capacities are edge counts)
+    uint32_t map_shift;       // level 1's LDS map of the coarse bins: id >> map_shift -> a kPbMap-entry table
+    uint32_t direct_end;      // destinations below this (the hubs' tiles, each over kPbFineIn in-degree: one
+                              // fine bin each, every record of a round into one LDS buffer) are delivered
+                              // at once, as the push does (a read of seen, then an atomic if bits are new)
+    const HeavyChunk* chunks; // the heavy rows' chunks (row order) ...
+    uint64_t n_chunks;
+    unsigned long long* nw;   // ... whose new words the split clears (set per round: the buffers rotate)
+};
+
+struct PbState {
+    uint32_t n_coarse = 0;
+    uint64_t n_fine = 0;
+    uint32_t *c_lo = nullptr, *c_fine = nullptr, *f_lo = nullptr;
+    uint32_t direct_end = 0, map_shift = 0;
+    uint64_t *s1_base = nullptr, *s2_base = nullptr;
+    uint32_t *s1_cap = nullptr, *s2_cap = nullptr, *s1_len = nullptr, *s2_len = nullptr, *err = nullptr;
+    uint32_t* r1_dst = nullptr;
+    unsigned long long* r1_w = nullptr;
+    uint16_t* r2_dst = nullptr;
+    unsigned long long* r2_w = nullptr;
+    uint64_t n1 = 0, n2 = 0;  // record capacities of the two levels
 };
 
 struct DeadReport {
@@ -190,8 +244,6 @@ struct RoundArgs {
                                    // first two entries of its row (col[rp[v]] | col[rp[v] + 1] << 32; no
                                    // masked edges), read with the sweep so a row's first step needs no
                                    // random col line
-    uint32_t pdefer;               // wide pull round (k_pull_rows): a row that learns stores only its nx
-                                   // word; its seen word is folded in by the next round (a.fold)
     uint64_t* front;               // pull rounds: 1 bit per source peer, set iff its new words are nonzero
     const uint64_t* nw_src;        // pull rounds: new words of every source, indexed by (global) peer id
     uint64_t n_src;                // peers covered by nw_src / front
@@ -251,8 +303,7 @@ hipError_t launch_inject(const RoundArgs& a, uint32_t W, const uint32_t* origin,
 hipError_t launch_push_heavy(const RoundArgs& a, uint32_t W, bool check_alive, bool remote, hipStream_t s);
 hipError_t launch_push_light(const RoundArgs& a, uint32_t W, bool check_alive, bool remote, hipStream_t s);
 hipError_t launch_frontier_bits(const RoundArgs& a, uint32_t W, hipStream_t s);
-hipError_t launch_pull_diag(const RoundArgs& a, uint32_t W, hipStream_t s);
-hipError_t launch_pull_light(const RoundArgs& a, uint32_t W, int unroll, hipStream_t s);
+hipError_t launch_pull_rows(const RoundArgs& a, uint32_t W, hipStream_t s);
 hipError_t launch_pull_heavy(const RoundArgs& a, uint32_t W, hipStream_t s);
 hipError_t launch_apply_remote(const RoundArgs& a, uint32_t W, const uint64_t* recv, uint32_t world,
                                uint64_t part_stride, hipStream_t s);
@@ -260,7 +311,6 @@ hipError_t launch_compact_send(const RoundArgs& a, uint32_t W, uint64_t chunk, u
                                uint64_t* seg, hipStream_t s);
 hipError_t launch_apply_records(const RoundArgs& a, uint32_t W, const uint64_t* rec, uint64_t n_rec, hipStream_t s);
 hipError_t launch_bin_scatter(const RoundArgs& a, const BinArgs& b, uint32_t W, hipStream_t s);
-extern int g_scatter_grid_probe;  // measurement only
 hipError_t launch_bin_apply(const RoundArgs& a, const BinArgs& b, uint32_t W, hipStream_t s);
 hipError_t launch_liveness_extra(const RoundArgs& a, hipStream_t s);
 hipError_t launch_push_extra(const RoundArgs& a, uint32_t W, bool check_alive, bool remote, hipStream_t s);
@@ -289,7 +339,6 @@ hipError_t launch_rejoin_select(const RoundArgs& a, const RebootArgs& r, const u
                                 const unsigned long long* n_list, uint64_t max_list, hipStream_t s);
 hipError_t launch_commit_nx(uint64_t* seen, const uint64_t* nx, uint64_t n_words, hipStream_t s);
 hipError_t launch_first2(const uint64_t* rp, const uint32_t* col, uint64_t n, uint64_t* out, hipStream_t s);
-hipError_t launch_count_nx(const RoundArgs& a, uint32_t W_, hipStream_t s);
 hipError_t launch_zero_words(uint64_t* words, uint64_t n_words, hipStream_t s);
 hipError_t launch_coverage(const uint64_t* words, uint64_t n_local, uint32_t W, unsigned long long* counts,
                            hipStream_t s);
@@ -297,6 +346,18 @@ hipError_t launch_heavy_count(const uint64_t* rp, uint64_t n_local, uint32_t hea
                               unsigned long long* n_chunks, hipStream_t s);
 hipError_t launch_heavy_fill(const uint64_t* rp, uint64_t n_local, uint32_t heavy, uint32_t clen, HeavyChunk* chunks,
                              unsigned long long* cursor, hipStream_t s);
+
+// ---- propagation-blocked push rounds (gossip_blocked.hip) ----
+// Bins and segments of both levels (P = 1; rows longer than heavy are the chunks', in row order).
+// hipErrorOutOfMemory: skipped (state untouched).
+hipError_t build_pb(const uint64_t* rp, const uint32_t* col, uint64_t n_local, uint64_t n_edges, uint32_t heavy,
+                    const HeavyChunk* chunks, uint64_t n_chunks, hipStream_t s, PbState* out, std::string* err);
+void free_pb(PbState* p);
+PbArgs pb_args(const PbState& p);
+// one blocked push round: level 1 (each workgroup's heavy rows, then its light rows), level 2, apply
+hipError_t launch_pb_scatter(const RoundArgs& a, const PbArgs& p, bool check_alive, uint32_t wd, hipStream_t s);
+hipError_t launch_pb_split(const PbArgs& p, hipStream_t s);
+hipError_t launch_pb_apply(const RoundArgs& a, const PbArgs& p, hipStream_t s);
 
 // ---- small overlays (gossip_tiny.hip) ----
 hipError_t launch_tiny_erow(const uint64_t* rp, uint32_t n, uint32_t* erow, hipStream_t s);
@@ -323,8 +384,10 @@ hipError_t build_powerlaw_device(uint64_t n_global, uint64_t begin, uint64_t end
 // bin-major (P = 1, or one vertex block of a partitioned run).  Returns
 // hipErrorOutOfMemory (state untouched) when the layout does not fit next to
 // what is already resident.
+// bin_words / chunk_words: LDS words of a bin / a source chunk (0: chosen from the overlay's size)
 hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local, uint64_t n_global, uint64_t n_edges,
-                      uint32_t heavy, uint32_t Wp, bool stream, hipStream_t s, BinState* out, std::string* err);
+                      uint32_t heavy, uint32_t Wp, bool stream, uint32_t bin_words, uint32_t chunk_words, hipStream_t s,
+                      BinState* out, std::string* err);
 void free_bins(BinState* b);
 
 // ---- library-driven multi-GPU rounds (gossip_dist.hip) ----

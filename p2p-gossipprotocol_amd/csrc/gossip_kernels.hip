@@ -17,102 +17,13 @@
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 
+#include "gossip_device.hpp"
 #include "gossip_internal.hpp"
 #include "philox.hpp"
 
 namespace gossip {
 
 namespace {
-
-constexpr int kWavesPerBlock = kBlock / 64;
-constexpr unsigned kMaxGrid = 2048;  // 256 CUs x 8 blocks of 256 threads
-
-__device__ __forceinline__ bool bit_alive(const uint32_t* bits, uint32_t v) { return (bits[v >> 5] >> (v & 31)) & 1u; }
-
-// the bits a peer can still learn: messages injected so far (at P = 1 the ones whose origin was alive to
-// inject them -- a never-injected message kept every row of config 5 scanning to its end)
-__device__ __forceinline__ uint64_t injm_full(const RoundArgs& a, int w) {
-    return a.inj_live ? a.inj_mask[w] & a.inj_live[w] : a.inj_mask[w];
-}
-// ... and of those, this round: only bits that are in some new word (P = 1: in_flight, the previous
-// round's receipts with this round's injections -- a bit outside it kept config 5's hubs and needy
-// rows scanning to their ends: a message injected at an isolated peer is never in flight)
-__device__ __forceinline__ uint64_t injm(const RoundArgs& a, int w) {
-    return injm_full(a, w) & (a.use_flight ? a.in_flight[w] : ~0ull);
-}
-
-__device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
-    return x;
-}
-
-__device__ __forceinline__ uint32_t lane_rank(unsigned long long mask) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-}
-
-typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
-
-struct Acc {
-    unsigned long long frontier = 0, trav = 0, deliv = 0, undeliv = 0, fresh = 0, digest = 0, covered = 0, died = 0,
-                       reports = 0, removals = 0, injected = 0, htrav = 0, checked = 0,
-                       activated = 0, pulled = 0, gathered = 0, reconnects = 0, rejoined = 0, atomics = 0,
-                       diag = 0, dead_cov = 0;
-    unsigned long long fresh_or[kMaxWords] = {};  // OR of the receipts (only the words a kernel touches stay)
-};
-
-// Block-level flush: wave sums -> LDS -> one atomic per nonzero field per
-// block, into stat line blockIdx % kStatLines of the round.  Same-line device
-// atomics serialise (~9 ns each measured); one line per round hit by every
-// wave cost ~0.65 ms per pull round at 2^20 peers.  Must be reached by every
-// wave of the block (it holds a barrier).
-// flush_into: the same with caller-provided LDS scratch (kWaves * kStatFields words).
-template <int kWaves>
-__device__ __forceinline__ void flush_into(Acc& acc, DevStats* st, unsigned long long (*red)[kStatFields]);
-
-template <int kWaves = kWavesPerBlock>
-__device__ __forceinline__ void flush(Acc& acc, DevStats* st) {
-    __shared__ unsigned long long red[kWaves][kStatFields];
-    flush_into<kWaves>(acc, st, red);
-}
-
-template <int kWaves>
-__device__ __forceinline__ void flush_into(Acc& acc, DevStats* st, unsigned long long (*red)[kStatFields]) {
-    constexpr int kF = kStatFields;
-    static_assert(sizeof(DevStats) == kF * 8, "one u64 per stat field");
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    // DevStats field order
-    const unsigned long long v[kF] = {acc.frontier, acc.trav,     acc.deliv,   acc.undeliv, acc.fresh,  acc.injected,
-                                      acc.died,     acc.reports,  acc.removals, acc.digest, acc.covered, acc.htrav,
-                                      acc.checked,  acc.activated, acc.pulled,  acc.gathered, acc.reconnects,
-                                      acc.rejoined, acc.atomics, acc.diag, acc.dead_cov,
-                                      acc.fresh_or[0], acc.fresh_or[1], acc.fresh_or[2], acc.fresh_or[3],
-                                      acc.fresh_or[4], acc.fresh_or[5], acc.fresh_or[6], acc.fresh_or[7]};
-#pragma unroll
-    for (int f = 0; f < kF; ++f) {
-        unsigned long long s_ = v[f];
-        if (f < kStatSums) {
-            s_ = wave_sum(s_);
-        } else {
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) s_ |= __shfl_xor(s_, off);
-        }
-        if (lane == 0) red[wave][f] = s_;
-    }
-    __syncthreads();
-    if (threadIdx.x < kF) {
-        unsigned long long s_ = 0;
-        const bool sum = threadIdx.x < kStatSums;
-#pragma unroll
-        for (int w = 0; w < kWaves; ++w) s_ = sum ? s_ + red[w][threadIdx.x] : s_ | red[w][threadIdx.x];
-        unsigned long long* f = reinterpret_cast<unsigned long long*>(st + blockIdx.x % kStatLines) + threadIdx.x;
-        if (s_) {
-            if (sum) atomicAdd(f, s_);
-            else atomicOr(f, s_);
-        }
-    }
-}
 
 // Edge-space expansion of one tile (64 rows, one wave).  deg = this lane's
 // row length (0 = skip), rb = its row begin.  f(src_lane, valid, e) runs once
@@ -142,18 +53,6 @@ __device__ __forceinline__ void tile_edges(uint32_t deg, uint64_t rb, F&& f) {
     }
 }
 
-// Source lane of edge position p within a tile: the number of rows whose
-// inclusive end is <= p (incl = in-wave inclusive scan of row lengths).
-__device__ __forceinline__ int src_lane(uint32_t incl, uint32_t p) {
-    int s = 0;
-#pragma unroll
-    for (int step = 32; step > 0; step >>= 1) {
-        const uint32_t val = __shfl(incl, s + step - 1);
-        if (val <= p) s += step;
-    }
-    return s;
-}
-
 // handleClient's dedup (peer.cpp:277-285) as a 64-bit test-and-set: deliver
 // the source's new words m to local peer lv whose seen words were read as cur.
 // The plain read first: seen only grows within a round, so a stale read can
@@ -178,12 +77,6 @@ __device__ __forceinline__ void deliver_local(const RoundArgs& a, uint64_t lv, c
     for (int w = 0; w < W; ++w) {
         const unsigned long long u = m[w] & ~cur[w];
         if (!u) continue;  // all duplicates: dropped (peer.cpp:281)
-        if (a.defer == 2) {  // no-return atomic: the round's receipts are counted from nx (k_count_nx)
-            atomicOr(np + w, u);
-            acc.atomics++;
-            acc.fresh_or[w] |= u;  // (a superset of the receipts)
-            continue;
-        }
         if (a.defer) {     // seen is the round-start set all round: one atomic, on nx
             const unsigned long long old = atomicOr(np + w, u);
             acc.atomics++;
@@ -288,19 +181,6 @@ __device__ __forceinline__ void deliver_batch(const RoundArgs& a, const uint32_t
             const uint64_t x = a.seen[loc[j] ? (uint64_t)(c[j] - (uint32_t)a.begin) * W + w : 0];
             cur[j][w] = x | (loc[j] && m[j][w] ? 0ull : ~0ull);  // (a select would sink the load into a branch)
         }
-    if (a.defer == 2) {  // no-return atomics on nx; the round's receipts are counted from nx (k_count_nx)
-#pragma unroll
-        for (int j = 0; j < kU; ++j)
-#pragma unroll
-            for (int w = 0; w < W; ++w) {
-                const uint64_t lv = (uint64_t)(c[j] - (uint32_t)a.begin);
-                const unsigned long long u = m[j][w] & ~cur[j][w];
-                if (u) atomicOr(reinterpret_cast<unsigned long long*>(a.nx) + lv * W + w, u);
-                acc.atomics += u != 0;
-                acc.fresh_or[w] |= u;  // (a superset of the receipts)
-            }
-        return;
-    }
     // the test-and-sets, every atomic of a phase issued before any result is used
     uint64_t old[kU][W];
 #pragma unroll
@@ -584,216 +464,15 @@ __global__ __launch_bounds__(kBlock) void k_frontier_bits(RoundArgs a) {
     }
 }
 
-// Streamed (touched-once) loads/stores of a pull round; NT marks them
-// non-temporal so they do not push the gathered new words out of L2/MALL.
-template <bool NT, class T>
-__device__ __forceinline__ T ld_s(const T* p) {
-    if constexpr (NT) return __builtin_nontemporal_load(p);
-    else return *p;
-}
-template <bool NT, class T>
-__device__ __forceinline__ void st_s(T* p, T v) {
-    if constexpr (NT) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
-
-// Measurement only (GOSSIP_PULL_DIAG=1, before k_pull_light): per light row
-// that can still learn, the gathers a sequential scan of its row with an early
-// exit would issue -- it stops at the edge where its words hold every bit it
-// can learn (need); a row whose need is not covered by its neighbours scans
-// all of them.  Into the round's diag counter: gathers << 32 | needy rows.
-template <int W>
-__global__ __launch_bounds__(kBlock) void k_pull_diag(RoundArgs a) {
-    Acc acc;
-    for (uint64_t v = (uint64_t)blockIdx.x * kBlock + threadIdx.x; v < a.n_local; v += (uint64_t)gridDim.x * kBlock) {
-        uint64_t need[W], got[W];
-        bool needy = false;
-#pragma unroll
-        for (int w = 0; w < W; ++w) {
-            need[w] = injm(a, w) & ~a.seen[v * W + w];
-            got[w] = 0;
-            needy |= need[w] != 0;
-        }
-        if (!needy) continue;
-        const uint64_t rb = a.rp[v], d = a.rp[v + 1] - rb;
-        if (d > a.heavy) continue;
-        uint64_t k = 0;
-        for (; k < d; ++k) {
-            const uint32_t u = a.col[rb + k];
-            if (u & kMaskedEdge) continue;
-            bool done = true;
-#pragma unroll
-            for (int w = 0; w < W; ++w) {
-                got[w] |= a.nw_src[(uint64_t)u * W + w] & need[w];
-                done &= got[w] == need[w];
-            }
-            if (done) {
-                ++k;
-                break;
-            }
-        }
-        acc.diag += (k << 32) + 1;
-    }
-    flush(acc, a.st);
-}
-
-template <int W, bool COV, bool FRONT, int kPullUnroll, bool NT>  // kPullUnroll: 64-edge batches in flight per wave
-__global__ __launch_bounds__(kBlock) void k_pull_light(RoundArgs a, uint32_t wd) {
-    __shared__ unsigned int cov_s[COV ? 64 * W : 1];
-    __shared__ unsigned long long acc_s[kWavesPerBlock][64 * W];
-    if (COV) {
-        for (int i = threadIdx.x; i < 64 * W; i += kBlock) cov_s[i] = 0;
-        __syncthreads();
-    }
-    Acc acc;
-    const int lane = threadIdx.x & 63;
-    unsigned long long* my = acc_s[threadIdx.x >> 6];
-    const uint64_t n_tiles = (a.n_local + 63) >> 6;
-    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
-    for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); t < n_tiles; t += nwaves) {
-        const uint64_t v = (t << 6) + lane;
-        const bool vv = v < a.n_local;
-        uint64_t m[W], need[W], sv[W];
-        bool act = false, needy = false;
-        const bool va = vv && (!a.dead_mode || bit_alive(a.alive, (uint32_t)(a.begin + v)));  // dead: no receive
-#pragma unroll
-        for (int w = 0; w < W; ++w) {
-            m[w] = vv ? ld_s<NT>(a.nw + v * W + w) : 0ull;
-            sv[w] = vv ? ld_s<NT>(a.seen + v * W + w) : ~0ull;
-            need[w] = va ? injm(a, w) & ~sv[w] : 0ull;
-            act |= m[w] != 0;
-            needy |= need[w] != 0;
-        }
-        if (!__any(act || needy)) {
-            if (vv)
-#pragma unroll
-                for (int w = 0; w < W; ++w) st_s<NT>(a.nx + v * W + w, (uint64_t)0);  // nx is written whole in a pull round
-            continue;
-        }
-        uint64_t rb = 0, d = 0;
-        if (vv) {
-            rb = ld_s<NT>(a.rp + v);
-            d = ld_s<NT>(a.rp + v + 1) - rb;
-        }
-        if (act) {  // source side of this peer's pushes (broadcastMessage, peer.cpp:310-316)
-            uint32_t pc = 0;
-#pragma unroll
-            for (int w = 0; w < W; ++w) {
-                pc += (uint32_t)__popcll(m[w]);
-                if (w < (int)wd) acc.digest += digest_weight((a.begin + v) * wd + w) * m[w];
-                if (COV)
-                    for (uint64_t x = m[w]; x; x &= x - 1) atomicAdd(&cov_s[w * 64 + __builtin_ctzll(x)], 1u);
-            }
-            acc.frontier++;
-            acc.covered += pc;
-            if (!a.dead_mode) {  // every edge alive and unmasked
-                acc.trav += d;
-                acc.deliv += (unsigned long long)pc * d;
-            } else if (a.dgone) {  // from the per-source counters; else k_src_count books them
-                const uint32_t g = a.dgone[v], k = a.dmask[v];
-                acc.trav += d - k;
-                acc.deliv += (unsigned long long)pc * (d - g);
-                acc.undeliv += (unsigned long long)pc * (g - k);
-            }
-        }
-        const bool light = d <= a.heavy;
-#pragma unroll
-        for (int w = 0; w < W; ++w) my[lane * W + w] = 0ull;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const uint32_t deg = needy && light ? (uint32_t)d : 0u;
-        uint32_t incl = deg;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t y = __shfl_up(incl, off);
-            if (lane >= off) incl += y;
-        }
-        const uint32_t excl = incl - deg;
-        const uint32_t total = __shfl(incl, 63);
-        for (uint32_t base = 0; base < total; base += 64 * kPullUnroll) {
-            // phase 1: edge positions (and which sources still want anything)
-            int src[kPullUnroll];
-            uint64_t e[kPullUnroll];
-            uint32_t ok = 0;
-#pragma unroll
-            for (int j = 0; j < kPullUnroll; ++j) {
-                const uint32_t p = base + j * 64 + lane;
-                src[j] = src_lane(incl, p);
-                e[j] = __shfl(rb, src[j]) + (uint64_t)(p - __shfl(excl, src[j]));
-                bool want = false;
-#pragma unroll
-                for (int w = 0; w < W; ++w)  // stale LDS read: only extra loads
-                    want |= (__shfl(need[w], src[j]) & ~my[src[j] * W + w]) != 0;
-                ok |= (p < total && want) ? 1u << j : 0u;
-            }
-            // phase 2..4: independent loads, kPullUnroll deep
-            uint32_t u[kPullUnroll];
-#pragma unroll
-            for (int j = 0; j < kPullUnroll; ++j) u[j] = (ok >> j) & 1 ? ld_s<NT>(a.col + e[j]) : 0u;
-            acc.pulled += (unsigned)__builtin_popcount(ok);
-#pragma unroll
-            for (int j = 0; j < kPullUnroll; ++j)  // masked: the neighbour is dead, its words are zero
-                if (u[j] & kMaskedEdge) ok &= ~(1u << j);
-            if (FRONT) {
-                uint64_t fb[kPullUnroll];
-#pragma unroll
-                for (int j = 0; j < kPullUnroll; ++j) fb[j] = (ok >> j) & 1 ? a.front[u[j] >> 6] : 0ull;
-#pragma unroll
-                for (int j = 0; j < kPullUnroll; ++j)
-                    if (!((fb[j] >> (u[j] & 63)) & 1ull)) ok &= ~(1u << j);  // u has nothing new: no gather
-            }
-            uint64_t x[kPullUnroll][W];
-#pragma unroll
-            for (int j = 0; j < kPullUnroll; ++j)
-#pragma unroll
-                for (int w = 0; w < W; ++w) x[j][w] = (ok >> j) & 1 ? a.nw_src[(uint64_t)u[j] * W + w] : 0ull;
-            acc.gathered += (unsigned)__builtin_popcount(ok);
-            // phase 5: fold into the sources' LDS accumulators
-#pragma unroll
-            for (int j = 0; j < kPullUnroll; ++j)
-#pragma unroll
-                for (int w = 0; w < W; ++w) {
-                    const uint64_t y = x[j][w] & __shfl(need[w], src[j]);
-                    if (y) atomicOr(&my[src[j] * W + w], (unsigned long long)y);  // LDS ds_or_b64
-                }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (vv) {
-#pragma unroll
-            for (int w = 0; w < W; ++w) {
-                const uint64_t fr = light ? (my[lane * W + w] & need[w]) : 0ull;
-                acc.fresh_or[w] |= fr;
-                if (fr) {  // handleClient: new -> Message-List insert (peer.cpp:281-282)
-                    st_s<NT>(a.seen + v * W + w, sv[w] | fr);
-                    acc.fresh += (unsigned long long)__popcll(fr);
-                    acc.activated++;
-                }
-                st_s<NT>(a.nx + v * W + w, fr);  // heavy rows: 0 here, OR-ed by k_pull_heavy afterwards
-            }
-        }
-    }
-    flush(acc, a.st);
-    if (COV) {
-        __syncthreads();
-        for (int i = threadIdx.x; i < 64 * W; i += kBlock)
-            if (cov_s[i]) atomicAdd(&a.cov[i], (unsigned long long)cov_s[i]);
-    }
-}
-
-// pull, light rows, as a row queue with an early exit (the default pull
-// kernel; k_pull_light is the tile-expansion form, GOSSIP_PULL_ROWS=0).  Each
-// wave sweeps 64-peer tiles: source side of the pushes, nx = 0, and every
+// pull, light rows, as a row queue with an early exit.  Each wave sweeps 64-peer tiles: source side of the pushes, nx = 0, and every
 // light row that can still learn something (need != 0) joins the wave's queue
 // in LDS.  Lanes take rows from the queue and scan them kRowB edges per step,
 // OR-ing the neighbours' new words into what they got; a row stops as soon as
 // it got every bit it can learn (need) -- most rows need one neighbour (config
 // 4, round 7: 90.1 M needy rows, 101 M gathers with the exit against 479 M
-// for whole rows) -- or at its end.  Finished lanes take the next row.  Same
-// results as k_pull_light: fr = (OR of the scanned neighbours) & need, and a
-// row that stops early already holds all of need.
+// for whole rows) -- or at its end.  Finished lanes take the next row:
+// fr = (OR of the scanned neighbours) & need, and a row that stops early
+// already holds all of need.
 constexpr int kRowQ = 128;    // queue entries per wave
 template <int W, bool COV, bool FRONT, int kRowB>  // kRowB: edges per lane per step
 __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) {
@@ -993,8 +672,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
                 const uint64_t fr = got[w];  // subset of need: bits this peer had not seen
                 acc.fresh_or[w] |= fr;
                 if (fr) {
-                    // a.pdefer: the next round folds nx into seen (a random 8-B store saved per row)
-                    if (!a.pdefer) a.seen[(uint64_t)rv * W + w] = (injm_full(a, w) & ~need[w]) | fr;  // within inj_mask
+                    a.seen[(uint64_t)rv * W + w] = (injm_full(a, w) & ~need[w]) | fr;  // within inj_mask
                     a.nx[(uint64_t)rv * W + w] = fr;
                     acc.fresh += (unsigned long long)__popcll(fr);
                     any = true;
@@ -1202,7 +880,7 @@ __device__ __forceinline__ void scatter_stage(const RoundArgs& a, const BinArgs&
     }
 }
 
-// The row loop shared by both scatters: member j of XCD x takes unit j of each
+// The row loop of the scatters: member j of XCD x takes unit j of each
 // row of the XCD's unit list (gossip_bins.hip), so the XCD's workgroups stage
 // consecutive chunks together and write adjacent slot runs into every bin (a
 // row barrier on top of that measured no gain: 71.4 against 71.3 ms per step).
@@ -1213,123 +891,7 @@ __device__ __forceinline__ void scatter_rows(const BinArgs& b, F&& unit) {
     for (uint64_t ui = b.xcd_units[xcd] + member; ui < u1; ui += members) unit(ui);
 }
 
-template <int W, bool COV, int kU>  // kU: cb entries in flight per lane
-__global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_lds(RoundArgs a, BinArgs b, uint32_t wd) {
-    constexpr int kWaves = kScatterBlock / 64;
-    __shared__ unsigned long long slice[kBinChunkWords];
-    // which of the chunk's sources have anything to write: nonzero new words.
-    // An idle source leaves its slots alone.  A slot may thus keep a word of
-    // an earlier binned round of the same run: that round OR-ed it into
-    // seen[dst] (deaths are permanent and dead peers never receive, so seen
-    // still holds it), and the apply masks with ~seen.  The first binned round
-    // after a reset (noskip) rewrites every slot, clearing the last run's words.
-    __shared__ unsigned long long live_s[kBinChunkWords / 64];
-    __shared__ unsigned int cov_s[COV ? 64 * W : 1];
-    if (COV) {
-        for (int i = threadIdx.x; i < 64 * W; i += kScatterBlock) cov_s[i] = 0;
-    }
-    Acc acc;
-    const int lane = threadIdx.x & 63;
-    auto scatter_unit = [&](const uint64_t ui) {
-        const BinUnit un = b.units[ui];
-        if (un.p0 >= un.p1 && !un.first) return;  // padding of a row (block-uniform)
-        scatter_stage<W, COV>(a, b, un, wd, slice, live_s, cov_s, acc);
-        __syncthreads();
-        if (b.probe == 1) return;
-        // consecutive lanes take consecutive entries: the stores of one
-        // instruction fall into a few slot runs (measured at config 4: 37 ms
-        // per step against 57 ms with 8 consecutive entries per lane; u16
-        // chunk-local sources 36-41 ms against 43-47 ms with u32 global ids).
-        // Each wave walks whole 64-entry groups (aligned), so a lane finds its
-        // run with one ballot of the run-start flags: run = cb_grp[group] +
-        // number of starts at lanes 1..lane; slot = position + cb_run[run].
-        // Three-stage software pipeline per wave, ordered so that every wait
-        // is for loads issued before the previous batch's stores (vmcnt
-        // counts loads and stores in issue order): resolve batch i+1 (its
-        // cb_run loads), load the entries of batch i+2, store batch i.  The
-        // loop has no branches -- loads use clamped addresses, raw values are
-        // masked only when resolved, and a lane with nothing to write stores
-        // to its own line of a small L2-resident dummy array -- so the
-        // compiler's waits count exactly instead of draining to vmcnt(0).
-        // positions fit 32 bits (build_bins: fewer than kNoSlot edges)
-        constexpr uint32_t step = (uint32_t)kScatterBlock * kU;
-        const uint32_t p0 = (uint32_t)un.p0, p1 = (uint32_t)un.p1, nb = (uint32_t)b.n_binned;
-        if (p0 >= p1) return;  // block-uniform; nb >= 1 below
-        const uint32_t base0 = (p0 & ~63u) + threadIdx.x;
-        const uint32_t n_grp = (nb + 63) >> 6;
-        const unsigned long long below = (lane == 63 ? ~0ull : ((2ull << lane) - 1)) & ~1ull;  // lanes 1..lane
-        uint64_t* const sink = b.dummy + ((uint64_t)blockIdx.x * kScatterBlock + threadIdx.x) * W;
-        using Buf = uint32_t[kU];
-        auto load = [&](uint32_t p, Buf& s_, Buf& g_) {
-#pragma unroll
-            for (int j = 0; j < kU; ++j) {
-                const uint32_t q = p + (uint32_t)j * kScatterBlock;
-                const uint32_t g = __builtin_amdgcn_readfirstlane(q >> 6);  // wave-uniform group
-                s_[j] = (uint32_t)__builtin_nontemporal_load(b.cb_src + min(q, nb - 1));  // raw: masked in resolve
-                g_[j] = b.cb_grp[min(g, n_grp - 1)];
-            }
-        };
-        // runs of a loaded batch: issues the cb_run loads (r_, used one
-        // iteration later), the chunk-local sources (u_) and the lanes with a
-        // slot to write (a_: inside the unit and an active source); past the
-        // end the flags are 0, so the run stays in range
-        auto resolve = [&](uint32_t p, const Buf& s_, const Buf& g_, Buf& r_, Buf& u_, uint32_t& a_) {
-            a_ = 0;
-#pragma unroll
-            for (int j = 0; j < kU; ++j) {
-                const uint32_t q = p + (uint32_t)j * kScatterBlock;
-                const uint32_t sv = q < nb ? s_[j] : 0u;
-                const unsigned long long starts = __ballot((sv & kRunStart) != 0);
-                const uint32_t run = g_[j] + (uint32_t)__popcll(starts & below);
-                const uint32_t u = sv & (kRunStart - 1u);  // < chunk: in range of the slice
-                const uint32_t live = (uint32_t)(live_s[u >> 6] >> (u & 63)) & 1u;  // unconditional (no branch)
-                a_ |= ((uint32_t)(q >= p0) & (uint32_t)(q < p1) & live) << j;
-                u_[j] = u;
-                r_[j] = b.cb_run[run];
-            }
-        };
-        auto store = [&](uint32_t p, const Buf& r_, const Buf& u_, uint32_t a_) {
-#pragma unroll
-            for (int j = 0; j < kU; ++j) {
-                const uint32_t q = p + (uint32_t)j * kScatterBlock;
-                // probe 3 (timing only, wrong results): entry p stores to val[p], i.e. sequentially
-                const uint64_t slot = b.probe == 3 ? (uint64_t)q : (uint64_t)(r_[j] + q);
-                uint64_t* const dst = ((a_ >> j) & 1u) && b.probe != 2 ? b.val + slot * W : sink;
-#pragma unroll
-                for (int w = 0; w < W; ++w) dst[w] = slice[(uint64_t)u_[j] * W + w];
-            }
-            acc.gathered += __popc(a_);  // slots written (byte accounting)
-        };
-        // two register sets, alternating (no loop-carried copies, which would
-        // wait for the loads just issued)
-        Buf s0, g0, r0, u0, s1, g1, r1, u1;
-        uint32_t a0, a1;
-        load(base0, s1, g1);
-        resolve(base0, s1, g1, r0, u0, a0);
-        load(base0 + step, s0, g0);
-        for (uint32_t base = p0 & ~63u;; base += 2 * step) {  // block-uniform: ballots see every lane
-            const uint32_t p = base + threadIdx.x;
-            resolve(p + step, s0, g0, r1, u1, a1);
-            load(p + 2 * step, s1, g1);
-            store(p, r0, u0, a0);
-            if (base + step >= p1) break;
-            resolve(p + 2 * step, s1, g1, r0, u0, a0);
-            load(p + 3 * step, s0, g0);
-            store(p + step, r1, u1, a1);
-            if (base + 2 * step >= p1) break;
-        }
-    };
-    scatter_rows(b, scatter_unit);
-    flush<kWaves>(acc, a.st);
-    if (COV) {
-        __syncthreads();
-        for (int i = threadIdx.x; i < 64 * W; i += kScatterBlock)
-            if (cov_s[i]) atomicAdd(&a.cov[i], (unsigned long long)cov_s[i]);
-    }
-}
-
-// Producer/consumer scatter (the default; GOSSIP_SCATTER_PC=0 selects
-// k_bin_scatter_lds).  Measured on the single-role kernel: a wave that both
+// Producer/consumer scatter (slot layout).  Measured on the round-1 single-role kernel: a wave that both
 // loads and stores cannot keep stores in flight -- vmcnt counts loads and
 // stores in issue order, and every wait for a load (the next cb entries)
 // also waited for the stores issued before it (the compiled loop drained to
@@ -1470,11 +1032,9 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_pc(RoundArgs a, B
                     lds_wait();
                     if (lane == 0)  // the ring slot is free again
                         __hip_atomic_store(&cons_cnt[pp], i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    const bool act = (su & kRunStart) && b.probe != 2;
-                    if (act) {
-                        const uint64_t at = b.probe == 3 ? (uint64_t)((g0 + pp + kPcProd * i) * 64 + lane) : slot;
+                    if (su & kRunStart) {
 #pragma unroll
-                        for (int w = 0; w < W; ++w) b.val[at * W + w] = x[w];
+                        for (int w = 0; w < W; ++w) b.val[(uint64_t)slot * W + w] = x[w];
                     }
                     acc.gathered += (su & kRunStart) ? 1u : 0u;  // slots written (byte accounting)
                 }
@@ -1487,7 +1047,6 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_pc(RoundArgs a, B
         scatter_stage<W, COV>(a, b, un, wd, slice, live_s, cov_s, acc);
         if (threadIdx.x < kPcProd) prod_cnt[threadIdx.x] = cons_cnt[threadIdx.x] = 0;
         __syncthreads();
-        if (b.probe == 1) return;
         run(un.p0, un.p1);
     };
     scatter_rows(b, scatter_unit);
@@ -1499,50 +1058,6 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_pc(RoundArgs a, B
         for (int i = threadIdx.x; i < 64 * W; i += kScatterBlock)
             if (cov_s[i]) atomicAdd(&a.cov[i], (unsigned long long)cov_s[i]);
     }
-}
-
-// Measurement only (GOSSIP_SCATTER_PC=9 with GOSSIP_KEEP_SLOTS=1): the slot of
-// every cb entry read from a kept u32 array, kD 64-entry groups per wave in
-// flight, stores by the same wave -- the store pattern of the binned scatter
-// with the least load-side work in front of it.
-template <int W, int kD>
-__global__ __launch_bounds__(kScatterBlock) void k_bin_scatter_flat(RoundArgs a, BinArgs b, uint32_t wd) {
-    constexpr int kWaves = kScatterBlock / 64;
-    __shared__ unsigned long long slice[kBinChunkWords];
-    __shared__ unsigned long long live_s[kBinChunkWords / 64 / W];
-    Acc acc;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t nb = (uint32_t)b.n_binned;
-    scatter_rows(b, [&](const uint64_t ui) {
-        const BinUnit un = b.units[ui];
-        if (un.p0 >= un.p1 && !un.first) return;
-        scatter_stage<W, false>(a, b, un, wd, slice, live_s, nullptr, acc);
-        __syncthreads();
-        if (un.p0 >= un.p1 || b.probe == 1) return;
-        const uint32_t p0 = (uint32_t)un.p0, p1 = (uint32_t)un.p1;
-        const uint32_t g_hi = ((p1 - 1) >> 6) + 1;
-        for (uint32_t g = (p0 >> 6) + wave; g < g_hi; g += kWaves * kD) {
-            uint32_t sl[kD], sv[kD];
-#pragma unroll
-            for (int j = 0; j < kD; ++j) {
-                const uint32_t q = min((g + kWaves * j) * 64 + lane, nb - 1);
-                sl[j] = b.cb_slot[q];
-                sv[j] = b.cb_src[q];
-            }
-#pragma unroll
-            for (int j = 0; j < kD; ++j) {
-                const uint32_t q = (g + kWaves * j) * 64 + lane;
-                const uint32_t u = sv[j] & (kRunStart - 1u);
-                const bool live = (live_s[u >> 6] >> (u & 63)) & 1ull;
-                if (q >= p0 && q < p1 && live) {
-#pragma unroll
-                    for (int w = 0; w < W; ++w) b.val[(uint64_t)sl[j] * W + w] = slice[u * W + w];
-                    acc.gathered++;
-                }
-            }
-        }
-    });
-    flush<kWaves>(acc, a.st);
 }
 
 // The source side of a binned round for a bin's peers (their pushes,
@@ -1589,21 +1104,9 @@ __global__ __launch_bounds__(kB) void k_bin_apply(RoundArgs a, BinArgs b, uint32
     __shared__ unsigned long long acc_s[kWords];
     __shared__ unsigned int cov_s[64 * W];
     Acc acc;
-    // workgroup -> (bin, part): a bin of b.split parts is applied by b.split workgroups, each keeping
-    // the slots of its own part's peers; the parts of a bin go to one XCD (block ids 8 apart, which the
-    // dispatcher deals to the same XCD) so that their reads of the bin's slots meet in its L2
-    uint32_t bi = blockIdx.x, part = 0;
-    if (b.split > 1) {
-        const uint32_t r = blockIdx.x >> 3;
-        part = r % b.split;
-        bi = r / b.split * 8 + (blockIdx.x & 7);
-    }
-    if (bi >= b.n_bins) return;  // (whole workgroup, before any barrier)
-    const Bin bn = b.bins[bi];
-    const uint32_t part_peers = b.bin_words / W, lo = part * part_peers;
-    if (lo >= bn.v1 - bn.v0) return;
-    const uint32_t nv = min(bn.v1 - bn.v0 - lo, part_peers);
-    const uint64_t v0 = bn.v0 + lo;
+    const Bin bn = b.bins[blockIdx.x];
+    const uint32_t nv = bn.v1 - bn.v0;
+    const uint64_t v0 = bn.v0;
     if (!b.src_stats) {
         if (a.cov)
             for (uint32_t i = threadIdx.x; i < 64 * W; i += kB) cov_s[i] = 0;
@@ -1634,7 +1137,7 @@ __global__ __launch_bounds__(kB) void k_bin_apply(RoundArgs a, BinArgs b, uint32
         cov_out();
         return;
     }
-    if (threadIdx.x == 0 && part == 0) acc.pulled = bn.s1 - bn.s0;  // slots scanned (byte accounting)
+    if (threadIdx.x == 0) acc.pulled = bn.s1 - bn.s0;  // slots scanned (byte accounting)
     // 8 slots per lane per step: 16 B of bdst, 64*W B of val
     for (uint64_t i = bn.s0 + (uint64_t)threadIdx.x * 8; i < bn.s1; i += (uint64_t)kB * 8) {
         const uint4 dd = *reinterpret_cast<const uint4*>(b.bdst + i);
@@ -1649,8 +1152,7 @@ __global__ __launch_bounds__(kB) void k_bin_apply(RoundArgs a, BinArgs b, uint32
         const uint32_t dw[4] = {dd.x, dd.y, dd.z, dd.w};
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const uint32_t dl = ((dw[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu) - lo;  // destination in this part
-            if (dl >= nv) continue;  // another part's slot (padding slots hold zero words)
+            const uint32_t dl = (dw[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;  // padding slots hold zero words
 #pragma unroll
             for (int w = 0; w < W; ++w)
                 if (x[k * W + w]) atomicOr(&acc_s[dl * W + w], (unsigned long long)x[k * W + w]);
@@ -2638,26 +2140,6 @@ __global__ __launch_bounds__(kBlock) void k_commit_nx(u64x2* seen, const u64x2* 
 
 // reset: zero a word array with 16-B stores (hipMemsetAsync's fill kernel
 // reached ~2.6 TB/s on the 2 GB arrays of config 4)
-// After a no-return deferred push round (RoundArgs.defer == 2): nx holds exactly the round's receipts
-// (bits not in the round-start seen), so new receipts = its popcount and activations = peers with a
-// nonzero word.
-template <int W>
-__global__ __launch_bounds__(kBlock) void k_count_nx(RoundArgs a) {
-    Acc acc;
-    for (uint64_t v = (uint64_t)blockIdx.x * kBlock + threadIdx.x; v < a.n_local; v += (uint64_t)gridDim.x * kBlock) {
-        bool any = false;
-#pragma unroll
-        for (int w = 0; w < W; ++w) {
-            const uint64_t x = a.nx[v * W + w];
-            any |= x != 0;
-            acc.fresh += (unsigned long long)__popcll(x);
-            acc.fresh_or[w] |= x;
-        }
-        acc.activated += any;
-    }
-    flush(acc, a.st);
-}
-
 __global__ __launch_bounds__(kBlock) void k_zero2(u64x2* p, uint64_t n2) {
     const u64x2 z = {0ull, 0ull};
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n2; i += (uint64_t)gridDim.x * kBlock) p[i] = z;
@@ -2712,12 +2194,6 @@ __global__ void k_heavy_fill(const uint64_t* rp, uint64_t n, uint32_t heavy, uin
     }
 }
 
-unsigned grid_for(uint64_t items, uint64_t per_block) {
-    uint64_t g = (items + per_block - 1) / per_block;
-    if (g < 1) g = 1;
-    if (g > kMaxGrid) g = kMaxGrid;
-    return (unsigned)g;
-}
 
 
 }  // namespace
@@ -2827,48 +2303,16 @@ hipError_t launch_frontier_bits(const RoundArgs& a, uint32_t W_, hipStream_t s) 
     return hipGetLastError();
 }
 
-hipError_t launch_pull_diag(const RoundArgs& a, uint32_t W_, hipStream_t s) {
-    GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_pull_diag<W>, dim3(grid_for(a.n_local, kBlock)), dim3(kBlock),
-                                                   0, s, a));
-    return hipGetLastError();
-}
-
-hipError_t launch_pull_light(const RoundArgs& a, uint32_t W_, int unroll, hipStream_t s) {
-    const uint64_t tiles = (a.n_local + 63) / 64;
-    const unsigned g = grid_for(tiles, kWavesPerBlock);
+hipError_t launch_pull_rows(const RoundArgs& a, uint32_t W_, hipStream_t s) {
+    // a row queue per wave: every wave resident at once (its queue carries its work)
+    const unsigned g = std::min(grid_for((a.n_local + 63) / 64, kWavesPerBlock), (unsigned)kMaxGrid);
     const uint32_t wd = wd_of(W_);
-    if (unroll & kPullRows) {  // row queue: every wave resident at once (its queue carries its work)
-        const unsigned gr = std::min(g, (unsigned)kMaxGrid);
-#define GOSSIP_ROWS(COV, FR)                                                                                    \
-        do {                                                                                                    \
-            hipLaunchKernelGGL((k_pull_rows<W, COV, FR, 2>), dim3(gr), dim3(kBlock), 0, s, a, wd);               \
-        } while (0)
-        GOSSIP_DISPATCH_W(wp_of(W_), {
-            if (a.cov) { if (a.front) GOSSIP_ROWS(true, true); else GOSSIP_ROWS(true, false); }
-            else { if (a.front) GOSSIP_ROWS(false, true); else GOSSIP_ROWS(false, false); }
-        });
-#undef GOSSIP_ROWS
-        return hipGetLastError();
-    }
-    const bool nt = (unroll & kPullNT) != 0;
-    unroll &= 0xFF;  // batches in flight (the flags above it are handled)
-#define GOSSIP_PULL_U(COV, FR, U)                                                                               \
-    do {                                                                                                        \
-        if (nt) hipLaunchKernelGGL((k_pull_light<W, COV, FR, U, true>), dim3(g), dim3(kBlock), 0, s, a, wd);    \
-        else hipLaunchKernelGGL((k_pull_light<W, COV, FR, U, false>), dim3(g), dim3(kBlock), 0, s, a, wd);      \
-    } while (0)
-#define GOSSIP_PULL(COV, FR)                                  \
-    do {                                                      \
-        if (unroll >= 4) GOSSIP_PULL_U(COV, FR, 4);           \
-        else if (unroll == 2) GOSSIP_PULL_U(COV, FR, 2);      \
-        else GOSSIP_PULL_U(COV, FR, 1);                       \
-    } while (0)
+#define GOSSIP_ROWS(COV, FR) hipLaunchKernelGGL((k_pull_rows<W, COV, FR, 2>), dim3(g), dim3(kBlock), 0, s, a, wd)
     GOSSIP_DISPATCH_W(wp_of(W_), {
-        if (a.cov) { if (a.front) GOSSIP_PULL(true, true); else GOSSIP_PULL(true, false); }
-        else { if (a.front) GOSSIP_PULL(false, true); else GOSSIP_PULL(false, false); }
+        if (a.cov) { if (a.front) GOSSIP_ROWS(true, true); else GOSSIP_ROWS(true, false); }
+        else { if (a.front) GOSSIP_ROWS(false, true); else GOSSIP_ROWS(false, false); }
     });
-#undef GOSSIP_PULL
-#undef GOSSIP_PULL_U
+#undef GOSSIP_ROWS
     return hipGetLastError();
 }
 
@@ -2906,32 +2350,8 @@ hipError_t launch_apply_records(const RoundArgs& a, uint32_t W_, const uint64_t*
     return hipGetLastError();
 }
 
-// cb entries in flight per lane in k_bin_scatter_lds (GOSSIP_SCATTER_U: 4 or 8)
-static int scatter_u() {
-    static const int u = [] {
-        const char* e = getenv("GOSSIP_SCATTER_U");
-        return e && atoi(e) == 8 ? 8 : 4;
-    }();
-    return u;
-}
-
-// producer/consumer scatter (default) or the single-role one (GOSSIP_SCATTER_PC=0)
-// (GOSSIP_SCATTER_PC: 0 single-role kernel; 1 = 8 producers resolving 2 groups per stage
-// into 4-slot rings (the default; measured best); 2 = 12 producers, 2 groups, 2 slots;
-// 4 = 8 producers, 4 groups, 4 slots)
-static int scatter_pc() {
-    static const int pc = [] {
-        const char* e = getenv("GOSSIP_SCATTER_PC");
-        return e ? atoi(e) : 1;
-    }();
-    return pc;
-}
-
-int g_scatter_grid_probe = 0;  // measurement only (overlap probe): scatter workgroups, 0 = kScatterGrid
-
 hipError_t launch_bin_scatter(const RoundArgs& a, const BinArgs& b, uint32_t W_, hipStream_t s) {
     const uint32_t wd = wd_of(W_);
-    const int kScatterGrid = g_scatter_grid_probe ? g_scatter_grid_probe : gossip::kScatterGrid;
     if (b.stream) {
         GOSSIP_DISPATCH_W(wp_of(W_), {
             if (a.cov) hipLaunchKernelGGL((k_bin_stream<W, true>), dim3(kScatterGrid), dim3(kScatterBlock), 0, s, a, b, wd);
@@ -2939,34 +2359,15 @@ hipError_t launch_bin_scatter(const RoundArgs& a, const BinArgs& b, uint32_t W_,
         });
         return hipGetLastError();
     }
-    if (scatter_pc() == 9 && b.cb_slot) {
-        GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_scatter_flat<W, 8>), dim3(kScatterGrid),
-                                                       dim3(kScatterBlock), 0, s, a, b, wd));
-        return hipGetLastError();
-    }
-    if (const int v = scatter_pc()) {
-#define GOSSIP_PC(P, G, R, N)                                                                              \
-        do {                                                                                               \
-            if (a.cov) hipLaunchKernelGGL((k_bin_scatter_pc<W, true, P, G, R, N>), dim3(kScatterGrid),       \
-                                          dim3(kScatterBlock), 0, s, a, b, wd);                            \
-            else hipLaunchKernelGGL((k_bin_scatter_pc<W, false, P, G, R, N>), dim3(kScatterGrid),            \
-                                    dim3(kScatterBlock), 0, s, a, b, wd);                                  \
-        } while (0)
-        GOSSIP_DISPATCH_W(wp_of(W_), {
-            if (v == 2) GOSSIP_PC(12, 2, 2, 3);
-            else if (v == 4) GOSSIP_PC(8, 4, 4, 3);
-            else GOSSIP_PC(8, 2, 4, 3);
-        });
-#undef GOSSIP_PC
-        return hipGetLastError();
-    }
-    GOSSIP_DISPATCH_W(wp_of(W_), {  // one workgroup per CU (128 KB of LDS each)
-        if (a.cov)
-            hipLaunchKernelGGL((k_bin_scatter_lds<W, true, 4>), dim3(kScatterGrid), dim3(kScatterBlock), 0, s, a, b, wd);
-        else if (scatter_u() == 8)
-            hipLaunchKernelGGL((k_bin_scatter_lds<W, false, 8>), dim3(kScatterGrid), dim3(kScatterBlock), 0, s, a, b, wd);
-        else hipLaunchKernelGGL((k_bin_scatter_lds<W, false, 4>), dim3(kScatterGrid), dim3(kScatterBlock), 0, s, a, b, wd);
+    // 8 producer waves resolving 2 groups per stage into 4-slot rings, 3 register sets (measured best:
+    // DESIGN.md section 6.1)
+#define GOSSIP_PC(COV) \
+    hipLaunchKernelGGL((k_bin_scatter_pc<W, COV, 8, 2, 4, 3>), dim3(kScatterGrid), dim3(kScatterBlock), 0, s, a, b, wd)
+    GOSSIP_DISPATCH_W(wp_of(W_), {
+        if (a.cov) GOSSIP_PC(true);
+        else GOSSIP_PC(false);
     });
+#undef GOSSIP_PC
     return hipGetLastError();
 }
 
@@ -2984,8 +2385,7 @@ hipError_t launch_bin_apply(const RoundArgs& a, const BinArgs& b, uint32_t W_, h
         }
         return hipGetLastError();
     }
-    // split bins: the parts of bin i at block ids 8 (i / 8 * split + part) + i % 8
-    const unsigned grid = (unsigned)(b.split > 1 ? (b.n_bins + 7) / 8 * 8 * b.split : b.n_bins);
+    const unsigned grid = (unsigned)b.n_bins;
     if (b.bin_words > kBinWords / 2) {  // up to 144 KB accumulators: one 16-wave workgroup per CU
         GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_apply<W, kBinWords, 1024>), dim3(grid), dim3(1024), 0,
                                                        s, a, b, wd));
@@ -3068,12 +2468,6 @@ hipError_t launch_src_count(const RoundArgs& a, uint32_t W_, hipStream_t s) {
     const uint64_t tiles = (a.n_local + 63) / 64;
     GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_src_count<W>, dim3(grid_for(tiles, kWavesPerBlock)), dim3(kBlock),
                                                    0, s, a));
-    return hipGetLastError();
-}
-
-hipError_t launch_count_nx(const RoundArgs& a, uint32_t W_, hipStream_t s) {
-    GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_count_nx<W>, dim3(grid_for(a.n_local, kBlock)), dim3(kBlock), 0, s,
-                                                   a));
     return hipGetLastError();
 }
 

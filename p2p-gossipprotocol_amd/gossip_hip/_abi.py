@@ -31,11 +31,14 @@ FLAG_FORCE_PUSH = 2
 FLAG_FORCE_PULL = 4
 FLAG_NO_BIN = 8
 FLAG_FORCE_BIN = 16
+FLAG_NO_BLOCKED = 32
+FLAG_FORCE_BLOCKED = 64
 MODE_AUTO = -1
 MODE_PUSH = 0
 MODE_PULL = 1
 MODE_PUSH_SPARSE = 2
 MODE_BIN = 3
+MODE_BLOCKED = 4
 
 
 class GossipConfig(C.Structure):
@@ -62,6 +65,7 @@ class GossipConfig(C.Structure):
         ("extra_cap", C.c_uint32),
         ("list_cap", C.c_uint32),
         ("rejoin_threshold", C.c_uint32),
+        ("blocked_permille", C.c_uint32),
     ]
 
 
@@ -137,6 +141,7 @@ def lib() -> C.CDLL:
         "gossip_enable_timing": (i32, [P, i32]),
         "gossip_kernel_time": (i32, [P, C.c_char_p, C.POINTER(C.c_double), pu64]),
         "gossip_kernel_bytes": (i32, [P, C.c_char_p, C.POINTER(C.c_double)]),
+        "gossip_set_tuning": (i32, [P, C.c_char_p, C.c_int64]),
         # library-driven multi-GPU rounds (gossip_dist.hip)
         "gossip_partition": (i32, [u64, u32, pu64]),
         "gossip_comm_unique_id": (i32, [pu8]),

@@ -63,7 +63,8 @@ def make_config(n_peers: int, n_msgs: int, *, rng_seed: int = 0, graph: str = "p
                 max_rounds: int = 4096, min_rounds: int = 0, device: int = -1, coverage_history: bool = False,
                 part: tuple[int, int] = (0, 0), report_capacity: int = 0, mode: str = "auto",
                 pull_permille: int = 0, front_permille: int = 0, bin_permille: int = 0, bins: bool = True,
-                extra_cap: int = 0, list_cap: int = 0, rejoin_threshold: int = 0) -> GossipConfig:
+                extra_cap: int = 0, list_cap: int = 0, rejoin_threshold: int = 0, blocked: str = "auto",
+                blocked_permille: int = 0) -> GossipConfig:
     """gossip_config from keyword arguments (the fields of include/gossip/gossip.h)."""
     cfg = GossipConfig()
     cfg.n_peers = n_peers
@@ -80,7 +81,8 @@ def make_config(n_peers: int, n_msgs: int, *, rng_seed: int = 0, graph: str = "p
     cfg.min_rounds = min_rounds
     cfg.device = device
     cfg.flags = (_abi.FLAG_COVERAGE_HISTORY if coverage_history else 0) | (0 if bins else _abi.FLAG_NO_BIN) | {
-        "auto": 0, "push": _abi.FLAG_FORCE_PUSH, "pull": _abi.FLAG_FORCE_PULL, "bin": _abi.FLAG_FORCE_BIN}[mode]
+        "auto": 0, "push": _abi.FLAG_FORCE_PUSH, "pull": _abi.FLAG_FORCE_PULL, "bin": _abi.FLAG_FORCE_BIN}[mode] | {
+        "auto": 0, "off": _abi.FLAG_NO_BLOCKED, "force": _abi.FLAG_FORCE_BLOCKED}[blocked]
     cfg.report_capacity = report_capacity
     cfg.pull_permille = pull_permille
     cfg.front_permille = front_permille
@@ -88,17 +90,21 @@ def make_config(n_peers: int, n_msgs: int, *, rng_seed: int = 0, graph: str = "p
     cfg.extra_cap = extra_cap
     cfg.list_cap = list_cap
     cfg.rejoin_threshold = rejoin_threshold
+    cfg.blocked_permille = blocked_permille
     return cfg
 
 
 class Engine:
-    def __init__(self, n_peers: int, n_msgs: int, *, part: tuple[int, int] = (0, 0), **kw):
+    def __init__(self, n_peers: int, n_msgs: int, *, part: tuple[int, int] = (0, 0), tuning: dict | None = None,
+                 **kw):
         self._L = _abi.lib()
         cfg = make_config(n_peers, n_msgs, part=part, **kw)
         self.cfg = cfg
         ctx = C.c_void_p()
         check(self._L.gossip_create(C.byref(cfg), C.byref(ctx)), "gossip_create")
         self._ctx = ctx
+        for key, value in (tuning or {}).items():
+            self.set_tuning(key, value)
         self.n_peers = n_peers
         self.n_msgs = n_msgs
         self.begin, self.end = (part if part != (0, 0) else (0, n_peers))
@@ -300,6 +306,11 @@ class Engine:
         out = np.zeros(self.n_peers, dtype=np.uint8)
         check(self._L.gossip_read_registered(self._ctx, _ptr(out, C.c_uint8)), "gossip_read_registered")
         return out
+
+    def set_tuning(self, key: str, value: int) -> None:
+        """gossip_set_tuning: a parity-tested engineering option of this ctx (layout keys apply at the
+        next build_graph / load_csr)."""
+        check(self._L.gossip_set_tuning(self._ctx, key.encode(), int(value)), f"gossip_set_tuning({key})")
 
     # -- measurement ------------------------------------------------------------
     def enable_timing(self, on: bool = True) -> None:

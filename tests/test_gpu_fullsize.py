@@ -64,6 +64,18 @@ def test_fullsize_config3_schedules_match_oracle(oracle, mode):
         _check_run(oracle, e, w, g, check_csr=False)
 
 
+@pytest.mark.parametrize("idx", [3, 5])
+def test_fullsize_forced_blocked_matches_oracle(oracle, idx):
+    """Every push and binned round propagation-blocked (gossip_blocked.hip) at
+    full size: config 3 (2^24 peers) and config 5 (2^26, churn: undelivered
+    sends to dead peers) against the same fixtures."""
+    g = GOLDEN[str(idx)]
+    w = config(idx)
+    with Engine(w.n, w.n_msgs, blocked="force", **w.engine_kwargs()) as e:
+        e.build_graph()
+        _check_run(oracle, e, w, g, check_csr=False)
+
+
 @pytest.mark.parametrize("idx,P", [(4, 2), (4, 4), (5, 2)])
 def test_fullsize_partitioned_group_matches_oracle(oracle, idx, P):
     """The N-GPU path at full size (BASELINE configs 4 and 5): the library's

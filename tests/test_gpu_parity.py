@@ -88,6 +88,31 @@ def test_workload_parity(oracle, idx, n, mode):
         assert e.run() == first
 
 
+@pytest.mark.parametrize("blocked", ["force", "auto"])
+@pytest.mark.parametrize("idx,n", [(2, 1 << 16), (3, 1 << 18), (5, 1 << 16), (5, 50_000), (3, 1 << 20)])
+def test_blocked_push_parity(oracle, idx, n, blocked):
+    """Propagation-blocked push rounds (gossip_blocked.hip): every push and binned
+    round forced blocked, and the default schedule with its blocked rounds --
+    against the oracle's per-round stats, seen sets, reports, alive and registry
+    (broadcastMessage peer.cpp:310-316 -> handleClient peer.cpp:277-285; dead
+    targets are undelivered sends, peer.cpp:312)."""
+    w = config(idx, n, pick=oracle.pick_origins)
+    rp, col = oracle.gen_workload(w)
+    ref = oracle.simulate_workload(w, rp, col)
+    with _engine(w, blocked=blocked) as e:
+        e.enable_timing(True)
+        e.build_graph()
+        e.inject(w.origins, w.inject_rounds)
+        if w.kills:
+            e.schedule_kills([k[0] for k in w.kills], [k[1] for k in w.kills])
+        e.reset()
+        first = _compare(e, ref, w)
+        if blocked == "force":
+            assert e.kernel_time("pb_apply")[1] > 0  # the blocked path ran
+        e.reset()
+        assert e.run() == first
+
+
 @pytest.mark.parametrize("mode", ["push", "pull", "bin"])
 @pytest.mark.parametrize("M", [65, 130, 300, 512])
 def test_multiword_messages(oracle, M, mode):
@@ -249,8 +274,7 @@ def test_closed_form_liveness_kills_and_hubs(oracle, max_missed, ping):
     of a dead peer are visited through its own row at its max_missed-th ping
     round; hubs (heavy rows, chunked) and light peers killed at various
     rounds, with churn on top; bit-exact against the oracle's per-edge miss
-    counters, and equal to the engine's own per-edge scan (GOSSIP_FULL_LIVENESS)."""
-    import os
+    counters, and equal to the engine's own per-edge scan ("full_liveness")."""
     base = config(2, 1 << 14, pick=oracle.pick_origins)
     kills = [(0, 1), (1, 2), (5, 2), (100, 4), (7777, 0), (2, 6)]
     w = dataclasses.replace(base, kills=kills, ping_every=ping, max_missed=max_missed, min_rounds=24,
@@ -259,17 +283,13 @@ def test_closed_form_liveness_kills_and_hubs(oracle, max_missed, ping):
     ref = oracle.simulate_workload(w, rp, col)
     assert sum(s["reports"] for s in ref["stats"]) > 0
     runs = []
-    for full in ("0", "1"):
-        os.environ["GOSSIP_FULL_LIVENESS"] = full
-        try:
-            with _engine(w) as e:
-                e.build_graph()
-                e.inject(w.origins, w.inject_rounds)
-                e.schedule_kills([k[0] for k in w.kills], [k[1] for k in w.kills])
-                e.reset()
-                runs.append(_compare(e, ref, w))
-        finally:
-            del os.environ["GOSSIP_FULL_LIVENESS"]
+    for full in (0, 1):
+        with _engine(w, tuning={"full_liveness": full}) as e:
+            e.build_graph()
+            e.inject(w.origins, w.inject_rounds)
+            e.schedule_kills([k[0] for k in w.kills], [k[1] for k in w.kills])
+            e.reset()
+            runs.append(_compare(e, ref, w))
     assert runs[0] == runs[1]
 
 
@@ -305,21 +325,29 @@ def test_reload_overlay_with_kills(oracle, mode):
             _compare(e, ref, w)
 
 
-@pytest.mark.parametrize("env", ["GOSSIP_DEFER_PM=1", "GOSSIP_BIN_STREAM=1", "GOSSIP_PULL_ROWS=0", "GOSSIP_BIN_SPLIT=2",
-                                 "GOSSIP_BIN_SPLIT=3", "GOSSIP_PULL_DEFER=1", "GOSSIP_BIN_PERMILLE=100000",
-                                 "GOSSIP_PULL_FIRST2=0", "GOSSIP_DEFER_NR=1", "GOSSIP_FLIGHT=0"])
+_VARIANTS = {"defer_1": ({"defer_permille": 1}, {"blocked": "off"}), "stream": ({"bin_stream": 1}, {}),
+             "slots": ({"bin_stream": 0}, {}), "no_first2": ({"pull_first2": 0}, {}),
+             "no_flight": ({"in_flight": 0}, {}), "no_heavy_exit": ({"heavy_exit": 0}, {}),
+             "small_bins": ({"bin_words": 4096, "bin_chunk": 2048}, {}), "apply_src": ({"src_stats": 0}, {}),
+             "heavy_64": ({"heavy_degree": 64, "heavy_chunk": 128}, {}), "all_pull": ({}, {"bin_permille": 100000}),
+             "blocked_wide": ({}, {"blocked_permille": 1000})}
+
+
+@pytest.mark.parametrize("variant", sorted(_VARIANTS))
 @pytest.mark.parametrize("idx,n,mode", [(2, 1 << 16, "auto"), (3, 1 << 18, "bin"), (5, 50_000, "auto"),
                                         (5, 1 << 16, "push"), (3, 1 << 18, "pull")])
-def test_engine_variants_match_oracle(oracle, monkeypatch, env, idx, n, mode):
-    """The A/B variants the engine keeps behind environment switches (read at
-    gossip_create): the deferred seen update of wide push rounds, the streamed
-    binned layout and the tile-expansion pull give the oracle's results too."""
-    k, v = env.split("=")
-    monkeypatch.setenv(k, v)
+def test_engine_variants_match_oracle(oracle, variant, idx, n, mode):
+    """The A/B variants the engine keeps as explicit options (gossip_set_tuning,
+    never the environment): the deferred seen update of wide push rounds, both
+    binned layouts, the row pull's first-two-entries and in-flight tests, the
+    heavy-row early exit and threshold, bin and chunk sizes, who books a binned
+    round's source side, and the schedule switches -- all give the oracle's
+    results."""
+    tuning, kw = _VARIANTS[variant]
     w = config(idx, n, pick=oracle.pick_origins)
     rp, col = oracle.gen_workload(w)
     ref = oracle.simulate_workload(w, rp, col)
-    with _engine(w, mode=mode) as e:
+    with _engine(w, mode=mode, tuning=tuning, **kw) as e:
         e.build_graph()
         e.inject(w.origins, w.inject_rounds)
         if w.kills:
@@ -328,24 +356,22 @@ def test_engine_variants_match_oracle(oracle, monkeypatch, env, idx, n, mode):
         _compare(e, ref, w)
 
 
-@pytest.mark.parametrize("env", [None, "GOSSIP_DEFER_PM=10", "GOSSIP_PULL_DEFER=1",
-                                 "GOSSIP_PULL_DEFER=1 GOSSIP_BIN_PERMILLE=100000"])
+@pytest.mark.parametrize("variant", ["auto", "defer_10", "all_pull", "defer_10_all_pull"])
 @pytest.mark.parametrize("stop", [3, 4, 5, 6, 7, 8])
-def test_deferred_round_fold(oracle, monkeypatch, env, stop):
-    """Auto mode defers the seen update of the wide push round before the binned
-    rounds (config 3 shape: round 2 here) and of wide pull rounds, and leaves
+def test_deferred_round_fold(oracle, variant, stop):
+    """With blocked push rounds off, auto mode defers the seen update of the wide
+    push round before the binned rounds (config 3 shape: round 2 here) and leaves
     the fold to the next round's apply or row-pull sweep.  A run stopped by
     max_rounds right after a deferred round, or after the fused fold, must still
-    read the oracle's seen set and coverage; the explicit switches force the
-    deferrals (committed when the fold cannot be fused), and a huge binned
-    threshold turns the binned rounds into pulls (pull -> pull folds)."""
-    for kv in (env or "").split():
-        k, v = kv.split("=")
-        monkeypatch.setenv(k, v)
+    read the oracle's seen set and coverage; the explicit option forces the
+    deferral (committed when the fold cannot be fused), and a huge binned
+    threshold turns the binned rounds into pulls (push -> pull folds)."""
+    tuning = {"defer_permille": 10} if "defer_10" in variant else {}
+    kw = {"bin_permille": 100000} if "all_pull" in variant else {}
     w = config(3, 1 << 18, pick=oracle.pick_origins)
     rp, col = oracle.gen_workload(w)
     ref = oracle.simulate_workload(w, rp, col, max_rounds=stop)
-    with Engine(w.n, w.n_msgs, max_rounds=stop, **w.engine_kwargs()) as e:
+    with Engine(w.n, w.n_msgs, max_rounds=stop, blocked="off", tuning=tuning, **kw, **w.engine_kwargs()) as e:
         e.build_graph()
         e.inject(w.origins, w.inject_rounds)
         e.reset()
@@ -358,19 +384,18 @@ def test_deferred_round_fold(oracle, monkeypatch, env, stop):
 @pytest.mark.parametrize("tiny", ["1", "0"])
 @pytest.mark.parametrize("idx,n,max_rounds", [(1, None, 0), (1, 40, 0), (1, 40, 20), (2, 4096, 0), (3, 2048, 0),
                                                (5, 4096, 0), (5, 6000, 7), (5, 6000, 0)])
-def test_small_overlay_one_launch_matches_oracle(oracle, monkeypatch, tiny, idx, n, max_rounds):
+def test_small_overlay_one_launch_matches_oracle(oracle, tiny, idx, n, max_rounds):
     """Small overlays (<= 65,536 peers and edges) run whole in one launch
     (gossip_tiny.hip: kills, churn, liveness with reports and registry,
-    injection, push, stats and termination on the device); GOSSIP_TINY=0 runs
-    them round by round.  Both give the oracle's every round, seen set,
+    injection, push, stats and termination on the device); the option runs
+    them round by round ("tiny" = 0).  Both give the oracle's every round, seen set,
     coverage, reports, alive flags and registry, also when max_rounds cuts the
     run short; a second run from reset repeats the first."""
-    monkeypatch.setenv("GOSSIP_TINY", tiny)
     w = config(idx, n, pick=oracle.pick_origins)
     kw = {"max_rounds": max_rounds} if max_rounds else {}
     rp, col = oracle.gen_workload(w)
     ref = oracle.simulate_workload(w, rp, col, **kw)
-    with _engine(w, **kw) as e:
+    with _engine(w, tuning={"tiny": int(tiny)}, **kw) as e:
         e.build_graph()
         e.inject(w.origins, w.inject_rounds)
         if w.kills:
