@@ -314,7 +314,11 @@ gossip_status gossip_kernel_bytes(gossip_ctx* ctx, const char* kernel, double* b
  * of the closed form), "defer_permille" (-1 auto), "bin_stream" (-1 by size,
  * 0/1 forced), "pull_first2", "in_flight", "heavy_exit", "heavy_degree",
  * "heavy_chunk", "bin_front_permille", "bin_words", "bin_chunk", "val_tune"
- * (-1 auto, 0, 1, 2 = print), "src_stats" (-1 auto, 0/1).  Layout keys apply at
+ * (-1 auto, 0, 1, 2 = print), "src_stats" (-1 auto, 0/1), "blocked_bin_slots"
+ * (slot-array size from which dense rounds below blocked_permille run
+ * blocked; -1 default 2^28), "blocked_direct_in" (layout: leading 64-peer
+ * tiles of more in-degree take direct deliveries; -1 default 2^18).  Layout
+ * keys apply at
  * the next gossip_build_graph / gossip_load_csr.  GOSSIP_EINVAL: unknown key. */
 gossip_status gossip_set_tuning(gossip_ctx* ctx, const char* key, int64_t value);
 

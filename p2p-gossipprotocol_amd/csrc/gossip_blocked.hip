@@ -131,14 +131,20 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_scatter(RoundArgs a, PbArgs p, 
             any |= dir[j];
         }
         if (!__ballot(any)) return;  // (most batches: no hub among the destinations)
+        // a.fold: the hub's own new words (nw, left for the split to clear) are not yet in seen everywhere
+        unsigned long long nwc[kPbU];
 #pragma unroll
-        for (int j = 0; j < kPbU; ++j) cur[j] = a.seen[dir[j] ? c[j] : 0];
+        for (int j = 0; j < kPbU; ++j) {
+            cur[j] = a.seen[dir[j] ? c[j] : 0];
+            nwc[j] = a.fold && dir[j] ? a.nw[c[j]] : 0ull;
+        }
 #pragma unroll
         for (int j = 0; j < kPbU; ++j) {
             if (!dir[j]) continue;
             rec[j] = false;
-            if (!(m[j] & ~cur[j])) continue;  // all duplicates: dropped (peer.cpp:281)
-            const unsigned long long fr = m[j] & ~atomicOr(reinterpret_cast<unsigned long long*>(a.seen) + c[j], m[j]);
+            if (!(m[j] & ~(cur[j] | nwc[j]))) continue;  // all duplicates: dropped (peer.cpp:281)
+            const unsigned long long fr =
+                m[j] & ~nwc[j] & ~atomicOr(reinterpret_cast<unsigned long long*>(a.seen) + c[j], m[j]);
             acc.atomics++;
             acc.fresh_or[0] |= fr;
             if (!fr) continue;
@@ -224,7 +230,9 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_scatter(RoundArgs a, PbArgs p, 
                 rb = a.rp[v];
                 const uint64_t d = a.rp[v + 1] - rb;
                 deg = d <= a.heavy ? (uint32_t)d : 0u;  // heavy rows: (1)
-                if (d <= a.heavy) a.nw[v] = 0ull;  // consumed: this buffer is the next round's accumulator
+                // consumed: this buffer is the next round's accumulator (the hubs' words are read by
+                // direct(), heavy rows' by their chunks: the split clears those)
+                if (d <= a.heavy && v >= p.direct_end) a.nw[v] = 0ull;
             }
             const uint32_t rest = n_pk - cnt;
             wave_sync();
@@ -277,6 +285,10 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_scatter(RoundArgs a, PbArgs p, 
             const unsigned long long bal = __ballot(act);
             if (!bal) return;
             if (act) {  // push start: the new words are the bits added to seen since the last one
+                if (a.fold) {  // the previous round deferred: its receipts (m) join seen here
+                    if (v < p.direct_end) atomicOr(reinterpret_cast<unsigned long long*>(a.seen) + v, m);
+                    else a.seen[v] |= m;  // (only direct() writes seen during this pass, hubs only)
+                }
                 acc.frontier++;
                 const uint32_t pc = (uint32_t)__popcll(m);
                 acc.covered += pc;
@@ -339,6 +351,8 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_split(PbArgs p) {
     __shared__ uint32_t tk_s[kPbFineMax], wr_s[kPbFineMax], dn_s[kPbFineMax];
     __shared__ unsigned long long base_s[kPbFineMax];  // this slice's segment of each fine bin
     __shared__ uint32_t cap_s[kPbFineMax];
+    __shared__ unsigned long long sb_s[kPbGrid / kPbSlices];  // the slice's level-1 segments of bin k
+    __shared__ uint32_t sn_s[kPbGrid / kPbSlices];
     __shared__ uint16_t bd_s[kPbFineMax * kPbB2];
     __shared__ unsigned long long bw_s[kPbFineMax * kPbB2];
     const uint32_t k = blockIdx.x / kPbSlices, sl = blockIdx.x % kPbSlices;
@@ -349,12 +363,20 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_split(PbArgs p) {
         base_s[i] = i < nf ? p.s2_base[(uint64_t)sl * p.n_fine + f0 + i] : 0ull;
         cap_s[i] = i < nf ? p.s2_cap[(uint64_t)sl * p.n_fine + f0 + i] : 0u;
     }
+    const uint32_t nc = p.n_coarse;
+    const uint32_t w0 = sl * (kPbGrid / kPbSlices);
+    for (uint32_t i = threadIdx.x; i < kPbGrid / kPbSlices; i += kPbBlock) {  // all at once, not one per pass
+        sb_s[i] = p.s1_base[(uint64_t)(w0 + i) * nc + k];
+        sn_s[i] = p.s1_len[(uint64_t)(w0 + i) * nc + k];
+    }
     // the heavy rows' new words, consumed by level 1 (one word per row: its first chunk)
     for (uint64_t ci = (uint64_t)blockIdx.x * kPbBlock + threadIdx.x; ci < p.n_chunks;
          ci += (uint64_t)gridDim.x * kPbBlock) {
         const HeavyChunk ch = p.chunks[ci];
         if (ch.first == ci) p.nw[ch.v] = 0ull;
     }
+    for (uint64_t v = (uint64_t)blockIdx.x * kPbBlock + threadIdx.x; v < p.direct_end; v += (uint64_t)gridDim.x * kPbBlock)
+        p.nw[v] = 0ull;  // and the hubs'
     __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     auto flush2 = [&](uint32_t f) {  // 64 destinations (128 B), 64 words (512 B)
@@ -371,11 +393,9 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_split(PbArgs p) {
             atomicOr(p.err, 2u);
         }
     };
-    const uint32_t nc = p.n_coarse;
-    const uint32_t w0 = sl * (kPbGrid / kPbSlices), w1 = w0 + kPbGrid / kPbSlices;
-    for (uint32_t w = w0; w < w1; ++w) {
-        const uint64_t base = p.s1_base[(uint64_t)w * nc + k];
-        const uint32_t n = p.s1_len[(uint64_t)w * nc + k];
+    for (uint32_t w = 0; w < kPbGrid / kPbSlices; ++w) {
+        const uint64_t base = sb_s[w];
+        const uint32_t n = sn_s[w];
         for (uint32_t i0 = (uint32_t)wave * 64 * kPbU; i0 < n; i0 += kPbBlock * kPbU) {  // wave-uniform
             uint32_t d[kPbU], f[kPbU], dl[kPbU];
             unsigned long long x[kPbU];
@@ -615,7 +635,8 @@ PbArgs pb_args(const PbState& p) {
     } while (0)
 
 hipError_t build_pb(const uint64_t* rp, const uint32_t* col, uint64_t n_local, uint64_t n_edges, uint32_t heavy,
-                    const HeavyChunk* chunks, uint64_t n_chunks, hipStream_t s, PbState* out, std::string* err) {
+                    const HeavyChunk* chunks, uint64_t n_chunks, uint64_t direct_in, hipStream_t s, PbState* out,
+                    std::string* err) {
     PbState st;
     uint32_t *d_cnt1 = nullptr, *d_cnt2 = nullptr;
     uint64_t* d_rpt = nullptr;
@@ -652,10 +673,10 @@ hipError_t build_pb(const uint64_t* rp, const uint32_t* col, uint64_t n_local, u
     }
     const uint64_t n_fine = f_lo.size();
     f_lo.push_back((uint32_t)n_local);
-    // the hubs: the leading tiles of over kPbFineIn in-degree each (a Chung-Lu overlay's lowest ids)
+    // the hubs: the leading tiles of over direct_in in-degree each (a Chung-Lu overlay's lowest ids)
     {
         uint64_t t = 0;
-        while (t < n_tiles && tin[t] > kPbFineIn) ++t;
+        while (t < n_tiles && tin[t] > direct_in) ++t;
         st.direct_end = (uint32_t)std::min<uint64_t>(t * 64, n_local);
     }
     // coarse bins: runs of whole fine bins of about equal in-degree, <= kPbFineMax fine bins each

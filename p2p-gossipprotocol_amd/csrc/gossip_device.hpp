@@ -111,7 +111,7 @@ __device__ __forceinline__ int src_lane(uint32_t incl, uint32_t p) {
     return s;
 }
 
-unsigned grid_for(uint64_t items, uint64_t per_block) {
+inline unsigned grid_for(uint64_t items, uint64_t per_block) {
     uint64_t g = (items + per_block - 1) / per_block;
     if (g < 1) g = 1;
     if (g > kMaxGrid) g = kMaxGrid;

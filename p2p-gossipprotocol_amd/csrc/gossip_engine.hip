@@ -165,6 +165,9 @@ struct gossip_ctx {
     int val_tune = -1;            // "val_tune": pick the slot array's allocation by trial scatters (-1: by size,
                                   // 0: never, 1: always, 2: and print the trials)
     int src_stats_req = -1;       // "src_stats": who books a binned round's source side (-1: by layout)
+    uint64_t pb_bin_slots = kPbBinSlots;  // "blocked_bin_slots": slot arrays from this size run their
+                                          // sparser dense rounds blocked
+    uint64_t pb_direct_in = kPbFineIn;    // "blocked_direct_in": leading tiles of more in-degree are hubs
     bool bin_stream = false;      // streamed binned layout (chosen in prepare_bins)
     int bin_stream_req = -1;      // "bin_stream": 0/1 forces the layout; -1: by slot-array size
     uint32_t defer_pm = kDeferAuto;  // "defer_permille": push rounds with a frontier of >= this per-mille defer
@@ -671,7 +674,7 @@ gossip_status prepare_pb(gossip_ctx* c) {
         return GOSSIP_OK;
     std::string err;
     const hipError_t e = build_pb(c->rp, c->col, c->n_local, c->n_edges, c->heavy, c->chunks, c->n_chunks,
-                                  c->stream, &c->pb, &err);
+                                  c->pb_direct_in, c->stream, &c->pb, &err);
     if (e == hipErrorOutOfMemory || e == hipErrorInvalidValue) return GOSSIP_OK;  // push rounds stay atomic
     if (e != hipSuccess) return fail(GOSSIP_EHIP, "blocked-push regions: " + err);
     c->pb_ready = true;
@@ -913,9 +916,12 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
         }
     }
     // propagation-blocked push (gossip_blocked.hip; one partition, one word per peer): a push round from a
-    // 0.2 % frontier estimate -- below it the atomic push's few deliveries cost less than the blocked
-    // round's sweeps -- and a binned round below blocked_permille (every edge streamed for a minority of
-    // active sources) write one record per delivery instead
+    // 5 % frontier estimate -- below it the atomic push's deliveries cost less than the blocked round's
+    // fixed passes (config 3 round 2, 2.1 %: push 0.25 ms, blocked 0.79 ms) -- and, where the slot array
+    // outgrows the MALL many times over (>= kPbBinSlots slots: its scattered stores go to HBM as partial
+    // lines), a binned round below blocked_permille (every edge streamed for a minority of active
+    // sources) write one record per delivery instead (config 4 round 4, 17 %: binned 15.6 ms, blocked
+    // 11.5 ms; config 3 round 3, 16 %, 1 GiB of slots: binned 1.17 ms, blocked 2.05 ms)
     c->cur_pb = false;
     if (c->pb_ready && !remote && c->world <= 1 && requested == GOSSIP_MODE_AUTO &&
         !(c->cfg.flags & (GOSSIP_FLAG_FORCE_PUSH | GOSSIP_FLAG_FORCE_PULL | GOSSIP_FLAG_FORCE_BIN))) {
@@ -925,16 +931,17 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
             c->cur_pb = !pull || bin;
         else
             c->cur_pb = (!pull && front * 1000 >= c->n_local * (uint64_t)kPbLoPermille) ||
-                        (bin && front * 1000 < c->n_local * (uint64_t)hi);
+                        (bin && (!c->bins_ready || c->bins.n_slots >= c->pb_bin_slots) &&
+                         front * 1000 < c->n_local * (uint64_t)hi);
         if (c->cur_pb) pull = bin = false;
     }
     c->cur_sparse = !pull && remote && requested == GOSSIP_MODE_PUSH_SPARSE && c->seg != nullptr;
     // a wide push round (the explosion before the dense rounds) is bound by memory-side atomics, two per
     // fresh delivery (seen, then nx); deferring the seen update halves them for one streamed pass
     // (k_commit_nx).  A per-rank choice: results do not depend on it.
-    // Auto: only where the fold can ride on the next binned round's apply (one partition, the
-    // slot layout, no churn); config 4 round 3: push 5.6 -> 4.1 ms, the 1.3 ms fold pass removed.
-    const bool fusable = c->world <= 1 && !remote && c->bins_ready && !c->cfg.churn_threshold &&
+    // Auto: only where the fold can ride on the next dense round's sweep (one partition, the slot layout
+    // or the blocked regions, no churn); config 4 round 3: push 5.6 -> 4.1 ms, the 1.3 ms fold pass removed.
+    const bool fusable = c->world <= 1 && !remote && (c->bins_ready || c->pb_ready) && !c->cfg.churn_threshold &&
                          !c->cfg.rejoin_threshold && requested == GOSSIP_MODE_AUTO;
     const uint32_t dpm = c->defer_pm == kDeferAuto ? (fusable ? 10u : 0u) : c->defer_pm;
     c->cur_defer = !pull && !c->cur_pb && dpm && (c->frontier_est + cnt) * 1000 >= c->n_local * (uint64_t)dpm;
@@ -942,8 +949,9 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
     a.defer = c->cur_defer ? 1u : 0u;
     const bool rows_pull = pull && !bin;  // k_pull_rows
     if (c->fold_pending) {  // the previous round deferred: its receipts are this round's nw
-        if ((bin || rows_pull) && c->world <= 1 && !remote) {
-            a.fold = 1;  // k_bin_apply / k_pull_rows's sweep folds them (before k_pull_heavy reads seen)
+        if ((bin || rows_pull || c->cur_pb) && c->world <= 1 && !remote) {
+            a.fold = 1;  // k_bin_apply / k_pull_rows's / k_pb_scatter's sweep folds them (before k_pull_heavy
+                         // or k_pb_apply read seen)
             c->fold_pending = false;
         } else if (gossip_status fs = settle_fold(c)) {
             return fs;
@@ -1441,6 +1449,8 @@ gossip_status gossip_set_tuning(gossip_ctx* c, const char* key, int64_t value) {
     else if (k == "bin_chunk") c->bin_chunk_req = u;
     else if (k == "val_tune") c->val_tune = value < 0 ? -1 : (int)std::min<int64_t>(value, 2);
     else if (k == "src_stats") c->src_stats_req = value < 0 ? -1 : (value != 0);
+    else if (k == "blocked_bin_slots") c->pb_bin_slots = value < 0 ? kPbBinSlots : (uint64_t)value;
+    else if (k == "blocked_direct_in") c->pb_direct_in = value < 0 ? kPbFineIn : (uint64_t)value;
     else return fail(GOSSIP_EINVAL, "unknown tuning option: " + k);
     return GOSSIP_OK;
 }

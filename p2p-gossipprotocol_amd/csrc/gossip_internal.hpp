@@ -149,7 +149,8 @@ constexpr int kPbBlock = 1024;         // 16 waves per workgroup, one workgroup 
 constexpr int kPbGrid = 256;           // level-1 workgroups (row ranges)
 constexpr uint32_t kPbPad = 0xFFFFFFFFu;  // level-1 padding record (level 2: 0xFFFF)
 constexpr uint32_t kPbMap = 4096;         // level 1's id buckets (coarse bin lookup)
-constexpr uint32_t kPbLoPermille = 20;    // push rounds from this frontier run blocked ...
+constexpr uint32_t kPbLoPermille = 50;    // push rounds from this frontier run blocked ...
+constexpr uint64_t kPbBinSlots = 1ull << 28;  // ... and dense rounds where the slot array has this many slots ...
 constexpr uint32_t kPbHiPermille = 300;   // ... and dense rounds below this one (gossip_config.blocked_permille)
 
 struct PbArgs {
@@ -235,11 +236,12 @@ struct RoundArgs {
     uint32_t tsparse;              // tcur is valid: push_light visits only its tiles
     uint32_t defer;                // push round with a deferred seen update: deliveries test against the
                                    // round-start seen and OR the unseen bits into nx only (one atomic per
-                                   // delivery); k_commit_nx folds nx into seen after the round.  2: the
-                                   // atomics return nothing and k_count_nx counts the receipts from nx
+                                   // delivery); the next round's sweep (fold), or k_commit_nx, folds nx
+                                   // into seen
     uint32_t fold;                 // round after a deferred round: seen lacks this round's new words (nw);
-                                   // k_bin_apply, or k_pull_rows's sweep, folds them in (seen | nw) for
-                                   // every owned peer before anything else of the round reads seen
+                                   // k_bin_apply, k_pull_rows's or k_pb_scatter's sweep folds them in
+                                   // (seen | nw) for every owned peer before anything else of the round
+                                   // reads seen (k_pb_scatter's hub deliveries test against seen | nw)
     const uint64_t* first2;        // pull rounds with many needy rows (nullptr otherwise): per owned peer the
                                    // first two entries of its row (col[rp[v]] | col[rp[v] + 1] << 32; no
                                    // masked edges), read with the sweep so a row's first step needs no
@@ -348,10 +350,12 @@ hipError_t launch_heavy_fill(const uint64_t* rp, uint64_t n_local, uint32_t heav
                              unsigned long long* cursor, hipStream_t s);
 
 // ---- propagation-blocked push rounds (gossip_blocked.hip) ----
-// Bins and segments of both levels (P = 1; rows longer than heavy are the chunks', in row order).
+// Bins and segments of both levels (P = 1; rows longer than heavy are the chunks', in row order); the
+// leading tiles of over direct_in in-degree each are delivered directly (kPbFineIn by default).
 // hipErrorOutOfMemory: skipped (state untouched).
 hipError_t build_pb(const uint64_t* rp, const uint32_t* col, uint64_t n_local, uint64_t n_edges, uint32_t heavy,
-                    const HeavyChunk* chunks, uint64_t n_chunks, hipStream_t s, PbState* out, std::string* err);
+                    const HeavyChunk* chunks, uint64_t n_chunks, uint64_t direct_in, hipStream_t s, PbState* out,
+                    std::string* err);
 void free_pb(PbState* p);
 PbArgs pb_args(const PbState& p);
 // one blocked push round: level 1 (each workgroup's heavy rows, then its light rows), level 2, apply

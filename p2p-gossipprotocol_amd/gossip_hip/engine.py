@@ -17,8 +17,8 @@ from ._abi import DeadReport, GossipConfig, RoundStats, check
 
 _GRAPHS = {"powerlaw": _abi.GRAPH_POWERLAW, "ref_bootstrap": _abi.GRAPH_REF_BOOTSTRAP}
 KERNELS = ("push_light", "push_heavy", "push_extra", "src_count", "frontier_bits", "pull_light", "pull_heavy", "bin_scatter",
-           "bin_apply", "liveness", "rebootstrap", "rejoin", "churn", "kills", "inject", "apply_remote", "commit", "count_nx",
-           "compact_send", "tiny")
+           "bin_apply", "pb_scatter", "pb_split", "pb_apply", "liveness", "rebootstrap", "rejoin", "churn", "kills",
+           "inject", "apply_remote", "commit", "compact_send", "tiny")
 # exchange steps of partitioned rounds, timed on each part's stream (gossip_dist.hip; bytes = received per part)
 EXCHANGES = ("all_gather", "all_to_all", "records")
 
@@ -204,7 +204,7 @@ class Engine:
         check(self._L.gossip_set_gather(self._ctx, C.c_void_p(gather_ptr)), "gossip_set_gather")
 
     def round_begin(self, mode: int) -> int:
-        """Phase 1 of a partitioned round; returns the mode actually run (0 push, 1 pull, 2 sparse push, 3 binned)."""
+        """Phase 1 of a partitioned round; returns the mode actually run (0 push, 1 pull, 2 sparse push, 3 binned, 4 blocked)."""
         got = C.c_int()
         check(self._L.gossip_round_begin(self._ctx, mode, C.byref(got)), "gossip_round_begin")
         return got.value

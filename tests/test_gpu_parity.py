@@ -88,18 +88,26 @@ def test_workload_parity(oracle, idx, n, mode):
         assert e.run() == first
 
 
-@pytest.mark.parametrize("blocked", ["force", "auto"])
+@pytest.mark.parametrize("blocked", ["force", "auto", "force_hubs", "auto_dense"])
 @pytest.mark.parametrize("idx,n", [(2, 1 << 16), (3, 1 << 18), (5, 1 << 16), (5, 50_000), (3, 1 << 20)])
 def test_blocked_push_parity(oracle, idx, n, blocked):
     """Propagation-blocked push rounds (gossip_blocked.hip): every push and binned
     round forced blocked, and the default schedule with its blocked rounds --
     against the oracle's per-round stats, seen sets, reports, alive and registry
     (broadcastMessage peer.cpp:310-316 -> handleClient peer.cpp:277-285; dead
-    targets are undelivered sends, peer.cpp:312)."""
+    targets are undelivered sends, peer.cpp:312).  force_hubs: the leading tiles
+    of in-degree > 1024 (twice the mean) take level 1's direct deliveries (at config 4's size only
+    the real hubs do); auto_dense: the binned rounds under 30 % run blocked as at
+    config 4's size."""
+    tuning = {}
+    if blocked == "force_hubs":
+        tuning["blocked_direct_in"] = 1024
+    if blocked == "auto_dense":
+        tuning["blocked_bin_slots"] = 0
     w = config(idx, n, pick=oracle.pick_origins)
     rp, col = oracle.gen_workload(w)
     ref = oracle.simulate_workload(w, rp, col)
-    with _engine(w, blocked=blocked) as e:
+    with _engine(w, blocked=blocked.split("_")[0], tuning=tuning) as e:
         e.enable_timing(True)
         e.build_graph()
         e.inject(w.origins, w.inject_rounds)
@@ -107,7 +115,7 @@ def test_blocked_push_parity(oracle, idx, n, blocked):
             e.schedule_kills([k[0] for k in w.kills], [k[1] for k in w.kills])
         e.reset()
         first = _compare(e, ref, w)
-        if blocked == "force":
+        if blocked.startswith("force"):
             assert e.kernel_time("pb_apply")[1] > 0  # the blocked path ran
         e.reset()
         assert e.run() == first
@@ -356,7 +364,8 @@ def test_engine_variants_match_oracle(oracle, variant, idx, n, mode):
         _compare(e, ref, w)
 
 
-@pytest.mark.parametrize("variant", ["auto", "defer_10", "all_pull", "defer_10_all_pull"])
+@pytest.mark.parametrize("variant", ["auto", "defer_10", "all_pull", "defer_10_all_pull", "defer_10_blocked",
+                                     "defer_3_blocked"])
 @pytest.mark.parametrize("stop", [3, 4, 5, 6, 7, 8])
 def test_deferred_round_fold(oracle, variant, stop):
     """With blocked push rounds off, auto mode defers the seen update of the wide
@@ -365,13 +374,24 @@ def test_deferred_round_fold(oracle, variant, stop):
     max_rounds right after a deferred round, or after the fused fold, must still
     read the oracle's seen set and coverage; the explicit option forces the
     deferral (committed when the fold cannot be fused), and a huge binned
-    threshold turns the binned rounds into pulls (push -> pull folds)."""
-    tuning = {"defer_permille": 10} if "defer_10" in variant else {}
+    threshold turns the binned rounds into pulls (push -> pull folds).  With
+    blocked rounds on and the dense rounds blocked at this size
+    (blocked_bin_slots 0), the fold rides on the blocked round's level-1
+    sweep, whose hub deliveries test against seen | nw."""
+    tuning = {}
+    if "defer_10" in variant:
+        tuning["defer_permille"] = 10
+    if "defer_3" in variant:
+        tuning["defer_permille"] = 3
+    if "blocked" in variant:  # defer_3: hub tiles (in-degree > 1024) take direct deliveries
+        tuning["blocked_bin_slots"] = 0
+        tuning["blocked_direct_in"] = 1024 if "defer_3" in variant else -1
     kw = {"bin_permille": 100000} if "all_pull" in variant else {}
     w = config(3, 1 << 18, pick=oracle.pick_origins)
     rp, col = oracle.gen_workload(w)
     ref = oracle.simulate_workload(w, rp, col, max_rounds=stop)
-    with Engine(w.n, w.n_msgs, max_rounds=stop, blocked="off", tuning=tuning, **kw, **w.engine_kwargs()) as e:
+    blocked = "auto" if "blocked" in variant else "off"
+    with Engine(w.n, w.n_msgs, max_rounds=stop, blocked=blocked, tuning=tuning, **kw, **w.engine_kwargs()) as e:
         e.build_graph()
         e.inject(w.origins, w.inject_rounds)
         e.reset()
