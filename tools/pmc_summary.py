@@ -4,7 +4,7 @@ WRITE_SIZE passes + the calibration passes of tools/calib_fetch) into one
 JSON: per-kernel launches, average duration, counted fetch/write bytes per
 launch and the calibration ratios used to read them.
 
-usage: pmc_summary.py <dir with c*_trace/ c*_fetch/ c*_write/ cal_fetch/ cal_write/> <out.json> [prefix]
+usage: pmc_summary.py <dir with c*_trace/ c*_fetch/ c*_write/ cal_fetch/ cal_write/> <out.json> [prefix] [note]
 """
 import csv
 import collections
@@ -31,7 +31,8 @@ def counters(path):
 def main():
     root, out = Path(sys.argv[1]), Path(sys.argv[2])
     pre = sys.argv[3] if len(sys.argv) > 3 else "c4"
-    res = {"source": str(root), "kernels": {}, "calibration": {}}
+    note = f" ({sys.argv[4]})" if len(sys.argv) > 4 else ""
+    res = {"source": str(root) + note, "kernels": {}, "calibration": {}}
     stats = list(csv.DictReader(open(root / f"{pre}_trace" / "run_kernel_stats.csv")))
     for r in stats:
         k = kname(r["Name"])
