@@ -316,7 +316,7 @@ def per_round_profile(run, n_peers: int) -> list[dict]:
         d = [{k: c[k] - q[k] for k in names if c[k] - q[k] > 0} for c, q in zip(cur, prev)]
         prev = cur
         mode = "bin" if any("bin_scatter" in x for x in d) else "blocked" if any("pb_scatter" in x for x in d) else \
-            "pull" if any("pull_light" in x for x in d) else "push"
+            "pull" if any("pull_light" in x or "pull_list" in x for x in d) else "push"
         kms = max(sum(v for k, v in x.items() if k in KERNELS) for x in d)
         xms = max(sum(v for k, v in x.items() if k in EXCHANGES) for x in d)
         dense = max(sum(x.get(k, 0.0) for k in DENSE_KERNELS) for x in d)

@@ -351,8 +351,9 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_split(PbArgs p) {
     __shared__ uint32_t tk_s[kPbFineMax], wr_s[kPbFineMax], dn_s[kPbFineMax];
     __shared__ unsigned long long base_s[kPbFineMax];  // this slice's segment of each fine bin
     __shared__ uint32_t cap_s[kPbFineMax];
-    __shared__ unsigned long long sb_s[kPbGrid / kPbSlices];  // the slice's level-1 segments of bin k
-    __shared__ uint32_t sn_s[kPbGrid / kPbSlices];
+    constexpr uint32_t kSeg = kPbGrid / kPbSlices;     // the slice's level-1 segments of bin k: one
+    __shared__ unsigned long long sb_s[kSeg];           // virtual array (prefix sums ps_s), so every wave
+    __shared__ uint32_t ps_s[kSeg + 1];                 // stays busy however short the segments are
     __shared__ uint16_t bd_s[kPbFineMax * kPbB2];
     __shared__ unsigned long long bw_s[kPbFineMax * kPbB2];
     const uint32_t k = blockIdx.x / kPbSlices, sl = blockIdx.x % kPbSlices;
@@ -365,9 +366,19 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_split(PbArgs p) {
     }
     const uint32_t nc = p.n_coarse;
     const uint32_t w0 = sl * (kPbGrid / kPbSlices);
-    for (uint32_t i = threadIdx.x; i < kPbGrid / kPbSlices; i += kPbBlock) {  // all at once, not one per pass
+    static_assert(kSeg == 64, "one wave scans the segment lengths");
+    if (threadIdx.x < 64) {
+        const uint32_t i = threadIdx.x;
         sb_s[i] = p.s1_base[(uint64_t)(w0 + i) * nc + k];
-        sn_s[i] = p.s1_len[(uint64_t)(w0 + i) * nc + k];
+        const uint32_t len = p.s1_len[(uint64_t)(w0 + i) * nc + k];
+        uint32_t incl = len;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(incl, off);
+            if ((int)i >= off) incl += y;
+        }
+        ps_s[i + 1] = incl;
+        if (i == 0) ps_s[0] = 0;
     }
     // the heavy rows' new words, consumed by level 1 (one word per row: its first chunk)
     for (uint64_t ci = (uint64_t)blockIdx.x * kPbBlock + threadIdx.x; ci < p.n_chunks;
@@ -393,9 +404,8 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_split(PbArgs p) {
             atomicOr(p.err, 2u);
         }
     };
-    for (uint32_t w = 0; w < kPbGrid / kPbSlices; ++w) {
-        const uint64_t base = sb_s[w];
-        const uint32_t n = sn_s[w];
+    {
+        const uint32_t n = ps_s[kSeg];
         for (uint32_t i0 = (uint32_t)wave * 64 * kPbU; i0 < n; i0 += kPbBlock * kPbU) {  // wave-uniform
             uint32_t d[kPbU], f[kPbU], dl[kPbU];
             unsigned long long x[kPbU];
@@ -404,8 +414,10 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_split(PbArgs p) {
             for (int j = 0; j < kPbU; ++j) {
                 const uint32_t i = i0 + j * 64 + lane;
                 const bool in = i < n;
-                d[j] = in ? p.r1_dst[base + i] : kPbPad;
-                x[j] = in ? p.r1_w[base + i] : 0ull;
+                const uint32_t sg = in ? find_bin<kSeg>(ps_s, i) : 0u;  // ps_s[sg] <= i < ps_s[sg + 1]
+                const uint64_t at = sb_s[sg] + (i - ps_s[sg]);
+                d[j] = in ? p.r1_dst[at] : kPbPad;
+                x[j] = in ? p.r1_w[at] : 0ull;
             }
 #pragma unroll
             for (int j = 0; j < kPbU; ++j) {

@@ -47,6 +47,47 @@ struct Acc {
     unsigned long long fresh_or[kMaxWords] = {};  // OR of the receipts (only the words a kernel touches stay)
 };
 
+// The next round's source side, booked where a peer is activated (RoundArgs.st_pre): per wave, one
+// atomic per nonzero field into a line of st_pre.  Every lane of the wave must call it.
+struct PreAcc {
+    unsigned long long frontier = 0, trav = 0, deliv = 0, digest = 0, covered = 0;
+};
+
+__device__ __forceinline__ void flush_pre(const PreAcc& p, DevStats* st) {
+    if (!st) return;
+    const unsigned long long v[5] = {wave_sum(p.frontier), wave_sum(p.trav), wave_sum(p.deliv), wave_sum(p.digest),
+                                     wave_sum(p.covered)};
+    if ((threadIdx.x & 63) != 0) return;
+    DevStats* l = st + (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % kStatLines;
+    unsigned long long* f[5] = {&l->frontier, &l->traversals, &l->deliveries, &l->digest, &l->covered};
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+        if (v[i]) atomicAdd(f[i], v[i]);
+}
+
+// Appends v (lanes with app) to a.lst_out: one counter atomic per wave.  Every lane of the wave must call it.
+__device__ __forceinline__ void list_push(const RoundArgs& a, bool app, uint32_t v) {
+    const unsigned long long b = __ballot(app);
+    if (!b) return;
+    const int lead = __builtin_ctzll(b);
+    uint32_t base = 0;
+    if ((int)(threadIdx.x & 63) == lead) base = atomicAdd(a.lst_n, (uint32_t)__popcll(b));
+    base = (uint32_t)__shfl((int)base, lead);
+    if (app) {
+        const uint32_t i = base + lane_rank(b);
+        if (i < a.lst_cap) a.lst_out[i] = v;  // past the cap: counted only (overflow)
+    }
+}
+
+// Appends a wave's n <= 64 staged rows (LDS, s[0..n)) to a.lst_out with one counter atomic.
+__device__ __forceinline__ void list_flush(const RoundArgs& a, const uint32_t* s, uint32_t n) {
+    const int lane = threadIdx.x & 63;
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(a.lst_n, n);
+    base = (uint32_t)__shfl((int)base, 0);
+    if ((uint32_t)lane < n && base + lane < a.lst_cap) a.lst_out[base + lane] = s[lane];
+}
+
 // Block-level flush: wave sums -> LDS -> one atomic per nonzero field per
 // block, into stat line blockIdx % kStatLines of the round.  Same-line device
 // atomics serialise (~9 ns each measured); one line per round hit by every

@@ -152,6 +152,22 @@ struct gossip_ctx {
     PbState pb;                  // propagation-blocked push rounds: record regions (gossip_blocked.hip)
     bool pb_ready = false;
     bool cur_pb = false;         // the round in flight runs propagation-blocked
+    // late pull rounds over needy lists (k_pull_list)
+    bool list_req = true;          // "list_rounds": 0 never
+    uint32_t list_cap_req = 0;     // "list_cap": entries per list (0: n_local / 16, at least 2^16)
+    uint32_t* lst[3] = {};         // needy lists (light rows that still lack a bit), three in rotation
+    uint32_t* d_lst_n = nullptr;   // their lengths (device counters)
+    uint32_t lst_cap = 0;
+    DevStats* st_pre = nullptr;    // the next round's source side (kStatLines lines)
+    bool pre_booked = false;       // the previous round booked the next one's source side into st_pre
+    int lst_in = -1;               // the list the previous round wrote (without overflow) and its length
+    uint32_t lst_in_n = 0;
+    bool cur_list = false;         // the round in flight pulls list lst_in ...
+    bool cur_pre = false;          // ... books the next round's source side ...
+    int cur_lst_out = -1;          // ... and writes list cur_lst_out
+    uint32_t lst_out_n = 0;        // (read with the round's stats)
+    int lin_idx[2] = {-1, -1};     // input lists of the last two rounds (-1: not a list round), lengths
+    uint32_t lin_n[2] = {0, 0};
     bool last_bin = false;       // the pull round in flight runs binned
     uint64_t last_fresh = 0;     // new receipts of the previous round
     bool bins_first = false;             // no binned round since the last reset: rewrite every slot
@@ -344,6 +360,15 @@ void free_state(gossip_ctx* c) {
     c->death_r = nullptr;
     c->dgone = c->dmask = c->rev = nullptr;
     hipFree(c->st);
+    hipFree(c->st_pre);
+    c->st_pre = nullptr;
+    for (auto& l : c->lst) {
+        hipFree(l);
+        l = nullptr;
+    }
+    hipFree(c->d_lst_n);
+    c->d_lst_n = nullptr;
+    c->lst_cap = 0;
     if (c->h_st) hipHostFree(c->h_st);
     hipFree(c->cov_hist);
     hipFree(c->reports);
@@ -708,6 +733,26 @@ gossip_status prepare_bins(gossip_ctx* c) {
     return prepare_pb(c);
 }
 
+// the needy lists and the booking lines of late pull rounds, on first use
+gossip_status ensure_lists(gossip_ctx* c) {
+    const uint32_t cap = c->list_cap_req ? c->list_cap_req
+                                         : (uint32_t)std::min<uint64_t>(std::max<uint64_t>(c->n_local / 16, 1u << 16),
+                                                                        0xFFFFFFFFull);
+    if (c->st_pre && c->lst_cap == cap) return GOSSIP_OK;
+    for (auto& l : c->lst) {
+        hipFree(l);
+        l = nullptr;
+    }
+    if (!c->st_pre) {
+        HIPCHK(hipMalloc((void**)&c->st_pre, kStatLines * sizeof(DevStats)));
+        HIPCHK(hipMemsetAsync(c->st_pre, 0, kStatLines * sizeof(DevStats), c->stream));
+    }
+    if (!c->d_lst_n) HIPCHK(hipMalloc((void**)&c->d_lst_n, 4 * sizeof(uint32_t)));
+    for (auto& l : c->lst) HIPCHK(hipMalloc((void**)&l, (uint64_t)cap * sizeof(uint32_t)));
+    c->lst_cap = cap;
+    return GOSSIP_OK;
+}
+
 // seen |= nw for a deferred round whose fold was left to the next binned round
 gossip_status settle_fold(gossip_ctx* c) {
     if (!c->fold_pending) return GOSSIP_OK;
@@ -793,6 +838,10 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
         if (c->cfg.rejoin_threshold || c->cfg.churn_threshold || kills_in_round(c, c->round, &kf))
             if (gossip_status fs = settle_fold(c)) return fs;
     }
+    // the previous round booked this round's source side (late pull rounds): those lines are this round's
+    const bool booked = c->pre_booked;
+    c->pre_booked = false;
+    if (booked) std::swap(c->st, c->st_pre);
     RoundArgs a = make_args(c);
     const uint32_t pw = pack_w(c);
     if (c->cfg.rejoin_threshold) {  // restarts first: a peer dying this round cannot restart in it
@@ -935,6 +984,36 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
                          front * 1000 < c->n_local * (uint64_t)hi);
         if (c->cur_pb) pull = bin = false;
     }
+    // late pull rounds over needy lists (k_pull_list): a round whose source side the previous one booked
+    // pulls that round's list -- or, when the list overflowed, sweeps as a row pull that books no source
+    // side.  A row pull on a shrinking frontier (the rounds after the dense ones: config 4 round 7), and
+    // every list round, books the next round's source side and lists its still-needy rows.  One word per
+    // peer, one partition, no deaths, no coverage history, nothing injected or killed later.
+    c->cur_list = c->cur_pre = false;
+    c->cur_lst_out = -1;
+    if (booked) {
+        pull = true;
+        bin = c->cur_pb = false;
+        c->cur_list = c->lst_in >= 0;
+    }
+    {
+        const bool later_inj = c->has_schedule && c->last_inject_round > c->round;
+        const bool later_kill = !c->kill_round_sorted.empty() && c->kill_round_sorted.back() > c->round;
+        const bool list_ok = c->list_req && c->world <= 1 && !remote && c->Wp == 1 && c->n_local == c->n &&
+                             c->symmetric && !c->any_dead && !later_kill && !later_inj && !c->cfg.churn_threshold &&
+                             !c->cfg.rejoin_threshold && !c->cfg.extra_cap && !c->cov_hist && !c->gather &&
+                             requested == GOSSIP_MODE_AUTO && !(c->cfg.flags & GOSSIP_FLAG_FORCE_BIN);
+        const bool rows = pull && !bin && !c->cur_pb;
+        if (list_ok && (c->cur_list || (rows && c->frontier_est < c->prev_frontier_est))) {
+            if (gossip_status ls = ensure_lists(c)) return ls;
+            // not this round's input, nor the previous round's (the next round clears by it)
+            int out = 0;
+            while (out == (c->cur_list ? c->lst_in : -1) || out == c->lin_idx[0]) ++out;
+            c->cur_lst_out = out;
+            c->cur_pre = true;
+            HIPCHK(hipMemsetAsync(c->d_lst_n + out, 0, sizeof(uint32_t), c->stream));
+        }
+    }
     c->cur_sparse = !pull && remote && requested == GOSSIP_MODE_PUSH_SPARSE && c->seg != nullptr;
     // a wide push round (the explosion before the dense rounds) is bound by memory-side atomics, two per
     // fresh delivery (seen, then nx); deferring the seen update halves them for one streamed pass
@@ -968,6 +1047,12 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
         HIPCHK(timed(c, "churn", [&] { return launch_dead_edges(a, lo, hi, c->stream); }));
         c->dgone_next = c->round + 1;
     }
+    a.src_booked = booked ? 1u : 0u;
+    a.st = c->st;
+    a.st_pre = c->cur_pre ? c->st_pre : nullptr;
+    a.lst_out = c->cur_lst_out >= 0 ? c->lst[c->cur_lst_out] : nullptr;
+    a.lst_n = c->cur_lst_out >= 0 ? c->d_lst_n + c->cur_lst_out : nullptr;
+    a.lst_cap = c->lst_cap;
     c->last_pull = pull;
     c->last_bin = bin;
     c->last_front = false;
@@ -991,7 +1076,7 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
         // its few needy rows stop after a gather or two, at hubs that are in the frontier anyway
         const uint32_t fpm = c->cfg.front_permille ? c->cfg.front_permille : 400;
         if (!bin && requested == GOSSIP_MODE_AUTO && (c->frontier_est + cnt) * 1000 < c->n_local * (uint64_t)fpm &&
-            (remote || c->cfg.front_permille || missing * 4 >= c->n_local)) {
+            (remote || c->cfg.front_permille || missing * 4 >= c->n_local) && !c->cur_list) {  // (list: no bitmap)
             a.front = c->front;
             c->last_front = true;
         } else {
@@ -1146,6 +1231,17 @@ gossip_status round_compute(gossip_ctx* c) {
         HIPCHK(timed(c, "pb_apply", [&] { return launch_pb_apply(a, p, c->stream); }));
         return GOSSIP_OK;
     }
+    if (c->cur_list) {
+        // nx holds the new words of the round before last: its list's rows (and the heavy rows) if that was
+        // a list round, anything otherwise
+        HIPCHK(timed(c, "list_zero", [&] {
+            if (c->lin_idx[1] >= 0) return launch_list_zero(a, c->lst[c->lin_idx[1]], c->lin_n[1], c->stream);
+            return hipMemsetAsync(c->nx, 0, c->n_local * sizeof(uint64_t), c->stream);
+        }));
+        HIPCHK(timed(c, "pull_list", [&] { return launch_pull_list(a, c->lst[c->lst_in], c->lst_in_n, c->stream); }));
+        HIPCHK(timed(c, "pull_heavy", [&] { return launch_pull_heavy(a, pw, c->stream); }));
+        return GOSSIP_OK;
+    }
     if (c->last_pull && a.dead_mode && !a.dgone)  // else the per-source counters give the source side
         HIPCHK(timed(c, "src_count", [&] { return launch_src_count(a, pw, c->stream); }));
     if (c->last_bin) {
@@ -1181,6 +1277,9 @@ gossip_status round_compute(gossip_ctx* c) {
 gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative) {
     if (c->last_st_round != c->round) {  // read once per round, then the lines are re-zeroed for the next
         HIPCHK(hipMemcpyAsync(c->h_st, c->st, kStatLines * sizeof(DevStats), hipMemcpyDeviceToHost, c->stream));
+        if (c->cur_lst_out >= 0)
+            HIPCHK(hipMemcpyAsync(&c->lst_out_n, c->d_lst_n + c->cur_lst_out, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                  c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         HIPCHK(hipMemsetAsync(c->st, 0, kStatLines * sizeof(DevStats), c->stream));
         if (c->cur_pb) {  // a record region that would have overflowed (cannot happen: capacities are in-degrees)
@@ -1232,6 +1331,13 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
         }
         if (c->last_bin) {
             // booked above
+        } else if (c->cur_list) {
+            // list, seen, row bounds per entry, 4 B per edge scanned, 8 B per gather, seen + nx per
+            // activated row, 4 B per entry listed; the clear: 12 B per entry of its list, or every nx word
+            c->kbytes["pull_list"] += 28.0 * c->lst_in_n + 4.0 * (double)d.pull_edges + 8.0 * (double)d.pull_gathers +
+                                      16.0 * (double)d.activated + 4.0 * std::min(c->lst_out_n, c->lst_cap);
+            c->kbytes["list_zero"] += c->lin_idx[1] >= 0 ? 12.0 * c->lin_n[1] : 8.0 * c->n_local;
+            c->kbytes["pull_heavy"] += 12.0 * (double)d.heavy_traversals;
         } else if (c->last_pull) {
             if (c->last_front) c->kbytes["frontier_bits"] += 8.125 * (c->gather ? c->n : c->n_local);
             c->kbytes["pull_light"] += 40.0 * c->n_local + 4.0 * (double)d.pull_edges + 8.0 * (double)d.pull_gathers;
@@ -1293,6 +1399,17 @@ gossip_status advance(gossip_ctx* c, uint64_t fresh_global) {
         c->cur_defer = false;
     }
     std::swap(c->nw, c->nx);
+    // late pull rounds: the next round's source side is booked; its list, unless it overflowed; this
+    // round's input list is kept two rounds (the round after next clears nx by it)
+    c->pre_booked = c->cur_pre;
+    c->lin_idx[1] = c->lin_idx[0];
+    c->lin_n[1] = c->lin_n[0];
+    c->lin_idx[0] = c->cur_list ? c->lst_in : -1;
+    c->lin_n[0] = c->cur_list ? c->lst_in_n : 0u;
+    c->lst_in = c->cur_lst_out >= 0 && c->lst_out_n <= c->lst_cap && c->last_st_round == c->round ? c->cur_lst_out : -1;
+    c->lst_in_n = c->lst_in >= 0 ? c->lst_out_n : 0u;
+    c->cur_list = c->cur_pre = false;
+    c->cur_lst_out = -1;
     c->fold_pending = pend;  // push: nw was cleared by push_light; pull: the old nw is stale
     // a push round clears every word it consumes; if nobody was activated nx stayed zero too
     // (only when this round's stats were read: frontier_est / last_fresh are then this round's)
@@ -1451,6 +1568,8 @@ gossip_status gossip_set_tuning(gossip_ctx* c, const char* key, int64_t value) {
     else if (k == "src_stats") c->src_stats_req = value < 0 ? -1 : (value != 0);
     else if (k == "blocked_bin_slots") c->pb_bin_slots = value < 0 ? kPbBinSlots : (uint64_t)value;
     else if (k == "blocked_direct_in") c->pb_direct_in = value < 0 ? kPbFineIn : (uint64_t)value;
+    else if (k == "list_rounds") c->list_req = value != 0;
+    else if (k == "list_cap") c->list_cap_req = u;
     else return fail(GOSSIP_EINVAL, "unknown tuning option: " + k);
     return GOSSIP_OK;
 }
@@ -1739,6 +1858,10 @@ gossip_status gossip_reset(gossip_ctx* c) {
         HIPCHK(hipMemsetAsync(c->dmask, 0, c->n_local * 4 + 4, s));
     }
     c->n_rep_seen = 0;
+    c->pre_booked = c->cur_list = c->cur_pre = false;
+    c->lst_in = c->cur_lst_out = -1;
+    c->lin_idx[0] = c->lin_idx[1] = -1;
+    if (c->st_pre) HIPCHK(hipMemsetAsync(c->st_pre, 0, kStatLines * sizeof(DevStats), s));
     c->any_masked = false;
     c->nx_dirty = false;
     c->last_pull = false;

@@ -264,6 +264,15 @@ struct RoundArgs {
     // k_pull_heavy: per heavy row (at its first chunk) the bits its chunks have found so far this
     // round, n_chunks * Wp words cleared per launch; a chunk stops once they cover the row's need
     uint64_t* hacc;
+    // late pull rounds (DESIGN.md section 6.5, P = 1, one word per peer, no deaths): a round may book the
+    // next round's source side at activation (st_pre: frontier, traversals, deliveries, digest, covered
+    // of the peers it activates) and list the light rows that still lack a bit (lst_out); the next round
+    // then pulls only those rows (k_pull_list) with its source side already booked (src_booked)
+    DevStats* st_pre;              // nullptr: no booking
+    uint32_t* lst_out;             // nullptr: no list
+    uint32_t* lst_n;               // entries appended (may pass lst_cap: the list overflowed)
+    uint32_t lst_cap;
+    uint32_t src_booked;           // k_pull_rows: the sweep books no source side
 };
 
 // Re-bootstrap draw (handleDeadPeer peer.cpp:398-404 -> selectAndConnectPeers
@@ -307,6 +316,10 @@ hipError_t launch_push_light(const RoundArgs& a, uint32_t W, bool check_alive, b
 hipError_t launch_frontier_bits(const RoundArgs& a, uint32_t W, hipStream_t s);
 hipError_t launch_pull_rows(const RoundArgs& a, uint32_t W, hipStream_t s);
 hipError_t launch_pull_heavy(const RoundArgs& a, uint32_t W, hipStream_t s);
+// late pull rounds over a needy list (one word per peer): the stale new words of the round before last
+// cleared (by its list, or n_local words), then the list's rows pulled
+hipError_t launch_list_zero(const RoundArgs& a, const uint32_t* lst, uint32_t n, hipStream_t s);
+hipError_t launch_pull_list(const RoundArgs& a, const uint32_t* lst, uint32_t n, hipStream_t s);
 hipError_t launch_apply_remote(const RoundArgs& a, uint32_t W, const uint64_t* recv, uint32_t world,
                                uint64_t part_stride, hipStream_t s);
 hipError_t launch_compact_send(const RoundArgs& a, uint32_t W, uint64_t chunk, unsigned long long* counts,

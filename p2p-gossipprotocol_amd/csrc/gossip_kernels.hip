@@ -482,13 +482,17 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
     __shared__ unsigned long long q_rb[kWavesPerBlock][kRowQ];
     __shared__ unsigned long long q_f2[kWavesPerBlock][kRowQ];  // the row's first two entries (a.first2)
     __shared__ unsigned long long q_need[kWavesPerBlock][kRowQ * W];
+    __shared__ uint32_t q_lst[kWavesPerBlock][128];  // rows for the next round's list (a.lst_out), staged
     if (COV) {
         for (int i = threadIdx.x; i < 64 * W; i += kBlock) cov_s[i] = 0;
         __syncthreads();
     }
     Acc acc;
+    PreAcc pre;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint32_t* qv = q_v[wv];
+    uint32_t* lq = q_lst[wv];
+    uint32_t lq_n = 0;  // wave-uniform
     uint32_t* qd = q_d[wv];
     unsigned long long* qrb = q_rb[wv];
     unsigned long long* qf2 = q_f2[wv];
@@ -551,7 +555,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
         }
         const uint64_t rb = d.r0, d_ = d.r1 - d.r0;
         const uint64_t dg = (act || needy) ? d_ : 0ull;
-        if (act) {  // source side of this peer's pushes (broadcastMessage, peer.cpp:310-316)
+        if (act && !a.src_booked) {  // source side of this peer's pushes (broadcastMessage, peer.cpp:310-316)
             uint32_t pc = 0;
 #pragma unroll
             for (int w = 0; w < W; ++w) {
@@ -665,23 +669,58 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
             done &= got[w] == (need[w] & injm(a, w));  // every bit it can still learn this round
         }
         rk += kRowB;
+        bool lacks = false;
         if (has && (done || rk >= rd)) {  // the row is finished: handleClient's test-and-set, owner stores
             bool any = false;
+            uint32_t pc = 0;
 #pragma unroll
             for (int w = 0; w < W; ++w) {
                 const uint64_t fr = got[w];  // subset of need: bits this peer had not seen
                 acc.fresh_or[w] |= fr;
+                // still lacking a bit in flight: the only rows that can learn later (no injections: the next
+                // round's bits in flight are this round's receipts, a subset of this round's)
+                lacks |= (need[w] & injm(a, w) & ~fr) != 0;
                 if (fr) {
                     a.seen[(uint64_t)rv * W + w] = (injm_full(a, w) & ~need[w]) | fr;  // within inj_mask
                     a.nx[(uint64_t)rv * W + w] = fr;
-                    acc.fresh += (unsigned long long)__popcll(fr);
+                    pc += (uint32_t)__popcll(fr);
+                    if (a.st_pre && w < (int)wd) pre.digest += digest_weight(((uint64_t)a.begin + rv) * wd + w) * fr;
                     any = true;
                 }
             }
+            acc.fresh += pc;
             acc.activated += any;
+            if (a.st_pre && any) {  // the next round's push from this peer (no deaths: every edge delivers)
+                pre.frontier++;
+                pre.covered += pc;
+                pre.trav += rd;
+                pre.deliv += (unsigned long long)pc * rd;
+            }
+            lacks = lacks && a.lst_out;
             has = false;
         }
+        if (a.lst_out) {  // staged per wave, one counter atomic per 64 entries
+            const unsigned long long lb = __ballot(lacks);
+            if (lb) {
+                if (lacks) lq[lq_n + lane_rank(lb)] = rv;
+                lq_n += (uint32_t)__popcll(lb);
+                if (lq_n >= 64) {
+                    wave_sync();
+                    list_flush(a, lq, 64);
+                    lq_n -= 64;
+                    const uint32_t mv = (uint32_t)lane < lq_n ? lq[64 + lane] : 0u;
+                    wave_sync();
+                    if ((uint32_t)lane < lq_n) lq[lane] = mv;
+                    wave_sync();
+                }
+            }
+        }
     }
+    if (a.lst_out && lq_n) {
+        wave_sync();
+        list_flush(a, lq, lq_n);
+    }
+    flush_pre(pre, a.st_pre);
     flush(acc, a.st);
     if (COV) {
         __syncthreads();
@@ -693,6 +732,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_pull_heavy(RoundArgs a) {
     Acc acc;
+    PreAcc pre;
     const int lane = threadIdx.x & 63;
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
     for (uint64_t ci = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); ci < a.n_chunks; ci += nwaves) {
@@ -770,12 +810,99 @@ __global__ __launch_bounds__(kBlock) void k_pull_heavy(RoundArgs a) {
                         atomicOr(reinterpret_cast<unsigned long long*>(a.nx) + (uint64_t)ch.v * W + w, fr);
                     acc.activated += onx == 0;
                     acc.fresh += (unsigned long long)__popcll(fr);
+                    if (a.st_pre) {  // one word per peer: the row's chunks' fr are disjoint, its push counted once
+                        const uint64_t deg = a.rp[ch.v + 1] - a.rp[ch.v];
+                        const uint32_t pc = (uint32_t)__popcll(fr);
+                        pre.covered += pc;
+                        pre.digest += digest_weight((uint64_t)a.begin + ch.v) * fr;
+                        pre.deliv += (unsigned long long)pc * deg;
+                        if (onx == 0) {
+                            pre.frontier++;
+                            pre.trav += deg;
+                        }
+                    }
                 }
             }
         }
     }
     acc.htrav = acc.pulled;  // heavy-row edges scanned
     acc.pulled = 0;
+    flush_pre(pre, a.st_pre);
+    flush(acc, a.st);
+}
+
+// ---------------------------------------------------------------------------
+// Late pull rounds over a needy list (P = 1, one word per peer, no deaths;
+// DESIGN.md section 6.5).  After the dense rounds few peers still lack a
+// message (config 4 round 8: 1.8 M of 2^28), yet a row-queue pull sweeps every
+// peer for the source side of the round and for its needy rows.  The round
+// before books this round's source side where it activates peers (st_pre) and
+// lists the light rows that still lack a bit; this round pulls just those
+// rows -- handleClient's test-and-set per row, the scan stopping once the row
+// holds every bit in flight that it lacks -- and lists the rows that still
+// lack one for the next.  Heavy rows stay k_pull_heavy's.
+// ---------------------------------------------------------------------------
+// nx is the buffer of the round before last's new words: only that round's list (or the heavy rows)
+// can have left anything in it
+__global__ __launch_bounds__(kBlock) void k_list_zero(RoundArgs a, const uint32_t* lst, uint32_t n) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) a.nx[lst[i]] = 0ull;
+    for (uint64_t ci = (uint64_t)blockIdx.x * kBlock + threadIdx.x; ci < a.n_chunks; ci += stride) {
+        const HeavyChunk ch = a.chunks[ci];
+        if (ch.first == ci) a.nx[ch.v] = 0ull;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_pull_list(RoundArgs a, const uint32_t* lst, uint32_t n) {
+    Acc acc;
+    PreAcc pre;
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    const uint64_t n_pad = ((uint64_t)n + 63) & ~63ull;
+    const uint64_t inj_all = injm_full(a, 0), inj_now = injm(a, 0);
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n_pad; i += stride) {
+        const bool in = i < n;
+        const uint32_t v = in ? lst[i] : 0u;
+        const uint64_t sv = in ? a.seen[v] : ~0ull;
+        const uint64_t need = inj_all & ~sv;  // every bit the peer lacks ...
+        const uint64_t want = need & inj_now;  // ... and of those, the ones in some new word this round
+        uint64_t r0 = 0, r1 = 0;
+        if (in) {
+            r0 = a.rp[v];
+            r1 = a.rp[v + 1];
+        }
+        uint64_t got = 0;
+        if (want) {
+            for (uint64_t e = r0; e < r1; e += 2) {  // two neighbours' words in flight per step
+                const bool two = e + 1 < r1;
+                const uint32_t u0 = a.col[e], u1 = two ? a.col[e + 1] : kMaskedEdge;
+                const bool ok0 = !(u0 & kMaskedEdge), ok1 = !(u1 & kMaskedEdge);  // (no deaths: none masked)
+                const uint64_t x0 = a.nw_src[ok0 ? u0 : 0u] & (ok0 ? ~0ull : 0ull);
+                const uint64_t x1 = a.nw_src[ok1 ? u1 : 0u] & (ok1 ? ~0ull : 0ull);
+                acc.pulled += two ? 2u : 1u;
+                acc.gathered += (unsigned)ok0 + (unsigned)ok1;
+                got |= (x0 | x1) & want;
+                if (got == want) break;  // every bit it can learn this round
+            }
+        }
+        if (got) {  // handleClient: new -> Message-List insert (peer.cpp:281-282)
+            a.seen[v] = sv | got;
+            a.nx[v] = got;
+            const uint32_t pc = (uint32_t)__popcll(got);
+            acc.fresh += pc;
+            acc.activated++;
+            acc.fresh_or[0] |= got;
+            if (a.st_pre) {  // the next round's push from this peer
+                const uint64_t d = r1 - r0;
+                pre.frontier++;
+                pre.covered += pc;
+                pre.digest += digest_weight((uint64_t)a.begin + v) * got;
+                pre.trav += d;
+                pre.deliv += (unsigned long long)pc * d;
+            }
+        }
+        if (a.lst_out) list_push(a, in && (want & ~got) != 0 && r1 > r0, v);  // (next round: a subset in flight)
+    }
+    flush_pre(pre, a.st_pre);
     flush(acc, a.st);
 }
 
@@ -2324,6 +2451,17 @@ hipError_t launch_pull_heavy(const RoundArgs& a, uint32_t W_, hipStream_t s) {
     }
     GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_pull_heavy<W>, dim3(grid_for(a.n_chunks, kWavesPerBlock)),
                                                    dim3(kBlock), 0, s, a));
+    return hipGetLastError();
+}
+
+hipError_t launch_list_zero(const RoundArgs& a, const uint32_t* lst, uint32_t n, hipStream_t s) {
+    hipLaunchKernelGGL(k_list_zero, dim3(grid_for(std::max<uint64_t>(n, a.n_chunks), kBlock)), dim3(kBlock), 0, s, a,
+                       lst, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_pull_list(const RoundArgs& a, const uint32_t* lst, uint32_t n, hipStream_t s) {
+    hipLaunchKernelGGL(k_pull_list, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, a, lst, n);
     return hipGetLastError();
 }
 

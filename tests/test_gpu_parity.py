@@ -401,6 +401,44 @@ def test_deferred_round_fold(oracle, variant, stop):
         assert np.array_equal(e.coverage(), ref["coverage"])
 
 
+@pytest.mark.parametrize("variant", ["on", "off", "cap_small", "stop"])
+@pytest.mark.parametrize("idx,n", [(2, 1 << 18), (3, 1 << 18), (3, 1 << 20), (2, 50_000)])
+def test_needy_list_rounds(oracle, idx, n, variant):
+    """Late pull rounds over needy lists (k_pull_list): the row pull after the
+    dense rounds books the next round's source side at activation and lists
+    the rows that still lack a bit; the rounds after it pull only those rows.
+    Against the oracle's per-round stats, seen sets and coverage: on (the
+    default), off, a list capacity of 64 (the lists overflow: the next round
+    sweeps as a row pull whose source side is already booked), and runs cut by
+    max_rounds inside the list chain (a reset clears the booking)."""
+    tuning = {"list_rounds": 0} if variant == "off" else {"list_cap": 64} if variant == "cap_small" else {}
+    w = config(idx, n, pick=oracle.pick_origins)
+    rp, col = oracle.gen_workload(w)
+    stops = [None] if variant != "stop" else [7, 8, 9, 10]
+    with _engine(w, tuning=tuning) as e:
+        e.enable_timing(True)
+        e.build_graph()
+        e.inject(w.origins, w.inject_rounds)
+        if w.kills:
+            e.schedule_kills([k[0] for k in w.kills], [k[1] for k in w.kills])
+        for stop in stops:
+            ref = oracle.simulate_workload(w, rp, col, **({"max_rounds": stop} if stop else {}))
+            e.reset()
+            got = []
+            while True:
+                st, fin = e.step()
+                got.append(st)
+                if fin or (stop and len(got) >= stop):
+                    break
+            assert got == ref["stats"][:len(got)]
+            if stop is None:
+                assert len(got) == len(ref["stats"])
+                assert np.array_equal(e.read_seen(), ref["seen"])
+                assert np.array_equal(e.coverage(), ref["coverage"])
+        if variant == "on" and not w.kills:
+            assert e.kernel_time("pull_list")[1] > 0  # the list rounds ran
+
+
 @pytest.mark.parametrize("tiny", ["1", "0"])
 @pytest.mark.parametrize("idx,n,max_rounds", [(1, None, 0), (1, 40, 0), (1, 40, 20), (2, 4096, 0), (3, 2048, 0),
                                                (5, 4096, 0), (5, 6000, 7), (5, 6000, 0)])
