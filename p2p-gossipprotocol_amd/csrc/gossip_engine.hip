@@ -215,6 +215,9 @@ struct gossip_ctx {
     uint32_t world = 1;
     std::vector<uint64_t> part_begins;
 
+    // small clears queued for the round's next kernel launch (one k_zero_batch instead of a fill each)
+    gossip::ZeroBatch zq{};
+
     // timing
     bool timing = false;
     std::map<std::string, TimerRec> timers;
@@ -290,8 +293,29 @@ hipEvent_t take_event(gossip_ctx* c) {
     return e;
 }
 
+// queued clears go out before the next kernel (every kernel that writes stats, tile marks or heavy-row
+// accumulators is launched through timed())
+hipError_t flush_zero(gossip_ctx* c) {
+    gossip::ZeroBatch& z = c->zq;
+    if (!z.count) return hipSuccess;
+    hipError_t e = z.count == 1 ? hipMemsetAsync(z.p[0], 0, (size_t)z.n[0] * 4, c->stream)
+                                : gossip::launch_zero_batch(z, c->stream);
+    z.count = 0;
+    return e;
+}
+
+hipError_t queue_zero(gossip_ctx* c, void* p, uint64_t bytes) {
+    if (c->zq.count == gossip::kZeroRanges)
+        if (hipError_t e = flush_zero(c)) return e;
+    c->zq.p[c->zq.count] = static_cast<uint32_t*>(p);
+    c->zq.n[c->zq.count] = (uint32_t)(bytes / 4);
+    c->zq.count++;
+    return hipSuccess;
+}
+
 template <class F>
 hipError_t timed(gossip_ctx* c, const char* name, F&& launch) {
+    if (hipError_t e = flush_zero(c)) return e;
     if (!c->timing) return launch();
     hipEvent_t a = take_event(c), b = take_event(c);
     hipEventRecord(a, c->stream);
@@ -343,6 +367,7 @@ void drain_timers(gossip_ctx* c) {
 }
 
 void free_state(gossip_ctx* c) {
+    c->zq.count = 0;
     hipFree(c->seen);
     hipFree(c->nw);
     hipFree(c->nx);
@@ -965,8 +990,9 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
         }
     }
     // propagation-blocked push (gossip_blocked.hip; one partition, one word per peer): a push round from a
-    // 5 % frontier estimate -- below it the atomic push's deliveries cost less than the blocked round's
-    // fixed passes (config 3 round 2, 2.1 %: push 0.25 ms, blocked 0.79 ms) -- and, where the slot array
+    // 5 % frontier estimate on overlays of >= kPbPushPeers peers -- below it the atomic push's deliveries
+    // cost less than the blocked round's fixed passes (config 3 round 2, 2.1 %: push 0.25 ms, blocked
+    // 0.79 ms; config 2 at 5.05 %: blocked 0.097 ms per round, 9 rounds a step) -- and, where the slot array
     // outgrows the MALL many times over (>= kPbBinSlots slots: its scattered stores go to HBM as partial
     // lines), a binned round below blocked_permille (every edge streamed for a minority of active
     // sources) write one record per delivery instead (config 4 round 4, 17 %: binned 15.6 ms, blocked
@@ -979,7 +1005,7 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
         if (c->cfg.flags & GOSSIP_FLAG_FORCE_BLOCKED)
             c->cur_pb = !pull || bin;
         else
-            c->cur_pb = (!pull && front * 1000 >= c->n_local * (uint64_t)kPbLoPermille) ||
+            c->cur_pb = (!pull && c->n_local >= kPbPushPeers && front * 1000 >= c->n_local * (uint64_t)kPbLoPermille) ||
                         (bin && (!c->bins_ready || c->bins.n_slots >= c->pb_bin_slots) &&
                          front * 1000 < c->n_local * (uint64_t)hi);
         if (c->cur_pb) pull = bin = false;
@@ -1011,7 +1037,7 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
             while (out == (c->cur_list ? c->lst_in : -1) || out == c->lin_idx[0]) ++out;
             c->cur_lst_out = out;
             c->cur_pre = true;
-            HIPCHK(hipMemsetAsync(c->d_lst_n + out, 0, sizeof(uint32_t), c->stream));
+            HIPCHK(queue_zero(c, c->d_lst_n + out, sizeof(uint32_t)));
         }
     }
     c->cur_sparse = !pull && remote && requested == GOSSIP_MODE_PUSH_SPARSE && c->seg != nullptr;
@@ -1058,7 +1084,7 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
     c->last_front = false;
     if (pull) {
         if (a.tcur) {  // pull / binned rounds set no tile marks: this round's go, the next push round scans
-            HIPCHK(hipMemsetAsync(a.tcur, 0, tact_bytes(c), c->stream));
+            HIPCHK(queue_zero(c, a.tcur, tact_bytes(c)));
             a.tcur = a.tnx = nullptr;
             a.tsparse = 0;
         }
@@ -1209,7 +1235,7 @@ gossip_status tiny_run(gossip_ctx* c, gossip_round_stats* per_round, uint32_t ca
 // Who books the source side of a binned round: the scatter's staging (slot layout) or the apply
 // (streamed layout; "src_stats" 0/1 overrides)
 uint32_t src_stats(const gossip_ctx* c) {
-    return c->src_stats_req >= 0 ? (uint32_t)(c->src_stats_req != 0) : (c->bin_stream ? 0u : 1u);
+    return c->src_stats_req >= 0 ? (uint32_t)(c->src_stats_req != 0) : 1u;
 }
 
 // Round phase 2: the push or pull kernels (after the caller's all-gather in a
@@ -1225,12 +1251,15 @@ gossip_status round_compute(gossip_ctx* c) {
         p.chunks = c->chunks;
         p.n_chunks = c->n_chunks;
         p.nw = reinterpret_cast<unsigned long long*>(c->nw);
-        if (a.tcur) HIPCHK(hipMemsetAsync(a.tcur, 0, tact_bytes(c), c->stream));  // unread marks go
+        if (a.tcur) HIPCHK(queue_zero(c, a.tcur, tact_bytes(c)));  // unread marks go
         HIPCHK(timed(c, "pb_scatter", [&] { return launch_pb_scatter(a, p, c->any_dead, c->W, c->stream); }));
         HIPCHK(timed(c, "pb_split", [&] { return launch_pb_split(p, c->stream); }));
         HIPCHK(timed(c, "pb_apply", [&] { return launch_pb_apply(a, p, c->stream); }));
         return GOSSIP_OK;
     }
+    // k_pull_heavy's per-row accumulators, cleared with the round's first kernel
+    const bool hz = c->hacc && c->n_chunks && (c->cur_list || c->last_bin || c->last_pull);
+    if (hz) HIPCHK(queue_zero(c, c->hacc, c->n_chunks * c->Wp * sizeof(uint64_t)));
     if (c->cur_list) {
         // nx holds the new words of the round before last: its list's rows (and the heavy rows) if that was
         // a list round, anything otherwise
@@ -1239,7 +1268,7 @@ gossip_status round_compute(gossip_ctx* c) {
             return hipMemsetAsync(c->nx, 0, c->n_local * sizeof(uint64_t), c->stream);
         }));
         HIPCHK(timed(c, "pull_list", [&] { return launch_pull_list(a, c->lst[c->lst_in], c->lst_in_n, c->stream); }));
-        HIPCHK(timed(c, "pull_heavy", [&] { return launch_pull_heavy(a, pw, c->stream); }));
+        HIPCHK(timed(c, "pull_heavy", [&] { return launch_pull_heavy(a, pw, c->stream, hz); }));
         return GOSSIP_OK;
     }
     if (c->last_pull && a.dead_mode && !a.dgone)  // else the per-source counters give the source side
@@ -1249,21 +1278,21 @@ gossip_status round_compute(gossip_ctx* c) {
         HIPCHK(timed(c, "bin_scatter", [&] { return launch_bin_scatter(a, b, pw, c->stream); }));
         HIPCHK(timed(c, "bin_apply", [&] { return launch_bin_apply(a, b, pw, c->stream); }));
         c->bins_first = false;
-        HIPCHK(timed(c, "pull_heavy", [&] { return launch_pull_heavy(a, pw, c->stream); }));
+        HIPCHK(timed(c, "pull_heavy", [&] { return launch_pull_heavy(a, pw, c->stream, hz); }));
         return GOSSIP_OK;
     }
     if (c->last_pull) {
         if (a.front) HIPCHK(timed(c, "frontier_bits", [&] { return launch_frontier_bits(a, pw, c->stream); }));
         // nx is written whole by the light rows' pull; heavy rows are OR-ed in afterwards
         HIPCHK(timed(c, "pull_light", [&] { return launch_pull_rows(a, pw, c->stream); }));
-        HIPCHK(timed(c, "pull_heavy", [&] { return launch_pull_heavy(a, pw, c->stream); }));
+        HIPCHK(timed(c, "pull_heavy", [&] { return launch_pull_heavy(a, pw, c->stream, hz); }));
         return GOSSIP_OK;
     }
     const bool remote = c->cur_remote;
     if (c->cfg.extra_cap)
         HIPCHK(timed(c, "push_extra", [&] { return launch_push_extra(a, pw, c->any_dead, remote, c->stream); }));
     HIPCHK(timed(c, "push_heavy", [&] { return launch_push_heavy(a, pw, c->any_dead, remote, c->stream); }));
-    if (a.tcur && !a.tsparse) HIPCHK(hipMemsetAsync(a.tcur, 0, tact_bytes(c), c->stream));  // unread marks go
+    if (a.tcur && !a.tsparse) HIPCHK(queue_zero(c, a.tcur, tact_bytes(c)));  // unread marks go
     HIPCHK(timed(c, "push_light", [&] { return launch_push_light(a, pw, c->any_dead, remote, c->stream); }));
     if (c->cur_sparse) {
         HIPCHK(timed(c, "compact_send", [&] {
@@ -1276,12 +1305,13 @@ gossip_status round_compute(gossip_ctx* c) {
 
 gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative) {
     if (c->last_st_round != c->round) {  // read once per round, then the lines are re-zeroed for the next
+        HIPCHK(flush_zero(c));
         HIPCHK(hipMemcpyAsync(c->h_st, c->st, kStatLines * sizeof(DevStats), hipMemcpyDeviceToHost, c->stream));
         if (c->cur_lst_out >= 0)
             HIPCHK(hipMemcpyAsync(&c->lst_out_n, c->d_lst_n + c->cur_lst_out, sizeof(uint32_t), hipMemcpyDeviceToHost,
                                   c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
-        HIPCHK(hipMemsetAsync(c->st, 0, kStatLines * sizeof(DevStats), c->stream));
+        HIPCHK(queue_zero(c, c->st, kStatLines * sizeof(DevStats)));  // cleared with the next round's first launch
         if (c->cur_pb) {  // a record region that would have overflowed (cannot happen: capacities are in-degrees)
             uint32_t e = 0;
             HIPCHK(hipMemcpy(&e, c->pb.err, sizeof(e), hipMemcpyDeviceToHost));

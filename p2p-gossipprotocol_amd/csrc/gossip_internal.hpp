@@ -150,6 +150,7 @@ constexpr int kPbGrid = 256;           // level-1 workgroups (row ranges)
 constexpr uint32_t kPbPad = 0xFFFFFFFFu;  // level-1 padding record (level 2: 0xFFFF)
 constexpr uint32_t kPbMap = 4096;         // level 1's id buckets (coarse bin lookup)
 constexpr uint32_t kPbLoPermille = 50;    // push rounds from this frontier run blocked ...
+constexpr uint64_t kPbPushPeers = 1ull << 22;  // ... on overlays of this many peers ...
 constexpr uint64_t kPbBinSlots = 1ull << 28;  // ... and dense rounds where the slot array has this many slots ...
 constexpr uint32_t kPbHiPermille = 300;   // ... and dense rounds below this one (gossip_config.blocked_permille)
 
@@ -315,7 +316,7 @@ hipError_t launch_push_heavy(const RoundArgs& a, uint32_t W, bool check_alive, b
 hipError_t launch_push_light(const RoundArgs& a, uint32_t W, bool check_alive, bool remote, hipStream_t s);
 hipError_t launch_frontier_bits(const RoundArgs& a, uint32_t W, hipStream_t s);
 hipError_t launch_pull_rows(const RoundArgs& a, uint32_t W, hipStream_t s);
-hipError_t launch_pull_heavy(const RoundArgs& a, uint32_t W, hipStream_t s);
+hipError_t launch_pull_heavy(const RoundArgs& a, uint32_t W, hipStream_t s, bool hacc_zeroed = false);
 // late pull rounds over a needy list (one word per peer): the stale new words of the round before last
 // cleared (by its list, or n_local words), then the list's rows pulled
 hipError_t launch_list_zero(const RoundArgs& a, const uint32_t* lst, uint32_t n, hipStream_t s);
@@ -355,6 +356,16 @@ hipError_t launch_rejoin_select(const RoundArgs& a, const RebootArgs& r, const u
 hipError_t launch_commit_nx(uint64_t* seen, const uint64_t* nx, uint64_t n_words, hipStream_t s);
 hipError_t launch_first2(const uint64_t* rp, const uint32_t* col, uint64_t n, uint64_t* out, hipStream_t s);
 hipError_t launch_zero_words(uint64_t* words, uint64_t n_words, hipStream_t s);
+// up to kZeroRanges small device ranges (whole 32-bit words) cleared by one launch: a round's stat lines,
+// tile marks, heavy-row accumulators and list counters, instead of one fill each (config 2: 55 rounds a
+// step, ~7 us of GPU time and launch gap per fill)
+constexpr int kZeroRanges = 8;
+struct ZeroBatch {
+    uint32_t* p[kZeroRanges];
+    uint32_t n[kZeroRanges];  // words
+    uint32_t count;
+};
+hipError_t launch_zero_batch(const ZeroBatch& z, hipStream_t s);
 hipError_t launch_coverage(const uint64_t* words, uint64_t n_local, uint32_t W, unsigned long long* counts,
                            hipStream_t s);
 hipError_t launch_heavy_count(const uint64_t* rp, uint64_t n_local, uint32_t heavy, uint32_t clen,

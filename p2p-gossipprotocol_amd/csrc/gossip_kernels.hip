@@ -2443,9 +2443,9 @@ hipError_t launch_pull_rows(const RoundArgs& a, uint32_t W_, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_pull_heavy(const RoundArgs& a, uint32_t W_, hipStream_t s) {
+hipError_t launch_pull_heavy(const RoundArgs& a, uint32_t W_, hipStream_t s, bool hacc_zeroed) {
     if (!a.n_chunks) return hipSuccess;
-    if (a.hacc) {
+    if (a.hacc && !hacc_zeroed) {
         const hipError_t e = hipMemsetAsync(a.hacc, 0, a.n_chunks * wp_of(W_) * sizeof(uint64_t), s);
         if (e != hipSuccess) return e;
     }
@@ -2619,6 +2619,20 @@ hipError_t launch_commit_nx(uint64_t* seen, const uint64_t* nx, uint64_t n_words
     const uint64_t n2 = (n_words + 1) / 2;  // the word arrays are allocated in whole pairs
     hipLaunchKernelGGL(k_commit_nx, dim3(grid_for(n2, kBlock)), dim3(kBlock), 0, s, reinterpret_cast<u64x2*>(seen),
                        reinterpret_cast<const u64x2*>(nx), n2);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(kBlock) void k_zero_batch(ZeroBatch z) {
+    for (uint32_t r = 0; r < z.count; ++r) {
+        uint32_t* p = z.p[r];
+        for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < z.n[r]; i += gridDim.x * kBlock) p[i] = 0u;
+    }
+}
+
+hipError_t launch_zero_batch(const ZeroBatch& z, hipStream_t s) {
+    uint32_t most = 0;
+    for (uint32_t r = 0; r < z.count; ++r) most = std::max(most, z.n[r]);
+    hipLaunchKernelGGL(k_zero_batch, dim3(grid_for(most, kBlock)), dim3(kBlock), 0, s, z);
     return hipGetLastError();
 }
 
