@@ -317,9 +317,12 @@ gossip_status gossip_kernel_bytes(gossip_ctx* ctx, const char* kernel, double* b
  * (-1 auto, 0, 1, 2 = print), "src_stats" (-1 auto, 0/1), "blocked_bin_slots"
  * (slot-array size from which dense rounds below blocked_permille run
  * blocked; -1 default 2^28), "blocked_direct_in" (layout: leading 64-peer
- * tiles of more in-degree take direct deliveries; -1 default 2^18).  Layout
- * keys apply at
- * the next gossip_build_graph / gossip_load_csr.  GOSSIP_EINVAL: unknown key. */
+ * tiles of more in-degree take direct deliveries; -1 default 2^18),
+ * "blocked_push_permille" (push rounds from this frontier per-mille run
+ * blocked on overlays of >= 2^26 peers; -1 default 10), "list_rounds" (0: no
+ * needy-list rounds), "list_cap" (layout of the needy lists: rows per list;
+ * 0 = max(n/16, 65536)).  Layout keys apply at the next gossip_build_graph /
+ * gossip_load_csr.  GOSSIP_EINVAL: unknown key. */
 gossip_status gossip_set_tuning(gossip_ctx* ctx, const char* key, int64_t value);
 
 #ifdef __cplusplus

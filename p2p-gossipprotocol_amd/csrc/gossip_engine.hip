@@ -48,9 +48,18 @@ namespace {
             return fail(GOSSIP_EHIP, std::string(#call) + " failed: " + hipGetErrorString(e_));   \
     } while (0)
 
+// clears the liveness masks of the last run: a read of col, and a store only for the 16-B pieces holding
+// a masked entry (config 5: 0.86 ms when every piece was rewritten)
 __global__ void k_unmask(uint32_t* col, uint64_t m) {
-    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (uint64_t)gridDim.x * blockDim.x)
-        col[e] &= ~kMaskedEdge;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint4* c4 = reinterpret_cast<uint4*>(col);
+    const uint32_t mk = kMaskedEdge;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m / 4; i += stride) {
+        const uint4 x = c4[i];
+        if ((x.x | x.y | x.z | x.w) & mk) c4[i] = make_uint4(x.x & ~mk, x.y & ~mk, x.z & ~mk, x.w & ~mk);
+    }
+    for (uint64_t e = m / 4 * 4 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += stride)
+        col[e] &= ~mk;
 }
 
 struct TimerRec {
@@ -184,6 +193,7 @@ struct gossip_ctx {
     uint64_t pb_bin_slots = kPbBinSlots;  // "blocked_bin_slots": slot arrays from this size run their
                                           // sparser dense rounds blocked
     uint64_t pb_direct_in = kPbFineIn;    // "blocked_direct_in": leading tiles of more in-degree are hubs
+    uint32_t pb_lo_pm = kPbLoPermille;    // "blocked_push_permille": push rounds from this frontier run blocked
     bool bin_stream = false;      // streamed binned layout (chosen in prepare_bins)
     int bin_stream_req = -1;      // "bin_stream": 0/1 forces the layout; -1: by slot-array size
     uint32_t defer_pm = kDeferAuto;  // "defer_permille": push rounds with a frontier of >= this per-mille defer
@@ -990,9 +1000,10 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
         }
     }
     // propagation-blocked push (gossip_blocked.hip; one partition, one word per peer): a push round from a
-    // 5 % frontier estimate on overlays of >= kPbPushPeers peers -- below it the atomic push's deliveries
-    // cost less than the blocked round's fixed passes (config 3 round 2, 2.1 %: push 0.25 ms, blocked
-    // 0.79 ms; config 2 at 5.05 %: blocked 0.097 ms per round, 9 rounds a step) -- and, where the slot array
+    // 1 % frontier estimate on overlays of >= kPbPushPeers peers (config 4 round 3, 1.25 %, 53.5 M
+    // traversals: push 4.4 ms, blocked 3.4-3.5 ms; smaller overlays lose to the blocked round's fixed
+    // passes: config 3 round 2, 2.1 %: push 0.25 ms, blocked 0.79 ms; config 2 at 5.05 %: blocked 0.097 ms
+    // per round, 9 rounds a step) -- and, where the slot array
     // outgrows the MALL many times over (>= kPbBinSlots slots: its scattered stores go to HBM as partial
     // lines), a binned round below blocked_permille (every edge streamed for a minority of active
     // sources) write one record per delivery instead (config 4 round 4, 17 %: binned 15.6 ms, blocked
@@ -1005,7 +1016,7 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
         if (c->cfg.flags & GOSSIP_FLAG_FORCE_BLOCKED)
             c->cur_pb = !pull || bin;
         else
-            c->cur_pb = (!pull && c->n_local >= kPbPushPeers && front * 1000 >= c->n_local * (uint64_t)kPbLoPermille) ||
+            c->cur_pb = (!pull && c->n_local >= kPbPushPeers && front * 1000 >= c->n_local * (uint64_t)c->pb_lo_pm) ||
                         (bin && (!c->bins_ready || c->bins.n_slots >= c->pb_bin_slots) &&
                          front * 1000 < c->n_local * (uint64_t)hi);
         if (c->cur_pb) pull = bin = false;
@@ -1599,6 +1610,7 @@ gossip_status gossip_set_tuning(gossip_ctx* c, const char* key, int64_t value) {
     else if (k == "blocked_bin_slots") c->pb_bin_slots = value < 0 ? kPbBinSlots : (uint64_t)value;
     else if (k == "blocked_direct_in") c->pb_direct_in = value < 0 ? kPbFineIn : (uint64_t)value;
     else if (k == "list_rounds") c->list_req = value != 0;
+    else if (k == "blocked_push_permille") c->pb_lo_pm = value < 0 ? kPbLoPermille : u;
     else if (k == "list_cap") c->list_cap_req = u;
     else return fail(GOSSIP_EINVAL, "unknown tuning option: " + k);
     return GOSSIP_OK;

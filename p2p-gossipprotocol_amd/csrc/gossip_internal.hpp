@@ -149,8 +149,8 @@ constexpr int kPbBlock = 1024;         // 16 waves per workgroup, one workgroup 
 constexpr int kPbGrid = 256;           // level-1 workgroups (row ranges)
 constexpr uint32_t kPbPad = 0xFFFFFFFFu;  // level-1 padding record (level 2: 0xFFFF)
 constexpr uint32_t kPbMap = 4096;         // level 1's id buckets (coarse bin lookup)
-constexpr uint32_t kPbLoPermille = 50;    // push rounds from this frontier run blocked ...
-constexpr uint64_t kPbPushPeers = 1ull << 22;  // ... on overlays of this many peers ...
+constexpr uint32_t kPbLoPermille = 10;    // push rounds from this frontier run blocked ...
+constexpr uint64_t kPbPushPeers = 1ull << 26;  // ... on overlays of this many peers ...
 constexpr uint64_t kPbBinSlots = 1ull << 28;  // ... and dense rounds where the slot array has this many slots ...
 constexpr uint32_t kPbHiPermille = 300;   // ... and dense rounds below this one (gossip_config.blocked_permille)
 

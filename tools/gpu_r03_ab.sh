@@ -1,11 +1,13 @@
 #!/bin/bash
-# Round 3 A/B: the engine-variant parity tests for the variants named in $K, then
-# per-round kernel times of config ${CFG:-4} once per env setting ("-" = defaults).
+# Round 3: per-round A/B of engine options on one config (round_profile.py, arms alternated).
+# usage: gpu_r03_ab.sh <config> "<optsA>" "<optsB>"   (opts: key=val ... passed to round_profile.py)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-mkdir -p gpurun_out/var
-if [ -n "$K" ]; then
-  timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -k "$K" > gpurun_out/var/pytest.log 2>&1 || { tail -30 gpurun_out/var/pytest.log; exit 1; }
-  tail -2 gpurun_out/var/pytest.log
-fi
-bash tools/gpu_rounds_env.sh "$@"
+O=gpurun_out/ab; mkdir -p $O
+C=$1; A=$2; B=$3
+for i in 1 2; do
+  timeout -k 10 300 python3 -u tools/round_profile.py $C $A > $O/a$i.txt 2>&1 || { tail -20 $O/a$i.txt; exit 1; }
+  echo "== A$i: $A"; cat $O/a$i.txt
+  timeout -k 10 300 python3 -u tools/round_profile.py $C $B > $O/b$i.txt 2>&1 || { tail -20 $O/b$i.txt; exit 1; }
+  echo "== B$i: $B"; cat $O/b$i.txt
+done

@@ -12,8 +12,9 @@ K = ("push_light", "push_heavy", "pull_light", "pull_heavy", "frontier_bits", "b
      "pb_scatter", "pb_split", "pb_apply", "pull_list", "list_zero")
 w = config(int(sys.argv[1]) if len(sys.argv) > 1 else 4)
 kw = dict(a.split("=", 1) for a in sys.argv[2:])  # extra engine options, e.g. blocked=off
-kw = {k: (int(v) if v.isdigit() else v) for k, v in kw.items()}
-e = Engine(w.n, w.n_msgs, device=0, **w.engine_kwargs(), **kw)
+kw = {k: (int(v) if v.lstrip("-").isdigit() else v) for k, v in kw.items()}
+tuning = {k[2:]: kw.pop(k) for k in list(kw) if k.startswith("t.")}  # t.<key>=<int>: gossip_set_tuning
+e = Engine(w.n, w.n_msgs, device=0, tuning=tuning, **w.engine_kwargs(), **kw)
 e.build_graph()
 e.inject(w.origins, w.inject_rounds)
 e.run()
