@@ -445,96 +445,133 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_split(PbArgs p) {
 }
 
 // ---------------------------------------------------------------------------
-// apply: one workgroup per fine bin (whole tiles, <= kBinWords peers).  handleClient's test-and-set for every peer a record
-// reached (peer.cpp:277-285): fr = (OR of its records) & ~seen.
+// apply: kPbApplyGrid workgroups, each looping over the fine bins f = w, w + grid, ... (whole tiles,
+// <= kBinWords peers).  handleClient's test-and-set for every peer a record reached (peer.cpp:277-285):
+// fr = (OR of its records) & ~seen.  A workgroup holds the 144 KB accumulator for its whole life: the
+// next bin's segment table is loaded while this bin is swept, the accumulator is cleared by the sweep
+// that reads it, and the statistics are flushed once (one workgroup per bin, 14.6 K of them at
+// config 4, paid a launch, a clear, three dependent round trips and a flush per bin: 1.8 ms for round
+// 3's 53.5 M records).
 // ---------------------------------------------------------------------------
+constexpr int kPbApplyGrid = 256;  // one per CU (the accumulator takes most of the LDS)
 __global__ __launch_bounds__(1024) void k_pb_apply(RoundArgs a, PbArgs p) {
     __shared__ unsigned long long acc_s[kBinWords];
-    const uint32_t f = blockIdx.x;
-    uint32_t any = 0;
-#pragma unroll
-    for (uint32_t s = 0; s < kPbSlices; ++s) any |= p.s2_len[(uint64_t)s * p.n_fine + f];
-    if (!any) return;  // no record: nothing changes (nx is zero at a push round's start)
-    const uint32_t v0 = p.f_lo[f], nv = p.f_lo[f + 1] - v0;
-    for (uint32_t i = threadIdx.x; i < nv; i += 1024) acc_s[i] = 0ull;
-    __syncthreads();
-    // the records of the bin's kPbSlices segments (one virtual array: prefix sums ps), kPbU per thread,
-    // the next batch's loads in flight while this one is folded
-    uint64_t sb[kPbSlices];
-    uint32_t ps[kPbSlices + 1];
-    ps[0] = 0;
-#pragma unroll
-    for (uint32_t s = 0; s < kPbSlices; ++s) {
-        sb[s] = p.s2_base[(uint64_t)s * p.n_fine + f];
-        ps[s + 1] = ps[s] + p.s2_len[(uint64_t)s * p.n_fine + f];
-    }
-    {
-        const uint32_t total = ps[kPbSlices];
-        auto load = [&](uint32_t v0_, uint16_t (&d)[kPbU], unsigned long long (&w)[kPbU]) {
-#pragma unroll
-            for (int j = 0; j < kPbU; ++j) {
-                const uint32_t vi = v0_ + j * 1024;
-                uint32_t sg = 0;
-#pragma unroll
-                for (uint32_t s = 1; s < kPbSlices; ++s) sg += vi >= ps[s];
-                const bool in = vi < total;
-                const uint64_t at = in ? sb[sg] + (vi - ps[sg]) : 0;
-                d[j] = in ? p.r2_dst[at] : (uint16_t)0xFFFFu;
-                w[j] = in ? p.r2_w[at] : 0ull;
-            }
-        };
-        uint16_t d[kPbU], d2[kPbU];
-        unsigned long long w[kPbU], w2[kPbU];
-        uint32_t vb = threadIdx.x;
-        load(vb, d, w);
-        while (vb < total) {
-            load(vb + 1024 * kPbU, d2, w2);
-#pragma unroll
-            for (int j = 0; j < kPbU; ++j)
-                if (d[j] != 0xFFFFu) atomicOr(&acc_s[d[j]], w[j]);  // ds_or_b64
-            vb += 1024 * kPbU;
-#pragma unroll
-            for (int j = 0; j < kPbU; ++j) {
-                d[j] = d2[j];
-                w[j] = w2[j];
-            }
-        }
-    }
-    __syncthreads();
+    __shared__ uint32_t meta_s[2][3 * kPbSlices + 2];  // per bin: s2_len[4], s2_base lo/hi [8], f_lo, f_lo + 1
+    for (uint32_t i = threadIdx.x; i < kBinWords; i += 1024) acc_s[i] = 0ull;
     Acc acc;
     const int lane = threadIdx.x & 63;
     const uint64_t inj = injm(a, 0);
-    // a thread's peers i = tid + 1024 j: every seen word it needs loaded at once (a wave covers one tile)
     constexpr int kJ = (kBinWords + 1023) / 1024;
-    unsigned long long x[kJ], sv[kJ];
-#pragma unroll
-    for (int j = 0; j < kJ; ++j) {
-        const uint32_t i = threadIdx.x + 1024u * j;
-        x[j] = i < nv ? acc_s[i] : 0ull;
-        sv[j] = x[j] ? a.seen[v0 + i] : 0ull;
-    }
-#pragma unroll
-    for (int j = 0; j < kJ; ++j) {
-        const uint32_t i = threadIdx.x + 1024u * j;
-        if (i >= ((nv + 63) & ~63u)) break;  // wave-uniform
-        const uint64_t v = v0 + i;
-        const unsigned long long fr = x[j] & inj & ~sv[j];
-        if (fr) {  // new -> Message-List insert (peer.cpp:281-282)
-            a.seen[v] = sv[j] | fr;
-            a.nx[v] = fr;
-            acc.fresh += (unsigned long long)__popcll(fr);
-            acc.activated++;
-            acc.fresh_or[0] |= fr;
+    // the segment table of bin f into meta_s[b] (threads 0 .. 3 kPbSlices + 1)
+    auto load_meta = [&](uint32_t f, int b) {
+        const uint32_t t = threadIdx.x;
+        if (f >= p.n_fine || t >= 3 * kPbSlices + 2) return;
+        uint32_t x;
+        if (t < kPbSlices) x = p.s2_len[(uint64_t)t * p.n_fine + f];
+        else if (t < 3 * kPbSlices) {
+            const uint32_t s = (t - kPbSlices) >> 1;
+            const uint64_t base = p.s2_base[(uint64_t)s * p.n_fine + f];
+            x = (t - kPbSlices) & 1 ? (uint32_t)(base >> 32) : (uint32_t)base;
+        } else {
+            x = p.f_lo[f + (t - 3 * kPbSlices)];
         }
-        if (a.tnx) {  // the tile joins the next round's frontier tiles
-            const unsigned long long b = __ballot(fr != 0);
-            if (b && lane == 0) {
-                const uint64_t t = v >> 6;
-                unsigned long long* tw = reinterpret_cast<unsigned long long*>(a.tnx) + (t >> 6);
-                const unsigned long long tb = 1ull << (t & 63);
-                if (!(*tw & tb)) atomicOr(tw, tb);
+        meta_s[b][t] = x;
+    };
+    int cb = 0;
+    load_meta(blockIdx.x, 0);
+    __syncthreads();
+    for (uint32_t f = blockIdx.x; f < p.n_fine; f += gridDim.x, cb ^= 1) {
+        const uint32_t* m = meta_s[cb];
+        uint32_t ps[kPbSlices + 1];
+        uint64_t sb[kPbSlices];
+        ps[0] = 0;
+#pragma unroll
+        for (uint32_t s = 0; s < kPbSlices; ++s) {
+            ps[s + 1] = ps[s] + m[s];
+            sb[s] = (uint64_t)m[kPbSlices + 2 * s] | ((uint64_t)m[kPbSlices + 2 * s + 1] << 32);
+        }
+        const uint32_t v0 = m[3 * kPbSlices], nv = m[3 * kPbSlices + 1] - v0;
+        const uint32_t total = ps[kPbSlices];
+        load_meta(f + gridDim.x, cb ^ 1);  // (its own buffer: read after the barriers below)
+        if (total == 0) {  // no record: nothing changes (nx is zero at a push round's start)
+            __syncthreads();
+            continue;
+        }
+        // the records of the bin's kPbSlices segments (one virtual array: prefix sums ps), kPbU per thread,
+        // the next batch's loads in flight while this one is folded
+        {
+            auto load = [&](uint32_t v0_, uint16_t (&d)[kPbU], unsigned long long (&w)[kPbU]) {
+#pragma unroll
+                for (int j = 0; j < kPbU; ++j) {
+                    const uint32_t vi = v0_ + j * 1024;
+                    uint32_t sg = 0;
+#pragma unroll
+                    for (uint32_t s = 1; s < kPbSlices; ++s) sg += vi >= ps[s];
+                    const bool in = vi < total;
+                    const uint64_t at = in ? sb[sg] + (vi - ps[sg]) : 0;
+                    d[j] = in ? p.r2_dst[at] : (uint16_t)0xFFFFu;
+                    w[j] = in ? p.r2_w[at] : 0ull;
+                }
+            };
+            uint16_t d[kPbU], d2[kPbU];
+            unsigned long long w[kPbU], w2[kPbU];
+            uint32_t vb = threadIdx.x;
+            load(vb, d, w);
+            while (vb < total) {
+                load(vb + 1024 * kPbU, d2, w2);
+#pragma unroll
+                for (int j = 0; j < kPbU; ++j)
+                    if (d[j] != 0xFFFFu) atomicOr(&acc_s[d[j]], w[j]);  // ds_or_b64
+                vb += 1024 * kPbU;
+#pragma unroll
+                for (int j = 0; j < kPbU; ++j) {
+                    d[j] = d2[j];
+                    w[j] = w2[j];
+                }
             }
         }
+        __syncthreads();
+        // a thread's peers i = tid + 1024 j (a wave covers one 64-peer tile): every seen word it needs
+        // loaded at once; the accumulator words read are cleared for the next bin.  A tile with a record
+        // reads and, if a peer of it learns, writes its seen and nx words whole (512 B each): single-word
+        // stores into a 64-B sector cost a read-modify-write at the memory, and at round 4's 17 % of
+        // peers learning nearly every sector gets one.  Untouched peers rewrite their own seen word and a
+        // zero nx word (nx is zero at a push round's start).
+        unsigned long long x[kJ], sv[kJ];
+#pragma unroll
+        for (int j = 0; j < kJ; ++j) {
+            const uint32_t i = threadIdx.x + 1024u * j;
+            x[j] = i < nv ? acc_s[i] : 0ull;
+            if (x[j]) acc_s[i] = 0ull;
+            const bool tile = __ballot(x[j] != 0) != 0ull;
+            sv[j] = tile && i < nv ? a.seen[v0 + i] : 0ull;
+        }
+#pragma unroll
+        for (int j = 0; j < kJ; ++j) {
+            const uint32_t i = threadIdx.x + 1024u * j;
+            if (i >= ((nv + 63) & ~63u)) break;  // wave-uniform
+            const uint64_t v = v0 + i;
+            const unsigned long long fr = x[j] & inj & ~sv[j];
+            const unsigned long long b = __ballot(fr != 0);
+            if (b && i < nv) {  // new -> Message-List insert (peer.cpp:281-282)
+                a.seen[v] = sv[j] | fr;
+                a.nx[v] = fr;
+            }
+            if (fr) {
+                acc.fresh += (unsigned long long)__popcll(fr);
+                acc.activated++;
+                acc.fresh_or[0] |= fr;
+            }
+            if (a.tnx) {  // the tile joins the next round's frontier tiles
+                if (b && lane == 0) {
+                    const uint64_t t = v >> 6;
+                    unsigned long long* tw = reinterpret_cast<unsigned long long*>(a.tnx) + (t >> 6);
+                    const unsigned long long tb = 1ull << (t & 63);
+                    if (!(*tw & tb)) atomicOr(tw, tb);
+                }
+            }
+        }
+        __syncthreads();  // the accumulator is clear and the next segment table is in
     }
     flush<1024 / 64>(acc, a.st);
 }
@@ -799,7 +836,8 @@ hipError_t launch_pb_split(const PbArgs& p, hipStream_t s) {
 
 hipError_t launch_pb_apply(const RoundArgs& a, const PbArgs& p, hipStream_t s) {
     if (!p.n_fine) return hipSuccess;
-    hipLaunchKernelGGL(k_pb_apply, dim3((unsigned)p.n_fine), dim3(1024), 0, s, a, p);
+    const unsigned g = (unsigned)std::min<uint64_t>(p.n_fine, kPbApplyGrid);
+    hipLaunchKernelGGL(k_pb_apply, dim3(g), dim3(1024), 0, s, a, p);
     return hipGetLastError();
 }
 

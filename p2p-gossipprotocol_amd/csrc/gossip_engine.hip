@@ -654,8 +654,8 @@ gossip_status upload_csr(gossip_ctx* c, const uint64_t* rp, const uint32_t* col,
 // binned rounds' scatter at 9.2-9.4 ms in some processes and 10.7-11.8 in others, the apply (a
 // sequential read of the same array) at 5.0-5.8 in all, and a physically contiguous array at 14 ms.
 // Allocations in one process differ too (trial scatters of 9.3 / 10.3 / 8.8 ms), though some processes
-// get only slow ones.  On big layouts, time one full scatter (every slot rewritten) into each of four
-// allocations and keep the fastest ("val_tune" 0: keep the first; 2: print the trials); config 4,
+// get only slow ones.  On big layouts, time one full scatter (every slot rewritten) into each of eight
+// allocations (four in round 2) and keep the fastest ("val_tune" 0: keep the first; 2: print the trials); config 4,
 // five processes each: scatter 9.3-11.3 (mean 9.9) against 9.7-11.7 (mean 10.4) ms.  The trial words
 // are garbage: the first binned round rewrites every slot.
 BinArgs bin_args(const gossip_ctx* c, bool noskip, uint32_t src_side) {
@@ -672,7 +672,7 @@ gossip_status tune_val(gossip_ctx* c) {
     if (c->val_tune == 0 || c->bin_stream || c->n_local != c->n || (c->val_tune < 0 && c->bins.n_slots < (1ull << 26)))
         return GOSSIP_OK;
     const uint64_t bytes = (c->bins.n_slots + 64) * c->Wp * sizeof(uint64_t);
-    constexpr int kCand = 4;
+    constexpr int kCand = 8;  // (8 x 16 GB at config 4, freed before the blocked regions are laid out)
     uint64_t* cand[kCand] = {c->bins.val};
     for (int k = 1; k < kCand; ++k)
         if (hipMalloc((void**)&cand[k], bytes) != hipSuccess) {
