@@ -321,7 +321,8 @@ gossip_status gossip_kernel_bytes(gossip_ctx* ctx, const char* kernel, double* b
  * "blocked_push_permille" (push rounds from this frontier per-mille run
  * blocked on overlays of >= 2^26 peers; -1 default 10), "list_rounds" (0: no
  * needy-list rounds), "list_cap" (layout of the needy lists: rows per list;
- * 0 = max(n/16, 65536)).  Layout keys apply at the next gossip_build_graph /
+ * 0 = max(n/16, 65536)), "pull_step" (neighbour words a row pull gathers
+ * per row per step: 1 default, or 2).  Layout keys apply at the next gossip_build_graph /
  * gossip_load_csr.  GOSSIP_EINVAL: unknown key. */
 gossip_status gossip_set_tuning(gossip_ctx* ctx, const char* key, int64_t value);
 

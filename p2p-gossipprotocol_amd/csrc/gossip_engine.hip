@@ -194,6 +194,9 @@ struct gossip_ctx {
                                           // sparser dense rounds blocked
     uint64_t pb_direct_in = kPbFineIn;    // "blocked_direct_in": leading tiles of more in-degree are hubs
     uint32_t pb_lo_pm = kPbLoPermille;    // "blocked_push_permille": push rounds from this frontier run blocked
+    uint32_t row_step = 1;                // "pull_step": k_pull_rows's neighbour words per row per step
+                                          // (config 4 round 7: 2 -> 1, 180 -> 101 M gathers, 6.6-6.8 ->
+                                          // 5.4-5.7 ms; most rows stop at their first neighbour)
     bool bin_stream = false;      // streamed binned layout (chosen in prepare_bins)
     int bin_stream_req = -1;      // "bin_stream": 0/1 forces the layout; -1: by slot-array size
     uint32_t defer_pm = kDeferAuto;  // "defer_permille": push rounds with a frontier of >= this per-mille defer
@@ -498,6 +501,7 @@ RoundArgs make_args(gossip_ctx* c) {
     a.chunks = c->chunks;
     a.n_chunks = c->n_chunks;
     a.hacc = c->hacc;
+    a.row_step = c->row_step;
     a.inj_live = c->world <= 1 && c->n_local == c->n ? c->inj_live : nullptr;  // a partition injects its own only
     a.n_local = c->n_local;
     a.begin = c->begin;
@@ -1610,6 +1614,7 @@ gossip_status gossip_set_tuning(gossip_ctx* c, const char* key, int64_t value) {
     else if (k == "blocked_bin_slots") c->pb_bin_slots = value < 0 ? kPbBinSlots : (uint64_t)value;
     else if (k == "blocked_direct_in") c->pb_direct_in = value < 0 ? kPbFineIn : (uint64_t)value;
     else if (k == "list_rounds") c->list_req = value != 0;
+    else if (k == "pull_step") c->row_step = value == 1 ? 1u : 2u;
     else if (k == "blocked_push_permille") c->pb_lo_pm = value < 0 ? kPbLoPermille : u;
     else if (k == "list_cap") c->list_cap_req = u;
     else return fail(GOSSIP_EINVAL, "unknown tuning option: " + k);

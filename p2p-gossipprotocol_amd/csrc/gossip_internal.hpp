@@ -274,6 +274,7 @@ struct RoundArgs {
     uint32_t* lst_n;               // entries appended (may pass lst_cap: the list overflowed)
     uint32_t lst_cap;
     uint32_t src_booked;           // k_pull_rows: the sweep books no source side
+    uint32_t row_step;             // k_pull_rows: neighbour words gathered per row per step (1 or 2)
 };
 
 // Re-bootstrap draw (handleDeadPeer peer.cpp:398-404 -> selectAndConnectPeers

@@ -639,9 +639,10 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
             // rows are sorted, so the scan meets the hubs first: their words are cache-hot (scanning
             // from the row's end measured 192 M gathers and 8.0-9.2 ms against 180 M, 7.3-7.5 ms at
             // config 4 round 7).  A row's first two entries may come with its queue entry (a.first2).
-            const bool f2 = a.first2 && rk == 0 && j < 2;
-            const uint32_t uc = a.col[ok[j] && !f2 ? rrb + rk + j : 0];
-            u[j] = f2 ? (uint32_t)(rf2 >> (32 * j)) : uc;
+            const uint32_t q = rk + j;
+            const bool f2 = a.first2 && q < 2;
+            const uint32_t uc = a.col[ok[j] && !f2 ? rrb + q : 0];
+            u[j] = f2 ? (uint32_t)(rf2 >> (32 * q)) : uc;
         }
         acc.pulled += (has ? min(kRowB, (int)(rd - rk)) : 0);
 #pragma unroll
@@ -1298,7 +1299,9 @@ __global__ __launch_bounds__(kB) void k_bin_apply(RoundArgs a, BinArgs b, uint32
             acc.fresh += (unsigned long long)__popcll(fr);
             acc.activated++;
         }
-        if (fr | p) a.seen[v0 * W + i] = sv | fr;
+        // seen rewritten whole for a tile where any word changes (a single-word store into a 64-B sector
+        // costs a read-modify-write at the memory)
+        if (__ballot((fr | p) != 0)) a.seen[v0 * W + i] = sv | fr;
         a.nx[v0 * W + i] = fr;  // heavy rows: 0 here, OR-ed by k_pull_heavy afterwards
     }
     flush<kB / 64>(acc, a.st);
@@ -1527,7 +1530,7 @@ __global__ __launch_bounds__(kB) void k_bin_apply_runs(RoundArgs a, BinArgs b, u
                 acc.fresh += (unsigned long long)__popcll(fr);
                 acc.activated++;
             }
-            if (fr | p) a.seen[v0 * W + i] = sv | fr;
+            if (__ballot((fr | p) != 0)) a.seen[v0 * W + i] = sv | fr;  // whole tiles (k_bin_apply)
             a.nx[v0 * W + i] = fr;  // heavy rows: 0 here, OR-ed by k_pull_heavy afterwards
         }
     };
@@ -2434,7 +2437,11 @@ hipError_t launch_pull_rows(const RoundArgs& a, uint32_t W_, hipStream_t s) {
     // a row queue per wave: every wave resident at once (its queue carries its work)
     const unsigned g = std::min(grid_for((a.n_local + 63) / 64, kWavesPerBlock), (unsigned)kMaxGrid);
     const uint32_t wd = wd_of(W_);
-#define GOSSIP_ROWS(COV, FR) hipLaunchKernelGGL((k_pull_rows<W, COV, FR, 2>), dim3(g), dim3(kBlock), 0, s, a, wd)
+#define GOSSIP_ROWS(COV, FR)                                                                        \
+    do {                                                                                            \
+        if (a.row_step == 1) hipLaunchKernelGGL((k_pull_rows<W, COV, FR, 1>), dim3(g), dim3(kBlock), 0, s, a, wd); \
+        else hipLaunchKernelGGL((k_pull_rows<W, COV, FR, 2>), dim3(g), dim3(kBlock), 0, s, a, wd);              \
+    } while (0)
     GOSSIP_DISPATCH_W(wp_of(W_), {
         if (a.cov) { if (a.front) GOSSIP_ROWS(true, true); else GOSSIP_ROWS(true, false); }
         else { if (a.front) GOSSIP_ROWS(false, true); else GOSSIP_ROWS(false, false); }

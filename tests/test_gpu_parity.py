@@ -338,7 +338,8 @@ _VARIANTS = {"defer_1": ({"defer_permille": 1}, {"blocked": "off"}), "stream": (
              "no_flight": ({"in_flight": 0}, {}), "no_heavy_exit": ({"heavy_exit": 0}, {}),
              "small_bins": ({"bin_words": 4096, "bin_chunk": 2048}, {}), "apply_src": ({"src_stats": 0}, {}),
              "heavy_64": ({"heavy_degree": 64, "heavy_chunk": 128}, {}), "all_pull": ({}, {"bin_permille": 100000}),
-             "blocked_wide": ({}, {"blocked_permille": 1000})}
+             "blocked_wide": ({}, {"blocked_permille": 1000}), "pull_step_2": ({"pull_step": 2}, {}),
+             "no_lists": ({"list_rounds": 0}, {})}
 
 
 @pytest.mark.parametrize("variant", sorted(_VARIANTS))
