@@ -84,9 +84,10 @@ typedef struct gossip_config {
                                   r restarts in r iff philox({seed,v},{7,r,0,0}).x < threshold -- re-registered,
                                   empty Message-List, old connections gone, fresh out-edges from one seed response
                                   into its overflow row (extra_cap > 0).  0 = never.  Single partition only */
-    uint32_t blocked_permille; /* propagation-blocked push (single partition, M <= 64): a push round from a 0.2 %
-                                  frontier estimate, or a binned round below this per-mille, runs blocked
-                                  (0 = 300) */
+    uint32_t blocked_permille; /* propagation-blocked rounds (single partition, M <= 64):
+                                  a binned round below this frontier per-mille runs blocked where the slot array
+                                  has >= 2^28 slots (0 = 300); push rounds from a 1 % frontier on overlays of
+                                  >= 2^26 peers ("blocked_push_permille" of gossip_set_tuning) */
 } gossip_config;
 
 /*
