@@ -33,6 +33,7 @@ typedef int gossip_status;
 #define GOSSIP_ESTATE (-4)  /* call out of order (e.g. step before graph) */
 #define GOSSIP_ENODEV (-5)  /* no gfx950 device visible */
 #define GOSSIP_EOVERFLOW (-6) /* report buffer overflowed (reports dropped) */
+#define GOSSIP_ESTALL (-8)    /* device work gave up waiting (a bounded spin tripped): results incomplete */
 
 /* Overlay models. */
 #define GOSSIP_GRAPH_POWERLAW 1      /* scale overlay: power-law pick (peer.cpp:219-222), skewed
@@ -313,9 +314,10 @@ gossip_status gossip_kernel_bytes(gossip_ctx* ctx, const char* kernel, double* b
  * environment; results are identical under every setting).  Keys: "tiny" (0:
  * small overlays run round by round), "full_liveness" (ping every edge instead
  * of the closed form), "defer_permille" (-1 auto), "bin_stream" (-1 by size,
- * 0/1 forced), "pull_first2", "in_flight", "heavy_exit", "heavy_degree",
- * "heavy_chunk", "bin_front_permille", "bin_words", "bin_chunk", "val_tune"
- * (-1 auto, 0, 1, 2 = print), "src_stats" (-1 auto, 0/1), "blocked_bin_slots"
+ * 0/1 forced), "pull_first2", "in_flight", "heavy_exit", "heavy_degree"
+ * (layout), "heavy_chunk", "bin_front_permille", "bin_words", "bin_chunk", "val_tune"
+ * (-1 auto, 0, 1, 2 = print), "src_stats" (who books a binned round's source
+ * side: -1 auto = 1 the scatter, 0 the apply), "blocked_bin_slots"
  * (slot-array size from which dense rounds below blocked_permille run
  * blocked; -1 default 2^28), "blocked_direct_in" (layout: leading 64-peer
  * tiles of more in-degree take direct deliveries; -1 default 2^18),
@@ -323,8 +325,9 @@ gossip_status gossip_kernel_bytes(gossip_ctx* ctx, const char* kernel, double* b
  * blocked on overlays of >= 2^26 peers; -1 default 10), "list_rounds" (0: no
  * needy-list rounds), "list_cap" (layout of the needy lists: rows per list;
  * 0 = max(n/16, 65536)), "pull_step" (neighbour words a row pull gathers
- * per row per step: 1 default, or 2).  Layout keys apply at the next gossip_build_graph /
- * gossip_load_csr.  GOSSIP_EINVAL: unknown key. */
+ * per row per step: 1 default, or 2; other values GOSSIP_EINVAL).  Layout keys
+ * apply at the next gossip_build_graph / gossip_load_csr ("list_cap": at the
+ * next chain of needy-list rounds, never inside one).  GOSSIP_EINVAL: unknown key. */
 gossip_status gossip_set_tuning(gossip_ctx* ctx, const char* key, int64_t value);
 
 #ifdef __cplusplus

@@ -74,18 +74,18 @@ template <bool CA, bool COV>
 __global__ __launch_bounds__(kPbBlock) void k_pb_scatter(RoundArgs a, PbArgs p, uint32_t wd) {
     __shared__ uint32_t lo_s[kPbCoarse + 1];
     __shared__ uint8_t cmap_s[kPbMap];  // coarse bin of each id bucket's first peer (then a short walk)
-    __shared__ uint32_t tk_s[kPbCoarse], wr_s[kPbCoarse], dn_s[kPbCoarse];
+    __shared__ uint32_t tk_s[kPbCoarse], wr_s[2 * kPbCoarse], gn_s[2 * kPbCoarse];
     __shared__ unsigned long long base_s[kPbCoarse];  // this workgroup's segment of each coarse bin
     __shared__ uint32_t cap_s[kPbCoarse];
-    __shared__ uint32_t bd_s[kPbCoarse * kPbB1];
-    __shared__ unsigned long long bw_s[kPbCoarse * kPbB1];
+    __shared__ uint32_t bd_s[kPbCoarse * 2 * kPbB1];
+    __shared__ unsigned long long bw_s[kPbCoarse * 2 * kPbB1];
     __shared__ uint32_t pk_v[kPbWaves][128];
     __shared__ unsigned long long pk_m[kPbWaves][128];
     __shared__ unsigned int cov_s[COV ? 64 : 1];
     const uint32_t nc = p.n_coarse, wg = blockIdx.x;
     for (uint32_t i = threadIdx.x; i <= kPbCoarse; i += kPbBlock) lo_s[i] = i <= nc ? p.c_lo[i] : 0xFFFFFFFFu;
+    stage_init(tk_s, wr_s, gn_s, kPbCoarse, threadIdx.x, kPbBlock);
     for (uint32_t i = threadIdx.x; i < kPbCoarse; i += kPbBlock) {
-        tk_s[i] = wr_s[i] = dn_s[i] = 0;
         base_s[i] = i < nc ? p.s1_base[(uint64_t)wg * nc + i] : 0ull;
         cap_s[i] = i < nc ? p.s1_cap[(uint64_t)wg * nc + i] : 0u;
     }
@@ -103,18 +103,19 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_scatter(RoundArgs a, PbArgs p, 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 
     // generation g of coarse bin k goes to place g * kPbB1 of the workgroup's segment:
-    // 32 lanes store the destinations (128 B), 32 the words (256 B)
-    auto flush1 = [&](uint32_t k) {
-        const uint32_t pos = lds_load(&dn_s[k]) * kPbB1;
-        const uint32_t i = lane & 31;
-        const uint32_t dv = bd_s[k * kPbB1 + i];
-        const unsigned long long wv = bw_s[k * kPbB1 + i];
+    // 16 lanes store the destinations (64 B), 16 the words (128 B)
+    auto flush1 = [&](uint32_t k, uint32_t g) {
+        const uint32_t pos = g * kPbB1;
+        const uint32_t i = lane & (kPbB1 - 1);
+        const uint32_t hb = k * 2 * kPbB1 + (g & 1) * kPbB1;
+        const uint32_t dv = bd_s[hb + i];
+        const unsigned long long wv = bw_s[hb + i];
         lds_fence();
-        if (lane == 0) stage_release(wr_s, dn_s, k);
+        if (lane == 0) stage_release(wr_s, gn_s, k, g);
         if (pos + kPbB1 <= cap_s[k]) {
             const uint64_t at = base_s[k] + pos + i;
-            if (lane < 32) p.r1_dst[at] = dv;
-            else p.r1_w[at] = wv;
+            if (lane < (int)kPbB1) p.r1_dst[at] = dv;
+            else if (lane < 2 * (int)kPbB1) p.r1_w[at] = wv;
         } else if (lane == 0) {
             atomicOr(p.err, 1u);
         }
@@ -181,7 +182,7 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_scatter(RoundArgs a, PbArgs p, 
         direct(c, m, rec);
 #pragma unroll
         for (int j = 0; j < kPbU; ++j) k[j] = rec[j] ? coarse_of(c[j]) : 0u;
-        stage<kPbU, kPbB1>(tk_s, wr_s, dn_s, bd_s, bw_s, k, c, m, rec, flush1, p.err);
+        stage<kPbU, kPbB1>(tk_s, wr_s, gn_s, bd_s, bw_s, k, c, m, rec, flush1, p.err);
     };
 
     // (1) heavy chunks wg, wg + kPbGrid, ..., one wave each (their rows' words are cleared by the split)
@@ -321,17 +322,19 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_scatter(RoundArgs a, PbArgs p, 
     // the partly filled buffers, padded to whole flushes; then the segments' lengths
     __syncthreads();
     for (uint32_t k = wave; k < nc; k += kPbWaves) {
-        const uint32_t n = stage_open(tk_s, k, kPbB1);
+        uint32_t g = 0;
+        const uint32_t n = stage_open(tk_s, k, kPbB1, &g);
         if (!n) continue;  // wave-uniform
         if ((uint32_t)lane >= n && lane < (int)kPbB1) {
-            bd_s[k * kPbB1 + lane] = kPbPad;
-            bw_s[k * kPbB1 + lane] = 0ull;
+            const uint32_t s = k * 2 * kPbB1 + (g & 1) * kPbB1 + lane;
+            bd_s[s] = kPbPad;
+            bw_s[s] = 0ull;
         }
         lds_fence();
-        flush1(k);
+        flush1(k, g);
     }
     __syncthreads();
-    for (uint32_t k = threadIdx.x; k < nc; k += kPbBlock) p.s1_len[(uint64_t)wg * nc + k] = dn_s[k] * kPbB1;
+    for (uint32_t k = threadIdx.x; k < nc; k += kPbBlock) p.s1_len[(uint64_t)wg * nc + k] = stage_len(tk_s, k, kPbB1);
     flush<kPbWaves>(acc, a.st);
     if (COV) {
         __syncthreads();
@@ -348,19 +351,19 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_split(PbArgs p) {
     constexpr uint32_t kN = 128;  // search table (>= kPbFineMax, a power of two)
     static_assert(kPbFineMax <= kN, "fine bins per coarse bin");
     __shared__ uint32_t flo_s[kN + 1];
-    __shared__ uint32_t tk_s[kPbFineMax], wr_s[kPbFineMax], dn_s[kPbFineMax];
+    __shared__ uint32_t tk_s[kPbFineMax], wr_s[2 * kPbFineMax], gn_s[2 * kPbFineMax];
     __shared__ unsigned long long base_s[kPbFineMax];  // this slice's segment of each fine bin
     __shared__ uint32_t cap_s[kPbFineMax];
     constexpr uint32_t kSeg = kPbGrid / kPbSlices;     // the slice's level-1 segments of bin k: one
     __shared__ unsigned long long sb_s[kSeg];           // virtual array (prefix sums ps_s), so every wave
     __shared__ uint32_t ps_s[kSeg + 1];                 // stays busy however short the segments are
-    __shared__ uint16_t bd_s[kPbFineMax * kPbB2];
-    __shared__ unsigned long long bw_s[kPbFineMax * kPbB2];
+    __shared__ uint16_t bd_s[kPbFineMax * 2 * kPbB2];
+    __shared__ unsigned long long bw_s[kPbFineMax * 2 * kPbB2];
     const uint32_t k = blockIdx.x / kPbSlices, sl = blockIdx.x % kPbSlices;
     const uint32_t f0 = p.c_fine[k], nf = p.c_fine[k + 1] - f0;
     for (uint32_t i = threadIdx.x; i <= kN; i += kPbBlock) flo_s[i] = i <= nf ? p.f_lo[f0 + i] : 0xFFFFFFFFu;
+    stage_init(tk_s, wr_s, gn_s, kPbFineMax, threadIdx.x, kPbBlock);
     for (uint32_t i = threadIdx.x; i < kPbFineMax; i += kPbBlock) {
-        tk_s[i] = wr_s[i] = dn_s[i] = 0;
         base_s[i] = i < nf ? p.s2_base[(uint64_t)sl * p.n_fine + f0 + i] : 0ull;
         cap_s[i] = i < nf ? p.s2_cap[(uint64_t)sl * p.n_fine + f0 + i] : 0u;
     }
@@ -390,16 +393,18 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_split(PbArgs p) {
         p.nw[v] = 0ull;  // and the hubs'
     __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    auto flush2 = [&](uint32_t f) {  // 64 destinations (128 B), 64 words (512 B)
-        const uint32_t pos = lds_load(&dn_s[f]) * kPbB2;
-        const uint16_t dv = bd_s[f * kPbB2 + lane];
-        const unsigned long long wv = bw_s[f * kPbB2 + lane];
+    auto flush2 = [&](uint32_t f, uint32_t g) {  // 32 destinations (64 B) by lanes 0-31, 32 words (256 B) by 32-63
+        const uint32_t pos = g * kPbB2;
+        const uint32_t i = lane & (kPbB2 - 1);
+        const uint32_t hb = f * 2 * kPbB2 + (g & 1) * kPbB2;
+        const uint16_t dv = bd_s[hb + i];
+        const unsigned long long wv = bw_s[hb + i];
         lds_fence();
-        if (lane == 0) stage_release(wr_s, dn_s, f);
+        if (lane == 0) stage_release(wr_s, gn_s, f, g);
         if (pos + kPbB2 <= cap_s[f]) {
-            const uint64_t at = base_s[f] + pos + lane;
-            p.r2_dst[at] = dv;
-            p.r2_w[at] = wv;
+            const uint64_t at = base_s[f] + pos + i;
+            if (lane < (int)kPbB2) p.r2_dst[at] = dv;
+            else p.r2_w[at] = wv;
         } else if (lane == 0) {
             atomicOr(p.err, 2u);
         }
@@ -425,23 +430,26 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_split(PbArgs p) {
                 f[j] = rec[j] ? find_bin<kN>(flo_s, d[j]) : 0u;
                 dl[j] = d[j] - flo_s[f[j]];
             }
-            stage<kPbU, kPbB2>(tk_s, wr_s, dn_s, bd_s, bw_s, f, dl, x, rec, flush2, p.err);
+            stage<kPbU, kPbB2>(tk_s, wr_s, gn_s, bd_s, bw_s, f, dl, x, rec, flush2, p.err);
         }
     }
 
     __syncthreads();
     for (uint32_t fb = wave; fb < nf; fb += kPbWaves) {
-        const uint32_t c = stage_open(tk_s, fb, kPbB2);
+        uint32_t g = 0;
+        const uint32_t c = stage_open(tk_s, fb, kPbB2, &g);
         if (!c) continue;
-        if ((uint32_t)lane >= c) {
-            bd_s[fb * kPbB2 + lane] = 0xFFFFu;
-            bw_s[fb * kPbB2 + lane] = 0ull;
+        if ((uint32_t)lane >= c && lane < (int)kPbB2) {
+            const uint32_t s = fb * 2 * kPbB2 + (g & 1) * kPbB2 + lane;
+            bd_s[s] = 0xFFFFu;
+            bw_s[s] = 0ull;
         }
         lds_fence();
-        flush2(fb);
+        flush2(fb, g);
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < nf; i += kPbBlock) p.s2_len[(uint64_t)sl * p.n_fine + f0 + i] = dn_s[i] * kPbB2;
+    for (uint32_t i = threadIdx.x; i < nf; i += kPbBlock)
+        p.s2_len[(uint64_t)sl * p.n_fine + f0 + i] = stage_len(tk_s, i, kPbB2);
 }
 
 // ---------------------------------------------------------------------------

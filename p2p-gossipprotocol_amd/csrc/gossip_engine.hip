@@ -189,7 +189,7 @@ struct gossip_ctx {
     uint32_t bin_chunk_req = 0;
     int val_tune = -1;            // "val_tune": pick the slot array's allocation by trial scatters (-1: by size,
                                   // 0: never, 1: always, 2: and print the trials)
-    int src_stats_req = -1;       // "src_stats": who books a binned round's source side (-1: by layout)
+    int src_stats_req = -1;       // "src_stats": who books a binned round's source side (-1 auto = 1: the scatter)
     uint64_t pb_bin_slots = kPbBinSlots;  // "blocked_bin_slots": slot arrays from this size run their
                                           // sparser dense rounds blocked
     uint64_t pb_direct_in = kPbFineIn;    // "blocked_direct_in": leading tiles of more in-degree are hubs
@@ -216,7 +216,9 @@ struct gossip_ctx {
     uint64_t* h_counts = nullptr;            // pinned copy
     bool cur_sparse = false;
     bool send_dirty = false;     // the dense staging buffer holds a dense push round's masks
-    uint32_t heavy = kHeavyDegree;  // "heavy_degree": light/heavy row threshold
+    uint32_t heavy = kHeavyDegree;      // light/heavy row threshold of the resident overlay (its chunks, bins and
+                                        // blocked segments were laid out with it)
+    uint32_t heavy_req = kHeavyDegree;  // "heavy_degree": the threshold of the next build
     uint64_t frontier_est = 0;   // activated peers of the previous round
     std::vector<uint64_t> inj_prefix;  // per sorted injection: cumulative mask words
     uint64_t cum_digest = 0, cum_covered = 0;
@@ -529,6 +531,7 @@ RoundArgs make_args(gossip_ctx* c) {
 // Upload a host-built CSR and derive the heavy-row chunk list.
 gossip_status install_graph(gossip_ctx* c, uint64_t* d_rp, uint32_t* d_col, uint64_t m) {
     free_graph(c);
+    c->heavy = c->heavy_req;  // layout key: the chunk list, bins and blocked segments below all use it
     c->rp = d_rp;
     c->col = d_col;
     c->n_edges = m;
@@ -777,7 +780,10 @@ gossip_status ensure_lists(gossip_ctx* c) {
     const uint32_t cap = c->list_cap_req ? c->list_cap_req
                                          : (uint32_t)std::min<uint64_t>(std::max<uint64_t>(c->n_local / 16, 1u << 16),
                                                                         0xFFFFFFFFull);
-    if (c->st_pre && c->lst_cap == cap) return GOSSIP_OK;
+    // a new capacity takes effect only between chains: a list in flight (this round's input, or the input of
+    // one of the last two rounds, which k_list_zero clears by) must stay where it is
+    const bool live = c->lst_in >= 0 || c->lin_idx[0] >= 0 || c->lin_idx[1] >= 0;
+    if (c->st_pre && (c->lst_cap == cap || live)) return GOSSIP_OK;
     for (auto& l : c->lst) {
         hipFree(l);
         l = nullptr;
@@ -1152,10 +1158,14 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
 
 // Small overlays run whole in one launch (gossip_tiny.hip) unless they use a feature only the round-by-round
 // engine has (re-bootstrap, join churn, coverage history) or are partitioned.
+// (the one-launch run writes every round's stats into one pinned buffer of max_rounds entries: a caller's
+// "no limit" max_rounds runs round by round instead of allocating it)
+constexpr uint32_t kTinyMaxRounds = 1u << 16;
+
 bool tiny_ok(const gossip_ctx* c) {
     return !c->tiny_off && c->graph_ready && c->n_local == c->n && c->world <= 1 && !c->dist && !c->gather &&
            c->n <= kTinyPeers && c->n_edges <= kTinyEdges && !c->cfg.extra_cap && !c->cfg.rejoin_threshold &&
-           !c->cov_hist && !c->in_round;
+           !c->cov_hist && !c->in_round && c->cfg.max_rounds <= kTinyMaxRounds;
 }
 
 TinyArgs tiny_args(gossip_ctx* c) {
@@ -1247,8 +1257,8 @@ gossip_status tiny_run(gossip_ctx* c, gossip_round_stats* per_round, uint32_t ca
     return GOSSIP_OK;
 }
 
-// Who books the source side of a binned round: the scatter's staging (slot layout) or the apply
-// (streamed layout; "src_stats" 0/1 overrides)
+// Who books the source side of a binned round: the scatter's staging (auto, both layouts) or the apply
+// ("src_stats" 0)
 uint32_t src_stats(const gossip_ctx* c) {
     return c->src_stats_req >= 0 ? (uint32_t)(c->src_stats_req != 0) : 1u;
 }
@@ -1327,10 +1337,15 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
                                   c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         HIPCHK(queue_zero(c, c->st, kStatLines * sizeof(DevStats)));  // cleared with the next round's first launch
-        if (c->cur_pb) {  // a record region that would have overflowed (cannot happen: capacities are in-degrees)
+        if (c->cur_pb) {
+            // bit 4: a wave gave up waiting for its staging generation (gossip_stage.hpp, kStageSpin: the
+            // protocol always progresses, so this means a bug, not load); bits 1/2: a record region that
+            // would have overflowed (cannot happen: capacities are in-degrees).  The round's results are
+            // incomplete either way; the flags stay set until the next reset.
             uint32_t e = 0;
             HIPCHK(hipMemcpy(&e, c->pb.err, sizeof(e), hipMemcpyDeviceToHost));
-            if (e) return fail(GOSSIP_EOVERFLOW, "blocked push: a record region overflowed");
+            if (e & 4u) return fail(GOSSIP_ESTALL, "blocked round: a record-staging wave stalled past its bound");
+            if (e) return fail(GOSSIP_EOVERFLOW, "blocked round: a record region overflowed");
         }
         DevStats sum{};
         const unsigned long long* src = reinterpret_cast<const unsigned long long*>(c->h_st);
@@ -1437,8 +1452,9 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
 gossip_status advance(gossip_ctx* c, uint64_t fresh_global) {
     bool pend = false;
     if (c->cur_defer) {  // every delivery of the round is in nx (remote applies included): fold it into seen
-        if (c->world <= 1 && c->bins_ready)
-            pend = true;  // after the swap, in nw: the next round folds it (settle_fold / k_bin_apply)
+        if (c->world <= 1 && (c->bins_ready || c->pb_ready))
+            pend = true;  // after the swap, in nw: the next round folds it (k_bin_apply, k_pb_scatter's or
+                          // k_pull_rows's sweep) or commits it first (settle_fold)
         else
             HIPCHK(timed(c, "commit", [&] { return launch_commit_nx(c->seen, c->nx, c->n_local * c->Wp, c->stream); }));
         c->cur_defer = false;
@@ -1485,6 +1501,7 @@ const char* gossip_strerror(gossip_status s) {
         case GOSSIP_ENODEV: return "no gfx950 device";
         case GOSSIP_EOVERFLOW: return "report buffer overflow";
         case GOSSIP_ECOMM: return "RCCL error";
+        case GOSSIP_ESTALL: return "device work stalled";
         default: return "unknown status";
     }
 }
@@ -1604,7 +1621,7 @@ gossip_status gossip_set_tuning(gossip_ctx* c, const char* key, int64_t value) {
     else if (k == "pull_first2") c->first_ok = value != 0;
     else if (k == "in_flight") c->flight_ok = value != 0;
     else if (k == "heavy_exit") c->heavy_exit = value != 0;
-    else if (k == "heavy_degree") c->heavy = std::max<uint32_t>(1u, u);
+    else if (k == "heavy_degree") c->heavy_req = std::max<uint32_t>(1u, u);
     else if (k == "heavy_chunk") c->heavy_chunk = u;
     else if (k == "bin_front_permille") c->bin_front_pm = u;
     else if (k == "bin_words") c->bin_words_req = u;
@@ -1614,7 +1631,10 @@ gossip_status gossip_set_tuning(gossip_ctx* c, const char* key, int64_t value) {
     else if (k == "blocked_bin_slots") c->pb_bin_slots = value < 0 ? kPbBinSlots : (uint64_t)value;
     else if (k == "blocked_direct_in") c->pb_direct_in = value < 0 ? kPbFineIn : (uint64_t)value;
     else if (k == "list_rounds") c->list_req = value != 0;
-    else if (k == "pull_step") c->row_step = value == 1 ? 1u : 2u;
+    else if (k == "pull_step") {
+        if (value != 1 && value != 2) return fail(GOSSIP_EINVAL, "pull_step must be 1 or 2");
+        c->row_step = (uint32_t)value;
+    }
     else if (k == "blocked_push_permille") c->pb_lo_pm = value < 0 ? kPbLoPermille : u;
     else if (k == "list_cap") c->list_cap_req = u;
     else return fail(GOSSIP_EINVAL, "unknown tuning option: " + k);
@@ -1904,6 +1924,7 @@ gossip_status gossip_reset(gossip_ctx* c) {
         HIPCHK(hipMemsetAsync(c->dgone, 0, c->n_local * 4 + 4, s));
         HIPCHK(hipMemsetAsync(c->dmask, 0, c->n_local * 4 + 4, s));
     }
+    if (c->pb_ready) HIPCHK(hipMemsetAsync(c->pb.err, 0, sizeof(uint32_t), s));  // error flags of the last run
     c->n_rep_seen = 0;
     c->pre_booked = c->cur_list = c->cur_pre = false;
     c->lst_in = c->cur_lst_out = -1;

@@ -142,8 +142,9 @@ constexpr uint32_t kPbCoarse = 256;    // level-1 bins (a power of two: the LDS 
 constexpr uint32_t kPbFineMax = 96;    // fine bins per coarse bin (level-2 LDS staging)
 constexpr uint32_t kPbFineIn = 1u << 18;  // a fine bin: whole tiles, <= kBinWords peers and <= this in-degree
                                           // (unless one tile has more): no hot bin in level 2
-constexpr uint32_t kPbB1 = 32;         // level-1 records per flush: 128 B of destinations, 256 B of words
-constexpr uint32_t kPbB2 = 64;         // level-2 records per flush: 128 B of destinations, 512 B of words
+constexpr uint32_t kPbB1 = 16;         // level-1 records per flush: 64 B of destinations, 128 B of words
+                                       // (two halves per bin in LDS, gossip_stage.hpp)
+constexpr uint32_t kPbB2 = 32;         // level-2 records per flush: 64 B of destinations, 256 B of words
 constexpr uint32_t kPbSlices = 4;      // level-2 workgroups per coarse bin
 constexpr int kPbBlock = 1024;         // 16 waves per workgroup, one workgroup per CU (level 1)
 constexpr int kPbGrid = 256;           // level-1 workgroups (row ranges)

@@ -22,6 +22,7 @@ GOSSIP_ESTATE = -4
 GOSSIP_ENODEV = -5
 GOSSIP_EOVERFLOW = -6
 GOSSIP_ECOMM = -7
+GOSSIP_ESTALL = -8
 COMM_ID_BYTES = 128
 
 GRAPH_POWERLAW = 1

@@ -76,7 +76,7 @@ def test_fullsize_forced_blocked_matches_oracle(oracle, idx):
         _check_run(oracle, e, w, g, check_csr=False)
 
 
-@pytest.mark.parametrize("idx,P", [(4, 2), (4, 4), (5, 2)])
+@pytest.mark.parametrize("idx,P", [(4, 2), (4, 4), (4, 8), (5, 2)])
 def test_fullsize_partitioned_group_matches_oracle(oracle, idx, P):
     """The N-GPU path at full size (BASELINE configs 4 and 5): the library's
     partitioned driver (gossip_group, gossip_dist.hip) with P parts on device 0,

@@ -462,3 +462,73 @@ def test_small_overlay_one_launch_matches_oracle(oracle, tiny, idx, n, max_round
         for _ in range(2):
             e.reset()
             _compare(e, ref, w)
+
+
+def test_heavy_degree_is_a_layout_key(oracle):
+    """"heavy_degree" set after the overlay is built takes effect only at the
+    next build: the resident chunk list, bins and blocked segments keep the
+    threshold they were laid out with (a row between the two thresholds
+    would otherwise be skipped by the light kernels and covered by no chunk,
+    losing its deliveries).  Then a rebuild applies it."""
+    w = config(3, 1 << 18, pick=oracle.pick_origins)
+    rp, col = oracle.gen_workload(w)
+    ref = oracle.simulate_workload(w, rp, col)
+    with _engine(w) as e:
+        e.build_graph()
+        e.inject(w.origins, w.inject_rounds)
+        e.set_tuning("heavy_degree", 16)  # held back: the layout was built with 256
+        e.reset()
+        _compare(e, ref, w)
+        e.build_graph()  # now rows > 16 are chunked
+        e.reset()
+        _compare(e, ref, w)
+
+
+def test_list_cap_change_inside_a_list_chain(oracle):
+    """"list_cap" changed while needy-list rounds are running must not
+    reallocate the lists in flight (the next rounds read them and clear nx by
+    them): the change waits for the next chain, and results stay the oracle's."""
+    w = config(3, 1 << 18, pick=oracle.pick_origins)
+    rp, col = oracle.gen_workload(w)
+    ref = oracle.simulate_workload(w, rp, col)
+    with _engine(w) as e:
+        e.enable_timing(True)
+        e.build_graph()
+        e.inject(w.origins, w.inject_rounds)
+        for rerun in range(2):
+            e.reset()
+            got, changed = [], False
+            while True:
+                st, fin = e.step()
+                got.append(st)
+                if not changed and e.kernel_time("pull_list")[1] > 0:
+                    e.set_tuning("list_cap", 1 << 20 if rerun == 0 else 128)
+                    changed = True
+                if fin:
+                    break
+            assert changed
+            assert got == ref["stats"]
+            assert np.array_equal(e.read_seen(), ref["seen"])
+
+
+def test_tuning_rejects_bad_values_and_huge_max_rounds_runs(oracle):
+    """"pull_step" takes 1 or 2 only; a small overlay with a "no limit"
+    max_rounds runs round by round instead of sizing the one-launch run's
+    stats buffer by it, with the oracle's results."""
+    from gossip_hip._abi import GossipError
+    w = config(2, 4096, pick=oracle.pick_origins)
+    rp, col = oracle.gen_workload(w)
+    ref = oracle.simulate_workload(w, rp, col)
+    kw = w.engine_kwargs()
+    kw["max_rounds"] = 1 << 30
+    with Engine(w.n, w.n_msgs, **kw) as e:
+        for bad in (0, -1, 3):
+            with pytest.raises(GossipError):
+                e.set_tuning("pull_step", bad)
+        e.set_tuning("pull_step", 2)
+        e.enable_timing(True)
+        e.build_graph()
+        e.inject(w.origins, w.inject_rounds)
+        e.reset()
+        _compare(e, ref, w)
+        assert e.kernel_time("tiny")[1] == 0
