@@ -63,7 +63,7 @@ def parse():
 
 
 # kernel timer name -> rocprofv3 kernel-name prefix in the PMC summary
-PMC_KERNELS = {"bin_scatter": ("k_bin_scatter_pc", "k_bin_stream"), "bin_apply": ("k_bin_apply",),
+PMC_KERNELS = {"bin_scatter": ("k_bin_scatter_pc", "k_bin_stream"), "bin_apply": ("k_bin_apply", "k_bin_apply_runs"),
                "pull_light": ("k_pull_rows", "k_pull_light"),  # the row-queue pull is the default
                "push_light": ("k_push_light",), "push_heavy": ("k_push_heavy",), "pull_heavy": ("k_pull_heavy",)}
 
@@ -299,30 +299,48 @@ class Ranked(Single):
         self.dist.barrier()
 
 
+LIVE_COUNTERS = ("#pings", "#pinging_peers")  # 8(d)'s liveness term of a ping round (k_live_count)
+
+
 def per_round_profile(run, n_peers: int) -> list[dict]:
     """One run, stepped round by round with per-kernel timing (untimed pass):
-    each round's mode, SURVEY 8(d)'s algorithmic bytes B_r = 32 F_r + 20 T_r
-    and the device time of its kernels (max over the parts of a partitioned
-    run) and exchanges."""
+    each round's mode; SURVEY 8(d)'s algorithmic bytes B_r = 32 F_r + 20 T_r,
+    plus 6.125 B per ping and 16 B per pinging peer in a ping round; the
+    kernels' own design bytes (DESIGN.md section 6, summed over the round's
+    kernels and parts); the device time of its kernels (max over the parts of
+    a partitioned run) and exchanges; and the round's fraction of the HBM
+    peak, frac = B_r / kernel time / peak.  Pull rounds (row, list and heavy
+    pulls) stop a row's scan once it holds every bit it can still learn, so
+    8(d)'s 20 B per traversal overstates what they touch: they are marked
+    work_avoiding (their frac can pass 1)."""
     from gossip_hip.engine import EXCHANGES, KERNELS
     names = KERNELS + EXCHANGES
     run.reset()
     run.timing(True)
+    kb = lambda: [{k: run.kbytes(p, k) for k in KERNELS + LIVE_COUNTERS} for p in range(run.parts)]  # noqa: E731
     prev = [{k: run.ktime(p, k)[0] for k in names} for p in range(run.parts)]
+    prev_b = kb()
     rows = []
     while True:
         st, fin = run.round_step()
         cur = [{k: run.ktime(p, k)[0] for k in names} for p in range(run.parts)]
+        cur_b = kb()
         d = [{k: c[k] - q[k] for k in names if c[k] - q[k] > 0} for c, q in zip(cur, prev)]
-        prev = cur
+        db = {k: sum(c[k] - q[k] for c, q in zip(cur_b, prev_b)) for k in KERNELS + LIVE_COUNTERS}
+        prev, prev_b = cur, cur_b
         mode = "bin" if any("bin_scatter" in x for x in d) else "blocked" if any("pb_scatter" in x for x in d) else \
             "pull" if any("pull_light" in x or "pull_list" in x for x in d) else "push"
         kms = max(sum(v for k, v in x.items() if k in KERNELS) for x in d)
         xms = max(sum(v for k, v in x.items() if k in EXCHANGES) for x in d)
         dense = max(sum(x.get(k, 0.0) for k in DENSE_KERNELS) for x in d)
+        live_b = 6.125 * db["#pings"] + 16 * db["#pinging_peers"]
+        alg = 32 * st["frontier"] + 20 * st["traversals"] + live_b
+        frac = alg / (kms / 1e3) / 1e9 / HBM_PEAK_GBS if kms > 0 else 0.0
         rows.append({"round": st["round"], "mode": mode, "frontier_frac": round(st["frontier"] / n_peers, 4),
-                     "traversals": st["traversals"], "alg_bytes": 32 * st["frontier"] + 20 * st["traversals"],
-                     "kernel_ms": round(kms, 3), "exchange_ms": round(xms, 3), "dense_ms": round(dense, 3)})
+                     "traversals": st["traversals"], "alg_bytes": round(alg), "liveness_bytes": round(live_b),
+                     "design_bytes": round(sum(db[k] for k in KERNELS)),
+                     "kernel_ms": round(kms, 3), "exchange_ms": round(xms, 3), "dense_ms": round(dense, 3),
+                     "frac": round(frac, 4), "work_avoiding": mode == "pull"})
         if fin:
             run.timing(False)
             return rows
@@ -408,8 +426,18 @@ def main():
         # the dominant kernel by device time (part 0's; every part runs the same schedule)
         dom = max((k for k in KERNELS), key=lambda k: k_ms[0][k][0])
         ms, launches = k_ms[0][dom]
+        # without the work-avoiding (pull) rounds: their 8(d) bytes out of the numerator, their kernel time
+        # out of the step
+        step_ms = dt / args.steps * 1e3
+        wa = [r for r in rounds_prof if r["work_avoiding"]]
+        rest_ms = step_ms - sum(r["kernel_ms"] + r["exchange_ms"] for r in wa)
+        rest_b = alg - sum(r["alg_bytes"] for r in wa)
         roofline = {"bound": "hbm", "peak": HBM_PEAK_GBS * run.n_gpus, "unit": "GB/s",
                     "step_frac": round(alg / (dt / args.steps) / 1e9 / (HBM_PEAK_GBS * run.n_gpus), 4),
+                    "step_frac_without_work_avoiding": round(rest_b / (rest_ms / 1e3) / 1e9 /
+                                                             (HBM_PEAK_GBS * run.n_gpus), 4) if rest_ms > 0 else None,
+                    "work_avoiding_rounds": [r["round"] for r in wa],
+                    "step_alg_bytes": round(alg), "step_liveness_bytes": sum(r["liveness_bytes"] for r in rounds_prof),
                     "timed_steps": timed_steps,
                     "ms_per_step_with_events": round(dt_timed / timed_steps * 1e3, 3),
                     "kernel_ms_per_step": {k: round(max(x[k][0] for x in k_ms) / timed_steps, 3)
@@ -474,7 +502,9 @@ def main():
             "traversal_gteps": round(args.steps * sum(s["traversals"] for s in stats) / dt / 1e9, 3),
         }
         if rounds_prof:
-            line["rounds"] = [{k: r[k] for k in ("round", "mode", "frontier_frac", "traversals", "kernel_ms")} |
+            line["rounds"] = [{k: r[k] for k in ("round", "mode", "frontier_frac", "traversals", "alg_bytes",
+                                                 "design_bytes", "kernel_ms", "frac", "work_avoiding")} |
+                              ({"liveness_bytes": r["liveness_bytes"]} if r["liveness_bytes"] else {}) |
                               ({"exchange_ms": r["exchange_ms"]} if run.parts > 1 or dist is not None else {})
                               for r in rounds_prof]
         if roofline:

@@ -325,7 +325,11 @@ gossip_status gossip_kernel_bytes(gossip_ctx* ctx, const char* kernel, double* b
  * blocked on overlays of >= 2^26 peers; -1 default 10), "list_rounds" (0: no
  * needy-list rounds), "list_cap" (layout of the needy lists: rows per list;
  * 0 = max(n/16, 65536)), "pull_step" (neighbour words a row pull gathers
- * per row per step: 1 default, or 2; other values GOSSIP_EINVAL).  Layout keys
+ * per row per step: 1 default, or 2; other values GOSSIP_EINVAL),
+ * "gather_permille" (partitioned runs, read from each driver's first part:
+ * dense rounds whose frontier is below this per-mille of the peers exchange
+ * a tile bitmap and the packed non-zero new words instead of every word;
+ * -1 default 600, 0 never, 1000 always).  Layout keys
  * apply at the next gossip_build_graph / gossip_load_csr ("list_cap": at the
  * next chain of needy-list rounds, never inside one).  GOSSIP_EINVAL: unknown key. */
 gossip_status gossip_set_tuning(gossip_ctx* ctx, const char* key, int64_t value);

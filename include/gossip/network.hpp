@@ -95,6 +95,7 @@ private:
     SimOptions opt_;
     uint32_t M_ = 0, W_ = 0;
     gossip_ctx* ctx_ = nullptr;
+    uint64_t groupReportCount() const;
     gossip_group* group_ = nullptr;
     bool started_ = false, finished_ = false, trace_ = false;
     std::atomic<bool> stop_{false};

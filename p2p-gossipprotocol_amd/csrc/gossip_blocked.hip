@@ -74,17 +74,17 @@ template <bool CA, bool COV>
 __global__ __launch_bounds__(kPbBlock) void k_pb_scatter(RoundArgs a, PbArgs p, uint32_t wd) {
     __shared__ uint32_t lo_s[kPbCoarse + 1];
     __shared__ uint8_t cmap_s[kPbMap];  // coarse bin of each id bucket's first peer (then a short walk)
-    __shared__ uint32_t tk_s[kPbCoarse], wr_s[2 * kPbCoarse], gn_s[2 * kPbCoarse];
+    __shared__ uint32_t tk_s[kPbCoarse], wr_s[kPbH1 * kPbCoarse], gn_s[kPbH1 * kPbCoarse];
     __shared__ unsigned long long base_s[kPbCoarse];  // this workgroup's segment of each coarse bin
     __shared__ uint32_t cap_s[kPbCoarse];
-    __shared__ uint32_t bd_s[kPbCoarse * 2 * kPbB1];
-    __shared__ unsigned long long bw_s[kPbCoarse * 2 * kPbB1];
+    __shared__ uint32_t bd_s[kPbCoarse * kPbH1 * kPbB1];
+    __shared__ unsigned long long bw_s[kPbCoarse * kPbH1 * kPbB1];
     __shared__ uint32_t pk_v[kPbWaves][128];
     __shared__ unsigned long long pk_m[kPbWaves][128];
     __shared__ unsigned int cov_s[COV ? 64 : 1];
     const uint32_t nc = p.n_coarse, wg = blockIdx.x;
     for (uint32_t i = threadIdx.x; i <= kPbCoarse; i += kPbBlock) lo_s[i] = i <= nc ? p.c_lo[i] : 0xFFFFFFFFu;
-    stage_init(tk_s, wr_s, gn_s, kPbCoarse, threadIdx.x, kPbBlock);
+    stage_init<kPbH1>(tk_s, wr_s, gn_s, kPbCoarse, threadIdx.x, kPbBlock);
     for (uint32_t i = threadIdx.x; i < kPbCoarse; i += kPbBlock) {
         base_s[i] = i < nc ? p.s1_base[(uint64_t)wg * nc + i] : 0ull;
         cap_s[i] = i < nc ? p.s1_cap[(uint64_t)wg * nc + i] : 0u;
@@ -103,15 +103,16 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_scatter(RoundArgs a, PbArgs p, 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 
     // generation g of coarse bin k goes to place g * kPbB1 of the workgroup's segment:
-    // 16 lanes store the destinations (64 B), 16 the words (128 B)
+    // 32 lanes store the destinations (128 B), 32 the words (256 B)
+    static_assert(2 * kPbB1 <= 64, "one wave flushes a generation");
     auto flush1 = [&](uint32_t k, uint32_t g) {
         const uint32_t pos = g * kPbB1;
         const uint32_t i = lane & (kPbB1 - 1);
-        const uint32_t hb = k * 2 * kPbB1 + (g & 1) * kPbB1;
+        const uint32_t hb = stage_at<kPbB1, kPbH1>(k, g, 0);
         const uint32_t dv = bd_s[hb + i];
         const unsigned long long wv = bw_s[hb + i];
         lds_fence();
-        if (lane == 0) stage_release(wr_s, gn_s, k, g);
+        if (lane == 0) stage_release<kPbH1>(wr_s, gn_s, k, g);
         if (pos + kPbB1 <= cap_s[k]) {
             const uint64_t at = base_s[k] + pos + i;
             if (lane < (int)kPbB1) p.r1_dst[at] = dv;
@@ -182,7 +183,7 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_scatter(RoundArgs a, PbArgs p, 
         direct(c, m, rec);
 #pragma unroll
         for (int j = 0; j < kPbU; ++j) k[j] = rec[j] ? coarse_of(c[j]) : 0u;
-        stage<kPbU, kPbB1>(tk_s, wr_s, gn_s, bd_s, bw_s, k, c, m, rec, flush1, p.err);
+        stage<kPbU, kPbB1, kPbH1>(tk_s, wr_s, gn_s, bd_s, bw_s, k, c, m, rec, flush1, p.err);
     };
 
     // (1) heavy chunks wg, wg + kPbGrid, ..., one wave each (their rows' words are cleared by the split)
@@ -326,7 +327,7 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_scatter(RoundArgs a, PbArgs p, 
         const uint32_t n = stage_open(tk_s, k, kPbB1, &g);
         if (!n) continue;  // wave-uniform
         if ((uint32_t)lane >= n && lane < (int)kPbB1) {
-            const uint32_t s = k * 2 * kPbB1 + (g & 1) * kPbB1 + lane;
+            const uint32_t s = stage_at<kPbB1, kPbH1>(k, g, lane);
             bd_s[s] = kPbPad;
             bw_s[s] = 0ull;
         }
@@ -351,18 +352,18 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_split(PbArgs p) {
     constexpr uint32_t kN = 128;  // search table (>= kPbFineMax, a power of two)
     static_assert(kPbFineMax <= kN, "fine bins per coarse bin");
     __shared__ uint32_t flo_s[kN + 1];
-    __shared__ uint32_t tk_s[kPbFineMax], wr_s[2 * kPbFineMax], gn_s[2 * kPbFineMax];
+    __shared__ uint32_t tk_s[kPbFineMax], wr_s[kPbH2 * kPbFineMax], gn_s[kPbH2 * kPbFineMax];
     __shared__ unsigned long long base_s[kPbFineMax];  // this slice's segment of each fine bin
     __shared__ uint32_t cap_s[kPbFineMax];
     constexpr uint32_t kSeg = kPbGrid / kPbSlices;     // the slice's level-1 segments of bin k: one
     __shared__ unsigned long long sb_s[kSeg];           // virtual array (prefix sums ps_s), so every wave
     __shared__ uint32_t ps_s[kSeg + 1];                 // stays busy however short the segments are
-    __shared__ uint16_t bd_s[kPbFineMax * 2 * kPbB2];
-    __shared__ unsigned long long bw_s[kPbFineMax * 2 * kPbB2];
+    __shared__ uint16_t bd_s[kPbFineMax * kPbH2 * kPbB2];
+    __shared__ unsigned long long bw_s[kPbFineMax * kPbH2 * kPbB2];
     const uint32_t k = blockIdx.x / kPbSlices, sl = blockIdx.x % kPbSlices;
     const uint32_t f0 = p.c_fine[k], nf = p.c_fine[k + 1] - f0;
     for (uint32_t i = threadIdx.x; i <= kN; i += kPbBlock) flo_s[i] = i <= nf ? p.f_lo[f0 + i] : 0xFFFFFFFFu;
-    stage_init(tk_s, wr_s, gn_s, kPbFineMax, threadIdx.x, kPbBlock);
+    stage_init<kPbH2>(tk_s, wr_s, gn_s, kPbFineMax, threadIdx.x, kPbBlock);
     for (uint32_t i = threadIdx.x; i < kPbFineMax; i += kPbBlock) {
         base_s[i] = i < nf ? p.s2_base[(uint64_t)sl * p.n_fine + f0 + i] : 0ull;
         cap_s[i] = i < nf ? p.s2_cap[(uint64_t)sl * p.n_fine + f0 + i] : 0u;
@@ -393,18 +394,18 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_split(PbArgs p) {
         p.nw[v] = 0ull;  // and the hubs'
     __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    auto flush2 = [&](uint32_t f, uint32_t g) {  // 32 destinations (64 B) by lanes 0-31, 32 words (256 B) by 32-63
+    static_assert(kPbB2 == 64, "a lane per record of a generation");
+    auto flush2 = [&](uint32_t f, uint32_t g) {  // 64 destinations (128 B), 64 words (512 B)
         const uint32_t pos = g * kPbB2;
-        const uint32_t i = lane & (kPbB2 - 1);
-        const uint32_t hb = f * 2 * kPbB2 + (g & 1) * kPbB2;
-        const uint16_t dv = bd_s[hb + i];
-        const unsigned long long wv = bw_s[hb + i];
+        const uint32_t hb = stage_at<kPbB2, kPbH2>(f, g, 0);
+        const uint16_t dv = bd_s[hb + lane];
+        const unsigned long long wv = bw_s[hb + lane];
         lds_fence();
-        if (lane == 0) stage_release(wr_s, gn_s, f, g);
+        if (lane == 0) stage_release<kPbH2>(wr_s, gn_s, f, g);
         if (pos + kPbB2 <= cap_s[f]) {
-            const uint64_t at = base_s[f] + pos + i;
-            if (lane < (int)kPbB2) p.r2_dst[at] = dv;
-            else p.r2_w[at] = wv;
+            const uint64_t at = base_s[f] + pos + lane;
+            p.r2_dst[at] = dv;
+            p.r2_w[at] = wv;
         } else if (lane == 0) {
             atomicOr(p.err, 2u);
         }
@@ -430,7 +431,7 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_split(PbArgs p) {
                 f[j] = rec[j] ? find_bin<kN>(flo_s, d[j]) : 0u;
                 dl[j] = d[j] - flo_s[f[j]];
             }
-            stage<kPbU, kPbB2>(tk_s, wr_s, gn_s, bd_s, bw_s, f, dl, x, rec, flush2, p.err);
+            stage<kPbU, kPbB2, kPbH2>(tk_s, wr_s, gn_s, bd_s, bw_s, f, dl, x, rec, flush2, p.err);
         }
     }
 
@@ -439,8 +440,8 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_split(PbArgs p) {
         uint32_t g = 0;
         const uint32_t c = stage_open(tk_s, fb, kPbB2, &g);
         if (!c) continue;
-        if ((uint32_t)lane >= c && lane < (int)kPbB2) {
-            const uint32_t s = fb * 2 * kPbB2 + (g & 1) * kPbB2 + lane;
+        if ((uint32_t)lane >= c) {
+            const uint32_t s = stage_at<kPbB2, kPbH2>(fb, g, lane);
             bd_s[s] = 0xFFFFu;
             bw_s[s] = 0ull;
         }

@@ -7,7 +7,11 @@
 // driver on the block's HIP stream:
 //   dense rounds (PULL / BIN): in-place ncclAllGather of every block's new
 //     words into a buffer indexed by global peer; each block then pulls or
-//     streams its in-edges from it (no second exchange, no atomics);
+//     streams its in-edges from it (no second exchange, no atomics).  Below
+//     gather_permille of frontier the blocks exchange a bitmap of their
+//     64-peer tiles' non-zero words and those words packed instead (an
+//     all-gather of the bitmaps, then of the packed words as send / recv
+//     pairs), expanded into the same buffer;
 //   push rounds: the block's pushes to remote peers are OR-ed into a dense
 //     staging buffer indexed by global peer, and an all-to-all of ncclSend /
 //     ncclRecv pairs (all ranks' sends and receives in one group, every link
@@ -30,6 +34,7 @@
 //     rehearsal of the partitioned path: the remote staging, record
 //     compaction and remote-apply kernels and this driver's schedule).
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -44,7 +49,7 @@ namespace gossip {
 
 namespace {
 
-constexpr int kStatSlots = 12;  // all-reduced stat fields (see pack_stats)
+constexpr int kStatSlots = 13;  // all-reduced stat fields (see pack_stats)
 
 struct DistRank {
     gossip_ctx* ctx = nullptr;
@@ -56,6 +61,11 @@ struct DistRank {
     uint64_t *send = nullptr, *recv = nullptr, *gather = nullptr, *seg = nullptr, *rec_in = nullptr;
     uint64_t* d_io = nullptr;  // device scratch: stats all-reduce, record counts
     uint64_t* h_io = nullptr;  // pinned mirror
+    // compact dense exchange: every block's tile bitmap (tpb words per block, block order), the exclusive
+    // prefix of their popcounts (a tile's first packed word), the packed words of all blocks (block order)
+    uint64_t *bits = nullptr, *pos = nullptr, *pk = nullptr;
+    void* scan_tmp = nullptr;
+    size_t scan_bytes = 0;
     std::vector<uint64_t> counts_out, counts_in;
     gossip_round_stats local{};
 };
@@ -68,10 +78,12 @@ struct DistDriver {
     bool emulate = false;         // every rank local on one device: device copies, one stream
     std::vector<uint64_t> part;
     uint64_t n = 0, chunk = 0;
+    uint64_t tpb = 0;  // 64-peer tiles per block (compact exchange)
     uint32_t X = 1, R = 2;
     uint32_t pull_pm = kPullPermille, sparse_pm = 250, bin_pm = 4000, bin_front_pm = 100;
     // schedule state, from global stats (identical on every rank)
     uint64_t prev_new = 0, injected = 0, cum_digest = 0, cum_covered = 0;
+    uint64_t front = 0;  // this round's frontier (the peers the last round activated, all ranks)
     bool finished = false;
     std::vector<int32_t> modes;
 };
@@ -97,6 +109,67 @@ std::vector<uint64_t> blocks(uint64_t n, uint32_t world) {
     return b;
 }
 
+// ---- compact dense exchange ----
+struct PopOp {
+    __host__ __device__ uint64_t operator()(uint64_t x) const { return (uint64_t)__builtin_popcountll(x); }
+};
+using TilePop = hipcub::TransformInputIterator<uint64_t, PopOp, const uint64_t*>;
+
+// bit i of bits[t] <=> peer 64 t + i of the block has a non-zero new word (one wave per tile)
+__global__ __launch_bounds__(256) void k_tile_bits(const uint64_t* words, uint64_t n, uint32_t X, uint64_t* bits) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t tiles = (n + 63) / 64;
+    for (uint64_t t = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; t < tiles;
+         t += ((uint64_t)gridDim.x * blockDim.x) >> 6) {
+        const uint64_t v = t * 64 + lane;
+        uint64_t any = 0;
+        if (v < n)
+            for (uint32_t x = 0; x < X; ++x) any |= words[v * X + x];
+        const unsigned long long b = __ballot(any != 0);
+        if (lane == 0) bits[t] = b;
+    }
+}
+
+// the block's non-zero words, packed in peer order at out[pos[t] + rank of the peer in its tile]
+__global__ __launch_bounds__(256) void k_tile_pack(const uint64_t* words, uint64_t n, uint32_t X, const uint64_t* bits,
+                                                   const uint64_t* pos, uint64_t* out) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t tiles = (n + 63) / 64;
+    for (uint64_t t = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; t < tiles;
+         t += ((uint64_t)gridDim.x * blockDim.x) >> 6) {
+        const uint64_t b = bits[t];
+        if (!((b >> lane) & 1)) continue;
+        const uint64_t at = pos[t] + (uint64_t)__builtin_popcountll(b & ((1ull << lane) - 1));
+        const uint64_t v = t * 64 + lane;
+        for (uint32_t x = 0; x < X; ++x) out[at * X + x] = words[v * X + x];
+    }
+}
+
+// every other block's words back into the gather buffer (zeros where the bitmap has none)
+__global__ __launch_bounds__(256) void k_tile_expand(uint64_t* gather, const uint64_t* bits, const uint64_t* pos,
+                                                     const uint64_t* pk, uint32_t X, uint32_t world, uint32_t own,
+                                                     uint64_t chunk, uint64_t n, uint64_t tpb) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t tiles = (uint64_t)world * tpb;
+    for (uint64_t T = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; T < tiles;
+         T += ((uint64_t)gridDim.x * blockDim.x) >> 6) {
+        const uint64_t q = T / tpb, t = T % tpb;
+        const uint64_t v = q * chunk + t * 64 + lane;
+        const uint64_t end = std::min<uint64_t>((q + 1) * chunk, n);
+        if (q == own || q * chunk + t * 64 >= end) continue;  // wave-uniform
+        const uint64_t b = bits[T];
+        const bool set = (b >> lane) & 1;
+        const uint64_t at = pos[T] + (uint64_t)__builtin_popcountll(b & ((1ull << lane) - 1));
+        if (v < end)
+            for (uint32_t x = 0; x < X; ++x) gather[v * X + x] = set ? pk[at * X + x] : 0ull;
+    }
+}
+
+__global__ void k_pick_offsets(const uint64_t* pos, uint32_t world, uint64_t tpb, uint64_t* out) {
+    const uint32_t q = threadIdx.x;
+    if (q <= world) out[q] = pos[(uint64_t)q * tpb];
+}
+
 // Buffers and communicator of one rank (its stream is released by dist_free).
 void free_rank(DistRank& r) {
     hipSetDevice(r.device);
@@ -108,8 +181,14 @@ void free_rank(DistRank& r) {
     hipFree(r.seg);
     hipFree(r.rec_in);
     hipFree(r.d_io);
+    hipFree(r.bits);
+    hipFree(r.pos);
+    hipFree(r.pk);
+    hipFree(r.scan_tmp);
     if (r.h_io) hipHostFree(r.h_io);
     r.send = r.recv = r.gather = r.seg = r.rec_in = r.d_io = r.h_io = nullptr;
+    r.bits = r.pos = r.pk = nullptr;
+    r.scan_tmp = nullptr;
     r.comm = nullptr;
 }
 
@@ -127,8 +206,17 @@ gossip_status setup_rank(DistDriver* d, DistRank& r) {
     DHIP(alloc(&r.gather, W * d->chunk * X));
     DHIP(alloc(&r.seg, W * d->chunk * R));
     DHIP(alloc(&r.rec_in, W * r.n_local * R));
-    DHIP(alloc(&r.d_io, 2 * std::max<uint64_t>(W, kStatSlots)));
-    DHIP(hipHostMalloc((void**)&r.h_io, 2 * std::max<uint64_t>(W, kStatSlots) * 8));
+    DHIP(alloc(&r.d_io, 2 * std::max<uint64_t>(W + 1, kStatSlots)));
+    DHIP(hipHostMalloc((void**)&r.h_io, 2 * std::max<uint64_t>(W + 1, kStatSlots) * 8));
+    if (W > 1) {  // compact dense exchange (a short last block's unused tiles stay zero)
+        const uint64_t tiles = W * d->tpb;
+        DHIP(alloc(&r.bits, tiles + 1));  // (+1: a zero past the last tile, so the scan yields the total)
+        DHIP(alloc(&r.pos, tiles + 1));
+        DHIP(alloc(&r.pk, W * d->chunk * X));
+        DHIP(hipcub::DeviceScan::ExclusiveSum(nullptr, r.scan_bytes, TilePop(r.bits, PopOp()), r.pos, (int)(tiles + 1),
+                                              r.stream));
+        DHIP(hipMalloc(&r.scan_tmp, r.scan_bytes + 16));
+    }
     r.counts_out.assign(W, 0);
     r.counts_in.assign(W, 0);
     DHIP(hipStreamSynchronize(r.stream));
@@ -161,6 +249,7 @@ void init_schedule(DistDriver* d, const gossip_config& cfg) {
     d->n = cfg.n_peers;
     d->part = blocks(d->n, d->world);
     d->chunk = d->part[1];
+    d->tpb = (d->chunk + 63) / 64;
     if (cfg.pull_permille) d->pull_pm = cfg.pull_permille;
     if (cfg.bin_permille) d->bin_pm = cfg.bin_permille;
 }
@@ -221,6 +310,84 @@ gossip_status all_gather(DistDriver* d) {
         DNCCL(ncclAllGather(r.gather + r.rank * words, r.gather, words, ncclUint64, r.comm, r.stream));
     }
     DNCCL(ncclGroupEnd());
+    return GOSSIP_OK;
+}
+
+// The same exchange for a sparse frontier: each block's tile bitmap, all-gathered; the prefix of the
+// tiles' popcounts (on every rank: where each block's packed words sit in the concatenation); the own
+// block's words packed there and exchanged as send / recv pairs (sizes from the prefix); every other
+// block expanded into the gather buffer.  Bytes received per rank: (P - 1) tpb 8 B of bitmap + 8 X B per
+// non-zero peer of the other blocks, against 8 X B per peer of them.
+gossip_status compact_gather(DistDriver* d) {
+    const uint32_t W = d->world;
+    const uint64_t X = d->X, tpb = d->tpb, tiles = (uint64_t)W * tpb;
+    ExchTimer t(d, "all_gather");
+    for (auto& r : d->ranks) {  // own tile bitmap
+        DHIP(hipSetDevice(r.device));
+        hipLaunchKernelGGL(k_tile_bits, dim3((unsigned)std::min<uint64_t>((tpb + 3) / 4, 8192)), dim3(256), 0,
+                           r.stream, r.gather + r.rank * d->chunk * X, r.n_local, (uint32_t)X, r.bits + r.rank * tpb);
+        DHIP(hipGetLastError());
+    }
+    if (d->emulate) {
+        for (auto& q : d->ranks)
+            for (auto& p : d->ranks)
+                if (p.rank != q.rank)
+                    DHIP(hipMemcpyAsync(q.bits + p.rank * tpb, p.bits + p.rank * tpb, tpb * 8, hipMemcpyDeviceToDevice,
+                                        q.stream));
+    } else {
+        DNCCL(ncclGroupStart());
+        for (auto& r : d->ranks) {
+            hipSetDevice(r.device);
+            DNCCL(ncclAllGather(r.bits + r.rank * tpb, r.bits, tpb, ncclUint64, r.comm, r.stream));
+        }
+        DNCCL(ncclGroupEnd());
+    }
+    std::vector<uint64_t> off(W + 1);
+    for (auto& r : d->ranks) {
+        DHIP(hipSetDevice(r.device));
+        size_t tb = r.scan_bytes;
+        DHIP(hipcub::DeviceScan::ExclusiveSum(r.scan_tmp, tb, TilePop(r.bits, PopOp()), r.pos, (int)(tiles + 1), r.stream));
+        hipLaunchKernelGGL(k_pick_offsets, dim3(1), dim3(64 * ((W + 64) / 64)), 0, r.stream, r.pos, W, tpb, r.d_io);
+        DHIP(hipGetLastError());
+        DHIP(hipMemcpyAsync(r.h_io, r.d_io, (W + 1) * 8, hipMemcpyDeviceToHost, r.stream));
+        DHIP(hipStreamSynchronize(r.stream));
+        std::memcpy(off.data(), r.h_io, (W + 1) * 8);  // (identical on every rank)
+        hipLaunchKernelGGL(k_tile_pack, dim3((unsigned)std::min<uint64_t>((tpb + 3) / 4, 8192)), dim3(256), 0,
+                           r.stream, r.gather + r.rank * d->chunk * X, r.n_local, (uint32_t)X, r.bits + r.rank * tpb,
+                           r.pos + r.rank * tpb, r.pk);
+        DHIP(hipGetLastError());
+    }
+    for (size_t i = 0; i < d->ranks.size(); ++i)
+        t.bytes(i, 8.0 * (double)((W - 1) * tpb) +
+                       8.0 * X * (double)(off[W] - (off[d->ranks[i].rank + 1] - off[d->ranks[i].rank])));
+    if (d->emulate) {
+        for (auto& q : d->ranks)
+            for (auto& p : d->ranks) {
+                const uint64_t c = off[p.rank + 1] - off[p.rank];
+                if (p.rank != q.rank && c)
+                    DHIP(hipMemcpyAsync(q.pk + off[p.rank] * X, p.pk + off[p.rank] * X, c * X * 8,
+                                        hipMemcpyDeviceToDevice, q.stream));
+            }
+    } else {
+        DNCCL(ncclGroupStart());
+        for (auto& r : d->ranks) {
+            hipSetDevice(r.device);
+            const uint64_t mine = off[r.rank + 1] - off[r.rank];
+            for (uint32_t q = 0; q < W; ++q) {  // every rank knows every block's count: empty pairs skipped
+                if (q == r.rank) continue;
+                if (mine) DNCCL(ncclSend(r.pk + off[r.rank] * X, mine * X, ncclUint64, (int)q, r.comm, r.stream));
+                const uint64_t theirs = off[q + 1] - off[q];
+                if (theirs) DNCCL(ncclRecv(r.pk + off[q] * X, theirs * X, ncclUint64, (int)q, r.comm, r.stream));
+            }
+        }
+        DNCCL(ncclGroupEnd());
+    }
+    for (auto& r : d->ranks) {
+        DHIP(hipSetDevice(r.device));
+        hipLaunchKernelGGL(k_tile_expand, dim3((unsigned)std::min<uint64_t>((tiles + 3) / 4, 16384)), dim3(256), 0,
+                           r.stream, r.gather, r.bits, r.pos, r.pk, (uint32_t)X, W, r.rank, d->chunk, d->n, tpb);
+        DHIP(hipGetLastError());
+    }
     return GOSSIP_OK;
 }
 
@@ -326,9 +493,12 @@ gossip_status exchange_records(DistDriver* d, std::vector<uint64_t>& total_in) {
     return GOSSIP_OK;
 }
 
-void pack_stats(const gossip_round_stats& s, uint64_t* v) {
-    const uint64_t f[kStatSlots] = {s.frontier, s.traversals, s.deliveries, s.undelivered, s.new_receipts, s.injected,
-                                    s.died,     s.reports,    s.reconnects, s.rejoined,    s.digest,       s.covered};
+// the rank's round stats, and the peers it activated (the next round's frontier)
+void pack_stats(DistRank& r, uint64_t* v) {
+    const gossip_round_stats& s = r.local;
+    const uint64_t f[kStatSlots] = {s.frontier, s.traversals, s.deliveries, s.undelivered, s.new_receipts,
+                                    s.injected, s.died,       s.reports,    s.reconnects,  s.rejoined,
+                                    s.digest,   s.covered,    ctx_frontier_est(r.ctx)};
     std::memcpy(v, f, sizeof(f));
 }
 
@@ -337,14 +507,14 @@ gossip_status all_reduce_stats(DistDriver* d, uint64_t* g) {
         std::fill(g, g + kStatSlots, 0ull);
         for (auto& r : d->ranks) {
             uint64_t v[kStatSlots];
-            pack_stats(r.local, v);
+            pack_stats(r, v);
             for (int i = 0; i < kStatSlots; ++i) g[i] += v[i];  // mod 2^64, like ncclSum on uint64
         }
         return GOSSIP_OK;
     }
     for (auto& r : d->ranks) {
         hipSetDevice(r.device);
-        pack_stats(r.local, r.h_io);
+        pack_stats(r, r.h_io);
         DHIP(hipMemcpyAsync(r.d_io, r.h_io, kStatSlots * 8, hipMemcpyHostToDevice, r.stream));
     }
     DNCCL(ncclGroupStart());
@@ -378,7 +548,10 @@ gossip_status dist_step(DistDriver* d, gossip_round_stats* out) {
     d->modes.push_back(mode);
     gossip_status s = GOSSIP_OK;
     if (mode == GOSSIP_MODE_PULL || mode == GOSSIP_MODE_BIN) {
-        if ((s = all_gather(d))) return s;
+        // a narrow frontier exchanges its non-zero words only (the same gather buffer either way)
+        const uint32_t gpm = ctx_gather_pm(d->ranks[0].ctx);
+        const bool compact = d->world > 1 && d->front * 1000 < (uint64_t)gpm * d->n;
+        if ((s = compact ? compact_gather(d) : all_gather(d))) return s;
         for (auto& r : d->ranks)
             if ((s = gossip_round_compute(r.ctx))) return s;
         for (auto& r : d->ranks)
@@ -415,6 +588,7 @@ gossip_status dist_step(DistDriver* d, gossip_round_stats* out) {
     o.rejoined = g[9];
     d->cum_digest += g[10];
     d->cum_covered += g[11];
+    d->front = g[12];
     o.digest = d->cum_digest;
     o.covered = d->cum_covered;
     o.duplicates = o.deliveries - o.new_receipts;
@@ -521,7 +695,7 @@ gossip_status dist_step_ctx(gossip_ctx* c, gossip_round_stats* out) {
 }
 
 void dist_reset(DistDriver* d) {
-    d->prev_new = d->injected = d->cum_digest = d->cum_covered = 0;
+    d->prev_new = d->injected = d->cum_digest = d->cum_covered = d->front = 0;
     d->finished = false;
     d->modes.clear();
 }

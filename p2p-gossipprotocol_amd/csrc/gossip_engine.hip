@@ -194,6 +194,8 @@ struct gossip_ctx {
                                           // sparser dense rounds blocked
     uint64_t pb_direct_in = kPbFineIn;    // "blocked_direct_in": leading tiles of more in-degree are hubs
     uint32_t pb_lo_pm = kPbLoPermille;    // "blocked_push_permille": push rounds from this frontier run blocked
+    uint32_t gather_pm = kGatherPermille; // "gather_permille": partitioned dense rounds below this frontier per-mille
+                                          // exchange {tile bitmap, packed non-zero words} (gossip_dist.hip)
     uint32_t row_step = 1;                // "pull_step": k_pull_rows's neighbour words per row per step
                                           // (config 4 round 7: 2 -> 1, 180 -> 101 M gathers, 6.6-6.8 ->
                                           // 5.4-5.7 ms; most rows stop at their first neighbour)
@@ -214,6 +216,9 @@ struct gossip_ctx {
     uint64_t* seg = nullptr;     // sparse push: per-destination record segments (world x chunk records)
     unsigned long long* d_counts = nullptr;  // records per destination rank
     uint64_t* h_counts = nullptr;            // pinned copy
+    uint64_t *sx_bits = nullptr, *sx_pos = nullptr;  // the compaction's tile bitmap and popcount prefix
+    void* sx_tmp = nullptr;
+    size_t sx_bytes = 0;
     bool cur_sparse = false;
     bool send_dirty = false;     // the dense staging buffer holds a dense push round's masks
     uint32_t heavy = kHeavyDegree;      // light/heavy row threshold of the resident overlay (its chunks, bins and
@@ -235,6 +240,8 @@ struct gossip_ctx {
 
     // timing
     bool timing = false;
+    unsigned long long* d_live = nullptr;  // ping rounds while timing: 8(d)'s pings and alive peers (k_live_count)
+    bool live_counted = false;             // this round's d_live holds a count
     std::map<std::string, TimerRec> timers;
     std::map<std::string, double> kbytes;
     std::vector<hipEvent_t> event_pool;
@@ -269,6 +276,8 @@ void ctx_attach_dist(gossip_ctx* c, DistDriver* d, bool owned) {
 }
 DistDriver* ctx_dist(gossip_ctx* c) { return c->dist; }
 bool ctx_timing(gossip_ctx* c) { return c->timing; }
+uint64_t ctx_frontier_est(gossip_ctx* c) { return c->frontier_est; }
+uint32_t ctx_gather_pm(gossip_ctx* c) { return c->gather_pm; }
 void ctx_clear_exchange(gossip_ctx* c) {
     c->send = nullptr;
     c->recv = nullptr;
@@ -910,7 +919,14 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
         HIPCHK(timed(c, "rejoin", [&] {
             return launch_rejoin_select(a, c->reboot, c->rj_list, c->rj_n, c->n_local, c->stream);
         }));
+    c->live_counted = false;
     if (c->cfg.ping_every && c->round % c->cfg.ping_every == 0) {
+        if (c->timing) {  // the pings this round sends (before its masking), for 8(d)'s liveness bytes
+            if (!c->d_live) HIPCHK(hipMalloc((void**)&c->d_live, 2 * sizeof(unsigned long long)));
+            HIPCHK(hipMemsetAsync(c->d_live, 0, 2 * sizeof(unsigned long long), c->stream));
+            HIPCHK(launch_live_count(a, c->d_live, c->stream));
+            c->live_counted = true;
+        }
         HIPCHK(timed(c, "liveness", [&] {
             hipError_t e = hipSuccess;
             if (c->closed_live) {
@@ -1141,7 +1157,6 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
             c->send_dirty = false;
         }
         if (remote && !c->cur_sparse) c->send_dirty = true;
-        if (c->cur_sparse) HIPCHK(hipMemsetAsync(c->d_counts, 0, c->world * sizeof(unsigned long long), c->stream));
     }
     if (c->cur_pb) a.tsparse = 0;  // the blocked round sweeps every tile (round_compute clears the marks)
     c->cur = a;
@@ -1321,7 +1336,8 @@ gossip_status round_compute(gossip_ctx* c) {
     HIPCHK(timed(c, "push_light", [&] { return launch_push_light(a, pw, c->any_dead, remote, c->stream); }));
     if (c->cur_sparse) {
         HIPCHK(timed(c, "compact_send", [&] {
-            return launch_compact_send(a, pw, c->part_begins[1], c->d_counts, c->seg, c->stream);
+            return launch_compact_send(a, pw, c->part_begins[1], c->world, c->d_counts, c->seg, c->sx_bits, c->sx_pos,
+                                       c->sx_tmp, c->sx_bytes, c->stream);
         }));
         HIPCHK(hipMemcpyAsync(c->h_counts, c->d_counts, c->world * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
     }
@@ -1407,6 +1423,13 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
             c->kbytes["push_heavy"] += 20.0 * (double)d.heavy_traversals;
         }
         c->kbytes["liveness"] += 6.125 * (double)d.live_checked;
+        if (c->live_counted) {  // 8(d): 6.125 B per ping + 16 B per alive peer of a ping round
+            unsigned long long lv[2] = {0, 0};
+            HIPCHK(hipMemcpy(lv, c->d_live, sizeof(lv), hipMemcpyDeviceToHost));
+            c->kbytes["#pings"] += (double)lv[0];
+            c->kbytes["#pinging_peers"] += (double)lv[1];
+            c->live_counted = false;
+        }
         // counters (not bytes): device-scope atomics on peer state, traversals by row class
         c->kbytes["#atomics"] += (double)d.atomics;
         c->kbytes["#heavy_trav"] += (double)d.heavy_traversals;
@@ -1637,6 +1660,7 @@ gossip_status gossip_set_tuning(gossip_ctx* c, const char* key, int64_t value) {
     }
     else if (k == "blocked_push_permille") c->pb_lo_pm = value < 0 ? kPbLoPermille : u;
     else if (k == "list_cap") c->list_cap_req = u;
+    else if (k == "gather_permille") c->gather_pm = value < 0 ? kGatherPermille : u;
     else return fail(GOSSIP_EINVAL, "unknown tuning option: " + k);
     return GOSSIP_OK;
 }
@@ -1658,6 +1682,10 @@ void gossip_destroy(gossip_ctx* c) {
     if (c->tiny_result) hipHostFree(c->tiny_result);
     hipFree(c->d_counts);
     if (c->h_counts) hipHostFree(c->h_counts);
+    hipFree(c->d_live);
+    hipFree(c->sx_bits);
+    hipFree(c->sx_pos);
+    hipFree(c->sx_tmp);
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
     if (c->dist && c->dist_owned) gossip::dist_free(c->dist);
     delete c;
@@ -2020,6 +2048,12 @@ gossip_status gossip_set_sparse(gossip_ctx* c, void* seg) {
     if (!c->d_counts) {
         HIPCHK(hipMalloc((void**)&c->d_counts, (c->world + 1) * sizeof(unsigned long long)));
         HIPCHK(hipHostMalloc((void**)&c->h_counts, (c->world + 1) * sizeof(uint64_t)));
+        const uint64_t tiles = (uint64_t)c->world * ((c->part_begins[1] + 63) / 64);
+        HIPCHK(hipMalloc((void**)&c->sx_bits, (tiles + 1) * sizeof(uint64_t)));
+        HIPCHK(hipMemset(c->sx_bits, 0, (tiles + 1) * sizeof(uint64_t)));
+        HIPCHK(hipMalloc((void**)&c->sx_pos, (tiles + 1) * sizeof(uint64_t)));
+        HIPCHK(compact_send_scratch(tiles, &c->sx_bytes));
+        HIPCHK(hipMalloc(&c->sx_tmp, c->sx_bytes + 16));
     }
     c->seg = (uint64_t*)seg;
     return GOSSIP_OK;

@@ -142,9 +142,10 @@ constexpr uint32_t kPbCoarse = 256;    // level-1 bins (a power of two: the LDS 
 constexpr uint32_t kPbFineMax = 96;    // fine bins per coarse bin (level-2 LDS staging)
 constexpr uint32_t kPbFineIn = 1u << 18;  // a fine bin: whole tiles, <= kBinWords peers and <= this in-degree
                                           // (unless one tile has more): no hot bin in level 2
-constexpr uint32_t kPbB1 = 16;         // level-1 records per flush: 64 B of destinations, 128 B of words
-                                       // (two halves per bin in LDS, gossip_stage.hpp)
-constexpr uint32_t kPbB2 = 32;         // level-2 records per flush: 64 B of destinations, 256 B of words
+constexpr uint32_t kPbB1 = 32;         // level-1 records per flush: 128 B of destinations, 256 B of words
+constexpr uint32_t kPbH1 = 1;          // ... one buffer per coarse bin (gossip_stage.hpp)
+constexpr uint32_t kPbB2 = 64;         // level-2 records per flush: 128 B of destinations, 512 B of words
+constexpr uint32_t kPbH2 = 2;          // ... two buffers per fine bin
 constexpr uint32_t kPbSlices = 4;      // level-2 workgroups per coarse bin
 constexpr int kPbBlock = 1024;         // 16 waves per workgroup, one workgroup per CU (level 1)
 constexpr int kPbGrid = 256;           // level-1 workgroups (row ranges)
@@ -325,8 +326,12 @@ hipError_t launch_list_zero(const RoundArgs& a, const uint32_t* lst, uint32_t n,
 hipError_t launch_pull_list(const RoundArgs& a, const uint32_t* lst, uint32_t n, hipStream_t s);
 hipError_t launch_apply_remote(const RoundArgs& a, uint32_t W, const uint64_t* recv, uint32_t world,
                                uint64_t part_stride, hipStream_t s);
-hipError_t launch_compact_send(const RoundArgs& a, uint32_t W, uint64_t chunk, unsigned long long* counts,
-                               uint64_t* seg, hipStream_t s);
+// sparse push exchange: send -> per-destination {peer, words} records at seg + q * chunk, counts[q] of them
+// (bits: world * ceil(chunk / 64) + 1 words, the last kept zero; pos: as many; scan_tmp: compact_send_scratch)
+hipError_t compact_send_scratch(uint64_t tiles, size_t* scan_bytes);
+hipError_t launch_compact_send(const RoundArgs& a, uint32_t W, uint64_t chunk, uint32_t world,
+                               unsigned long long* counts, uint64_t* seg, uint64_t* bits, uint64_t* pos,
+                               void* scan_tmp, size_t scan_bytes, hipStream_t s);
 hipError_t launch_apply_records(const RoundArgs& a, uint32_t W, const uint64_t* rec, uint64_t n_rec, hipStream_t s);
 hipError_t launch_bin_scatter(const RoundArgs& a, const BinArgs& b, uint32_t W, hipStream_t s);
 hipError_t launch_bin_apply(const RoundArgs& a, const BinArgs& b, uint32_t W, hipStream_t s);
@@ -345,6 +350,9 @@ hipError_t launch_dead_edges(const RoundArgs& a, uint32_t lo, uint32_t hi, hipSt
 // death rounds [lo, hi] reach max_missed misses now; alive reporters mask them,
 // report and (dmask) count them
 hipError_t launch_liveness_window(const RoundArgs& a, uint32_t lo, uint32_t hi, hipStream_t s);
+// measurement (timing on): a ping round's pings (unmasked out-edges of alive owned peers) and those peers,
+// added to out[0], out[1]
+hipError_t launch_live_count(const RoundArgs& a, unsigned long long* out, hipStream_t s);
 // rev[] of the symmetric overlay (once per overlay)
 hipError_t launch_reverse_edges(const RoundArgs& a, hipStream_t s);
 // join churn, before the round's kills and deaths: peers dead at round start
@@ -400,6 +408,10 @@ constexpr uint32_t kTinyEdges = 65536;
 // a push touches deg x frontier edges with atomics, a binned round streams all of them; measured
 // crossover 6-9 % (config 2: 5.05 %-frontier rounds cost 0.03 ms pushed, 0.13 ms binned)
 constexpr uint32_t kPullPermille = 60;
+// partitioned dense rounds exchange every block's {64-peer tile bitmap, packed non-zero new words} instead of
+// its whole slice of new words while the round's frontier is below this per-mille of the peers
+// (gossip_dist.hip; "gather_permille": 0 never, 1000 always)
+constexpr uint32_t kGatherPermille = 600;
 // the streamed bin layout is chosen while the slot array (8 B x edges x padded words) is at most this
 constexpr uint64_t kStreamSlotBytes = 128ull << 20;
 
@@ -430,6 +442,8 @@ void ctx_range(gossip_ctx* c, uint64_t* begin, uint64_t* end);
 void ctx_attach_dist(gossip_ctx* c, DistDriver* d, bool owned);
 DistDriver* ctx_dist(gossip_ctx* c);
 bool ctx_timing(gossip_ctx* c);
+uint64_t ctx_frontier_est(gossip_ctx* c);  // peers the last round activated (this round's frontier)
+uint32_t ctx_gather_pm(gossip_ctx* c);     // "gather_permille"
 // forget the exchange buffers registered by gossip_set_exchange / _gather / _sparse (they are being freed)
 void ctx_clear_exchange(gossip_ctx* c);
 // time device work issued on the ctx's stream under `name` (gossip_kernel_time) while timing is on

@@ -15,6 +15,7 @@
 // threshold (RoundArgs.heavy) are cut into kHeavyChunk-edge chunks, one wave
 // each, so no wave walks a long tail.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 #include <stdlib.h>
 
 #include "gossip_device.hpp"
@@ -2066,6 +2067,34 @@ __global__ __launch_bounds__(kBlock) void k_rejoin_select(RoundArgs a, RebootArg
 }
 
 // ---------------------------------------------------------------------------
+// Measurement only (while timing is on): SURVEY.md 8(d)'s liveness term of a ping round counts the pings
+// pingLoop sends (peer.cpp:328-346) -- every connected (unmasked) out-edge of every alive owned peer, the
+// overflow rows included -- and those peers.  The closed-form ping round visits far fewer edges; this
+// count is what its bytes are charged against.  out[0] += edges, out[1] += peers.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_live_count(RoundArgs a, unsigned long long* out) {
+    unsigned long long e = 0, nv = 0;
+    for (uint64_t v = (uint64_t)blockIdx.x * kBlock + threadIdx.x; v < a.n_local; v += (uint64_t)gridDim.x * kBlock) {
+        if (!bit_alive(a.alive, (uint32_t)(a.begin + v))) continue;
+        ++nv;
+        const uint64_t r0 = a.rp[v], r1 = a.rp[v + 1];
+        if (a.dmask) {
+            e += (r1 - r0) - a.dmask[v];
+        } else {
+            for (uint64_t i = r0; i < r1; ++i) e += !(a.col[i] & kMaskedEdge);
+        }
+        if (a.ex_cnt)
+            for (uint32_t k = 0; k < a.ex_cnt[v]; ++k) e += !(a.ex_col[v * a.ex_cap + k] & kMaskedEdge);
+    }
+    e = wave_sum(e);
+    nv = wave_sum(nv);
+    if ((threadIdx.x & 63) == 0 && (e | nv)) {
+        atomicAdd(out, e);
+        atomicAdd(out + 1, nv);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // churn / kills: a dead peer stops receiving, forwarding and pinging.  Its
 // pending new words are dropped, but they are already in seen, so their
 // digest/coverage contribution is booked here.
@@ -2183,45 +2212,55 @@ __global__ __launch_bounds__(kBlock) void k_apply_remote(RoundArgs a, const uint
 // buffer (send, one entry per global peer, OR of everything this rank pushed
 // to that peer) is compacted into per-destination-rank records
 // {peer, words[W]} and cleared in the same pass, so only the touched peers
-// cross xGMI.  Records of a destination stay <= its block size.
+// cross xGMI.  Records of a destination stay <= its block size.  Deterministic
+// and without atomics: a bitmap of each destination block's 64-peer tiles
+// (k_send_bits), the exclusive prefix of their popcounts (hipcub scan), then
+// every touched peer's record at its rank in its block (k_send_pack).  (Round
+// 3's version took each record's place from one global counter per
+// destination: millions of same-address atomics per round -- config 4 at
+// P = 8, 69 ms of compaction per step.)
 // ---------------------------------------------------------------------------
 template <int W>
-__global__ __launch_bounds__(kBlock) void k_compact_send(RoundArgs a, uint64_t chunk, unsigned long long* counts,
-                                                         uint64_t* seg) {
+__global__ __launch_bounds__(kBlock) void k_send_bits(RoundArgs a, uint64_t chunk, uint64_t tpb, uint32_t world,
+                                                      uint64_t* bits) {
     const int lane = threadIdx.x & 63;
-    const uint64_t n_tiles = (a.n_global + 63) >> 6;
+    const uint64_t tiles = (uint64_t)world * tpb;
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
-    for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); t < n_tiles; t += nwaves) {
-        const uint64_t v = (t << 6) + lane;
-        uint64_t m[W];
+    for (uint64_t T = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); T < tiles; T += nwaves) {
+        const uint64_t q = T / tpb, t = T % tpb;
+        const uint64_t end = min((q + 1) * chunk, a.n_global);
+        const uint64_t v = q * chunk + t * 64 + lane;
         bool any = false;
+        if (v < end) {
+#pragma unroll
+            for (int w = 0; w < W; ++w) any |= a.send[v * W + w] != 0ull;
+        }
+        const unsigned long long b = __ballot(any);
+        if (lane == 0) bits[T] = b;
+    }
+}
+
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_send_pack(RoundArgs a, uint64_t chunk, uint64_t tpb, uint32_t world,
+                                                      const uint64_t* bits, const uint64_t* pos,
+                                                      unsigned long long* counts, uint64_t* seg) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t tiles = (uint64_t)world * tpb;
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    const uint64_t gid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (gid < world) counts[gid] = pos[(gid + 1) * tpb] - pos[gid * tpb];  // records per destination
+    for (uint64_t T = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); T < tiles; T += nwaves) {
+        const uint64_t b = bits[T];
+        if (!((b >> lane) & 1)) continue;
+        const uint64_t q = T / tpb, t = T % tpb;
+        const uint64_t v = q * chunk + t * 64 + lane;
+        const uint64_t idx = pos[T] - pos[q * tpb] + (uint64_t)__popcll(b & ((1ull << lane) - 1));
+        uint64_t* rec = seg + (q * chunk + idx) * (1 + W);
+        rec[0] = v;
 #pragma unroll
         for (int w = 0; w < W; ++w) {
-            m[w] = v < a.n_global ? a.send[v * W + w] : 0ull;
-            any |= m[w] != 0;
-        }
-        const unsigned long long act = __ballot(any);
-        if (!act) continue;
-        const uint64_t q = v / chunk;
-        const int lead = __builtin_ctzll(act);
-        const uint64_t q0 = __shfl(q, lead);
-        const bool uniform = __ballot(any && q != q0) == 0ull;  // the tile's active peers share one block
-        unsigned long long idx = 0;
-        if (uniform) {
-            unsigned long long base = 0;
-            if (lane == lead) base = atomicAdd(&counts[q0], (unsigned long long)__popcll(act));
-            idx = __shfl(base, lead) + lane_rank(act);
-        } else if (any) {
-            idx = atomicAdd(&counts[q], 1ull);
-        }
-        if (any) {
-            uint64_t* rec = seg + (q * chunk + idx) * (1 + W);
-            rec[0] = v;
-#pragma unroll
-            for (int w = 0; w < W; ++w) {
-                rec[1 + w] = m[w];
-                a.send[v * W + w] = 0ull;
-            }
+            rec[1 + w] = a.send[v * W + w];
+            a.send[v * W + w] = 0ull;
         }
     }
 }
@@ -2480,11 +2519,31 @@ hipError_t launch_apply_remote(const RoundArgs& a, uint32_t W_, const uint64_t* 
     return hipGetLastError();
 }
 
-hipError_t launch_compact_send(const RoundArgs& a, uint32_t W_, uint64_t chunk, unsigned long long* counts,
-                               uint64_t* seg, hipStream_t s) {
-    const uint64_t tiles = (a.n_global + 63) / 64;
-    GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_compact_send<W>, dim3(grid_for(tiles, kWavesPerBlock)),
-                                                   dim3(kBlock), 0, s, a, chunk, counts, seg));
+namespace {
+struct PopOp {
+    __host__ __device__ uint64_t operator()(uint64_t x) const { return (uint64_t)__builtin_popcountll(x); }
+};
+}  // namespace
+
+hipError_t compact_send_scratch(uint64_t tiles, size_t* scan_bytes) {
+    hipcub::TransformInputIterator<uint64_t, PopOp, const uint64_t*> it(nullptr, PopOp());
+    return hipcub::DeviceScan::ExclusiveSum(nullptr, *scan_bytes, it, (uint64_t*)nullptr, (int)(tiles + 1));
+}
+
+hipError_t launch_compact_send(const RoundArgs& a, uint32_t W_, uint64_t chunk, uint32_t world,
+                               unsigned long long* counts, uint64_t* seg, uint64_t* bits, uint64_t* pos,
+                               void* scan_tmp, size_t scan_bytes, hipStream_t s) {
+    const uint64_t tpb = (chunk + 63) / 64, tiles = (uint64_t)world * tpb;
+    const unsigned grid = (unsigned)std::min<uint64_t>(grid_for(tiles, kWavesPerBlock), 16384);
+    GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_send_bits<W>, dim3(grid), dim3(kBlock), 0, s, a, chunk, tpb,
+                                                   world, bits));
+    if (hipError_t e = hipGetLastError()) return e;
+    // (bits[tiles] is zero from the allocation: the scan's last element is the total)
+    hipcub::TransformInputIterator<uint64_t, PopOp, const uint64_t*> it(bits, PopOp());
+    size_t tb = scan_bytes;
+    if (hipError_t e = hipcub::DeviceScan::ExclusiveSum(scan_tmp, tb, it, pos, (int)(tiles + 1), s)) return e;
+    GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_send_pack<W>, dim3(grid), dim3(kBlock), 0, s, a, chunk, tpb,
+                                                   world, bits, pos, counts, seg));
     return hipGetLastError();
 }
 
@@ -2601,6 +2660,12 @@ static hipError_t launch_rows(const RoundArgs& a, uint32_t lo, uint32_t hi, hipS
 
 hipError_t launch_dead_edges(const RoundArgs& a, uint32_t lo, uint32_t hi, hipStream_t s) {
     return launch_rows<kRowsDead>(a, lo, hi, s);
+}
+
+hipError_t launch_live_count(const RoundArgs& a, unsigned long long* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_live_count, dim3(std::min<uint64_t>(grid_for(a.n_local, kBlock), 4096)), dim3(kBlock), 0, s, a,
+                       out);
+    return hipGetLastError();
 }
 
 hipError_t launch_liveness_window(const RoundArgs& a, uint32_t lo, uint32_t hi, hipStream_t s) {

@@ -333,7 +333,7 @@ class Group:
     ncclCommInitAll; all the same GPU: device-copy exchange).  Takes the
     Engine's keyword arguments (except part/device)."""
 
-    def __init__(self, n_peers: int, n_msgs: int, devices, **kw):
+    def __init__(self, n_peers: int, n_msgs: int, devices, tuning: dict | None = None, **kw):
         self._L = _abi.lib()
         cfg = make_config(n_peers, n_msgs, **kw)
         devs = (C.c_int32 * len(devices))(*devices)
@@ -343,6 +343,10 @@ class Group:
         self.n_peers, self.n_msgs = n_peers, n_msgs
         self.W = (n_msgs + 63) // 64
         self.n_parts = len(devices)
+        for key, value in (tuning or {}).items():  # every part gets the same options
+            for p in range(self.n_parts):
+                check(self._L.gossip_set_tuning(self.part_ctx(p), key.encode(), int(value)),
+                      f"gossip_set_tuning({key})")
 
     def close(self) -> None:
         if getattr(self, "_g", None) and self._g.value:

@@ -244,12 +244,10 @@ int GossipNetwork::step() {
     }
     rounds_.push_back(st);
     if (trace_) captureRound(st.round);
-    if (rc == 1) {
-        finished_ = true;
-        // a partitioned run's seed removals come from the merged reports once it ends
-        // (single-partition stats carry them every round)
-        if (group_) seedRemovalsFromReports();
-    }
+    if (rc == 1) finished_ = true;
+    // a partitioned run's seed removals come from the merged reports (single-partition stats carry them every
+    // round): every round while the reports are few (or traced), else once the run ends
+    if (group_ && (finished_ || trace_ || groupReportCount() < (1u << 20))) seedRemovalsFromReports();
     return rc;
 }
 
@@ -274,6 +272,17 @@ std::vector<gossip_dead_report> GossipNetwork::reports() const {
     std::vector<gossip_dead_report> out(count);
     gossip_read_reports(ctx_, out.data(), count, &count);
     return out;
+}
+
+// Reports held by the parts of a group (their counters only: no merge)
+uint64_t GossipNetwork::groupReportCount() const {
+    uint64_t total = 0;
+    gossip_ctx* part = nullptr;
+    for (uint32_t p = 0; group_ && gossip_group_part(group_, p, &part) == GOSSIP_OK; ++p) {
+        uint64_t n = 0;
+        if (gossip_read_reports(part, nullptr, 0, &n) == GOSSIP_OK) total += n;
+    }
+    return total;
 }
 
 // The registry drops a peer on its first report (SeedNode::handleDeadNode,

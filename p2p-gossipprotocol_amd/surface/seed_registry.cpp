@@ -45,11 +45,18 @@ bool SeedNode::start() {
 
 void SeedNode::stop() { running_ = false; }
 
+// peerList[peer] = now (seed.cpp:153-156): a new key keeps the time of its first insertion (the key's
+// lastSeen, which getPeerList reports, seed.cpp:169-177); a repeated registration only updates the mapped value
 void SeedNode::addPeer(const PeerInfo& peer) {
     std::lock_guard<std::mutex> g(mu_);
+    const auto now = std::chrono::system_clock::time_point(std::chrono::seconds(clock_));
     auto it = peers_.find(peer);
-    if (it == peers_.end()) order_.push_back(peer);
-    peers_[peer] = std::chrono::system_clock::time_point(std::chrono::seconds(clock_));
+    if (it == peers_.end()) {
+        PeerInfo key = peer;
+        key.lastSeen = now;
+        order_.push_back(key);
+    }
+    peers_[peer] = now;
 }
 
 void SeedNode::handleDeadNode(const std::string& deadIP, int deadPort) {
@@ -58,7 +65,7 @@ void SeedNode::handleDeadNode(const std::string& deadIP, int deadPort) {
     if (peers_.erase(dead) > 0) {
         order_.erase(std::remove(order_.begin(), order_.end(), dead), order_.end());
         const std::string msg = "Removed dead peer: " + deadIP + ":" + std::to_string(deadPort);
-        if (!logPath_.empty()) std::cout << msg << std::endl;
+        std::cout << msg << std::endl;  // unconditionally, as seed.cpp:164
         log(msg);
     }
 }
@@ -67,11 +74,7 @@ std::vector<PeerInfo> SeedNode::getPeerList() {
     std::lock_guard<std::mutex> g(mu_);
     std::vector<PeerInfo> out;
     out.reserve(order_.size());
-    for (const PeerInfo& p : order_) {
-        PeerInfo q = p;
-        q.lastSeen = peers_[p];
-        out.push_back(q);
-    }
+    for (const PeerInfo& p : order_) out.push_back(p);  // keys, with their first-insert lastSeen
     return out;
 }
 

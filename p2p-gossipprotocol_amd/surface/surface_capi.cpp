@@ -4,8 +4,11 @@
 #include <exception>
 #include <string>
 
+#include <sstream>
+
 #include "gossip/config.hpp"
 #include "gossip/formats.hpp"
+#include "gossip/seed.hpp"
 
 namespace {
 
@@ -60,6 +63,25 @@ int gossip_surface_register(const char* ip, int port, char* out, size_t cap) {
 
 int gossip_surface_dead_node(const char* ip, int port, char* out, size_t cap) {
     return put(gossip::dead_node_json(ip, port), out, cap);
+}
+
+// A SeedNode driven by requests, one per line "<unix seconds> <json>" (the seed's clock, then
+// handleRequest); out gets each request's response (empty for dead_node) on a line of its own.
+int gossip_surface_seed(const char* ops, char* out, size_t cap) {
+    try {
+        SeedNode seed("127.0.0.1", 8000);
+        std::istringstream in(ops ? ops : "");
+        std::string line, res;
+        while (std::getline(in, line)) {
+            const size_t sp = line.find(' ');
+            if (sp == std::string::npos) continue;
+            seed.setClock(std::stoll(line.substr(0, sp)));
+            res += seed.handleRequest(line.substr(sp + 1)) + "\n";
+        }
+        return put(res, out, cap);
+    } catch (const std::exception&) {
+        return -2;
+    }
 }
 
 int gossip_surface_log(int seed_style, long long t, const char* msg, char* out, size_t cap) {

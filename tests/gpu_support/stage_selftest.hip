@@ -20,7 +20,7 @@ using namespace gossip;
 namespace {
 
 constexpr int kBlockT = 1024;
-constexpr uint32_t kMaxBins = 128;
+constexpr uint32_t kMaxBins = 128;  // 96 in level 2's geometry (kb = 64), as kPbFineMax
 
 __device__ uint32_t hash32(uint32_t x) {
     x ^= x >> 16;
@@ -41,16 +41,16 @@ uint32_t bin_of(uint32_t id, uint32_t nb, uint32_t skew) {  // host copy of the 
     return skew ? (h % 8 == 0 ? h % nb : 0u) : h % nb;
 }
 
-template <uint32_t kB, class TD>
+template <uint32_t kB, uint32_t kH, class TD, uint32_t kNB>
 __global__ __launch_bounds__(kBlockT) void k_stage(uint32_t nb, uint32_t per_wg, uint32_t skew, uint32_t* out_id,
                                                    unsigned long long* out_w, const uint64_t* seg_base,
                                                    const uint32_t* seg_cap, uint32_t* err) {
-    __shared__ uint32_t tk_s[kMaxBins], wr_s[2 * kMaxBins], gn_s[2 * kMaxBins];
-    __shared__ uint64_t base_s[kMaxBins];  // this workgroup's segment of each bin
-    __shared__ uint32_t cap_s[kMaxBins];
-    __shared__ TD bd_s[kMaxBins * 2 * kB];
-    __shared__ unsigned long long bw_s[kMaxBins * 2 * kB];
-    stage_init(tk_s, wr_s, gn_s, kMaxBins, threadIdx.x, kBlockT);
+    __shared__ uint32_t tk_s[kNB], wr_s[kH * kNB], gn_s[kH * kNB];
+    __shared__ uint64_t base_s[kNB];  // this workgroup's segment of each bin
+    __shared__ uint32_t cap_s[kNB];
+    __shared__ TD bd_s[kNB * kH * kB];
+    __shared__ unsigned long long bw_s[kNB * kH * kB];
+    stage_init<kH>(tk_s, wr_s, gn_s, kNB, threadIdx.x, kBlockT);
     __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (uint32_t f = threadIdx.x; f < nb; f += kBlockT) {
@@ -60,18 +60,19 @@ __global__ __launch_bounds__(kBlockT) void k_stage(uint32_t nb, uint32_t per_wg,
     __syncthreads();
     auto flush = [&](uint32_t f, uint32_t g) {
         const uint32_t i = lane & (kB - 1);
-        const uint32_t hb = f * 2 * kB + (g & 1) * kB;
+        const uint32_t hb = stage_at<kB, kH>(f, g, 0);
         const TD dv = bd_s[hb + i];
         const unsigned long long wv = bw_s[hb + i];
         lds_fence();
-        if (lane == 0) stage_release(wr_s, gn_s, f, g);
+        if (lane == 0) stage_release<kH>(wr_s, gn_s, f, g);
         if ((uint64_t)g * kB + kB > cap_s[f]) {  // the segment would overflow
             if (lane == 0) atomicOr(err, 2u);
             return;
         }
         const uint64_t at = base_s[f] + (uint64_t)g * kB + i;
-        if (lane < (int)kB) out_id[at] = (TD)~dv == 0 ? 0xFFFFFFFFu : (uint32_t)(wv >> 32);
-        else if (lane < 2 * (int)kB) out_w[at] = wv;
+        // (kB = 64: one lane per record, both stores; kB = 32: lanes 0-31 destinations, 32-63 words)
+        if (kB == 64 || lane < (int)kB) out_id[at] = (TD)~dv == 0 ? 0xFFFFFFFFu : (uint32_t)(wv >> 32);
+        if (kB == 64 || (lane >= (int)kB && lane < 2 * (int)kB)) out_w[at] = wv;
     };
     constexpr int kU = 4;
     for (uint32_t i0 = (uint32_t)wave * 64 * kU; i0 < per_wg; i0 += kBlockT * kU) {
@@ -87,7 +88,7 @@ __global__ __launch_bounds__(kBlockT) void k_stage(uint32_t nb, uint32_t per_wg,
             d[j] = k[j];
             w[j] = ((unsigned long long)id << 32) | k[j];
         }
-        stage<kU, kB>(tk_s, wr_s, gn_s, bd_s, bw_s, k, d, w, pend, flush, err);
+        stage<kU, kB, kH>(tk_s, wr_s, gn_s, bd_s, bw_s, k, d, w, pend, flush, err);
     }
     __syncthreads();
     for (uint32_t f = wave; f < nb; f += kBlockT / 64) {
@@ -96,7 +97,7 @@ __global__ __launch_bounds__(kBlockT) void k_stage(uint32_t nb, uint32_t per_wg,
         if (lane == 0) atomicAdd(&err[1], stage_len(tk_s, f, kB));
         if (!c) continue;
         if ((uint32_t)lane >= c && lane < (int)kB) {
-            const uint32_t s = f * 2 * kB + (g & 1) * kB + lane;
+            const uint32_t s = stage_at<kB, kH>(f, g, lane);
             bd_s[s] = (TD)~0u;
             bw_s[s] = 0ull;
         }
@@ -111,11 +112,13 @@ __global__ __launch_bounds__(kBlockT) void k_stage(uint32_t nb, uint32_t per_wg,
 // out[2] records expected, out[3] misplaced, out[4] duplicates, out[5] error flags (bit 4: a stuck wave),
 // out[6] = Σ of the segments' lengths (stage_len: whole generations), out[7] = the same from the host
 // (the segments' capacities).
-// kb: 16 (32-bit destinations, level 1's geometry) or 32 (16-bit destinations, level 2's).
+// kb: 32 (32-bit destinations, one buffer per bin: level 1's geometry) or 64 (16-bit destinations, two
+// buffers per bin: level 2's); 16 and 128 are the same protocol at other sizes (16: two buffers).
 // Returns 0, or -1 on a HIP error / bad argument.
 extern "C" int stage_selftest(uint32_t nb, uint32_t per_wg, uint32_t skew, uint32_t grid, uint32_t kb,
                               uint64_t* out) {
-    if (!out || nb < 1 || nb > kMaxBins || (kb != 16 && kb != 32) || !grid) return -1;
+    if (!out || nb < 1 || nb > (kb == 64 ? 96u : kMaxBins) || (kb != 16 && kb != 32 && kb != 64) || !grid)
+        return -1;
     const uint64_t total = (uint64_t)grid * per_wg;
     // segments: (workgroup, bin) pairs in bin-major order, each its records rounded up to whole generations
     std::vector<uint64_t> base((uint64_t)grid * nb);
@@ -152,11 +155,14 @@ extern "C" int stage_selftest(uint32_t nb, uint32_t per_wg, uint32_t skew, uint3
         return -1;
     }
     if (kb == 16)
-        hipLaunchKernelGGL((k_stage<16, uint32_t>), dim3(grid), dim3(kBlockT), 0, 0, nb, per_wg, skew, out_id, out_w,
-                           d_base, d_cap, err);
+        hipLaunchKernelGGL((k_stage<16, 2, uint32_t, kMaxBins>), dim3(grid), dim3(kBlockT), 0, 0, nb, per_wg, skew, out_id,
+                           out_w, d_base, d_cap, err);
+    else if (kb == 32)
+        hipLaunchKernelGGL((k_stage<32, 1, uint32_t, kMaxBins>), dim3(grid), dim3(kBlockT), 0, 0, nb, per_wg, skew, out_id,
+                           out_w, d_base, d_cap, err);
     else
-        hipLaunchKernelGGL((k_stage<32, uint16_t>), dim3(grid), dim3(kBlockT), 0, 0, nb, per_wg, skew, out_id, out_w,
-                           d_base, d_cap, err);
+        hipLaunchKernelGGL((k_stage<64, 2, uint16_t, 96>), dim3(grid), dim3(kBlockT), 0, 0, nb, per_wg, skew, out_id,
+                           out_w, d_base, d_cap, err);
     uint32_t hx[8] = {};
     std::vector<uint32_t> hid(slots + 1);
     std::vector<unsigned long long> hw(slots + 1);

@@ -44,6 +44,27 @@ def test_group_on_one_device_equals_oracle(oracle, idx, n, P):
     assert again == stats
 
 
+@pytest.mark.parametrize("gather", ["compact", "whole"])
+@pytest.mark.parametrize("P", [2, 3, 5])
+@pytest.mark.parametrize("idx,n", [(3, 100_003), (5, 1 << 15), (2, 40_000)])
+def test_group_dense_exchange_forms_equal_oracle(oracle, idx, n, P, gather):
+    """Dense rounds at P > 1 exchange either every block's whole slice of new
+    words or, forced here for every dense round, the blocks' tile bitmaps and
+    packed non-zero words (gossip_dist.hip compact_gather: bitmap all-gather,
+    offsets from the tiles' popcount prefix, packed words as send / recv
+    pairs, expansion into the gather buffer) -- on blocks that do not end on a
+    tile boundary (n = 100,003) and a short last block (P = 3, 5).  Both forms
+    give the oracle's run."""
+    w = config(idx, n, pick=oracle.pick_origins)
+    rp, col = oracle.gen_workload(w)
+    ref = oracle.simulate_workload(w, rp, col)
+    stats, seen, reps, again = _run_group(w, [0] * P, tuning={"gather_permille": 1000 if gather == "compact" else 0})
+    assert stats == ref["stats"]
+    assert np.array_equal(seen, ref["seen"])
+    assert np.array_equal(reps, ref["reports"])
+    assert again == stats
+
+
 @pytest.mark.parametrize("idx,n", [(2, 1 << 15), (5, 1 << 15)])
 def test_group_one_part_rccl_equals_oracle(oracle, idx, n):
     """ncclCommInitAll over device 0: every collective of the driver through RCCL."""

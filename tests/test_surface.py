@@ -19,7 +19,7 @@ GOLDEN = REPO / "tests" / "golden"
 def surf():
     L = C.CDLL(str(BUILD / "libgossip_surface.so"))
     for name in ("gossip_surface_netcfg", "gossip_surface_message", "gossip_surface_hash", "gossip_surface_register",
-                 "gossip_surface_dead_node", "gossip_surface_log"):
+                 "gossip_surface_dead_node", "gossip_surface_log", "gossip_surface_seed"):
         getattr(L, name).restype = C.c_int
     return L
 
@@ -106,3 +106,26 @@ def test_reference_main_compiles_against_dropin_headers(tmp_path):
                         f"-Wl,-rpath,{BUILD}", "-o", str(exe)], input=src, capture_output=True)
     assert r.returncode == 0, r.stderr.decode()
     assert exe.exists()
+
+
+def test_seed_registry_first_insert_lastseen_and_removal_print(surf, capfd):
+    """SeedNode as seed.cpp:109-178 has it: peerList is a map keyed by
+    (ip, port), so a repeated registration keeps the key -- and the key's
+    lastSeen, which getPeerList reports -- from the first insertion
+    (seed.cpp:155,173-175); a dead_node report erases the key and prints
+    "Removed dead peer" to stdout unconditionally (seed.cpp:164); a later
+    registration inserts it afresh."""
+    a, b = json.dumps({"ip": "127.0.0.1", "port": 5001, "type": "register"}), \
+        json.dumps({"ip": "127.0.0.1", "port": 5002, "type": "register"})
+    dead = json.dumps({"dead_ip": "127.0.0.1", "dead_port": 5001, "type": "dead_node"})
+    ops = f"100 {a}\n105 {b}\n110 {a}\n115 {dead}\n120 {a}\n"
+    out = _call(surf.gossip_surface_seed, ops.encode()).split("\n")
+    lists = [json.loads(x)["peers"] for x in out if x.startswith("{")]
+    assert lists[0] == [{"ip": "127.0.0.1", "lastSeen": 100, "port": 5001}]
+    assert lists[1] == [{"ip": "127.0.0.1", "lastSeen": 100, "port": 5001},
+                        {"ip": "127.0.0.1", "lastSeen": 105, "port": 5002}]
+    assert lists[2] == lists[1]  # re-registration at 110: the key (and its lastSeen) stays
+    assert out[3] == ""          # dead_node: no response
+    assert lists[3] == [{"ip": "127.0.0.1", "lastSeen": 105, "port": 5002},
+                        {"ip": "127.0.0.1", "lastSeen": 120, "port": 5001}]
+    assert "Removed dead peer: 127.0.0.1:5001" in capfd.readouterr().out
