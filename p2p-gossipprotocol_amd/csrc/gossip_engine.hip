@@ -213,6 +213,9 @@ struct gossip_ctx {
     uint32_t dgone_next = 0;      // first round whose deaths dgone does not count yet
     bool cur_defer = false;       // this round defers: advance() folds nx into seen
     bool full_liveness = false;  // "full_liveness": ping every edge each ping round (A/B against closed form)
+    uint64_t cur_missing = 0;    // (peer, message) pairs still missing at the round's push start (round_begin)
+    bool needy_skip = true;      // "bin_needy_skip": binned rounds with over one missing pair per peer skip the
+                                 // apply's needy test
     uint64_t* seg = nullptr;     // sparse push: per-destination record segments (world x chunk records)
     unsigned long long* d_counts = nullptr;  // records per destination rank
     uint64_t* h_counts = nullptr;            // pinned copy
@@ -254,6 +257,18 @@ struct gossip_ctx {
     uint32_t* tiny_result = nullptr;       // device [rounds, buffers swapped]
     uint32_t* d_inj_round = nullptr;       // the sorted schedule rounds on the device
     uint32_t* d_kill_round = nullptr;
+
+    // recorded schedule (gossip_run on one partition): the host decisions of a run depend only on the
+    // round's stats, and a rerun from reset of the same inputs produces the same stats, so the first run
+    // records each round's stat sums and the next ones issue every round without waiting for its stats
+    // (replay_run); the device still computes and stores every round's stats, and they are checked
+    // against the recording at the end.  Anything that could change a run drops the recording.
+    bool replay_req = true;                // "replay": 0 never
+    bool recording = false, replaying = false, rec_valid = false;
+    std::vector<DevStats> rec_st;          // per round: the decoded stat sums
+    std::vector<uint32_t> rec_lst;         // per round: entries its needy list received
+    DevStats* d_hist = nullptr;            // replay: every round's kStatLines stat lines
+    uint32_t hist_cap = 0, rep_round = 0;
 
     // library-driven multi-GPU rounds (gossip_dist.hip): the driver that issues
     // this ctx's collectives; owned here for gossip_comm_init, by the group otherwise
@@ -479,6 +494,8 @@ void free_graph(gossip_ctx* c) {
     c->graph_ready = false;
 }
 
+void rec_drop(gossip_ctx* c);  // forget a recorded schedule (gossip_run)
+
 uint64_t tact_bytes(const gossip_ctx* c) { return (((c->n_local + 63) / 64 + 63) / 64 + 1) * 8; }
 
 RoundArgs make_args(gossip_ctx* c) {
@@ -587,6 +604,7 @@ gossip_status install_graph(gossip_ctx* c, uint64_t* d_rp, uint32_t* d_col, uint
     HIPCHK(hipMalloc((void**)&c->first2, (c->n_local + 1) * sizeof(uint64_t)));
     HIPCHK(launch_first2(c->rp, c->col, c->n_local, c->first2, c->stream));
     c->graph_ready = true;
+    rec_drop(c);  // a new overlay
     return GOSSIP_OK;
 }
 
@@ -679,7 +697,7 @@ BinArgs bin_args(const gossip_ctx* c, bool noskip, uint32_t src_side) {
     return BinArgs{s.bins,      s.n_bins,   s.cb_src,    s.cb_run,   s.cb_grp,   s.n_binned, s.chunk_begin,
                    s.n_chunks,  s.chunk,    s.units,     s.xcd_units, s.bdst,    s.val,      s.bin_words,
                    s.dummy,     noskip ? 1u : 0u, s.n_runs ? s.n_runs - 1 : 0, s.ap_run, s.ap_grp,
-                   c->bin_stream ? 1u : 0u, s.deg, src_side};
+                   c->bin_stream ? 1u : 0u, s.deg, src_side, 1u};
 }
 
 gossip_status tune_val(gossip_ctx* c) {
@@ -1010,6 +1028,7 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
         const uint64_t total = injected * peers;
         missing = total > have ? total - have : 0;
     }
+    c->cur_missing = missing;
     if (!remote && pull_ok && c->bins_ready && requested == GOSSIP_MODE_AUTO) {
         if (c->cfg.flags & GOSSIP_FLAG_FORCE_BIN) {
             pull = bin = true;
@@ -1314,7 +1333,9 @@ gossip_status round_compute(gossip_ctx* c) {
     if (c->last_pull && a.dead_mode && !a.dgone)  // else the per-source counters give the source side
         HIPCHK(timed(c, "src_count", [&] { return launch_src_count(a, pw, c->stream); }));
     if (c->last_bin) {
-        const BinArgs b = bin_args(c, c->bins_first, src_stats(c));
+        BinArgs b = bin_args(c, c->bins_first, src_stats(c));
+        // every bin is needy while more than one (peer, message) pair per peer is missing: no check pass
+        b.needy_check = c->cur_missing > c->n_local && c->needy_skip ? 0u : 1u;
         HIPCHK(timed(c, "bin_scatter", [&] { return launch_bin_scatter(a, b, pw, c->stream); }));
         HIPCHK(timed(c, "bin_apply", [&] { return launch_bin_apply(a, b, pw, c->stream); }));
         c->bins_first = false;
@@ -1345,6 +1366,17 @@ gossip_status round_compute(gossip_ctx* c) {
 }
 
 gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative) {
+    if (c->replaying && c->last_st_round != c->round) {  // the recorded sums; the lines go to the history
+        HIPCHK(flush_zero(c));
+        HIPCHK(hipMemcpyAsync(c->d_hist + (uint64_t)c->rep_round * kStatLines, c->st, kStatLines * sizeof(DevStats),
+                              hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(queue_zero(c, c->st, kStatLines * sizeof(DevStats)));
+        c->last_st = c->rec_st[c->rep_round];
+        c->lst_out_n = c->rec_lst[c->rep_round];
+        c->last_st_round = c->round;
+        for (int w = 0; w < kMaxWords; ++w) c->flight[w] = c->last_st.fresh_or[w];
+        c->flight_round = c->round;
+    }
     if (c->last_st_round != c->round) {  // read once per round, then the lines are re-zeroed for the next
         HIPCHK(flush_zero(c));
         HIPCHK(hipMemcpyAsync(c->h_st, c->st, kStatLines * sizeof(DevStats), hipMemcpyDeviceToHost, c->stream));
@@ -1371,6 +1403,10 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
                 dst[f] = f < kStatSums ? dst[f] + src[l * kStatFields + f] : dst[f] | src[l * kStatFields + f];
         c->last_st = sum;
         c->last_st_round = c->round;
+        if (c->recording) {
+            c->rec_st.push_back(sum);
+            c->rec_lst.push_back(c->cur_lst_out >= 0 ? c->lst_out_n : 0u);
+        }
         // the bits of the round's receipts: the next round's new words (with its injections)
         for (int w = 0; w < kMaxWords; ++w) c->flight[w] = sum.fresh_or[w];
         c->flight_round = c->round;
@@ -1510,6 +1546,83 @@ gossip_status advance(gossip_ctx* c, uint64_t fresh_global) {
     return GOSSIP_OK;
 }
 
+// the host decisions of a run may be replayed from its recording: one partition, nothing that reads device
+// state mid-round (re-bootstrap reads the report count, join churn its restarts), no timing
+bool replay_eligible(const gossip_ctx* c) {
+    return c->replay_req && !c->timing && c->world <= 1 && !c->dist && !c->gather && c->n_local == c->n &&
+           !c->cfg.extra_cap && !c->cfg.rejoin_threshold && c->graph_ready && c->has_schedule;
+}
+
+void rec_drop(gossip_ctx* c) {
+    c->rec_valid = c->recording = false;
+    c->rec_st.clear();
+    c->rec_lst.clear();
+}
+
+gossip_status step_round(gossip_ctx* c, gossip_round_stats* out);
+
+// Every round of the recorded run issued back to back (no host wait between rounds), each round's stat lines
+// copied to d_hist; then one read of them, checked field by field against the recording.
+gossip_status replay_run(gossip_ctx* c, gossip_round_stats* per_round, uint32_t cap, uint32_t* rounds) {
+    const uint32_t R = (uint32_t)c->rec_st.size();
+    if (c->hist_cap < R) {
+        hipFree(c->d_hist);
+        c->d_hist = nullptr;
+        c->hist_cap = 0;
+        HIPCHK(hipMalloc((void**)&c->d_hist, (uint64_t)R * kStatLines * sizeof(DevStats)));
+        c->hist_cap = R;
+    }
+    c->replaying = true;
+    uint32_t k = 0;
+    gossip_status s = GOSSIP_OK;
+    bool any_pb = false;
+    for (c->rep_round = 0; c->rep_round < R && !c->finished; ++c->rep_round) {
+        gossip_round_stats st;
+        s = step_round(c, &st);
+        if (s < 0) break;
+        any_pb |= c->cur_pb;
+        if (per_round && k < cap) per_round[k] = st;
+        ++k;
+    }
+    c->replaying = false;
+    if (s < 0) {
+        rec_drop(c);
+        return s;
+    }
+    std::vector<DevStats> h((uint64_t)R * kStatLines);
+    HIPCHK(hipMemcpyAsync(h.data(), c->d_hist, h.size() * sizeof(DevStats), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    bool same = k == R && c->finished;
+    for (uint32_t r = 0; same && r < R; ++r) {
+        DevStats sum{};
+        const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&h[(uint64_t)r * kStatLines]);
+        unsigned long long* dst = reinterpret_cast<unsigned long long*>(&sum);
+        for (int l = 0; l < kStatLines; ++l)
+            for (int f = 0; f < kStatFields; ++f)
+                dst[f] = f < kStatSums ? dst[f] + src[l * kStatFields + f] : dst[f] | src[l * kStatFields + f];
+        // every result field (the measurement counters -- heavy-row edges scanned, pull edges scanned and
+        // gathers, atomics issued, diag -- depend on timing: an early exit racing another chunk's find, a
+        // plain read racing another thread's atomic)
+        const unsigned long long* x = reinterpret_cast<const unsigned long long*>(&sum);
+        const unsigned long long* y = reinterpret_cast<const unsigned long long*>(&c->rec_st[r]);
+        for (int f = 0; same && f < kStatFields; ++f)
+            same = f == 11 || f == 14 || f == 15 || f == 18 || f == 19 || x[f] == y[f];
+    }
+    if (same && any_pb) {
+        uint32_t e = 0;
+        HIPCHK(hipMemcpy(&e, c->pb.err, sizeof(e), hipMemcpyDeviceToHost));
+        if (e & 4u) return fail(GOSSIP_ESTALL, "blocked round: a record-staging wave stalled past its bound");
+        if (e) return fail(GOSSIP_EOVERFLOW, "blocked round: a record region overflowed");
+    }
+    if (!same) {
+        rec_drop(c);
+        return fail(GOSSIP_ESTATE, "a replayed run's device stats differ from its recording");
+    }
+    c->kbytes["#replayed_runs"] += 1.0;  // (gossip_kernel_bytes: how many runs issued from their recording)
+    if (rounds) *rounds = k;
+    return GOSSIP_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1637,6 +1750,7 @@ gossip_status gossip_set_tuning(gossip_ctx* c, const char* key, int64_t value) {
     if (!c || !key) return fail(GOSSIP_EINVAL, "null argument");
     const std::string k(key);
     const uint32_t u = value < 0 ? 0u : (uint32_t)std::min<int64_t>(value, 0xFFFFFFFFll);
+    rec_drop(c);  // (any option may change the schedule the recording holds)
     if (k == "tiny") c->tiny_off = value == 0;
     else if (k == "full_liveness") c->full_liveness = value != 0;
     else if (k == "defer_permille") c->defer_pm = value < 0 ? kDeferAuto : u;
@@ -1660,6 +1774,8 @@ gossip_status gossip_set_tuning(gossip_ctx* c, const char* key, int64_t value) {
     }
     else if (k == "blocked_push_permille") c->pb_lo_pm = value < 0 ? kPbLoPermille : u;
     else if (k == "list_cap") c->list_cap_req = u;
+    else if (k == "bin_needy_skip") c->needy_skip = value != 0;
+    else if (k == "replay") c->replay_req = value != 0;
     else if (k == "gather_permille") c->gather_pm = value < 0 ? kGatherPermille : u;
     else return fail(GOSSIP_EINVAL, "unknown tuning option: " + k);
     return GOSSIP_OK;
@@ -1832,6 +1948,7 @@ gossip_status gossip_inject(gossip_ctx* c, const uint32_t* origin, const uint32_
     HIPCHK(hipMalloc((void**)&c->d_inj_round, n_msgs * sizeof(uint32_t)));
     HIPCHK(hipMemcpy(c->d_inj_round, c->inj_round_sorted.data(), n_msgs * sizeof(uint32_t), hipMemcpyHostToDevice));
     c->has_schedule = true;
+    rec_drop(c);
     return GOSSIP_OK;
 }
 
@@ -1843,6 +1960,7 @@ gossip_status gossip_schedule_kills(gossip_ctx* c, const uint32_t* peer, const u
         k[i] = {round[i], peer[i]};
     }
     std::sort(k.begin(), k.end());
+    rec_drop(c);
     c->kill_round_sorted.resize(n);
     std::vector<uint32_t> p(n + 1);
     for (uint32_t i = 0; i < n; ++i) {
@@ -1982,6 +2100,14 @@ gossip_status gossip_step(gossip_ctx* c, gossip_round_stats* out) {
     if (set_dev(c)) return GOSSIP_EHIP;
     if (c->dist) return gossip::dist_step_ctx(c, out);  // the library's own collectives (gossip_comm_init)
     if (c->world > 1) return fail(GOSSIP_ESTATE, "partitioned ctx: use gossip_comm_init or gossip_round_*");
+    c->recording = false;  // (a run driven round by round records nothing)
+    return step_round(c, out);
+}
+
+}  // extern "C"
+
+namespace {
+gossip_status step_round(gossip_ctx* c, gossip_round_stats* out) {
     TraceRange tr("gossip round %u", c->round);
     gossip_status s = round_begin(c, false, GOSSIP_MODE_AUTO, nullptr);
     if (!s) s = round_compute(c);
@@ -1992,6 +2118,9 @@ gossip_status gossip_step(gossip_ctx* c, gossip_round_stats* out) {
     if ((s = advance(c, st.new_receipts))) return s;
     return c->finished ? 1 : 0;
 }
+}  // namespace
+
+extern "C" {
 
 gossip_status gossip_run(gossip_ctx* c, gossip_round_stats* per_round, uint32_t cap, uint32_t* rounds) {
     if (!c) return fail(GOSSIP_EINVAL, "null ctx");
@@ -1999,14 +2128,38 @@ gossip_status gossip_run(gossip_ctx* c, gossip_round_stats* per_round, uint32_t 
         if (set_dev(c)) return GOSSIP_EHIP;
         return tiny_run(c, per_round, cap, rounds);
     }
+    if (c->dist || c->world > 1) {
+        uint32_t k = 0;
+        while (!c->finished) {
+            gossip_round_stats st;
+            gossip_status s = gossip_step(c, &st);
+            if (s < 0) return s;
+            if (per_round && k < cap) per_round[k] = st;
+            ++k;
+        }
+        if (rounds) *rounds = k;
+        return GOSSIP_OK;
+    }
+    if (set_dev(c)) return GOSSIP_EHIP;
+    const bool fresh = c->round == 0 && !c->finished && replay_eligible(c);
+    if (fresh && c->rec_valid) return replay_run(c, per_round, cap, rounds);
+    if (fresh) {
+        rec_drop(c);
+        c->recording = true;
+    }
     uint32_t k = 0;
     while (!c->finished) {
         gossip_round_stats st;
-        gossip_status s = gossip_step(c, &st);
-        if (s < 0) return s;
+        gossip_status s = step_round(c, &st);
+        if (s < 0) {
+            rec_drop(c);
+            return s;
+        }
         if (per_round && k < cap) per_round[k] = st;
         ++k;
     }
+    c->rec_valid = c->recording;
+    c->recording = false;
     if (rounds) *rounds = k;
     return GOSSIP_OK;
 }

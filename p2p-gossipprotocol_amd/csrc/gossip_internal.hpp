@@ -100,6 +100,11 @@ struct BinArgs {
     const uint32_t* ap_grp;       // per 64-slot group: runs that start before the group
     uint32_t stream;              // 1: streamed layout, 0: val in slot order (k_bin_scatter_*)
     const uint32_t* deg;          // per owned peer: its row length (source-side stats booked by the apply)
+    uint32_t needy_check;         // 1: the apply first tests whether any peer of the bin can still learn
+                                  // something (a pass over the bin's seen words) and skips its slots if not;
+                                  // 0 on rounds with more than one missing pair per peer, where every bin is
+                                  // needy and the pass only costs a read of seen (2 GB at config 4) and a
+                                  // round trip per bin
     uint32_t src_stats;           // 1: the scatter books the source side of the round's pushes (its first
                                   // unit of each chunk, row bounds loaded after the slice); 0: the apply
                                   // does, for its bin's peers (bin_src_stats), and the scatter's staging is

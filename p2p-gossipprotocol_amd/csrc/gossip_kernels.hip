@@ -1245,9 +1245,10 @@ __global__ __launch_bounds__(kB) void k_bin_apply(RoundArgs a, BinArgs b, uint32
     // a.fold: the previous (deferred) push round's receipts are this round's new words and not yet
     // in seen; every peer of the bin (heavy rows included) gets seen |= nw here, before k_pull_heavy
     auto pend = [&](uint32_t i) { return a.fold ? a.nw[v0 * W + i] : 0ull; };
-    bool needy = false;
+    bool needy = !b.needy_check;
     for (uint32_t i = threadIdx.x; i < nv * W; i += kB) {
         acc_s[i] = 0ull;
+        if (!b.needy_check) continue;
         const bool va = !a.dead_mode || bit_alive(a.alive, (uint32_t)(a.begin + v0 + i / W));
         needy |= va && (injm(a, i % W) & ~(a.seen[v0 * W + i] | pend(i))) != 0;
     }
@@ -1436,9 +1437,10 @@ __global__ __launch_bounds__(kB) void k_bin_apply_runs(RoundArgs a, BinArgs b, u
         __syncthreads();  // the previous bin is done with acc_s (and cov_s is initialised)
         if (!b.src_stats) bin_src_stats<W, kB>(a, b, v0, nv, wd, cov_s, acc);
         auto pend = [&](uint32_t i) { return a.fold ? a.nw[v0 * W + i] : 0ull; };
-        bool needy = false;
+        bool needy = !b.needy_check;
         for (uint32_t i = threadIdx.x; i < nv * W; i += kB) {
             acc_s[i] = 0ull;
+            if (!b.needy_check) continue;
             const bool va = !a.dead_mode || bit_alive(a.alive, (uint32_t)(a.begin + v0 + i / W));
             needy |= va && (injm(a, i % W) & ~(a.seen[v0 * W + i] | pend(i))) != 0;
         }
@@ -2118,22 +2120,26 @@ __device__ __forceinline__ void retire_peer(const RoundArgs& a, uint32_t v, uint
     }
 }
 
+// One lane per peer (a wave covers two words of the alive bitset): each peer alive at the start of the
+// round draws its churn number, the wave's ballot of the deaths clears both words at once.  (Round 3 ran one
+// thread per word, drawing for its alive peers in turn: a chain of up to 32 Philox evaluations per thread,
+// 0.14 ms per round at config 5.)
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_churn(RoundArgs a, uint32_t wd, uint32_t seed, uint32_t thr) {
     Acc acc;
-    const uint64_t n_words = (a.n_global + 31) >> 5;
-    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n_words; i += (uint64_t)gridDim.x * kBlock) {
-        const uint32_t word = a.alive[i];
-        if (!word) continue;
-        uint32_t dead = 0;
-        for (uint32_t x = word; x; x &= x - 1) {
-            const uint32_t b = (uint32_t)__builtin_ctz(x);
-            const uint32_t v = (uint32_t)(i * 32 + b);
-            if (philox4x32_10(P_CHURN, a.round, 0, 0, seed, v).x < thr) dead |= 1u << b;
+    const int lane = threadIdx.x & 63;
+    const uint64_t n_pad = (a.n_global + 63) & ~63ull;
+    for (uint64_t v = (uint64_t)blockIdx.x * kBlock + threadIdx.x; v < n_pad; v += (uint64_t)gridDim.x * kBlock) {
+        const uint32_t word = v < a.n_global ? a.alive[v >> 5] : 0u;
+        const bool live = (word >> (v & 31)) & 1u;
+        const bool die = live && philox4x32_10(P_CHURN, a.round, 0, 0, seed, (uint32_t)v).x < thr;
+        const unsigned long long dead = __ballot(die);
+        if (!dead) continue;  // wave-uniform
+        if ((lane & 31) == 0) {  // lanes 0 and 32: their words
+            const uint32_t dw = (uint32_t)(dead >> (lane & 32));
+            if (dw) a.alive[v >> 5] = word & ~dw;
         }
-        if (!dead) continue;
-        a.alive[i] = word & ~dead;
-        for (uint32_t x = dead; x; x &= x - 1) retire_peer<W>(a, (uint32_t)(i * 32 + __builtin_ctz(x)), wd, acc);
+        if (die) retire_peer<W>(a, (uint32_t)v, wd, acc);
     }
     flush(acc, a.st);
 }
@@ -2383,7 +2389,7 @@ static inline uint32_t wp_of(uint32_t w) { return w & 0xFFFFu; }
 static inline uint32_t wd_of(uint32_t w) { return w >> 16; }
 
 hipError_t launch_churn(const RoundArgs& a, uint32_t W_, uint32_t seed, uint32_t threshold, hipStream_t s) {
-    const unsigned g = grid_for((a.n_global + 31) / 32, kBlock);
+    const unsigned g = (unsigned)std::min<uint64_t>(grid_for(a.n_global, kBlock), 16384);
     GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_churn<W>, dim3(g), dim3(kBlock), 0, s, a, wd_of(W_), seed,
                                                    threshold));
     return hipGetLastError();
@@ -2584,8 +2590,9 @@ hipError_t launch_bin_apply(const RoundArgs& a, const BinArgs& b, uint32_t W_, h
             GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_apply_runs<W, kBinWords, 1024>),
                                                            dim3(sgrid), dim3(1024), 0, s, a, b, wd));
         } else {
-            GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_apply_runs<W, kBinWords / 2, kBlock>),
-                                                           dim3(sgrid), dim3(kBlock), 0, s, a, b, wd));
+            // 72 KB accumulators: two 8-wave workgroups per CU, one's per-bin phases under the other's slots
+            GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_apply_runs<W, kBinWords / 2, 512>),
+                                                           dim3(sgrid), dim3(512), 0, s, a, b, wd));
         }
         return hipGetLastError();
     }

@@ -339,7 +339,8 @@ _VARIANTS = {"defer_1": ({"defer_permille": 1}, {"blocked": "off"}), "stream": (
              "small_bins": ({"bin_words": 4096, "bin_chunk": 2048}, {}), "apply_src": ({"src_stats": 0}, {}),
              "heavy_64": ({"heavy_degree": 64, "heavy_chunk": 128}, {}), "all_pull": ({}, {"bin_permille": 100000}),
              "blocked_wide": ({}, {"blocked_permille": 1000}), "pull_step_2": ({"pull_step": 2}, {}),
-             "no_lists": ({"list_rounds": 0}, {})}
+             "no_lists": ({"list_rounds": 0}, {}), "needy_test": ({"bin_needy_skip": 0}, {}),
+             "stream_needy_test": ({"bin_stream": 1, "bin_needy_skip": 0}, {})}
 
 
 @pytest.mark.parametrize("variant", sorted(_VARIANTS))
@@ -532,3 +533,36 @@ def test_tuning_rejects_bad_values_and_huge_max_rounds_runs(oracle):
         e.reset()
         _compare(e, ref, w)
         assert e.kernel_time("tiny")[1] == 0
+
+
+@pytest.mark.parametrize("idx,n", [(2, 1 << 18), (3, 1 << 18), (5, 1 << 16), (4, 1 << 18)])
+def test_recorded_schedule_replay(oracle, idx, n):
+    """gossip_run records the first run's per-round stats; a rerun from reset
+    of the same inputs issues every round without waiting for its stats and
+    checks the device's stats against the recording at the end.  Both runs
+    give the oracle's results; a changed option drops the recording (the next
+    run records again), and "replay" 0 never replays."""
+    w = config(idx, n, pick=oracle.pick_origins)
+    rp, col = oracle.gen_workload(w)
+    ref = oracle.simulate_workload(w, rp, col)
+    with _engine(w) as e:
+        e.build_graph()
+        e.inject(w.origins, w.inject_rounds)
+        if w.kills:
+            e.schedule_kills([k[0] for k in w.kills], [k[1] for k in w.kills])
+        for i in range(3):
+            e.reset()
+            _compare(e, ref, w)
+            assert e.kernel_bytes("#replayed_runs") == i  # run 0 records, runs 1 and 2 replay
+        e.set_tuning("pull_step", 2)  # drops the recording
+        e.reset()
+        _compare(e, ref, w)
+        assert e.kernel_bytes("#replayed_runs") == 2
+        e.reset()
+        _compare(e, ref, w)
+        assert e.kernel_bytes("#replayed_runs") == 3
+        e.set_tuning("replay", 0)
+        for _ in range(2):
+            e.reset()
+            _compare(e, ref, w)
+        assert e.kernel_bytes("#replayed_runs") == 3
