@@ -784,11 +784,13 @@ gossip_status prepare_bins(gossip_ctx* c) {
     free_pb(&c->pb);
     c->pb_ready = false;
     if (c->symmetric && !(c->cfg.flags & GOSSIP_FLAG_NO_BIN) && c->n_edges) {
-        // streamed layout while the slot array fits the 256 MB MALL with room to spare: its runs are then
-        // re-read from MALL, not HBM (config 2: 6.59 vs 7.04 ms per step); beyond that the slot layout's
-        // sequential apply wins (config 4: 62.6 vs 64.5 ms, config 3: 6.03 vs 6.88 ms)
-        c->bin_stream = c->bin_stream_req >= 0 ? c->bin_stream_req != 0
-                                               : (uint64_t)c->n_edges * 8ull * c->Wp <= kStreamSlotBytes;
+        // the streamed layout (values in cb order: the scatter writes front to back, the apply reads runs) at
+        // every size since round 4.  Round 2 kept it for slot arrays under 128 MB (config 4: 62.6 vs 64.5 ms
+        // per step for the slot layout); since its scatter's whole-line pieces and its apply's pipelined run
+        // loads it wins everywhere (round 4, alternated on one box: config 4 49.5 vs 51.8 ms per step, config 5
+        // 25.5-25.9 vs 26.3-27.2, config 3 4.87-5.09 vs 5.24-5.34; config 4's dense rounds: scatter 4.4 ms,
+        // no partial-sector stores, no allocation trials).  "bin_stream" 0 keeps the slot layout (A/B, tests).
+        c->bin_stream = c->bin_stream_req != 0;
         std::string err;
         const hipError_t e = build_bins(c->rp, c->col, c->n_local, c->n, c->n_edges, c->heavy, c->Wp, c->bin_stream,
                                         c->bin_words_req, c->bin_chunk_req, c->stream, &c->bins, &err);

@@ -417,8 +417,6 @@ constexpr uint32_t kPullPermille = 60;
 // its whole slice of new words while the round's frontier is below this per-mille of the peers
 // (gossip_dist.hip; "gather_permille": 0 never, 1000 always)
 constexpr uint32_t kGatherPermille = 600;
-// the streamed bin layout is chosen while the slot array (8 B x edges x padded words) is at most this
-constexpr uint64_t kStreamSlotBytes = 128ull << 20;
 
 // ---- overlay generator (gossip_graph.hip) ----
 // Builds the owned rows of the powerlaw overlay on the device.  On success

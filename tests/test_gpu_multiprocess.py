@@ -1,0 +1,53 @@
+"""The one-process-per-GPU deployment (bench.py --gpus N under torchrun:
+gossip_comm_init, libgossip_hip issuing every round's RCCL collectives) with
+world size > 1, on the one GPU a test box has: N ranks, each its own process,
+all on device 0.  If RCCL refuses ranks that share a device the test skips and
+says so; otherwise every rank's global stats, the merged reports and the
+blocks' seen words must equal the single-partition oracle run (P-invariance,
+SURVEY.md 8(e)), in both dense-exchange forms (whole slices / tile bitmap and
+packed words)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from gossip_hip.workloads import config
+
+pytestmark = pytest.mark.gpu
+REPO = Path(__file__).resolve().parent.parent
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("gather", [0, 1000])
+@pytest.mark.parametrize("world,idx,n", [(2, 3, 100_003), (3, 5, 1 << 15), (2, 2, 40_000)])
+def test_comm_init_world_n_on_one_gpu(oracle, tmp_path, world, idx, n, gather):
+    w = config(idx, n, pick=oracle.pick_origins)
+    rp, col = oracle.gen_workload(w)
+    ref = oracle.simulate_workload(w, rp, col)
+    out = tmp_path / "res.json"
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           str(REPO / "tests" / "gpu_support" / "rank_run.py"), "--config", str(idx), "--peers", str(n),
+           "--gather", str(gather), "--out", str(out)]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=150)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    ranks = json.loads(out.read_text())["ranks"]
+    if any(r["status"] != "ok" for r in ranks):
+        pytest.skip("RCCL refused ranks on one device: " + "; ".join(r["status"] for r in ranks))
+    for r in ranks:
+        assert r["stats"] == ref["stats"]
+        assert r["reports"] == ref["reports"].tolist()
+    assert np.array_equal(np.load(out.with_suffix(".npy")), ref["seen"])
