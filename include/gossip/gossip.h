@@ -331,7 +331,9 @@ gossip_status gossip_kernel_bytes(gossip_ctx* ctx, const char* kernel, double* b
  * a tile bitmap and the packed non-zero new words instead of every word;
  * -1 default 600, 0 never, 1000 always), "bin_needy_skip" (binned rounds
  * with over one missing pair per peer skip the apply's per-bin needy test:
- * 1 default, 0 always test).  Layout keys
+ * 1 default, 0 always test), "apply_pipe" (the streamed apply's load
+ * pipeline shape, 0-3, A/B), "replay" (0: gossip_run never replays a
+ * recorded schedule).  Layout keys
  * apply at the next gossip_build_graph / gossip_load_csr ("list_cap": at the
  * next chain of needy-list rounds, never inside one).  GOSSIP_EINVAL: unknown key. */
 gossip_status gossip_set_tuning(gossip_ctx* ctx, const char* key, int64_t value);

@@ -214,6 +214,7 @@ struct gossip_ctx {
     bool cur_defer = false;       // this round defers: advance() folds nx into seen
     bool full_liveness = false;  // "full_liveness": ping every edge each ping round (A/B against closed form)
     uint64_t cur_missing = 0;    // (peer, message) pairs still missing at the round's push start (round_begin)
+    uint32_t apply_pipe = 0;     // "apply_pipe": the streamed apply's pipeline shape (0-3, A/B)
     bool needy_skip = true;      // "bin_needy_skip": binned rounds with over one missing pair per peer skip the
                                  // apply's needy test
     uint64_t* seg = nullptr;     // sparse push: per-destination record segments (world x chunk records)
@@ -697,7 +698,7 @@ BinArgs bin_args(const gossip_ctx* c, bool noskip, uint32_t src_side) {
     return BinArgs{s.bins,      s.n_bins,   s.cb_src,    s.cb_run,   s.cb_grp,   s.n_binned, s.chunk_begin,
                    s.n_chunks,  s.chunk,    s.units,     s.xcd_units, s.bdst,    s.val,      s.bin_words,
                    s.dummy,     noskip ? 1u : 0u, s.n_runs ? s.n_runs - 1 : 0, s.ap_run, s.ap_grp,
-                   c->bin_stream ? 1u : 0u, s.deg, src_side, 1u};
+                   c->bin_stream ? 1u : 0u, s.deg, src_side, c->apply_pipe, 1u};
 }
 
 gossip_status tune_val(gossip_ctx* c) {
@@ -1778,6 +1779,10 @@ gossip_status gossip_set_tuning(gossip_ctx* c, const char* key, int64_t value) {
     else if (k == "list_cap") c->list_cap_req = u;
     else if (k == "bin_needy_skip") c->needy_skip = value != 0;
     else if (k == "replay") c->replay_req = value != 0;
+    else if (k == "apply_pipe") {
+        if (value < 0 || value > 3) return fail(GOSSIP_EINVAL, "apply_pipe must be 0..3");
+        c->apply_pipe = (uint32_t)value;
+    }
     else if (k == "gather_permille") c->gather_pm = value < 0 ? kGatherPermille : u;
     else return fail(GOSSIP_EINVAL, "unknown tuning option: " + k);
     return GOSSIP_OK;

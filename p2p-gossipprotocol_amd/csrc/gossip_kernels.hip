@@ -1417,11 +1417,20 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_stream(RoundArgs a, BinAr
 // per-row sync, so that neighbouring bins walk their chunks together, was slower: 10.3-11.5 against
 // 9.6-9.8 ms per launch.)  The end of each bin is k_bin_apply's: test-and-set of its peers with plain
 // stores (and the fold of a deferred push round's words, a.fold).
-template <int W, int kWords, int kB>
+// Pipeline shape (kPipe, W = 1 only; others use 0): groups per stage kG, and how many iterations ahead
+// each load is issued -- bdst + ap_grp LA, ap_run LB, val LC (LA > LB > LC >= 1), kS = LA + 1 register sets.
+template <int W, int kPipe> struct ApplyPipe { static constexpr int kG = W == 1 ? 4 : W == 2 ? 2 : 1, LA = 3, LB = 2, LC = 1; };
+template <> struct ApplyPipe<1, 1> { static constexpr int kG = 2, LA = 5, LB = 3, LC = 1; };
+template <> struct ApplyPipe<1, 2> { static constexpr int kG = 2, LA = 5, LB = 4, LC = 2; };
+template <> struct ApplyPipe<1, 3> { static constexpr int kG = 3, LA = 4, LB = 2, LC = 1; };
+
+template <int W, int kWords, int kB, int kPipe = 0>
 __global__ __launch_bounds__(kB) void k_bin_apply_runs(RoundArgs a, BinArgs b, uint32_t wd) {
     constexpr int kWaves = kB / 64;
-    constexpr int kG = W == 1 ? 4 : W == 2 ? 2 : 1;  // groups per stage
-    constexpr int kS = 4;                             // stages in flight
+    constexpr int kG = ApplyPipe<W, kPipe>::kG;                      // groups per stage
+    constexpr int LA = ApplyPipe<W, kPipe>::LA, LB = ApplyPipe<W, kPipe>::LB, LC = ApplyPipe<W, kPipe>::LC;
+    constexpr int kS = LA + 1;                                        // stages in flight
+    static_assert(LA > LB && LB > LC && LC >= 1, "load lags");
     __shared__ unsigned long long acc_s[kWords];
     __shared__ unsigned int cov_s[64 * W];
     Acc acc;
@@ -1501,21 +1510,21 @@ __global__ __launch_bounds__(kB) void k_bin_apply_runs(RoundArgs a, BinArgs b, u
                         if (x[st][j][w]) atomicOr(&acc_s[dl * W + w], (unsigned long long)x[st][j][w]);  // ds_or_b64
                 }
             };
-            // prologue: stages 0..2 partly issued
-            ld_a(0, 0);
-            ld_a(1, 1);
-            ld_b(0, 0);
-            ld_a(2, 2);
-            ld_b(1, 1);
-            ld_c(0, 0);
+            // prologue: the loads of stages 0 .. LA - 1 issued as the loop would have issued them
+#pragma unroll
+            for (int t = -LA; t < 0; ++t) {
+                if (t + LA >= 0) ld_a((t + LA) % kS, (uint32_t)(t + LA));
+                if (t + LB >= 0) ld_b((t + LB) % kS, (uint32_t)(t + LB));
+                if (t + LC >= 0) ld_c((t + LC) % kS, (uint32_t)(t + LC));
+            }
             for (uint32_t i0 = 0; i0 < n_it; i0 += kS) {
 #pragma unroll
                 for (int k = 0; k < kS; ++k) {
                     const uint32_t i = i0 + k;
                     if (i >= n_it) break;  // wave-uniform
-                    ld_a((k + 3) % kS, i + 3);
-                    ld_b((k + 2) % kS, i + 2);
-                    ld_c((k + 1) % kS, i + 1);
+                    ld_a((k + LA) % kS, i + LA);
+                    ld_b((k + LB) % kS, i + LB);
+                    ld_c((k + LC) % kS, i + LC);
                     fold(k, i);
                 }
             }
@@ -2586,7 +2595,14 @@ hipError_t launch_bin_apply(const RoundArgs& a, const BinArgs& b, uint32_t W_, h
     const uint32_t wd = wd_of(W_);
     if (b.stream) {
         const unsigned sgrid = (unsigned)((b.n_bins + 7) / 8 * 8);  // whole groups of 8 (XCD-contiguous bins)
-        if (b.bin_words > kBinWords / 2) {
+        if (b.bin_words > kBinWords / 2 && wp_of(W_) == 1 && b.apply_pipe) {  // A/B pipeline shapes (one word)
+            if (b.apply_pipe == 1)
+                hipLaunchKernelGGL((k_bin_apply_runs<1, kBinWords, 1024, 1>), dim3(sgrid), dim3(1024), 0, s, a, b, wd);
+            else if (b.apply_pipe == 2)
+                hipLaunchKernelGGL((k_bin_apply_runs<1, kBinWords, 1024, 2>), dim3(sgrid), dim3(1024), 0, s, a, b, wd);
+            else
+                hipLaunchKernelGGL((k_bin_apply_runs<1, kBinWords, 1024, 3>), dim3(sgrid), dim3(1024), 0, s, a, b, wd);
+        } else if (b.bin_words > kBinWords / 2) {
             GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_apply_runs<W, kBinWords, 1024>),
                                                            dim3(sgrid), dim3(1024), 0, s, a, b, wd));
         } else {

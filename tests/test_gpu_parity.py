@@ -340,7 +340,9 @@ _VARIANTS = {"defer_1": ({"defer_permille": 1}, {"blocked": "off"}), "stream": (
              "heavy_64": ({"heavy_degree": 64, "heavy_chunk": 128}, {}), "all_pull": ({}, {"bin_permille": 100000}),
              "blocked_wide": ({}, {"blocked_permille": 1000}), "pull_step_2": ({"pull_step": 2}, {}),
              "no_lists": ({"list_rounds": 0}, {}), "needy_test": ({"bin_needy_skip": 0}, {}),
-             "stream_needy_test": ({"bin_stream": 1, "bin_needy_skip": 0}, {})}
+             "stream_needy_test": ({"bin_stream": 1, "bin_needy_skip": 0}, {}),
+             "apply_pipe_1": ({"apply_pipe": 1}, {}), "apply_pipe_2": ({"apply_pipe": 2}, {}),
+             "apply_pipe_3": ({"apply_pipe": 3}, {}), "slots_needy_test": ({"bin_stream": 0, "bin_needy_skip": 0}, {})}
 
 
 @pytest.mark.parametrize("variant", sorted(_VARIANTS))
