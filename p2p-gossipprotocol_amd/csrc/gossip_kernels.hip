@@ -1224,6 +1224,47 @@ __device__ __forceinline__ void bin_src_stats(const RoundArgs& a, const BinArgs&
     }
 }
 
+// The end of a bin (k_bin_apply, k_bin_apply_runs): handleClient's test-and-set of the bin's peers from the
+// LDS accumulator (peer.cpp:277-285): fr = acc & ~seen.  Every seen word a thread tests (and, after a
+// deferred push round, a.fold, its pending new word) is loaded before any is used: a loop that loads,
+// tests and stores one word per iteration waited a memory round trip per word -- 18 per thread and bin at
+// 18432 peers, ≈ 57 bins per CU and launch.  seen is rewritten whole for a tile where any word changes (a
+// single-word store into a 64-B sector costs a read-modify-write at the memory); nx is written whole (heavy
+// rows: 0 here, OR-ed by k_pull_heavy afterwards).
+template <int W, int kWords, int kB>
+__device__ __forceinline__ void bin_finish(const RoundArgs& a, uint64_t v0, uint32_t nv,
+                                           const unsigned long long* acc_s, Acc& acc) {
+    constexpr int kJ = (kWords + kB - 1) / kB;
+    const uint32_t n = nv * W, n_pad = (n + 63) & ~63u;
+    uint64_t sv[kJ], pv[kJ];
+#pragma unroll
+    for (int j = 0; j < kJ; ++j) {
+        const uint32_t i = threadIdx.x + (uint32_t)j * kB;
+        sv[j] = i < n ? a.seen[v0 * W + i] : 0ull;
+        pv[j] = a.fold && i < n ? a.nw[v0 * W + i] : 0ull;
+    }
+#pragma unroll
+    for (int j = 0; j < kJ; ++j) {
+        const uint32_t i = threadIdx.x + (uint32_t)j * kB;
+        if (i >= n_pad) break;  // wave-uniform
+        const bool in = i < n;
+        const uint64_t p = pv[j];
+        const uint64_t s = sv[j] | p;
+        const bool va = in && (!a.dead_mode || bit_alive(a.alive, (uint32_t)(a.begin + v0 + i / W)));  // dead: no receive
+        const uint64_t fr = va ? acc_s[i] & injm(a, i % W) & ~s : 0ull;
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+            if (i % W == w) acc.fresh_or[w] |= fr;  // (constant register indices)
+        if (fr) {  // handleClient: new -> Message-List insert (peer.cpp:281-282)
+            acc.fresh += (unsigned long long)__popcll(fr);
+            acc.activated++;
+        }
+        const bool tile = __ballot((fr | p) != 0) != 0ull;
+        if (in && tile) a.seen[v0 * W + i] = s | fr;
+        if (in) a.nx[v0 * W + i] = fr;
+    }
+}
+
 // Phase 2: one workgroup per bin folds the bin's slots into an LDS
 // accumulator (ds_or_b64), then applies handleClient's test-and-set to the
 // bin's peers with plain stores.  A bin none of whose peers can still learn
@@ -1289,23 +1330,7 @@ __global__ __launch_bounds__(kB) void k_bin_apply(RoundArgs a, BinArgs b, uint32
         }
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < nv * W; i += kB) {
-        const uint64_t p = pend(i);
-        const uint64_t sv = a.seen[v0 * W + i] | p;
-        const bool va = !a.dead_mode || bit_alive(a.alive, (uint32_t)(a.begin + v0 + i / W));  // dead: no receive
-        const uint64_t fr = va ? acc_s[i] & injm(a, i % W) & ~sv : 0ull;
-#pragma unroll
-        for (int w = 0; w < W; ++w)
-            if (i % W == w) acc.fresh_or[w] |= fr;  // (constant register indices)
-        if (fr) {  // handleClient: new -> Message-List insert (peer.cpp:281-282)
-            acc.fresh += (unsigned long long)__popcll(fr);
-            acc.activated++;
-        }
-        // seen rewritten whole for a tile where any word changes (a single-word store into a 64-B sector
-        // costs a read-modify-write at the memory)
-        if (__ballot((fr | p) != 0)) a.seen[v0 * W + i] = sv | fr;
-        a.nx[v0 * W + i] = fr;  // heavy rows: 0 here, OR-ed by k_pull_heavy afterwards
-    }
+    bin_finish<W, kWords, kB>(a, v0, nv, acc_s, acc);
     flush<kB / 64>(acc, a.st);
     cov_out();
 }
@@ -1530,21 +1555,7 @@ __global__ __launch_bounds__(kB) void k_bin_apply_runs(RoundArgs a, BinArgs b, u
             }
         }
         __syncthreads();
-        for (uint32_t i = threadIdx.x; i < nv * W; i += kB) {
-            const uint64_t p = pend(i);
-            const uint64_t sv = a.seen[v0 * W + i] | p;
-            const bool va = !a.dead_mode || bit_alive(a.alive, (uint32_t)(a.begin + v0 + i / W));  // dead: no receive
-            const uint64_t fr = va ? acc_s[i] & injm(a, i % W) & ~sv : 0ull;
-#pragma unroll
-            for (int w = 0; w < W; ++w)
-                if (i % W == w) acc.fresh_or[w] |= fr;  // (constant register indices)
-            if (fr) {  // handleClient: new -> Message-List insert (peer.cpp:281-282)
-                acc.fresh += (unsigned long long)__popcll(fr);
-                acc.activated++;
-            }
-            if (__ballot((fr | p) != 0)) a.seen[v0 * W + i] = sv | fr;  // whole tiles (k_bin_apply)
-            a.nx[v0 * W + i] = fr;  // heavy rows: 0 here, OR-ed by k_pull_heavy afterwards
-        }
+        bin_finish<W, kWords, kB>(a, v0, nv, acc_s, acc);
     };
     // bins of XCD group x: [x * per, (x + 1) * per), block x + 8 j applying bin j of it (the blocks in flight
     // on an XCD apply consecutive bins)
