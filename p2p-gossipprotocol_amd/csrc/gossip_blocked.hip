@@ -74,18 +74,18 @@ template <bool CA, bool COV>
 __global__ __launch_bounds__(kPbBlock) void k_pb_scatter(RoundArgs a, PbArgs p, uint32_t wd) {
     __shared__ uint32_t lo_s[kPbCoarse + 1];
     __shared__ uint8_t cmap_s[kPbMap];  // coarse bin of each id bucket's first peer (then a short walk)
-    __shared__ uint32_t tk_s[kPbCoarse], wr_s[kPbH1 * kPbCoarse], gn_s[kPbH1 * kPbCoarse];
-    __shared__ unsigned long long base_s[kPbCoarse];  // this workgroup's segment of each coarse bin
-    __shared__ uint32_t cap_s[kPbCoarse];
-    __shared__ uint32_t bd_s[kPbCoarse * kPbH1 * kPbB1];
-    __shared__ unsigned long long bw_s[kPbCoarse * kPbH1 * kPbB1];
+    __shared__ uint32_t tk_s[kPbCoarseMax], wr_s[kPbH1 * kPbCoarseMax], gn_s[kPbH1 * kPbCoarseMax];
+    __shared__ unsigned long long base_s[kPbCoarseMax];  // this workgroup's segment of each coarse bin
+    __shared__ uint32_t cap_s[kPbCoarseMax];
+    __shared__ uint32_t bd_s[kPbCoarseMax * kPbH1 * kPbB1];
+    __shared__ unsigned long long bw_s[kPbCoarseMax * kPbH1 * kPbB1];
     __shared__ uint32_t pk_v[kPbWaves][128];
     __shared__ unsigned long long pk_m[kPbWaves][128];
     __shared__ unsigned int cov_s[COV ? 64 : 1];
     const uint32_t nc = p.n_coarse, wg = blockIdx.x;
     for (uint32_t i = threadIdx.x; i <= kPbCoarse; i += kPbBlock) lo_s[i] = i <= nc ? p.c_lo[i] : 0xFFFFFFFFu;
-    stage_init<kPbH1>(tk_s, wr_s, gn_s, kPbCoarse, threadIdx.x, kPbBlock);
-    for (uint32_t i = threadIdx.x; i < kPbCoarse; i += kPbBlock) {
+    stage_init<kPbH1>(tk_s, wr_s, gn_s, kPbCoarseMax, threadIdx.x, kPbBlock);
+    for (uint32_t i = threadIdx.x; i < kPbCoarseMax; i += kPbBlock) {
         base_s[i] = i < nc ? p.s1_base[(uint64_t)wg * nc + i] : 0ull;
         cap_s[i] = i < nc ? p.s1_cap[(uint64_t)wg * nc + i] : 0u;
     }
@@ -737,9 +737,15 @@ hipError_t build_pb(const uint64_t* rp, const uint32_t* col, uint64_t n_local, u
         while (t < n_tiles && tin[t] > direct_in) ++t;
         st.direct_end = (uint32_t)std::min<uint64_t>(t * 64, n_local);
     }
-    // coarse bins: runs of whole fine bins of about equal in-degree, <= kPbFineMax fine bins each
+    // coarse bins: runs of whole fine bins of about equal in-degree, <= kPbFineMax fine bins each, at most
+    // kPbCoarseMax of them (an overlay with more fine bins than fit gets no blocked rounds)
+    if (n_fine > (uint64_t)kPbCoarseMax * kPbFineMax) {
+        if (err) *err = "blocked rounds: more fine bins than the level-2 staging can hold";
+        free_pb(&st);
+        return hipErrorInvalidValue;
+    }
     std::vector<uint32_t> c_fine;
-    for (uint64_t target = (n_edges + kPbCoarse - 1) / kPbCoarse;; target += target / 8 + 1) {
+    for (uint64_t target = (n_edges + kPbCoarseMax - 1) / kPbCoarseMax;; target += target / 8 + 1) {
         c_fine.assign(1, 0u);
         uint64_t sum = 0;
         for (uint64_t b = 0; b < n_fine; ++b) {
@@ -750,7 +756,7 @@ hipError_t build_pb(const uint64_t* rp, const uint32_t* col, uint64_t n_local, u
             sum += f_in[b];
         }
         c_fine.push_back((uint32_t)n_fine);
-        if (c_fine.size() - 1 <= kPbCoarse) break;
+        if (c_fine.size() - 1 <= kPbCoarseMax) break;
     }
     st.n_coarse = (uint32_t)(c_fine.size() - 1);
     st.n_fine = n_fine;

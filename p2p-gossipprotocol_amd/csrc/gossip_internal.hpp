@@ -144,12 +144,14 @@ struct BinState {
 // edge counts (its worst case: every source active), so records are written without global atomics:
 // a level-1 workgroup owns every kPbGrid-th tile and heavy chunk, a level-2 slice the segments of
 // kPbGrid / kPbSlices of them.
-constexpr uint32_t kPbCoarse = 256;    // level-1 bins (a power of two: the LDS search is branch-free)
-constexpr uint32_t kPbFineMax = 96;    // fine bins per coarse bin (level-2 LDS staging)
+constexpr uint32_t kPbCoarse = 256;    // level-1 search table (a power of two: the LDS search is branch-free)
+constexpr uint32_t kPbCoarseMax = 160; // level-1 bins: two 32-record buffers each fit the LDS (round 4; 256 bins
+                                       // with one buffer each in round 3)
+constexpr uint32_t kPbFineMax = 100;   // fine bins per coarse bin (level-2 LDS staging)
 constexpr uint32_t kPbFineIn = 1u << 18;  // a fine bin: whole tiles, <= kBinWords peers and <= this in-degree
                                           // (unless one tile has more): no hot bin in level 2
 constexpr uint32_t kPbB1 = 32;         // level-1 records per flush: 128 B of destinations, 256 B of words
-constexpr uint32_t kPbH1 = 1;          // ... one buffer per coarse bin (gossip_stage.hpp)
+constexpr uint32_t kPbH1 = 2;          // ... two buffers per coarse bin (gossip_stage.hpp)
 constexpr uint32_t kPbB2 = 64;         // level-2 records per flush: 128 B of destinations, 512 B of words
 constexpr uint32_t kPbH2 = 2;          // ... two buffers per fine bin
 constexpr uint32_t kPbSlices = 4;      // level-2 workgroups per coarse bin

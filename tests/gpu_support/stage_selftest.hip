@@ -20,7 +20,7 @@ using namespace gossip;
 namespace {
 
 constexpr int kBlockT = 1024;
-constexpr uint32_t kMaxBins = 128;  // 96 in level 2's geometry (kb = 64), as kPbFineMax
+constexpr uint32_t kMaxBins = 160;  // as kPbCoarseMax; 100 in level 2's geometry (kb = 64), as kPbFineMax
 
 __device__ uint32_t hash32(uint32_t x) {
     x ^= x >> 16;
@@ -112,12 +112,12 @@ __global__ __launch_bounds__(kBlockT) void k_stage(uint32_t nb, uint32_t per_wg,
 // out[2] records expected, out[3] misplaced, out[4] duplicates, out[5] error flags (bit 4: a stuck wave),
 // out[6] = Σ of the segments' lengths (stage_len: whole generations), out[7] = the same from the host
 // (the segments' capacities).
-// kb: 32 (32-bit destinations, one buffer per bin: level 1's geometry) or 64 (16-bit destinations, two
-// buffers per bin: level 2's); 16 and 128 are the same protocol at other sizes (16: two buffers).
+// kb: 32 (32-bit destinations, two buffers per bin: level 1's geometry), 64 (16-bit destinations, two
+// buffers per bin: level 2's) or 16 (32-bit destinations, two buffers: the protocol at another size).
 // Returns 0, or -1 on a HIP error / bad argument.
 extern "C" int stage_selftest(uint32_t nb, uint32_t per_wg, uint32_t skew, uint32_t grid, uint32_t kb,
                               uint64_t* out) {
-    if (!out || nb < 1 || nb > (kb == 64 ? 96u : kMaxBins) || (kb != 16 && kb != 32 && kb != 64) || !grid)
+    if (!out || nb < 1 || nb > (kb == 64 ? 100u : kMaxBins) || (kb != 16 && kb != 32 && kb != 64) || !grid)
         return -1;
     const uint64_t total = (uint64_t)grid * per_wg;
     // segments: (workgroup, bin) pairs in bin-major order, each its records rounded up to whole generations
@@ -158,10 +158,10 @@ extern "C" int stage_selftest(uint32_t nb, uint32_t per_wg, uint32_t skew, uint3
         hipLaunchKernelGGL((k_stage<16, 2, uint32_t, kMaxBins>), dim3(grid), dim3(kBlockT), 0, 0, nb, per_wg, skew, out_id,
                            out_w, d_base, d_cap, err);
     else if (kb == 32)
-        hipLaunchKernelGGL((k_stage<32, 1, uint32_t, kMaxBins>), dim3(grid), dim3(kBlockT), 0, 0, nb, per_wg, skew, out_id,
+        hipLaunchKernelGGL((k_stage<32, 2, uint32_t, kMaxBins>), dim3(grid), dim3(kBlockT), 0, 0, nb, per_wg, skew, out_id,
                            out_w, d_base, d_cap, err);
     else
-        hipLaunchKernelGGL((k_stage<64, 2, uint16_t, 96>), dim3(grid), dim3(kBlockT), 0, 0, nb, per_wg, skew, out_id,
+        hipLaunchKernelGGL((k_stage<64, 2, uint16_t, 100>), dim3(grid), dim3(kBlockT), 0, 0, nb, per_wg, skew, out_id,
                            out_w, d_base, d_cap, err);
     uint32_t hx[8] = {};
     std::vector<uint32_t> hid(slots + 1);
