@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--mode", default="auto", choices=["auto", "push", "pull"])
     ap.add_argument("--rebootstrap", type=int, default=0,
                     help="re-bootstrap after a death with this many extra out-edges per peer (configs 1, 5)")
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
+                    help="gossip_set_tuning option for every part (A/B measurements; repeatable)")
     ap.add_argument("--force-partitioned", action="store_true",
                     help="use the library's multi-GPU driver (RCCL collectives) even at WORLD_SIZE 1")
     return ap.parse_args()
@@ -360,6 +362,8 @@ def main():
 
     w = config(args.config, args.n or None, rebootstrap=args.rebootstrap)
     tune = dict(pull_permille=args.pull_permille, front_permille=args.front_permille, mode=args.mode)
+    if args.tune:
+        tune["tuning"] = {k: int(v) for k, v in (t.split("=", 1) for t in args.tune)}
     dist = None
     if world > 1 or args.force_partitioned:
         # one process per GPU; libgossip_hip drives every round's RCCL collectives

@@ -333,7 +333,9 @@ gossip_status gossip_kernel_bytes(gossip_ctx* ctx, const char* kernel, double* b
  * with over one missing pair per peer skip the apply's per-bin needy test:
  * 1 default, 0 always test), "apply_pipe" (the streamed apply's load
  * pipeline shape, 0-3, A/B), "replay" (0: gossip_run never replays a
- * recorded schedule).  Layout keys
+ * recorded schedule), "scatter_direct" (partitioned runs: a block's binned
+ * scatter reads other blocks' source words from the gather buffer instead of
+ * staging them; 0 default).  Layout keys
  * apply at the next gossip_build_graph / gossip_load_csr ("list_cap": at the
  * next chain of needy-list rounds, never inside one).  GOSSIP_EINVAL: unknown key. */
 gossip_status gossip_set_tuning(gossip_ctx* ctx, const char* key, int64_t value);

@@ -215,6 +215,7 @@ struct gossip_ctx {
     bool full_liveness = false;  // "full_liveness": ping every edge each ping round (A/B against closed form)
     uint64_t cur_missing = 0;    // (peer, message) pairs still missing at the round's push start (round_begin)
     uint32_t apply_pipe = 0;     // "apply_pipe": the streamed apply's pipeline shape (0-3, A/B)
+    bool scatter_direct = false; // "scatter_direct": a vertex block's scatter reads other blocks' words directly
     bool needy_skip = true;      // "bin_needy_skip": binned rounds with over one missing pair per peer skip the
                                  // apply's needy test
     uint64_t* seg = nullptr;     // sparse push: per-destination record segments (world x chunk records)
@@ -698,7 +699,8 @@ BinArgs bin_args(const gossip_ctx* c, bool noskip, uint32_t src_side) {
     return BinArgs{s.bins,      s.n_bins,   s.cb_src,    s.cb_run,   s.cb_grp,   s.n_binned, s.chunk_begin,
                    s.n_chunks,  s.chunk,    s.units,     s.xcd_units, s.bdst,    s.val,      s.bin_words,
                    s.dummy,     noskip ? 1u : 0u, s.n_runs ? s.n_runs - 1 : 0, s.ap_run, s.ap_grp,
-                   c->bin_stream ? 1u : 0u, s.deg, src_side, c->apply_pipe, 1u};
+                   c->bin_stream ? 1u : 0u, s.deg, src_side, c->apply_pipe, c->scatter_direct && c->gather ? 1u : 0u,
+                   1u};
 }
 
 gossip_status tune_val(gossip_ctx* c) {
@@ -1779,6 +1781,7 @@ gossip_status gossip_set_tuning(gossip_ctx* c, const char* key, int64_t value) {
     else if (k == "list_cap") c->list_cap_req = u;
     else if (k == "bin_needy_skip") c->needy_skip = value != 0;
     else if (k == "replay") c->replay_req = value != 0;
+    else if (k == "scatter_direct") c->scatter_direct = value != 0;
     else if (k == "apply_pipe") {
         if (value < 0 || value > 3) return fail(GOSSIP_EINVAL, "apply_pipe must be 0..3");
         c->apply_pipe = (uint32_t)value;

@@ -101,6 +101,8 @@ struct BinArgs {
     uint32_t stream;              // 1: streamed layout, 0: val in slot order (k_bin_scatter_*)
     const uint32_t* deg;          // per owned peer: its row length (source-side stats booked by the apply)
     uint32_t apply_pipe;          // streamed apply's pipeline shape (k_bin_apply_runs, "apply_pipe"; 0 default)
+    uint32_t direct;              // streamed scatter of a vertex block: chunks without owned sources read their
+                                  // words from the gather buffer instead of staging them ("scatter_direct")
     uint32_t needy_check;         // 1: the apply first tests whether any peer of the bin can still learn
                                   // something (a pass over the bin's seen words) and skips its slots if not;
                                   // 0 on rounds with more than one missing pair per peer, where every bin is

@@ -1364,8 +1364,16 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_stream(RoundArgs a, BinAr
     auto unit = [&](const uint64_t ui) {
         const BinUnit un = b.units[ui];
         if (un.p0 >= un.p1 && !un.first) return;  // padding of a row (block-uniform)
-        scatter_stage<W, COV>(a, b, un, wd, slice, live_s, cov_s, acc);
-        __syncthreads();
+        // b.direct (a vertex block of a partitioned run): a chunk with no owned source books no stats, and
+        // its few entries (1/P of a whole overlay's) read their words straight from the gather buffer (the
+        // chunk's 144 KB stay in L2 after the first touch) instead of paying the chunk's staging
+        const uint64_t vb = (uint64_t)un.c * b.chunk;
+        const bool direct = b.direct && !(vb < a.end && vb + b.chunk > a.begin);  // block-uniform
+        const uint64_t* src = a.nw_src + vb * W;
+        if (!direct) {
+            scatter_stage<W, COV>(a, b, un, wd, slice, live_s, cov_s, acc);
+            __syncthreads();
+        }
         if (un.p0 >= un.p1) return;
         acc.gathered += threadIdx.x == 0 ? un.p1 - un.p0 : 0;  // slots written (byte accounting)
         if (W == 1) {
@@ -1381,8 +1389,9 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_stream(RoundArgs a, BinAr
                 for (int j = 0; j < kU; ++j) {
                     const uint64_t k = kb + (uint64_t)j * kScatterBlock;
                     if (k >= k1) break;
-                    const uint64_t x0 = slice[sv[j] & (kRunStart - 1u)];
-                    const uint64_t x1 = slice[(sv[j] >> 16) & (kRunStart - 1u)];
+                    const uint32_t u0 = sv[j] & (kRunStart - 1u), u1 = (sv[j] >> 16) & (kRunStart - 1u);
+                    const uint64_t x0 = direct ? src[u0] : slice[u0];
+                    const uint64_t x1 = direct ? src[u1] : slice[u1];
                     const uint64_t e = 2 * k;
                     if (e >= un.p0 && e + 2 <= un.p1) {
                         u64x2 y;
@@ -1409,8 +1418,8 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_stream(RoundArgs a, BinAr
                     const uint32_t u = sv[j] & (kRunStart - 1u);
                     const uint32_t w0 = (uint32_t)(k % kPW) * 2;
                     u64x2 y;
-                    y.x = slice[(uint64_t)u * W + w0];
-                    y.y = slice[(uint64_t)u * W + w0 + 1];
+                    y.x = direct ? src[(uint64_t)u * W + w0] : slice[(uint64_t)u * W + w0];
+                    y.y = direct ? src[(uint64_t)u * W + w0 + 1] : slice[(uint64_t)u * W + w0 + 1];
                     reinterpret_cast<u64x2*>(b.val)[k] = y;  // entry k / kPW, words w0, w0 + 1
                 }
             }

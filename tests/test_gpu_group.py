@@ -44,7 +44,7 @@ def test_group_on_one_device_equals_oracle(oracle, idx, n, P):
     assert again == stats
 
 
-@pytest.mark.parametrize("gather", ["compact", "whole"])
+@pytest.mark.parametrize("gather", ["compact", "whole", "direct"])
 @pytest.mark.parametrize("P", [2, 3, 5])
 @pytest.mark.parametrize("idx,n", [(3, 100_003), (5, 1 << 15), (2, 40_000)])
 def test_group_dense_exchange_forms_equal_oracle(oracle, idx, n, P, gather):
@@ -54,11 +54,15 @@ def test_group_dense_exchange_forms_equal_oracle(oracle, idx, n, P, gather):
     offsets from the tiles' popcount prefix, packed words as send / recv
     pairs, expansion into the gather buffer) -- on blocks that do not end on a
     tile boundary (n = 100,003) and a short last block (P = 3, 5).  Both forms
-    give the oracle's run."""
+    give the oracle's run, as does the scatter reading other blocks' words
+    straight from the gather buffer ("direct": scatter_direct)."""
     w = config(idx, n, pick=oracle.pick_origins)
     rp, col = oracle.gen_workload(w)
     ref = oracle.simulate_workload(w, rp, col)
-    stats, seen, reps, again = _run_group(w, [0] * P, tuning={"gather_permille": 1000 if gather == "compact" else 0})
+    tuning = {"gather_permille": 0 if gather == "whole" else 1000}
+    if gather == "direct":
+        tuning["scatter_direct"] = 1
+    stats, seen, reps, again = _run_group(w, [0] * P, tuning=tuning)
     assert stats == ref["stats"]
     assert np.array_equal(seen, ref["seen"])
     assert np.array_equal(reps, ref["reports"])
