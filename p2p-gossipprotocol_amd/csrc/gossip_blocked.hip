@@ -234,7 +234,7 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_scatter(RoundArgs a, PbArgs p, 
                 deg = d <= a.heavy ? (uint32_t)d : 0u;  // heavy rows: (1)
                 // consumed: this buffer is the next round's accumulator (the hubs' words are read by
                 // direct(), heavy rows' by their chunks: the split clears those)
-                if (d <= a.heavy && v >= p.direct_end) a.nw[v] = 0ull;
+                if (!p.clear_all && d <= a.heavy && v >= p.direct_end) a.nw[v] = 0ull;
             }
             const uint32_t rest = n_pk - cnt;
             wave_sync();
@@ -384,14 +384,22 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_split(PbArgs p) {
         ps_s[i + 1] = incl;
         if (i == 0) ps_s[0] = 0;
     }
-    // the heavy rows' new words, consumed by level 1 (one word per row: its first chunk)
-    for (uint64_t ci = (uint64_t)blockIdx.x * kPbBlock + threadIdx.x; ci < p.n_chunks;
-         ci += (uint64_t)gridDim.x * kPbBlock) {
-        const HeavyChunk ch = p.chunks[ci];
-        if (ch.first == ci) p.nw[ch.v] = 0ull;
+    if (p.clear_all) {  // a wide frontier: every new word, consumed by level 1, cleared in whole 16-B pieces
+        u64x2* nw2 = reinterpret_cast<u64x2*>(p.nw);
+        const uint64_t n2 = (p.n_local + 1) / 2;  // (the word arrays are allocated in whole pairs)
+        for (uint64_t i = (uint64_t)blockIdx.x * kPbBlock + threadIdx.x; i < n2; i += (uint64_t)gridDim.x * kPbBlock)
+            nw2[i] = u64x2{0ull, 0ull};
+    } else {
+        // the heavy rows' new words, consumed by level 1 (one word per row: its first chunk)
+        for (uint64_t ci = (uint64_t)blockIdx.x * kPbBlock + threadIdx.x; ci < p.n_chunks;
+             ci += (uint64_t)gridDim.x * kPbBlock) {
+            const HeavyChunk ch = p.chunks[ci];
+            if (ch.first == ci) p.nw[ch.v] = 0ull;
+        }
+        for (uint64_t v = (uint64_t)blockIdx.x * kPbBlock + threadIdx.x; v < p.direct_end;
+             v += (uint64_t)gridDim.x * kPbBlock)
+            p.nw[v] = 0ull;  // and the hubs'
     }
-    for (uint64_t v = (uint64_t)blockIdx.x * kPbBlock + threadIdx.x; v < p.direct_end; v += (uint64_t)gridDim.x * kPbBlock)
-        p.nw[v] = 0ull;  // and the hubs'
     __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     static_assert(kPbB2 == 64, "a lane per record of a generation");

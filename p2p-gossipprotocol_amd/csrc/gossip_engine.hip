@@ -215,6 +215,8 @@ struct gossip_ctx {
     bool full_liveness = false;  // "full_liveness": ping every edge each ping round (A/B against closed form)
     uint64_t cur_missing = 0;    // (peer, message) pairs still missing at the round's push start (round_begin)
     uint32_t apply_pipe = 0;     // "apply_pipe": the streamed apply's pipeline shape (0-3, A/B)
+    bool pb_clear_all = true;    // "blocked_clear_all": wide blocked rounds clear new words whole in level 2
+    bool cur_clear_all = false;  // (the round in flight does)
     bool scatter_direct = false; // "scatter_direct": a vertex block's scatter reads other blocks' words directly
     bool needy_skip = true;      // "bin_needy_skip": binned rounds with over one missing pair per peer skip the
                                  // apply's needy test
@@ -1315,6 +1317,10 @@ gossip_status round_compute(gossip_ctx* c) {
         p.chunks = c->chunks;
         p.n_chunks = c->n_chunks;
         p.nw = reinterpret_cast<unsigned long long*>(c->nw);
+        p.n_local = c->n_local;
+        // whole-array clear from a 5 % frontier (config 4 round 4: 17 %; round 3, 1.25 %, clears per peer)
+        p.clear_all = c->pb_clear_all && c->frontier_est * 20 >= c->n_local ? 1u : 0u;
+        c->cur_clear_all = p.clear_all != 0;
         if (a.tcur) HIPCHK(queue_zero(c, a.tcur, tact_bytes(c)));  // unread marks go
         HIPCHK(timed(c, "pb_scatter", [&] { return launch_pb_scatter(a, p, c->any_dead, c->W, c->stream); }));
         HIPCHK(timed(c, "pb_split", [&] { return launch_pb_split(p, c->stream); }));
@@ -1443,7 +1449,7 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
             // apply: 10 B per record + the seen read and seen / nx writes of the activated peers
             const double t = (double)d.traversals;
             c->kbytes["pb_scatter"] += 8.0 * c->n_local + 24.0 * d.frontier + 16.0 * t;
-            c->kbytes["pb_split"] += 22.0 * t;
+            c->kbytes["pb_split"] += 22.0 * t + (c->cur_clear_all ? 8.0 * c->n_local : 0.0);
             c->kbytes["pb_apply"] += 10.0 * t + 24.0 * (double)d.activated;
         }
         if (c->last_bin) {
@@ -1782,6 +1788,7 @@ gossip_status gossip_set_tuning(gossip_ctx* c, const char* key, int64_t value) {
     else if (k == "bin_needy_skip") c->needy_skip = value != 0;
     else if (k == "replay") c->replay_req = value != 0;
     else if (k == "scatter_direct") c->scatter_direct = value != 0;
+    else if (k == "blocked_clear_all") c->pb_clear_all = value != 0;
     else if (k == "apply_pipe") {
         if (value < 0 || value > 3) return fail(GOSSIP_EINVAL, "apply_pipe must be 0..3");
         c->apply_pipe = (uint32_t)value;

@@ -191,6 +191,10 @@ struct PbArgs {
     const HeavyChunk* chunks; // the heavy rows' chunks (row order) ...
     uint64_t n_chunks;
     unsigned long long* nw;   // ... whose new words the split clears (set per round: the buffers rotate)
+    uint32_t clear_all;       // a wide frontier: the split clears every new word in whole pieces, and level 1
+                              // clears none (scattered 8-B clears of a dense frontier cost a read-modify-write
+                              // per touched sector)
+    uint64_t n_local;
 };
 
 struct PbState {
