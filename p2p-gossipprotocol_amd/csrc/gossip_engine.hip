@@ -2066,7 +2066,11 @@ gossip_status gossip_reset(gossip_ctx* c) {
         HIPCHK(hipMemsetAsync(c->st, 0, kStatLines * sizeof(DevStats), s));
         HIPCHK(hipMemsetAsync(c->n_reports, 0, sizeof(unsigned long long), s));
         HIPCHK(hipMemsetAsync(c->inj_live, 0, kMaxWords * sizeof(uint64_t), s));
-        if (c->miss) HIPCHK(hipMemsetAsync(c->miss, 0, c->n_edges + 1, s));
+        // per-edge miss counters: only the per-edge liveness scan uses them (the closed form, below, never
+        // does; config 5: a 0.5 GB clear per step saved)
+        const bool closed = c->n_local == c->n && c->symmetric && !c->cfg.rejoin_threshold &&
+                            c->cfg.max_rounds < 0xFFFF && !c->full_liveness;
+        if (c->miss && !closed) HIPCHK(hipMemsetAsync(c->miss, 0, c->n_edges + 1, s));
         if (c->any_masked && c->col && c->n_edges) {
             hipLaunchKernelGGL(k_unmask, dim3(2048), dim3(256), 0, s, c->col, c->n_edges);
             HIPCHK(hipGetLastError());
