@@ -304,19 +304,29 @@ class Ranked(Single):
 LIVE_COUNTERS = ("#pings", "#pinging_peers")  # 8(d)'s liveness term of a ping round (k_live_count)
 
 
+def part_agg(run):
+    """How per-part device times combine into the run's: the max over the parts
+    when each part has its own GPU (they run concurrently), the sum when P parts
+    share one GPU (their kernels run one after another on it)."""
+    return max if run.parts == run.n_gpus else sum
+
+
 def per_round_profile(run, n_peers: int) -> list[dict]:
     """One run, stepped round by round with per-kernel timing (untimed pass):
     each round's mode; SURVEY 8(d)'s algorithmic bytes B_r = 32 F_r + 20 T_r,
     plus 6.125 B per ping and 16 B per pinging peer in a ping round; the
     kernels' own design bytes (DESIGN.md section 6, summed over the round's
     kernels and parts); the device time of its kernels (max over the parts of
-    a partitioned run) and exchanges; and the round's fraction of the HBM
+    a partitioned run on one GPU per part, the sum over the parts of one run
+    emulating P parts on a single GPU, where they run one after another) and
+    exchanges; and the round's fraction of the HBM
     peak, frac = B_r / kernel time / peak.  Pull rounds (row, list and heavy
     pulls) stop a row's scan once it holds every bit it can still learn, so
     8(d)'s 20 B per traversal overstates what they touch: they are marked
     work_avoiding (their frac can pass 1)."""
     from gossip_hip.engine import EXCHANGES, KERNELS
     names = KERNELS + EXCHANGES
+    agg = part_agg(run)
     run.reset()
     run.timing(True)
     kb = lambda: [{k: run.kbytes(p, k) for k in KERNELS + LIVE_COUNTERS} for p in range(run.parts)]  # noqa: E731
@@ -332,9 +342,9 @@ def per_round_profile(run, n_peers: int) -> list[dict]:
         prev, prev_b = cur, cur_b
         mode = "bin" if any("bin_scatter" in x for x in d) else "blocked" if any("pb_scatter" in x for x in d) else \
             "pull" if any("pull_light" in x or "pull_list" in x for x in d) else "push"
-        kms = max(sum(v for k, v in x.items() if k in KERNELS) for x in d)
-        xms = max(sum(v for k, v in x.items() if k in EXCHANGES) for x in d)
-        dense = max(sum(x.get(k, 0.0) for k in DENSE_KERNELS) for x in d)
+        kms = agg(sum(v for k, v in x.items() if k in KERNELS) for x in d)
+        xms = agg(sum(v for k, v in x.items() if k in EXCHANGES) for x in d)
+        dense = agg(sum(x.get(k, 0.0) for k in DENSE_KERNELS) for x in d)
         live_b = 6.125 * db["#pings"] + 16 * db["#pinging_peers"]
         alg = 32 * st["frontier"] + 20 * st["traversals"] + live_b
         frac = alg / (kms / 1e3) / 1e9 / HBM_PEAK_GBS if kms > 0 else 0.0
@@ -423,6 +433,7 @@ def main():
         k_ms = [{k: run.ktime(p, k) for k in KERNELS + EXCHANGES} for p in range(run.parts)]
         k_b = [{k: run.kbytes(p, k) for k in KERNELS + EXCHANGES} for p in range(run.parts)]
         run.timing(False)
+        agg = part_agg(run)
         # the per-round pass: which rounds ran binned / pull / push, their 8(d) bytes and device time
         rounds_prof = per_round_profile(run, w.n)
         dense = [r for r in rounds_prof if r["mode"] == "bin"]
@@ -444,15 +455,15 @@ def main():
                     "step_alg_bytes": round(alg), "step_liveness_bytes": sum(r["liveness_bytes"] for r in rounds_prof),
                     "timed_steps": timed_steps,
                     "ms_per_step_with_events": round(dt_timed / timed_steps * 1e3, 3),
-                    "kernel_ms_per_step": {k: round(max(x[k][0] for x in k_ms) / timed_steps, 3)
+                    "kernel_ms_per_step": {k: round(agg(x[k][0] for x in k_ms) / timed_steps, 3)
                                            for k in KERNELS if k_ms[0][k][1]},
-                    "exchange_ms_per_step": {k: round(max(x[k][0] for x in k_ms) / timed_steps, 3)
+                    "exchange_ms_per_step": {k: round(agg(x[k][0] for x in k_ms) / timed_steps, 3)
                                              for k in EXCHANGES if k_ms[0][k][1]},
                     "exchange_gb_per_step": {k: round(sum(x[k] for x in k_b) / timed_steps / 1e9, 3)
                                              for k in EXCHANGES if k_ms[0][k][1]}}
         if dense:
             # SURVEY 8(d)'s bytes of the binned rounds over the device time of their kernels
-            # (bin_scatter + bin_apply + pull_heavy; max over parts): the honest dense-round fraction
+            # (bin_scatter + bin_apply + pull_heavy; part_agg over the parts): the honest dense-round fraction
             d_b = sum(r["alg_bytes"] for r in dense)
             d_ms = sum(r["dense_ms"] for r in dense)
             ach = d_b / (d_ms / 1e3) / 1e9

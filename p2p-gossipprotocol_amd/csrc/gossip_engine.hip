@@ -218,11 +218,13 @@ struct gossip_ctx {
     bool pb_clear_all = true;    // "blocked_clear_all": wide blocked rounds clear new words whole in level 2
     bool cur_clear_all = false;  // (the round in flight does)
     bool scatter_direct = false; // "scatter_direct": a vertex block's scatter reads other blocks' words directly
+    unsigned long long* d_probe = nullptr;  // "apply_probe": the streamed apply's phase clocks (kProbeN slots)
     bool needy_skip = true;      // "bin_needy_skip": binned rounds with over one missing pair per peer skip the
                                  // apply's needy test
     uint64_t* seg = nullptr;     // sparse push: per-destination record segments (world x chunk records)
     unsigned long long* d_counts = nullptr;  // records per destination rank
     uint64_t* h_counts = nullptr;            // pinned copy
+    unsigned long long* smark = nullptr;     // sparse push rounds' staging marks (RoundArgs.smark)
     uint64_t *sx_bits = nullptr, *sx_pos = nullptr;  // the compaction's tile bitmap and popcount prefix
     void* sx_tmp = nullptr;
     size_t sx_bytes = 0;
@@ -702,7 +704,7 @@ BinArgs bin_args(const gossip_ctx* c, bool noskip, uint32_t src_side) {
                    s.n_chunks,  s.chunk,    s.units,     s.xcd_units, s.bdst,    s.val,      s.bin_words,
                    s.dummy,     noskip ? 1u : 0u, s.n_runs ? s.n_runs - 1 : 0, s.ap_run, s.ap_grp,
                    c->bin_stream ? 1u : 0u, s.deg, src_side, c->apply_pipe, c->scatter_direct && c->gather ? 1u : 0u,
-                   1u};
+                   1u,          c->d_probe};
 }
 
 gossip_status tune_val(gossip_ctx* c) {
@@ -1184,6 +1186,7 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
         }
         if (remote && !c->cur_sparse) c->send_dirty = true;
     }
+    a.smark = remote && c->cur_sparse ? c->smark : nullptr;
     if (c->cur_pb) a.tsparse = 0;  // the blocked round sweeps every tile (round_compute clears the marks)
     c->cur = a;
     c->cur_remote = remote;
@@ -1793,6 +1796,17 @@ gossip_status gossip_set_tuning(gossip_ctx* c, const char* key, int64_t value) {
         if (value < 0 || value > 3) return fail(GOSSIP_EINVAL, "apply_pipe must be 0..3");
         c->apply_pipe = (uint32_t)value;
     }
+    else if (k == "apply_probe") {  // diagnostics: the streamed apply's phase clocks, read back as #probe_*
+        if (value && !c->d_probe) {
+            if (hipMalloc((void**)&c->d_probe, kProbeN * sizeof(unsigned long long)) != hipSuccess)
+                return fail(GOSSIP_ENOMEM, "apply_probe buffer");
+            if (hipMemset(c->d_probe, 0, kProbeN * sizeof(unsigned long long)) != hipSuccess)
+                return fail(GOSSIP_EHIP, "apply_probe buffer");
+        } else if (!value && c->d_probe) {
+            hipFree(c->d_probe);
+            c->d_probe = nullptr;
+        }
+    }
     else if (k == "gather_permille") c->gather_pm = value < 0 ? kGatherPermille : u;
     else return fail(GOSSIP_EINVAL, "unknown tuning option: " + k);
     return GOSSIP_OK;
@@ -1817,6 +1831,8 @@ void gossip_destroy(gossip_ctx* c) {
     if (c->h_counts) hipHostFree(c->h_counts);
     hipFree(c->d_live);
     hipFree(c->sx_bits);
+    hipFree(c->smark);
+    hipFree(c->d_probe);
     hipFree(c->sx_pos);
     hipFree(c->sx_tmp);
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
@@ -2228,6 +2244,8 @@ gossip_status gossip_set_sparse(gossip_ctx* c, void* seg) {
         HIPCHK(hipMalloc((void**)&c->sx_pos, (tiles + 1) * sizeof(uint64_t)));
         HIPCHK(compact_send_scratch(tiles, &c->sx_bytes));
         HIPCHK(hipMalloc(&c->sx_tmp, c->sx_bytes + 16));
+        HIPCHK(hipMalloc((void**)&c->smark, smark_bytes(c->n)));
+        HIPCHK(hipMemset(c->smark, 0, smark_bytes(c->n)));
     }
     c->seg = (uint64_t*)seg;
     return GOSSIP_OK;
@@ -2405,6 +2423,17 @@ gossip_status gossip_kernel_time(gossip_ctx* c, const char* kernel, double* ms, 
 
 gossip_status gossip_kernel_bytes(gossip_ctx* c, const char* kernel, double* bytes) {
     if (!c || !kernel || !bytes) return fail(GOSSIP_EINVAL, "null argument");
+    if (c->d_probe && !strncmp(kernel, "#probe_", 7)) {  // apply_probe's clocks (a device read: syncs)
+        static const char* const names[] = {"src", "init", "slots", "finish", "bins", "slots_n"};
+        unsigned long long h[kProbeN];
+        if (hipStreamSynchronize(c->stream) != hipSuccess ||
+            hipMemcpy(h, c->d_probe, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess)
+            return fail(GOSSIP_EHIP, "apply_probe read");
+        *bytes = 0.0;
+        for (int i = 0; i < 6; ++i)
+            if (!strcmp(kernel + 7, names[i])) *bytes = (double)h[i];
+        return GOSSIP_OK;
+    }
     auto it = c->kbytes.find(kernel);
     *bytes = it == c->kbytes.end() ? 0.0 : it->second;
     return GOSSIP_OK;

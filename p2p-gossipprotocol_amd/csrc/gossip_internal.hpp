@@ -112,7 +112,11 @@ struct BinArgs {
                                   // unit of each chunk, row bounds loaded after the slice); 0: the apply
                                   // does, for its bin's peers (bin_src_stats), and the scatter's staging is
                                   // one round trip
+    unsigned long long* probe;    // "apply_probe" (diagnostics): the streamed apply's per-phase wall-clock
+                                  // ticks summed over bins (kProbe* slots); null otherwise
 };
+// apply_probe slots: wall-clock (100 MHz) ticks of the streamed apply's phases, summed over bins
+enum { kProbeSrc = 0, kProbeInit, kProbeSlots, kProbeFinish, kProbeBins, kProbeSlotsN, kProbeN = 8 };
 
 struct BinState {
     Bin* bins = nullptr;
@@ -225,6 +229,8 @@ struct RoundArgs {
     uint64_t* nw;           // this round's new words (sources); cleared by push_light
     uint64_t* nx;           // next round's new words (fresh)
     uint64_t* send;         // dense remote staging (n_global * W) or null
+    unsigned long long* smark;  // sparse push rounds: 1 bit per 64 global peers whose staging words this round
+                                // wrote (the compaction reads only those tiles); null otherwise
     uint8_t* miss;          // per-edge miss counters
     DevStats* st;           // this round's kStatLines striped lines
     unsigned long long* cov;  // per-message coverage increments of this round (history) or null
@@ -343,6 +349,9 @@ hipError_t launch_apply_remote(const RoundArgs& a, uint32_t W, const uint64_t* r
 // sparse push exchange: send -> per-destination {peer, words} records at seg + q * chunk, counts[q] of them
 // (bits: world * ceil(chunk / 64) + 1 words, the last kept zero; pos: as many; scan_tmp: compact_send_scratch)
 hipError_t compact_send_scratch(uint64_t tiles, size_t* scan_bytes);
+// a sparse round's staging marks: 1 bit per 64 global peers (+ a word of slack)
+inline uint64_t smark_bytes(uint64_t n_global) { return ((n_global + 4095) / 4096 + 1) * 8; }
+// (smark: the round's staging marks, cleared here for the next sparse round)
 hipError_t launch_compact_send(const RoundArgs& a, uint32_t W, uint64_t chunk, uint32_t world,
                                unsigned long long* counts, uint64_t* seg, uint64_t* bits, uint64_t* pos,
                                void* scan_tmp, size_t scan_bytes, hipStream_t s);

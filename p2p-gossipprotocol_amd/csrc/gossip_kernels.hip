@@ -16,6 +16,7 @@
 // each, so no wave walks a long tail.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <type_traits>
 #include <stdlib.h>
 
 #include "gossip_device.hpp"
@@ -104,6 +105,15 @@ __device__ __forceinline__ void deliver_local(const RoundArgs& a, uint64_t lv, c
     }
 }
 
+// A sparse push round's staging write to global peer c marks c's 64-peer tile (each staging word written in
+// the round was written by an atomic that marked it: the compaction reads only marked tiles).
+__device__ __forceinline__ void mark_send(const RoundArgs& a, uint32_t c) {
+    if (!a.smark) return;
+    unsigned long long* w = a.smark + (c >> 12);
+    const unsigned long long bit = 1ull << ((c >> 6) & 63);
+    if (!(*w & bit)) atomicOr(w, bit);
+}
+
 // One delivery to global peer c (bit 31: masked edge): liveness, remote
 // staging or the local test-and-set.
 template <int W, bool CA, bool RM>
@@ -118,6 +128,7 @@ __device__ __forceinline__ void deliver(const RoundArgs& a, uint32_t c, const ui
     acc.deliv += pc;  // sentTo.insert (peer.cpp:314)
     if (RM && (c < a.begin || c >= a.end)) {
         unsigned long long* dst = reinterpret_cast<unsigned long long*>(a.send) + (uint64_t)c * W;
+        bool wrote = false;
 #pragma unroll
         for (int w = 0; w < W; ++w) {
             if (!m[w]) continue;
@@ -125,8 +136,10 @@ __device__ __forceinline__ void deliver(const RoundArgs& a, uint32_t c, const ui
             if ((cur & m[w]) != m[w]) {
                 atomicOr(dst + w, (unsigned long long)m[w]);
                 acc.atomics++;
+                wrote = true;
             }
         }
+        if (wrote) mark_send(a, c);
         return;
     }
     const uint64_t lv = (uint64_t)(c - (uint32_t)a.begin);
@@ -162,14 +175,17 @@ __device__ __forceinline__ void deliver_batch(const RoundArgs& a, const uint32_t
         }
         if (RM && loc[j] && (c[j] < a.begin || c[j] >= a.end)) {
             unsigned long long* dst = reinterpret_cast<unsigned long long*>(a.send) + (uint64_t)c[j] * W;
+            bool wrote = false;
 #pragma unroll
             for (int w = 0; w < W; ++w) {
                 if (!m[j][w]) continue;
                 if ((dst[w] & m[j][w]) != m[j][w]) {
                     atomicOr(dst + w, (unsigned long long)m[j][w]);
                     acc.atomics++;
+                    wrote = true;
                 }
             }
+            if (wrote) mark_send(a, c[j]);
             loc[j] = false;
         }
     }
@@ -1376,6 +1392,10 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_stream(RoundArgs a, BinAr
         }
         if (un.p0 >= un.p1) return;
         acc.gathered += threadIdx.x == 0 ? un.p1 - un.p0 : 0;  // slots written (byte accounting)
+        // the word source as a compile-time choice (a select would issue both loads)
+        auto pieces = [&](auto dir) {
+        constexpr bool kDirect = decltype(dir)::value;
+        auto word = [&](uint64_t u) { return kDirect ? src[u] : (uint64_t)slice[u]; };
         if (W == 1) {
             // piece k = entries 2k, 2k + 1 (cb_src read as one u32: 4-B aligned)
             const uint64_t k0 = un.p0 >> 1, k1 = (un.p1 + 1) >> 1;
@@ -1390,8 +1410,8 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_stream(RoundArgs a, BinAr
                     const uint64_t k = kb + (uint64_t)j * kScatterBlock;
                     if (k >= k1) break;
                     const uint32_t u0 = sv[j] & (kRunStart - 1u), u1 = (sv[j] >> 16) & (kRunStart - 1u);
-                    const uint64_t x0 = direct ? src[u0] : slice[u0];
-                    const uint64_t x1 = direct ? src[u1] : slice[u1];
+                    const uint64_t x0 = word(u0);
+                    const uint64_t x1 = word(u1);
                     const uint64_t e = 2 * k;
                     if (e >= un.p0 && e + 2 <= un.p1) {
                         u64x2 y;
@@ -1418,12 +1438,15 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_stream(RoundArgs a, BinAr
                     const uint32_t u = sv[j] & (kRunStart - 1u);
                     const uint32_t w0 = (uint32_t)(k % kPW) * 2;
                     u64x2 y;
-                    y.x = direct ? src[(uint64_t)u * W + w0] : slice[(uint64_t)u * W + w0];
-                    y.y = direct ? src[(uint64_t)u * W + w0 + 1] : slice[(uint64_t)u * W + w0 + 1];
+                    y.x = word((uint64_t)u * W + w0);
+                    y.y = word((uint64_t)u * W + w0 + 1);
                     reinterpret_cast<u64x2*>(b.val)[k] = y;  // entry k / kPW, words w0, w0 + 1
                 }
             }
         }
+        };
+        if (direct) pieces(std::true_type{});
+        else pieces(std::false_type{});
     };
     scatter_rows(b, unit);
     flush<kWaves>(acc, a.st);
@@ -1478,7 +1501,19 @@ __global__ __launch_bounds__(kB) void k_bin_apply_runs(RoundArgs a, BinArgs b, u
         const uint32_t nv = bn.v1 - bn.v0;
         const uint64_t v0 = bn.v0;
         __syncthreads();  // the previous bin is done with acc_s (and cov_s is initialised)
+        // apply_probe (diagnostics): thread 0 clocks the phases, with a barrier after each one
+        uint64_t tk = b.probe ? wall_clock64() : 0;
+        auto tick = [&](int slot) {
+            if (!b.probe) return;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                const uint64_t t = wall_clock64();
+                atomicAdd(&b.probe[slot], (unsigned long long)(t - tk));
+                tk = t;
+            }
+        };
         if (!b.src_stats) bin_src_stats<W, kB>(a, b, v0, nv, wd, cov_s, acc);
+        tick(kProbeSrc);
         auto pend = [&](uint32_t i) { return a.fold ? a.nw[v0 * W + i] : 0ull; };
         bool needy = !b.needy_check;
         for (uint32_t i = threadIdx.x; i < nv * W; i += kB) {
@@ -1486,6 +1521,11 @@ __global__ __launch_bounds__(kB) void k_bin_apply_runs(RoundArgs a, BinArgs b, u
             if (!b.needy_check) continue;
             const bool va = !a.dead_mode || bit_alive(a.alive, (uint32_t)(a.begin + v0 + i / W));
             needy |= va && (injm(a, i % W) & ~(a.seen[v0 * W + i] | pend(i))) != 0;
+        }
+        tick(kProbeInit);
+        if (b.probe && threadIdx.x == 0) {
+            atomicAdd(&b.probe[kProbeBins], 1ull);
+            atomicAdd(&b.probe[kProbeSlotsN], (unsigned long long)(bn.s1 - bn.s0));
         }
         if (!__syncthreads_or(needy)) {
             for (uint32_t i = threadIdx.x; i < nv * W; i += kB) {
@@ -1564,7 +1604,9 @@ __global__ __launch_bounds__(kB) void k_bin_apply_runs(RoundArgs a, BinArgs b, u
             }
         }
         __syncthreads();
+        tick(kProbeSlots);
         bin_finish<W, kWords, kB>(a, v0, nv, acc_s, acc);
+        tick(kProbeFinish);
     };
     // bins of XCD group x: [x * per, (x + 1) * per), block x + 8 j applying bin j of it (the blocks in flight
     // on an XCD apply consecutive bins)
@@ -2152,14 +2194,20 @@ __device__ __forceinline__ void retire_peer(const RoundArgs& a, uint32_t v, uint
 // One lane per peer (a wave covers two words of the alive bitset): each peer alive at the start of the
 // round draws its churn number, the wave's ballot of the deaths clears both words at once.  (Round 3 ran one
 // thread per word, drawing for its alive peers in turn: a chain of up to 32 Philox evaluations per thread,
-// 0.14 ms per round at config 5.)
+// 0.14 ms per round at config 5.)  The grid is kept small (each block ends with one atomic per stats field
+// on its stats line: 16384 blocks of them cost more than the draws, 0.2 ms per round) and strides with the
+// next alive word loaded ahead.
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_churn(RoundArgs a, uint32_t wd, uint32_t seed, uint32_t thr) {
     Acc acc;
     const int lane = threadIdx.x & 63;
-    const uint64_t n_pad = (a.n_global + 63) & ~63ull;
-    for (uint64_t v = (uint64_t)blockIdx.x * kBlock + threadIdx.x; v < n_pad; v += (uint64_t)gridDim.x * kBlock) {
-        const uint32_t word = v < a.n_global ? a.alive[v >> 5] : 0u;
+    const uint64_t n_pad = (a.n_global + 63) & ~63ull, stride = (uint64_t)gridDim.x * kBlock;
+    uint64_t v = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    uint32_t next = v < a.n_global ? a.alive[v >> 5] : 0u;
+    for (; v < n_pad; v += stride) {
+        // the word of the next iteration is loaded ahead (only this wave writes it, and later)
+        const uint32_t word = next;
+        next = v + stride < a.n_global ? a.alive[(v + stride) >> 5] : 0u;
         const bool live = (word >> (v & 31)) & 1u;
         const bool die = live && philox4x32_10(P_CHURN, a.round, 0, 0, seed, (uint32_t)v).x < thr;
         const unsigned long long dead = __ballot(die);
@@ -2258,20 +2306,38 @@ __global__ __launch_bounds__(kBlock) void k_apply_remote(RoundArgs a, const uint
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_send_bits(RoundArgs a, uint64_t chunk, uint64_t tpb, uint32_t world,
                                                       uint64_t* bits) {
+    // a wave per 64 tiles: lane l tests tile T0 + l against the round's marks (its peers span at most two
+    // marked 64-peer tiles), unmarked tiles get a zero bitmap word, and the wave reads the staging words of
+    // the marked ones in turn (a sparse round's send buffer is 2 GB at config 4; the marked tiles are few)
     const int lane = threadIdx.x & 63;
     const uint64_t tiles = (uint64_t)world * tpb;
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
-    for (uint64_t T = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); T < tiles; T += nwaves) {
-        const uint64_t q = T / tpb, t = T % tpb;
-        const uint64_t end = min((q + 1) * chunk, a.n_global);
-        const uint64_t v = q * chunk + t * 64 + lane;
-        bool any = false;
-        if (v < end) {
-#pragma unroll
-            for (int w = 0; w < W; ++w) any |= a.send[v * W + w] != 0ull;
+    for (uint64_t T0 = ((uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * 64; T0 < tiles;
+         T0 += nwaves * 64) {
+        const uint64_t T = T0 + lane;
+        bool mk = false;
+        if (T < tiles) {
+            const uint64_t q = T / tpb, t = T % tpb;
+            const uint64_t v0 = q * chunk + t * 64, end = min((q + 1) * chunk, a.n_global);
+            if (v0 < end) {
+                const uint64_t g0 = v0 >> 6, g1 = (min(v0 + 64, end) - 1) >> 6;
+                mk = ((a.smark[g0 >> 6] >> (g0 & 63)) | (a.smark[g1 >> 6] >> (g1 & 63))) & 1ull;
+            }
+            if (!mk) bits[T] = 0ull;
         }
-        const unsigned long long b = __ballot(any);
-        if (lane == 0) bits[T] = b;
+        for (unsigned long long todo = __ballot(mk); todo; todo &= todo - 1) {  // wave-uniform
+            const uint64_t Tm = T0 + (uint64_t)__builtin_ctzll(todo);
+            const uint64_t q = Tm / tpb, t = Tm % tpb;
+            const uint64_t end = min((q + 1) * chunk, a.n_global);
+            const uint64_t v = q * chunk + t * 64 + lane;
+            bool any = false;
+            if (v < end) {
+#pragma unroll
+                for (int w = 0; w < W; ++w) any |= a.send[v * W + w] != 0ull;
+            }
+            const unsigned long long b = __ballot(any);
+            if (lane == 0) bits[Tm] = b;
+        }
     }
 }
 
@@ -2418,7 +2484,7 @@ static inline uint32_t wp_of(uint32_t w) { return w & 0xFFFFu; }
 static inline uint32_t wd_of(uint32_t w) { return w >> 16; }
 
 hipError_t launch_churn(const RoundArgs& a, uint32_t W_, uint32_t seed, uint32_t threshold, hipStream_t s) {
-    const unsigned g = (unsigned)std::min<uint64_t>(grid_for(a.n_global, kBlock), 16384);
+    const unsigned g = (unsigned)std::min<uint64_t>(grid_for(a.n_global, kBlock), 2048);
     GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_churn<W>, dim3(g), dim3(kBlock), 0, s, a, wd_of(W_), seed,
                                                    threshold));
     return hipGetLastError();
@@ -2568,9 +2634,11 @@ hipError_t compact_send_scratch(uint64_t tiles, size_t* scan_bytes) {
 hipError_t launch_compact_send(const RoundArgs& a, uint32_t W_, uint64_t chunk, uint32_t world,
                                unsigned long long* counts, uint64_t* seg, uint64_t* bits, uint64_t* pos,
                                void* scan_tmp, size_t scan_bytes, hipStream_t s) {
+    if (!a.smark) return hipErrorInvalidValue;
     const uint64_t tpb = (chunk + 63) / 64, tiles = (uint64_t)world * tpb;
     const unsigned grid = (unsigned)std::min<uint64_t>(grid_for(tiles, kWavesPerBlock), 16384);
-    GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_send_bits<W>, dim3(grid), dim3(kBlock), 0, s, a, chunk, tpb,
+    const unsigned grid_b = (unsigned)std::min<uint64_t>(grid_for((tiles + 63) / 64, kWavesPerBlock), 4096);
+    GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_send_bits<W>, dim3(grid_b), dim3(kBlock), 0, s, a, chunk, tpb,
                                                    world, bits));
     if (hipError_t e = hipGetLastError()) return e;
     // (bits[tiles] is zero from the allocation: the scan's last element is the total)
@@ -2579,7 +2647,8 @@ hipError_t launch_compact_send(const RoundArgs& a, uint32_t W_, uint64_t chunk, 
     if (hipError_t e = hipcub::DeviceScan::ExclusiveSum(scan_tmp, tb, it, pos, (int)(tiles + 1), s)) return e;
     GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_send_pack<W>, dim3(grid), dim3(kBlock), 0, s, a, chunk, tpb,
                                                    world, bits, pos, counts, seg));
-    return hipGetLastError();
+    if (hipError_t e = hipGetLastError()) return e;
+    return hipMemsetAsync(a.smark, 0, smark_bytes(a.n_global), s);
 }
 
 hipError_t launch_apply_records(const RoundArgs& a, uint32_t W_, const uint64_t* rec, uint64_t n_rec, hipStream_t s) {

@@ -21,6 +21,8 @@ e.run()
 e.reset()
 e.enable_timing(True)
 C = ("#atomics", "#trav", "#heavy_trav", "#pulled", "#gathers", "#needy_rows", "#exit_gathers")
+if tuning.get("apply_probe"):  # the streamed apply's phase clocks (100 MHz ticks summed over bins)
+    C = C + ("#probe_src", "#probe_init", "#probe_slots", "#probe_finish", "#probe_bins", "#probe_slots_n")
 prev = {k: e.kernel_time(k)[0] for k in K}
 prevc = {k: e.kernel_bytes(k) for k in C}
 while True:
@@ -29,7 +31,16 @@ while True:
     d = {k: round(cur[k] - prev[k], 3) for k in K if cur[k] - prev[k] > 0}
     curc = {k: e.kernel_bytes(k) for k in C}
     dc = {k[1:]: int(curc[k] - prevc[k]) for k in C if curc[k] - prevc[k] > 0}
-    print(st["round"], f"F={st['frontier'] / w.n:.4f}", d, dc, flush=True)
+    extra = ""
+    if dc.get("probe_bins"):  # per-bin microseconds of each phase, and the phase's share of 256 CUs' time
+        nb = dc["probe_bins"]
+        extra = " probe us/bin " + str({k[6:]: round(dc.get(k, 0) / nb / 100, 2)
+                                        for k in ("probe_src", "probe_init", "probe_slots", "probe_finish")}) + \
+            " ms@256CU " + str({k[6:]: round(dc.get(k, 0) / 1e5 / 256, 3)
+                                for k in ("probe_src", "probe_init", "probe_slots", "probe_finish")}) + \
+            f" slots/bin {dc.get('probe_slots_n', 0) // nb}"
+        dc = {k: v for k, v in dc.items() if not k.startswith("probe")}
+    print(st["round"], f"F={st['frontier'] / w.n:.4f}", d, dc, extra, flush=True)
     prev, prevc = cur, curc
     if fin:
         break
