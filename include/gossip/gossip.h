@@ -335,7 +335,11 @@ gossip_status gossip_kernel_bytes(gossip_ctx* ctx, const char* kernel, double* b
  * pipeline shape, 0-3, A/B), "replay" (0: gossip_run never replays a
  * recorded schedule), "scatter_direct" (partitioned runs: a block's binned
  * scatter reads other blocks' source words from the gather buffer instead of
- * staging them; 0 default).  Layout keys
+ * staging them; 0 default), "apply_probe" (diagnostics: 1 clocks the
+ * streamed apply's phases per bin; gossip_kernel_bytes "#probe_src",
+ * "#probe_init", "#probe_slots", "#probe_finish" give 100 MHz ticks summed
+ * over bins, "#probe_bins" and "#probe_slots_n" the bins and slots; 0 off).
+ * Layout keys
  * apply at the next gossip_build_graph / gossip_load_csr ("list_cap": at the
  * next chain of needy-list rounds, never inside one).  GOSSIP_EINVAL: unknown key. */
 gossip_status gossip_set_tuning(gossip_ctx* ctx, const char* key, int64_t value);

@@ -1880,9 +1880,15 @@ __global__ __launch_bounds__(kBlock) void k_rows_light(RoundArgs a, uint32_t lo,
     const int lane = threadIdx.x & 63;
     const uint64_t n_tiles = (a.n_local + 63) >> 6;
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
-    for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); t < n_tiles; t += nwaves) {
+    // (a strided sweep: the death round of the tile after next is loaded ahead)
+    auto death = [&](uint64_t v) { return MODE != kRowsRev && v < a.n_local ? (uint32_t)a.death_r[v] : 0xFFFFu; };
+    uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    uint32_t dn = death((t << 6) + lane);
+    for (; t < n_tiles; t += nwaves) {
         const uint64_t v = (t << 6) + lane;
-        const bool act = v < a.n_local && row_selected<MODE>(a, v, lo, hi);
+        const uint32_t d = dn;
+        dn = death(((t + nwaves) << 6) + lane);
+        const bool act = v < a.n_local && (MODE == kRowsRev || (d != 0xFFFFu && d >= lo && d <= hi));
         if (!__any(act)) continue;
         uint32_t deg = 0;
         uint64_t rb = 0;
@@ -2765,8 +2771,9 @@ template <int MODE>
 static hipError_t launch_rows(const RoundArgs& a, uint32_t lo, uint32_t hi, hipStream_t s) {
     if (a.n_chunks)
         hipLaunchKernelGGL(k_rows_heavy<MODE>, dim3(grid_for(a.n_chunks, kWavesPerBlock)), dim3(kBlock), 0, s, a, lo, hi);
-    hipLaunchKernelGGL(k_rows_light<MODE>, dim3(grid_for((a.n_local + 63) / 64, kWavesPerBlock)), dim3(kBlock), 0, s, a,
-                       lo, hi);
+    // a strided sweep (a block per 4 tiles was 262 K blocks at config 5, most of them selecting nothing)
+    const unsigned g = (unsigned)std::min<uint64_t>(grid_for((a.n_local + 63) / 64, kWavesPerBlock), 8192);
+    hipLaunchKernelGGL(k_rows_light<MODE>, dim3(g), dim3(kBlock), 0, s, a, lo, hi);
     return hipGetLastError();
 }
 
