@@ -67,6 +67,30 @@ __host__ __device__ __forceinline__ uint32_t find_bin(const uint32_t* lo, uint32
     return i;
 }
 
+// Level 1's per-lane counters: Acc's fields, the counts held in 32 bits (a lane's share of one round stays
+// far below 2^32; deliveries, undelivered sends and the digest stay 64-bit).  Acc's 64-bit counters took
+// 22 of the kernel's 128 VGPRs and, with them, the staging loop spilled to scratch.
+struct PbAcc {
+    uint32_t frontier = 0, trav = 0, htrav = 0, covered = 0, fresh = 0, activated = 0, atomics = 0;
+    unsigned long long deliv = 0, undeliv = 0, digest = 0;
+    unsigned long long fresh_or[1] = {};
+    __device__ Acc full() const {
+        Acc f;
+        f.frontier = frontier;
+        f.trav = trav;
+        f.htrav = htrav;
+        f.covered = covered;
+        f.fresh = fresh;
+        f.activated = activated;
+        f.atomics = atomics;
+        f.deliv = deliv;
+        f.undeliv = undeliv;
+        f.digest = digest;
+        f.fresh_or[0] = fresh_or[0];
+        return f;
+    }
+};
+
 // ---------------------------------------------------------------------------
 // level 1: workgroup w's share of the frontier's deliveries -> coarse-bin records
 // ---------------------------------------------------------------------------
@@ -99,7 +123,7 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_scatter(RoundArgs a, PbArgs p, 
         while (c >= lo_s[k + 1]) ++k;
         return k;
     };
-    Acc acc;
+    PbAcc acc;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 
     // generation g of coarse bin k goes to place g * kPbB1 of the workgroup's segment:
@@ -162,7 +186,9 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_scatter(RoundArgs a, PbArgs p, 
         }
     };
     // kPbU deliveries per lane (c: destination, bit 31 = masked or no edge): statistics, then records
-    auto emit = [&](const uint32_t (&c)[kPbU], const unsigned long long (&m)[kPbU], const uint32_t (&pc)[kPbU]) {
+    // (each delivery's message count is the popcount of its word, recomputed here: carried per record it
+    // cost kPbU registers twice over and pushed the kernel past 128 VGPRs into scratch spills)
+    auto emit = [&](const uint32_t (&c)[kPbU], const unsigned long long (&m)[kPbU]) {
         bool rec[kPbU];
         uint32_t k[kPbU], al[kPbU];
 #pragma unroll
@@ -174,10 +200,10 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_scatter(RoundArgs a, PbArgs p, 
 #pragma unroll
         for (int j = 0; j < kPbU; ++j) {
             if (CA && rec[j] && !((al[j] >> (c[j] & 31)) & 1u)) {  // send() to a dead peer fails (peer.cpp:312)
-                acc.undeliv += pc[j];
+                acc.undeliv += (uint32_t)__popcll(m[j]);
                 rec[j] = false;
             } else if (rec[j]) {
-                acc.deliv += pc[j];  // sentTo.insert (peer.cpp:314)
+                acc.deliv += (uint32_t)__popcll(m[j]);  // sentTo.insert (peer.cpp:314)
             }
         }
         direct(c, m, rec);
@@ -188,19 +214,14 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_scatter(RoundArgs a, PbArgs p, 
 
     // (1) heavy chunks wg, wg + kPbGrid, ..., one wave each (their rows' words are cleared by the split)
     {
-        const unsigned long long trav0 = acc.trav;
+        const uint32_t trav0 = acc.trav;
         for (uint64_t ci = wg + (uint64_t)wave * kPbGrid; ci < a.n_chunks; ci += (uint64_t)kPbGrid * kPbWaves) {
             const HeavyChunk ch = a.chunks[ci];
             const unsigned long long m = a.nw[ch.v];
             if (!m) continue;  // wave-uniform
-            const uint32_t pc = (uint32_t)__popcll(m);
             unsigned long long ms[kPbU];
-            uint32_t pcs[kPbU];
 #pragma unroll
-            for (int j = 0; j < kPbU; ++j) {
-                ms[j] = m;
-                pcs[j] = pc;
-            }
+            for (int j = 0; j < kPbU; ++j) ms[j] = m;
             for (uint64_t b = ch.e0; b < ch.e1; b += 64 * kPbU) {
                 uint32_t c[kPbU];
 #pragma unroll
@@ -208,7 +229,7 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_scatter(RoundArgs a, PbArgs p, 
                     const uint64_t e = b + j * 64 + lane;
                     c[j] = e < ch.e1 ? a.col[e] : kMaskedEdge;
                 }
-                emit(c, ms, pcs);
+                emit(c, ms);
             }
         }
         acc.htrav = acc.trav - trav0;
@@ -225,7 +246,6 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_scatter(RoundArgs a, PbArgs p, 
             const bool have = (uint32_t)lane < cnt;
             const uint64_t v = have ? pv[lane] : 0;
             const unsigned long long m = have ? pm[lane] : 0ull;
-            const uint32_t pc = (uint32_t)__popcll(m);
             uint32_t deg = 0;
             uint64_t rb = 0;
             if (have) {
@@ -252,31 +272,29 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_scatter(RoundArgs a, PbArgs p, 
             const uint32_t excl = incl - deg;
             const uint32_t total = __shfl(incl, 63);
             // batch base's deliveries; the next batch's col loads are issued before this one is emitted
-            uint32_t c[kPbU], pcs[kPbU], c2[kPbU], pcs2[kPbU];
+            uint32_t c[kPbU], c2[kPbU];
             unsigned long long ms[kPbU], ms2[kPbU];
-            auto batch = [&](uint32_t base, uint32_t (&c_)[kPbU], uint32_t (&pc_)[kPbU], unsigned long long (&m_)[kPbU]) {
+            auto batch = [&](uint32_t base, uint32_t (&c_)[kPbU], unsigned long long (&m_)[kPbU]) {
                 uint64_t e[kPbU];
 #pragma unroll
                 for (int j = 0; j < kPbU; ++j) {
                     const uint32_t q = base + j * 64 + lane;
                     const int s = src_lane(incl, q);
                     e[j] = __shfl(rb, s) + (uint64_t)(q - __shfl(excl, s));
-                    pc_[j] = __shfl(pc, s);
                     m_[j] = __shfl(m, s);
                 }
 #pragma unroll
                 for (int j = 0; j < kPbU; ++j) c_[j] = base + j * 64 + lane < total ? a.col[e[j]] : kMaskedEdge;
             };
-            if (total) batch(0, c, pcs, ms);
+            if (total) batch(0, c, ms);
             for (uint32_t base = 0; base < total; base += 64 * kPbU) {
                 const bool more = base + 64 * kPbU < total;  // wave-uniform
-                if (more) batch(base + 64 * kPbU, c2, pcs2, ms2);
-                emit(c, ms, pcs);
+                if (more) batch(base + 64 * kPbU, c2, ms2);
+                emit(c, ms);
                 if (!more) break;
 #pragma unroll
                 for (int j = 0; j < kPbU; ++j) {
                     c[j] = c2[j];
-                    pcs[j] = pcs2[j];
                     ms[j] = ms2[j];
                 }
             }
@@ -336,7 +354,8 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_scatter(RoundArgs a, PbArgs p, 
     }
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < nc; k += kPbBlock) p.s1_len[(uint64_t)wg * nc + k] = stage_len(tk_s, k, kPbB1);
-    flush<kPbWaves>(acc, a.st);
+    Acc fa = acc.full();
+    flush<kPbWaves>(fa, a.st);
     if (COV) {
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < 64; i += kPbBlock)

@@ -1396,15 +1396,27 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_stream(RoundArgs a, BinAr
         auto pieces = [&](auto dir) {
         constexpr bool kDirect = decltype(dir)::value;
         auto word = [&](uint64_t u) { return kDirect ? src[u] : (uint64_t)slice[u]; };
+        // Software-pipelined: the cb entries of a lane's next batch are loaded before the current batch's
+        // words are stored.  vmcnt counts loads and stores in issue order, so a batch whose loads follow the
+        // previous batch's stores waits for those stores' acknowledgements as well; issued one batch ahead,
+        // the loads only wait behind one batch of stores.  (Unpipelined, and with the scheduler free to sink
+        // the first piece's LDS read and its wait between the loads, a wave had about one batch in flight.)
+        constexpr uint64_t kStep = (uint64_t)kScatterBlock * kU;
         if (W == 1) {
             // piece k = entries 2k, 2k + 1 (cb_src read as one u32: 4-B aligned)
             const uint64_t k0 = un.p0 >> 1, k1 = (un.p1 + 1) >> 1;
             const uint32_t* cb2 = reinterpret_cast<const uint32_t*>(b.cb_src);
-            for (uint64_t kb = k0 + threadIdx.x; kb < k1; kb += (uint64_t)kScatterBlock * kU) {
-                uint32_t sv[kU];
+            auto load = [&](uint64_t kb, uint32_t (&o)[kU]) {
 #pragma unroll
                 for (int j = 0; j < kU; ++j)
-                    sv[j] = __builtin_nontemporal_load(cb2 + min(kb + (uint64_t)j * kScatterBlock, k1 - 1));
+                    o[j] = __builtin_nontemporal_load(cb2 + min(kb + (uint64_t)j * kScatterBlock, k1 - 1));
+            };
+            uint32_t sv[kU], nv[kU];
+            uint64_t kb = k0 + threadIdx.x;
+            if (kb < k1) load(kb, sv);
+            for (; kb < k1; kb += kStep) {
+                load(kb + kStep, nv);  // (unconditional: clamped, and one wait count on every path)
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int j = 0; j < kU; ++j) {
                     const uint64_t k = kb + (uint64_t)j * kScatterBlock;
@@ -1423,14 +1435,21 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_stream(RoundArgs a, BinAr
                         if (e + 1 >= un.p0 && e + 1 < un.p1) b.val[e + 1] = x1;
                     }
                 }
+#pragma unroll
+                for (int j = 0; j < kU; ++j) sv[j] = nv[j];
             }
         } else {
             const uint64_t k0 = un.p0 * kPW, k1 = un.p1 * kPW;
-            for (uint64_t kb = k0 + threadIdx.x; kb < k1; kb += (uint64_t)kScatterBlock * kU) {
-                uint32_t sv[kU];
+            auto load = [&](uint64_t kb, uint32_t (&o)[kU]) {
 #pragma unroll
-                for (int j = 0; j < kU; ++j)
-                    sv[j] = b.cb_src[min(kb + (uint64_t)j * kScatterBlock, k1 - 1) / kPW];
+                for (int j = 0; j < kU; ++j) o[j] = b.cb_src[min(kb + (uint64_t)j * kScatterBlock, k1 - 1) / kPW];
+            };
+            uint32_t sv[kU], nv[kU];
+            uint64_t kb = k0 + threadIdx.x;
+            if (kb < k1) load(kb, sv);
+            for (; kb < k1; kb += kStep) {
+                load(kb + kStep, nv);  // (unconditional: clamped, and one wait count on every path)
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int j = 0; j < kU; ++j) {
                     const uint64_t k = kb + (uint64_t)j * kScatterBlock;
@@ -1442,6 +1461,8 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_stream(RoundArgs a, BinAr
                     y.y = word((uint64_t)u * W + w0 + 1);
                     reinterpret_cast<u64x2*>(b.val)[k] = y;  // entry k / kPW, words w0, w0 + 1
                 }
+#pragma unroll
+                for (int j = 0; j < kU; ++j) sv[j] = nv[j];
             }
         }
         };

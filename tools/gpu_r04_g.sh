@@ -6,7 +6,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/${1:-r04g}; mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests/test_gpu_group.py -x -q --timeout 200 --timeout-method thread > $O/group.log 2>&1 || { grep -E "FAIL|Error|assert|Timeout" $O/group.log | head -30; tail -5 $O/group.log; exit 1; }
 tail -1 $O/group.log
-timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread -k "stream or workload_parity or rejoin or apply_probe" > $O/parity.log 2>&1 || { grep -E "FAIL|Error|assert|Timeout" $O/parity.log | head -30; tail -5 $O/parity.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread -k "stream or workload_parity or rejoin or apply_probe or blocked or deferred" > $O/parity.log 2>&1 || { grep -E "FAIL|Error|assert|Timeout" $O/parity.log | head -30; tail -5 $O/parity.log; exit 1; }
 tail -1 $O/parity.log
 timeout -k 10 300 python3 -u tools/round_profile.py 4 t.apply_probe=1 > $O/rounds_c4_probe.txt 2>&1 || { tail -20 $O/rounds_c4_probe.txt; exit 1; }
 grep -E "^(3|4|5|6|7) " $O/rounds_c4_probe.txt | cut -c1-400
