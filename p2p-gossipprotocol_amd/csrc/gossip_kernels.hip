@@ -583,15 +583,21 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
             }
             acc.frontier++;
             acc.covered += pc;
-            if (!a.dead_mode) {  // every edge alive and unmasked
-                acc.trav += dg;
-                acc.deliv += (unsigned long long)pc * dg;
-            } else if (a.dgone) {  // from the per-source counters; else k_src_count books them
-                const uint32_t g = a.dgone[v], k = a.dmask[v];
-                acc.trav += dg - k;
-                acc.deliv += (unsigned long long)pc * (dg - g);
-                acc.undeliv += (unsigned long long)pc * (g - k);
+            // (the increments as values added once: written as two branches' own updates, the compiler merged
+            // them into one store through a selected address and moved the counters to scratch memory)
+            uint64_t dt = dg, dd = (uint64_t)pc * dg, du = 0;  // every edge alive and unmasked
+            if (a.dead_mode) {
+                dt = dd = 0;
+                if (a.dgone) {  // from the per-source counters; else k_src_count books them
+                    const uint32_t g = a.dgone[v], k = a.dmask[v];
+                    dt = dg - k;
+                    dd = (uint64_t)pc * (dg - g);
+                    du = (uint64_t)pc * (g - k);
+                }
             }
+            acc.trav += dt;
+            acc.deliv += dd;
+            acc.undeliv += du;
         }
         const bool enq = needy && dg > 0 && dg <= a.heavy;  // heavy rows: k_pull_heavy
         const unsigned long long bal = __ballot(enq);
