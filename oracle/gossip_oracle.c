@@ -588,7 +588,7 @@ static uint64_t do_churn(oracle_sim* s, uint32_t r) {
     if (s->cfg.churn_threshold) {
         for (uint64_t v = 0; v < s->n; ++v) {
             if (!s->alive[v]) continue;
-            uint32_t x = philox_x(s->cfg.seed, (uint32_t)v, ORACLE_P_CHURN, r, 0, 0, 0);
+            uint32_t x = philox_x(s->cfg.seed, (uint32_t)(v >> 2), ORACLE_P_CHURN, r, 0, 0, (int)(v & 3));
             if (x < s->cfg.churn_threshold) { s->alive[v] = 0; ++died; }
         }
     }
@@ -985,7 +985,7 @@ int oracle_part_begin(oracle_part* p, int requested_pull) {
     if (p->cfg.churn_threshold) {
         for (uint64_t v = 0; v < p->n; ++v) {
             if (!p->alive[v]) continue;
-            if (philox_x(p->cfg.seed, (uint32_t)v, ORACLE_P_CHURN, r, 0, 0, 0) < p->cfg.churn_threshold) {
+            if (philox_x(p->cfg.seed, (uint32_t)(v >> 2), ORACLE_P_CHURN, r, 0, 0, (int)(v & 3)) < p->cfg.churn_threshold) {
                 p->alive[v] = 0;
                 if (owned(p, v)) st->died++;
             }

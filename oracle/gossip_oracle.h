@@ -40,7 +40,7 @@ enum {
     ORACLE_P_DEGREE = 1,  /* ctr {1, response, 0, 0}.x  -> k draw (peer.cpp:220-222) */
     ORACLE_P_TARGET = 2,  /* ctr {2, response, i>>2, 0}[i&3] -> candidate i (powerlaw) */
     ORACLE_P_SHUFFLE = 3, /* ctr {3, response, d>>2, 0}[d&3] -> Fisher-Yates draw d (peer.cpp:224-225) */
-    ORACLE_P_CHURN = 4,   /* ctr {4, round, 0, 0}.x -> peer dies if < churn_threshold */
+    ORACLE_P_CHURN = 4,   /* key {seed, v >> 2}, ctr {4, round, 0, 0}, lane v & 3 -> peer v dies if < churn_threshold */
     ORACLE_P_ORIGIN = 5,  /* key {seed, 0xFFFFFFFF}, ctr {5, k, attempt, 0}.x -> origin k */
     ORACLE_P_REBOOT = 6,  /* ctr {6, round, dead, 0}.x -> k draw; ctr {6, round, dead, 1+(i>>2)}[i&3] -> candidate i */
     ORACLE_P_REJOIN = 7   /* ctr {7, round, 0, 0}.x -> a dead peer restarts if < rejoin_threshold, .y -> k draw;

@@ -2224,32 +2224,42 @@ __device__ __forceinline__ void retire_peer(const RoundArgs& a, uint32_t v, uint
     }
 }
 
-// One lane per peer (a wave covers two words of the alive bitset): each peer alive at the start of the
-// round draws its churn number, the wave's ballot of the deaths clears both words at once.  (Round 3 ran one
-// thread per word, drawing for its alive peers in turn: a chain of up to 32 Philox evaluations per thread,
-// 0.14 ms per round at config 5.)  The grid is kept small (each block ends with one atomic per stats field
-// on its stats line: 16384 blocks of them cost more than the draws, 0.2 ms per round) and strides with the
-// next alive word loaded ahead.
+// One lane per quad of peers (P_CHURN: one Philox draw per 4 peers, lane v & 3 of it is peer v's churn
+// number), so a wave covers eight words of the alive bitset: each peer alive at the start of the round is
+// tested, the eight lanes of a word OR their deaths together and one of them clears the word.  The draws
+// bound the kernel (VALU: ten rounds of 32-bit multiplies each); round 3 drew once per peer, in a chain of
+// up to 32 per thread, and took 0.14 ms per round at config 5, one draw per peer and lane 0.2 ms.  A small
+// grid strides over the quads with the next alive word loaded ahead.
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_churn(RoundArgs a, uint32_t wd, uint32_t seed, uint32_t thr) {
     Acc acc;
     const int lane = threadIdx.x & 63;
-    const uint64_t n_pad = (a.n_global + 63) & ~63ull, stride = (uint64_t)gridDim.x * kBlock;
-    uint64_t v = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    uint32_t next = v < a.n_global ? a.alive[v >> 5] : 0u;
-    for (; v < n_pad; v += stride) {
+    const uint64_t n_quads = (a.n_global + 3) >> 2;
+    const uint64_t q_pad = (n_quads + 63) & ~63ull, stride = (uint64_t)gridDim.x * kBlock;
+    uint64_t q = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    uint32_t next = q < n_quads ? a.alive[q >> 3] : 0u;
+    for (; q < q_pad; q += stride) {  // (wave-uniform: q_pad and the wave's quads are 64-aligned)
         // the word of the next iteration is loaded ahead (only this wave writes it, and later)
         const uint32_t word = next;
-        next = v + stride < a.n_global ? a.alive[(v + stride) >> 5] : 0u;
-        const bool live = (word >> (v & 31)) & 1u;
-        const bool die = live && philox4x32_10(P_CHURN, a.round, 0, 0, seed, (uint32_t)v).x < thr;
-        const unsigned long long dead = __ballot(die);
-        if (!dead) continue;  // wave-uniform
-        if ((lane & 31) == 0) {  // lanes 0 and 32: their words
-            const uint32_t dw = (uint32_t)(dead >> (lane & 32));
-            if (dw) a.alive[v >> 5] = word & ~dw;
+        next = q + stride < n_quads ? a.alive[(q + stride) >> 3] : 0u;
+        const uint64_t v0 = q << 2;
+        uint32_t live = (word >> (v0 & 31)) & 0xFu;
+        if (v0 + 4 > a.n_global) live &= v0 < a.n_global ? (1u << (uint32_t)(a.n_global - v0)) - 1u : 0u;
+        uint32_t die = 0;
+        if (live) {
+            const u32x4 r = philox4x32_10(P_CHURN, a.round, 0, 0, seed, (uint32_t)q);
+            die = (uint32_t)(r.x < thr) | (uint32_t)(r.y < thr) << 1 | (uint32_t)(r.z < thr) << 2 |
+                  (uint32_t)(r.w < thr) << 3;
+            die &= live;
         }
-        if (die) retire_peer<W>(a, (uint32_t)v, wd, acc);
+        // lanes 8k .. 8k + 7 hold the quads of one alive word
+        uint32_t dw = die << (4 * (lane & 7));
+        dw |= (uint32_t)__shfl_xor((int)dw, 1);
+        dw |= (uint32_t)__shfl_xor((int)dw, 2);
+        dw |= (uint32_t)__shfl_xor((int)dw, 4);
+        if (!__ballot(die != 0)) continue;  // wave-uniform
+        if ((lane & 7) == 0 && dw) a.alive[q >> 3] = word & ~dw;
+        for (uint32_t m = die; m; m &= m - 1) retire_peer<W>(a, (uint32_t)(v0 + (uint32_t)__builtin_ctz(m)), wd, acc);
     }
     flush(acc, a.st);
 }
@@ -2517,7 +2527,7 @@ static inline uint32_t wp_of(uint32_t w) { return w & 0xFFFFu; }
 static inline uint32_t wd_of(uint32_t w) { return w >> 16; }
 
 hipError_t launch_churn(const RoundArgs& a, uint32_t W_, uint32_t seed, uint32_t threshold, hipStream_t s) {
-    const unsigned g = (unsigned)std::min<uint64_t>(grid_for(a.n_global, kBlock), 2048);
+    const unsigned g = (unsigned)std::min<uint64_t>(grid_for((a.n_global + 3) / 4, kBlock), 2048);
     GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_churn<W>, dim3(g), dim3(kBlock), 0, s, a, wd_of(W_), seed,
                                                    threshold));
     return hipGetLastError();

@@ -146,7 +146,7 @@ __global__ __launch_bounds__(kB) void k_tiny_run(TinyArgs t) {
             __syncthreads();
             for (uint32_t p = threadIdx.x; p < t.n; p += kB) {
                 if (!tbit(alive, p)) continue;
-                if (philox4x32_10(P_CHURN, r, 0, 0, t.seed, p).x >= t.churn) continue;
+                if (lane_of(philox4x32_10(P_CHURN, r, 0, 0, t.seed, p >> 2), p & 3) >= t.churn) continue;
                 atomicAnd(&alive[p >> 5], ~(1u << (p & 31)));
                 v[kTDied]++;
 #pragma unroll

@@ -15,7 +15,7 @@ enum : uint32_t {
     P_DEGREE = 1,   // {1, response, 0, 0}.x        k draw            (peer.cpp:220-222)
     P_TARGET = 2,   // {2, response, i>>2, 0}[i&3]  candidate i       (powerlaw list)
     P_SHUFFLE = 3,  // {3, response, d>>2, 0}[d&3]  Fisher-Yates draw (peer.cpp:224-225)
-    P_CHURN = 4,    // {4, round, 0, 0}.x           death test
+    P_CHURN = 4,    // key {seed, v >> 2}, {4, round, 0, 0}[v & 3]: death test of peer v (one draw per 4 peers)
     P_ORIGIN = 5,   // key {seed, ~0u}, {5, k, attempt, 0}.x  origin pick
     P_REBOOT = 6,   // {6, round, dead, 0}.x k draw; {6, round, dead, 1+(i>>2)}[i&3] candidate i (re-bootstrap)
     P_REJOIN = 7,   // {7, round, 0, 0}.x restart test, .y k draw; {7, round, 1+(i>>2), 0}[i&3] candidate i
