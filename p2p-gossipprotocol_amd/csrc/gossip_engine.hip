@@ -219,6 +219,9 @@ struct gossip_ctx {
     bool cur_clear_all = false;  // (the round in flight does)
     bool scatter_direct = false; // "scatter_direct": a vertex block's scatter reads other blocks' words directly
     unsigned long long* d_probe = nullptr;  // "apply_probe": the streamed apply's phase clocks (kProbeN slots)
+    bool apply_persist = true;   // "apply_persist": the streamed apply as 256 workgroups taking bins from
+                                 // per-XCD counters (d_work), not one workgroup per bin
+    uint32_t* d_work = nullptr;  // (8 counters, zeroed by each launch)
     bool needy_skip = true;      // "bin_needy_skip": binned rounds with over one missing pair per peer skip the
                                  // apply's needy test
     uint64_t* seg = nullptr;     // sparse push: per-destination record segments (world x chunk records)
@@ -704,7 +707,7 @@ BinArgs bin_args(const gossip_ctx* c, bool noskip, uint32_t src_side) {
                    s.n_chunks,  s.chunk,    s.units,     s.xcd_units, s.bdst,    s.val,      s.bin_words,
                    s.dummy,     noskip ? 1u : 0u, s.n_runs ? s.n_runs - 1 : 0, s.ap_run, s.ap_grp,
                    c->bin_stream ? 1u : 0u, s.deg, src_side, c->apply_pipe, c->scatter_direct && c->gather ? 1u : 0u,
-                   1u,          c->d_probe};
+                   1u,          c->apply_persist && c->bin_stream ? c->d_work : nullptr, c->d_probe};
 }
 
 gossip_status tune_val(gossip_ctx* c) {
@@ -1347,6 +1350,8 @@ gossip_status round_compute(gossip_ctx* c) {
     if (c->last_pull && a.dead_mode && !a.dgone)  // else the per-source counters give the source side
         HIPCHK(timed(c, "src_count", [&] { return launch_src_count(a, pw, c->stream); }));
     if (c->last_bin) {
+        if (c->apply_persist && c->bin_stream && !c->d_work)
+            HIPCHK(hipMalloc((void**)&c->d_work, 8 * sizeof(uint32_t)));
         BinArgs b = bin_args(c, c->bins_first, src_stats(c));
         // every bin is needy while more than one (peer, message) pair per peer is missing: no check pass
         b.needy_check = c->cur_missing > c->n_local && c->needy_skip ? 0u : 1u;
@@ -1796,6 +1801,7 @@ gossip_status gossip_set_tuning(gossip_ctx* c, const char* key, int64_t value) {
         if (value < 0 || value > 3) return fail(GOSSIP_EINVAL, "apply_pipe must be 0..3");
         c->apply_pipe = (uint32_t)value;
     }
+    else if (k == "apply_persist") c->apply_persist = value != 0;
     else if (k == "apply_probe") {  // diagnostics: the streamed apply's phase clocks, read back as #probe_*
         if (value && !c->d_probe) {
             if (hipMalloc((void**)&c->d_probe, kProbeN * sizeof(unsigned long long)) != hipSuccess)
@@ -1804,6 +1810,7 @@ gossip_status gossip_set_tuning(gossip_ctx* c, const char* key, int64_t value) {
                 return fail(GOSSIP_EHIP, "apply_probe buffer");
         } else if (!value && c->d_probe) {
             hipFree(c->d_probe);
+    hipFree(c->d_work);
             c->d_probe = nullptr;
         }
     }

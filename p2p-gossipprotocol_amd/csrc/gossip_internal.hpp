@@ -112,6 +112,8 @@ struct BinArgs {
                                   // unit of each chunk, row bounds loaded after the slice); 0: the apply
                                   // does, for its bin's peers (bin_src_stats), and the scatter's staging is
                                   // one round trip
+    uint32_t* work;               // persistent streamed apply ("apply_persist"): one bin counter per XCD group
+                                  // of workgroups, zeroed by the launch; null: one workgroup per bin
     unsigned long long* probe;    // "apply_probe" (diagnostics): the streamed apply's per-phase wall-clock
                                   // ticks summed over bins (kProbe* slots); null otherwise
 };

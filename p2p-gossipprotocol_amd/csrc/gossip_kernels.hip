@@ -1635,10 +1635,25 @@ __global__ __launch_bounds__(kB) void k_bin_apply_runs(RoundArgs a, BinArgs b, u
         bin_finish<W, kWords, kB>(a, v0, nv, acc_s, acc);
         tick(kProbeFinish);
     };
-    // bins of XCD group x: [x * per, (x + 1) * per), block x + 8 j applying bin j of it (the blocks in flight
-    // on an XCD apply consecutive bins)
-    const uint32_t xg = blockIdx.x & 7, member = blockIdx.x >> 3, per = (uint32_t)((b.n_bins + 7) / 8);
-    if (member < per && xg * per + member < b.n_bins) apply_bin(xg * per + member);
+    // bins of XCD group x: [x * per, (x + 1) * per), applied by the blocks x + 8 j (the blocks in flight on
+    // an XCD apply consecutive bins): block x + 8 j applies bin j, or (b.work) the 32 resident blocks of the
+    // group take the group's bins in turn from its counter.  Persistent, a block flushes its stats once and no
+    // block is launched per bin: the phase clocks of apply_probe summed to 5.8 ms of the 8.2 ms launch at
+    // config 4 with one block per bin.
+    const uint32_t xg = blockIdx.x & 7, per = (uint32_t)((b.n_bins + 7) / 8);
+    if (b.work) {
+        __shared__ uint32_t next_s;
+        while (true) {
+            if (threadIdx.x == 0) next_s = atomicAdd(&b.work[xg], 1u);
+            __syncthreads();  // (every thread read the previous value before apply_bin's first barrier)
+            const uint32_t j = next_s;
+            if (j >= per || xg * per + j >= b.n_bins) break;  // block-uniform
+            apply_bin(xg * per + j);
+        }
+    } else {
+        const uint32_t member = blockIdx.x >> 3;
+        if (member < per && xg * per + member < b.n_bins) apply_bin(xg * per + member);
+    }
     flush<kWaves>(acc, a.st);
     if (!b.src_stats && a.cov) {
         __syncthreads();
@@ -2726,7 +2741,12 @@ hipError_t launch_bin_apply(const RoundArgs& a, const BinArgs& b, uint32_t W_, h
     if (!b.n_bins) return hipSuccess;
     const uint32_t wd = wd_of(W_);
     if (b.stream) {
-        const unsigned sgrid = (unsigned)((b.n_bins + 7) / 8 * 8);  // whole groups of 8 (XCD-contiguous bins)
+        unsigned sgrid = (unsigned)((b.n_bins + 7) / 8 * 8);  // whole groups of 8 (XCD-contiguous bins)
+        if (b.work) {  // persistent: the resident blocks (one per CU at either accumulator size's occupancy)
+            const unsigned resident = b.bin_words > kBinWords / 2 ? 256u : 512u;
+            sgrid = std::min(sgrid, resident);
+            if (hipError_t e = hipMemsetAsync(b.work, 0, 8 * sizeof(uint32_t), s)) return e;
+        }
         if (b.bin_words > kBinWords / 2 && wp_of(W_) == 1 && b.apply_pipe) {  // A/B pipeline shapes (one word)
             if (b.apply_pipe == 1)
                 hipLaunchKernelGGL((k_bin_apply_runs<1, kBinWords, 1024, 1>), dim3(sgrid), dim3(1024), 0, s, a, b, wd);
