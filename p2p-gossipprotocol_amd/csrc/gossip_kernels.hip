@@ -2408,18 +2408,28 @@ __global__ __launch_bounds__(kBlock) void k_send_pack(RoundArgs a, uint64_t chun
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
     const uint64_t gid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (gid < world) counts[gid] = pos[(gid + 1) * tpb] - pos[gid * tpb];  // records per destination
-    for (uint64_t T = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); T < tiles; T += nwaves) {
-        const uint64_t b = bits[T];
-        if (!((b >> lane) & 1)) continue;
-        const uint64_t q = T / tpb, t = T % tpb;
-        const uint64_t v = q * chunk + t * 64 + lane;
-        const uint64_t idx = pos[T] - pos[q * tpb] + (uint64_t)__popcll(b & ((1ull << lane) - 1));
-        uint64_t* rec = seg + (q * chunk + idx) * (1 + W);
-        rec[0] = v;
+    // a wave per 64 tiles: one coalesced read of their bitmap words, then the tiles with records in turn
+    // (a wave per tile waited on one bitmap word per tile: 64 round trips per wave at config 4, P = 8)
+    for (uint64_t T0 = ((uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * 64; T0 < tiles;
+         T0 += nwaves * 64) {
+        const uint64_t bl = T0 + lane < tiles ? bits[T0 + lane] : 0ull;
+        for (unsigned long long todo = __ballot(bl != 0); todo; todo &= todo - 1) {  // wave-uniform
+            const int src = __builtin_ctzll(todo);
+            const uint64_t T = T0 + (uint64_t)src;
+            const uint64_t b = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(bl >> 32), src) << 32) |
+                               (uint32_t)__shfl((int)(uint32_t)bl, src);
+            if ((b >> lane) & 1) {
+                const uint64_t q = T / tpb, t = T % tpb;
+                const uint64_t v = q * chunk + t * 64 + lane;
+                const uint64_t idx = pos[T] - pos[q * tpb] + (uint64_t)__popcll(b & ((1ull << lane) - 1));
+                uint64_t* rec = seg + (q * chunk + idx) * (1 + W);
+                rec[0] = v;
 #pragma unroll
-        for (int w = 0; w < W; ++w) {
-            rec[1 + w] = a.send[v * W + w];
-            a.send[v * W + w] = 0ull;
+                for (int w = 0; w < W; ++w) {
+                    rec[1 + w] = a.send[v * W + w];
+                    a.send[v * W + w] = 0ull;
+                }
+            }
         }
     }
 }
@@ -2694,7 +2704,6 @@ hipError_t launch_compact_send(const RoundArgs& a, uint32_t W_, uint64_t chunk, 
                                void* scan_tmp, size_t scan_bytes, hipStream_t s) {
     if (!a.smark) return hipErrorInvalidValue;
     const uint64_t tpb = (chunk + 63) / 64, tiles = (uint64_t)world * tpb;
-    const unsigned grid = (unsigned)std::min<uint64_t>(grid_for(tiles, kWavesPerBlock), 16384);
     const unsigned grid_b = (unsigned)std::min<uint64_t>(grid_for((tiles + 63) / 64, kWavesPerBlock), 4096);
     GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_send_bits<W>, dim3(grid_b), dim3(kBlock), 0, s, a, chunk, tpb,
                                                    world, bits));
@@ -2703,8 +2712,8 @@ hipError_t launch_compact_send(const RoundArgs& a, uint32_t W_, uint64_t chunk, 
     hipcub::TransformInputIterator<uint64_t, PopOp, const uint64_t*> it(bits, PopOp());
     size_t tb = scan_bytes;
     if (hipError_t e = hipcub::DeviceScan::ExclusiveSum(scan_tmp, tb, it, pos, (int)(tiles + 1), s)) return e;
-    GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_send_pack<W>, dim3(grid), dim3(kBlock), 0, s, a, chunk, tpb,
-                                                   world, bits, pos, counts, seg));
+    GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_send_pack<W>, dim3(std::max(grid_b, grid_for(world, kBlock))),
+                                                   dim3(kBlock), 0, s, a, chunk, tpb, world, bits, pos, counts, seg));
     if (hipError_t e = hipGetLastError()) return e;
     return hipMemsetAsync(a.smark, 0, smark_bytes(a.n_global), s);
 }
