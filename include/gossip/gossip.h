@@ -338,7 +338,9 @@ gossip_status gossip_kernel_bytes(gossip_ctx* ctx, const char* kernel, double* b
  * staging them; 0 default), "apply_probe" (diagnostics: 1 clocks the
  * streamed apply's phases per bin; gossip_kernel_bytes "#probe_src",
  * "#probe_init", "#probe_slots", "#probe_finish" give 100 MHz ticks summed
- * over bins, "#probe_bins" and "#probe_slots_n" the bins and slots; 0 off).
+ * over bins, "#probe_bins" and "#probe_slots_n" the bins and slots,
+ * "#probe_block" and "#probe_blocks" the workgroups' lifetimes and count;
+ * 0 off).
  * Layout keys
  * apply at the next gossip_build_graph / gossip_load_csr ("list_cap": at the
  * next chain of needy-list rounds, never inside one).  GOSSIP_EINVAL: unknown key. */

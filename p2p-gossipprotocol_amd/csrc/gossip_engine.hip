@@ -2431,13 +2431,14 @@ gossip_status gossip_kernel_time(gossip_ctx* c, const char* kernel, double* ms, 
 gossip_status gossip_kernel_bytes(gossip_ctx* c, const char* kernel, double* bytes) {
     if (!c || !kernel || !bytes) return fail(GOSSIP_EINVAL, "null argument");
     if (c->d_probe && !strncmp(kernel, "#probe_", 7)) {  // apply_probe's clocks (a device read: syncs)
-        static const char* const names[] = {"src", "init", "slots", "finish", "bins", "slots_n"};
+        static const char* const names[] = {"src",    "init",   "slots",  "finish", "bins",   "slots_n", "block", "blocks",
+                                            "xcd0",   "xcd1",   "xcd2",   "xcd3",   "xcd4",   "xcd5",    "xcd6",  "xcd7"};
         unsigned long long h[kProbeN];
         if (hipStreamSynchronize(c->stream) != hipSuccess ||
             hipMemcpy(h, c->d_probe, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess)
             return fail(GOSSIP_EHIP, "apply_probe read");
         *bytes = 0.0;
-        for (int i = 0; i < 6; ++i)
+        for (int i = 0; i < kProbeN; ++i)
             if (!strcmp(kernel + 7, names[i])) *bytes = (double)h[i];
         return GOSSIP_OK;
     }

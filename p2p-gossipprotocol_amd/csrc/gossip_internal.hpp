@@ -118,7 +118,8 @@ struct BinArgs {
                                   // ticks summed over bins (kProbe* slots); null otherwise
 };
 // apply_probe slots: wall-clock (100 MHz) ticks of the streamed apply's phases, summed over bins
-enum { kProbeSrc = 0, kProbeInit, kProbeSlots, kProbeFinish, kProbeBins, kProbeSlotsN, kProbeN = 8 };
+enum { kProbeSrc = 0, kProbeInit, kProbeSlots, kProbeFinish, kProbeBins, kProbeSlotsN, kProbeBlock, kProbeBlocks,
+       kProbeXcd, kProbeN = kProbeXcd + 8 };  // kProbeXcd + x: lifetimes of the blocks of XCD group x
 
 struct BinState {
     Bin* bins = nullptr;

@@ -1523,6 +1523,7 @@ __global__ __launch_bounds__(kB) void k_bin_apply_runs(RoundArgs a, BinArgs b, u
         for (uint32_t i = threadIdx.x; i < 64 * W; i += kB) cov_s[i] = 0;
     const unsigned long long upto = lane == 63 ? ~0ull : (2ull << lane) - 1;  // lanes 0..lane
     const uint32_t run_max = (uint32_t)b.n_runs_m1;
+    const uint64_t t_block = b.probe ? wall_clock64() : 0;  // apply_probe: the block's lifetime
     auto apply_bin = [&](const uint32_t bi) {
         const Bin bn = b.bins[bi];
         const uint32_t nv = bn.v1 - bn.v0;
@@ -1653,6 +1654,12 @@ __global__ __launch_bounds__(kB) void k_bin_apply_runs(RoundArgs a, BinArgs b, u
     } else {
         const uint32_t member = blockIdx.x >> 3;
         if (member < per && xg * per + member < b.n_bins) apply_bin(xg * per + member);
+    }
+    if (b.probe && threadIdx.x == 0) {
+        const unsigned long long life = wall_clock64() - t_block;
+        atomicAdd(&b.probe[kProbeBlock], life);
+        atomicAdd(&b.probe[kProbeXcd + xg], life);
+        atomicAdd(&b.probe[kProbeBlocks], 1ull);
     }
     flush<kWaves>(acc, a.st);
     if (!b.src_stats && a.cov) {
