@@ -2432,7 +2432,8 @@ gossip_status gossip_kernel_bytes(gossip_ctx* c, const char* kernel, double* byt
     if (!c || !kernel || !bytes) return fail(GOSSIP_EINVAL, "null argument");
     if (c->d_probe && !strncmp(kernel, "#probe_", 7)) {  // apply_probe's clocks (a device read: syncs)
         static const char* const names[] = {"src",    "init",   "slots",  "finish", "bins",   "slots_n", "block", "blocks",
-                                            "xcd0",   "xcd1",   "xcd2",   "xcd3",   "xcd4",   "xcd5",    "xcd6",  "xcd7"};
+                                            "xcd0",   "xcd1",   "xcd2",   "xcd3",   "xcd4",   "xcd5",    "xcd6",  "xcd7",
+                                            "sxcd0",  "sxcd1",  "sxcd2",  "sxcd3",  "sxcd4",  "sxcd5",   "sxcd6", "sxcd7"};
         unsigned long long h[kProbeN];
         if (hipStreamSynchronize(c->stream) != hipSuccess ||
             hipMemcpy(h, c->d_probe, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess)

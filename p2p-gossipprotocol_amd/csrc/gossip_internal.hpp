@@ -119,7 +119,8 @@ struct BinArgs {
 };
 // apply_probe slots: wall-clock (100 MHz) ticks of the streamed apply's phases, summed over bins
 enum { kProbeSrc = 0, kProbeInit, kProbeSlots, kProbeFinish, kProbeBins, kProbeSlotsN, kProbeBlock, kProbeBlocks,
-       kProbeXcd, kProbeN = kProbeXcd + 8 };  // kProbeXcd + x: lifetimes of the blocks of XCD group x
+       kProbeXcd, kProbeSXcd = kProbeXcd + 8, kProbeN = kProbeSXcd + 8 };
+// (kProbeXcd + x: lifetimes of the apply's blocks of XCD group x; kProbeSXcd + x: the streamed scatter's)
 
 struct BinState {
     Bin* bins = nullptr;

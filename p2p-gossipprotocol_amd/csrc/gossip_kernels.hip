@@ -1383,6 +1383,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_stream(RoundArgs a, BinAr
         for (int i = threadIdx.x; i < 64 * W; i += kScatterBlock) cov_s[i] = 0;
     }
     Acc acc;
+    const uint64_t t_block = b.probe ? wall_clock64() : 0;  // apply_probe: the block's lifetime
     auto unit = [&](const uint64_t ui) {
         const BinUnit un = b.units[ui];
         if (un.p0 >= un.p1 && !un.first) return;  // padding of a row (block-uniform)
@@ -1476,6 +1477,8 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_stream(RoundArgs a, BinAr
         else pieces(std::false_type{});
     };
     scatter_rows(b, unit);
+    if (b.probe && threadIdx.x == 0)
+        atomicAdd(&b.probe[kProbeSXcd + (blockIdx.x & 7)], (unsigned long long)(wall_clock64() - t_block));
     flush<kWaves>(acc, a.st);
     if (COV) {
         __syncthreads();
@@ -1636,24 +1639,23 @@ __global__ __launch_bounds__(kB) void k_bin_apply_runs(RoundArgs a, BinArgs b, u
         bin_finish<W, kWords, kB>(a, v0, nv, acc_s, acc);
         tick(kProbeFinish);
     };
-    // bins of XCD group x: [x * per, (x + 1) * per), applied by the blocks x + 8 j (the blocks in flight on
-    // an XCD apply consecutive bins): block x + 8 j applies bin j, or (b.work) the 32 resident blocks of the
-    // group take the group's bins in turn from its counter.  Persistent, a block flushes its stats once and no
-    // block is launched per bin: the phase clocks of apply_probe summed to 5.8 ms of the 8.2 ms launch at
-    // config 4 with one block per bin.
-    const uint32_t xg = blockIdx.x & 7, per = (uint32_t)((b.n_bins + 7) / 8);
+    // bins j * 8 + x go to XCD group x (the blocks x + 8 i): with one block per bin, block i applies bin i;
+    // persistent (b.work), the 32 resident blocks of group x take j from the group's counter.  Bins of
+    // low peer ids cost more (config 4: contiguous eighths of the bins per XCD group took 7.9 ms for the
+    // first and 5.5 ms for the last, and the launch lasted as long as the first), so every group takes
+    // every eighth bin.  Persistent, a block also flushes its stats once.
+    const uint32_t xg = blockIdx.x & 7;
     if (b.work) {
         __shared__ uint32_t next_s;
         while (true) {
             if (threadIdx.x == 0) next_s = atomicAdd(&b.work[xg], 1u);
             __syncthreads();  // (every thread read the previous value before apply_bin's first barrier)
-            const uint32_t j = next_s;
-            if (j >= per || xg * per + j >= b.n_bins) break;  // block-uniform
-            apply_bin(xg * per + j);
+            const uint64_t bi = (uint64_t)next_s * 8 + xg;
+            if (bi >= b.n_bins) break;  // block-uniform
+            apply_bin((uint32_t)bi);
         }
-    } else {
-        const uint32_t member = blockIdx.x >> 3;
-        if (member < per && xg * per + member < b.n_bins) apply_bin(xg * per + member);
+    } else if (blockIdx.x < b.n_bins) {
+        apply_bin(blockIdx.x);
     }
     if (b.probe && threadIdx.x == 0) {
         const unsigned long long life = wall_clock64() - t_block;
