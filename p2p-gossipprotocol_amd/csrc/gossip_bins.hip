@@ -468,17 +468,19 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
     }
 
     // scatter work units (every chunk has at least one: its first unit books
-    // the chunk's source-side stats).  The chunk sequence is cut into 8
-    // contiguous ranges of equal entry counts, one per XCD.  Row mode (the
-    // default): inside an XCD's range a unit is a whole chunk, except hub
-    // chunks (more than kHubFactor times the mean), which are cut into units
-    // of about the mean; the list is padded to rows of kScatterGrid / 8 units,
-    // member j of the XCD takes unit j of every row, so the workgroups of a
-    // row stage consecutive chunks and write adjacent slot runs in every bin
-    // at about the same time (adjacent runs can merge in the XCD's L2; with
-    // the single-role scatter 36.0 against 39.2 ms per step for capped units
-    // dealt round-robin; global rows over all XCDs
-    // measured no better).
+    // the chunk's source-side stats).  Row mode: a unit is a whole chunk, except
+    // hub chunks (more than kHubFactor times the mean), which are cut into units
+    // of about the mean; the units, in chunk order, form rows of kScatterGrid / 8,
+    // row r goes to XCD r % 8, and member j of the XCD takes unit j of each of
+    // its rows, so the workgroups of a row stage consecutive chunks and write
+    // adjacent slot runs in every bin at about the same time (adjacent runs can
+    // merge in the XCD's L2; with the single-role scatter 36.0 against 39.2 ms
+    // per step for capped units dealt round-robin; global
+    // rows over all XCDs measured no better).  Rows are dealt round-robin over
+    // the XCDs (round 4): cut into 8 contiguous ranges of equal entry counts,
+    // the XCD of the high-id chunks (more, shorter chunks: more staging per
+    // entry) took 4.8 ms and the first 3.6 (config 4, k_bin_stream).
+    // xcd_units[8] holds the unit count (a multiple of the row length).
     {
         std::vector<uint64_t> cbeg(n_chunks + 1);
         BCHECK(hipMemcpy(cbeg.data(), st.chunk_begin, (n_chunks + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost));
@@ -487,20 +489,14 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
         const uint64_t members = kScatterGrid / 8;
         {
             const uint64_t mean = std::max<uint64_t>(1024, upos / std::max<uint64_t>(1, n_chunks));
-            uint64_t c = 0, acc = 0;
-            for (int x = 0; x < 8; ++x) {
-                xu[x] = units.size();
-                const uint64_t want = upos * (uint64_t)(x + 1) / 8;
-                for (; c < n_chunks && (x == 7 || acc < want); ++c) {
-                    const uint64_t len = cbeg[c + 1] - cbeg[c];
-                    acc += len;
-                    const uint64_t k = len > kHubFactor * mean ? (len + mean - 1) / mean : 1;
-                    for (uint64_t j = 0; j < k; ++j)
-                        units.push_back(
-                            BinUnit{(uint32_t)c, j == 0 ? 1u : 0u, cbeg[c] + len * j / k, cbeg[c] + len * (j + 1) / k});
-                }
-                while ((units.size() - xu[x]) % members) units.push_back(BinUnit{0u, 0u, 0, 0});  // empty: skipped
+            for (uint64_t c = 0; c < n_chunks; ++c) {
+                const uint64_t len = cbeg[c + 1] - cbeg[c];
+                const uint64_t k = len > kHubFactor * mean ? (len + mean - 1) / mean : 1;
+                for (uint64_t j = 0; j < k; ++j)
+                    units.push_back(
+                        BinUnit{(uint32_t)c, j == 0 ? 1u : 0u, cbeg[c] + len * j / k, cbeg[c] + len * (j + 1) / k});
             }
+            while (units.size() % members) units.push_back(BinUnit{0u, 0u, 0, 0});  // empty: skipped
             xu[8] = units.size();
         }
         st.n_units = units.size();

@@ -61,6 +61,7 @@ constexpr uint32_t kBinChunkWords = 18432;     // source chunk: its new words (1
 constexpr uint64_t kHubFactor = 4;             // chunks with more than 4x the mean cb entries are split into units
 constexpr int kScatterBlock = 1024;            // k_bin_scatter_lds: one 16-wave workgroup per CU
 constexpr int kScatterGrid = 256;              // one workgroup per CU
+constexpr uint32_t kApplyRow = 32;            // streamed apply: consecutive bins one XCD group applies together
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 constexpr uint16_t kRunStart = 0x8000u;        // cb_src flag; chunk-local sources are < kBinChunkWords < 2^15
 static_assert(kBinChunkWords < kRunStart, "chunk-local sources fit 15 bits");

@@ -1037,9 +1037,10 @@ __device__ __forceinline__ void scatter_stage(const RoundArgs& a, const BinArgs&
 // row barrier on top of that measured no gain: 71.4 against 71.3 ms per step).
 template <class F>
 __device__ __forceinline__ void scatter_rows(const BinArgs& b, F&& unit) {
+    // rows of `members` units, row r on XCD r % 8 (gossip_bins.hip; xcd_units[8]: the unit count)
     const uint32_t xcd = blockIdx.x & 7, member = blockIdx.x >> 3, members = gridDim.x >> 3;
-    const uint64_t u1 = b.xcd_units[xcd + 1];
-    for (uint64_t ui = b.xcd_units[xcd] + member; ui < u1; ui += members) unit(ui);
+    const uint64_t rows = b.xcd_units[8] / members;
+    for (uint64_t r = xcd; r < rows; r += 8) unit(r * members + member);
 }
 
 // Producer/consumer scatter (slot layout).  Measured on the round-1 single-role kernel: a wave that both
@@ -1639,23 +1640,29 @@ __global__ __launch_bounds__(kB) void k_bin_apply_runs(RoundArgs a, BinArgs b, u
         bin_finish<W, kWords, kB>(a, v0, nv, acc_s, acc);
         tick(kProbeFinish);
     };
-    // bins j * 8 + x go to XCD group x (the blocks x + 8 i): with one block per bin, block i applies bin i;
-    // persistent (b.work), the 32 resident blocks of group x take j from the group's counter.  Bins of
-    // low peer ids cost more (config 4: contiguous eighths of the bins per XCD group took 7.9 ms for the
-    // first and 5.5 ms for the last, and the launch lasted as long as the first), so every group takes
-    // every eighth bin.  Persistent, a block also flushes its stats once.
+    // Rows of kApplyRow consecutive bins, row r to XCD group r % 8 (the blocks x + 8 i): member j of group x
+    // applies bin (j / kApplyRow * 8 + x) * kApplyRow + j % kApplyRow.  The blocks resident on an XCD apply
+    // consecutive bins, whose runs sit next to each other in every chunk (lines shared at run ends come
+    // through that XCD's L2 once), and every group gets every eighth row.  (Measured at config 4, per XCD
+    // group: contiguous eighths of the bins took 7.9 ms for the first and 5.5 ms for the last -- bins of
+    // low peer ids hold more, shorter runs -- and the launch lasted as long as the first; single bins dealt
+    // round-robin balanced the groups but every bin's slots took 114 instead of 88 us.)  With one block per
+    // bin, member j is blockIdx.x / 8; persistent (b.work), the group's resident blocks take j from its
+    // counter, and a block flushes its stats once.
     const uint32_t xg = blockIdx.x & 7;
+    auto bin_of = [&](uint64_t j) { return ((j / kApplyRow) * 8 + xg) * kApplyRow + j % kApplyRow; };
     if (b.work) {
         __shared__ uint32_t next_s;
         while (true) {
             if (threadIdx.x == 0) next_s = atomicAdd(&b.work[xg], 1u);
             __syncthreads();  // (every thread read the previous value before apply_bin's first barrier)
-            const uint64_t bi = (uint64_t)next_s * 8 + xg;
-            if (bi >= b.n_bins) break;  // block-uniform
+            const uint64_t bi = bin_of(next_s);
+            if (bi >= b.n_bins) break;  // block-uniform; later j only map further
             apply_bin((uint32_t)bi);
         }
-    } else if (blockIdx.x < b.n_bins) {
-        apply_bin(blockIdx.x);
+    } else {
+        const uint64_t bi = bin_of(blockIdx.x >> 3);
+        if (bi < b.n_bins) apply_bin((uint32_t)bi);
     }
     if (b.probe && threadIdx.x == 0) {
         const unsigned long long life = wall_clock64() - t_block;
@@ -2759,7 +2766,9 @@ hipError_t launch_bin_apply(const RoundArgs& a, const BinArgs& b, uint32_t W_, h
     if (!b.n_bins) return hipSuccess;
     const uint32_t wd = wd_of(W_);
     if (b.stream) {
-        unsigned sgrid = (unsigned)((b.n_bins + 7) / 8 * 8);  // whole groups of 8 (XCD-contiguous bins)
+        // one block per bin: every (row, member) of every group's rows (k_bin_apply_runs: bin_of)
+        const uint64_t rows = (b.n_bins + kApplyRow - 1) / kApplyRow;
+        unsigned sgrid = (unsigned)((rows + 7) / 8 * 8 * kApplyRow);
         if (b.work) {  // persistent: the resident blocks (one per CU at either accumulator size's occupancy)
             const unsigned resident = b.bin_words > kBinWords / 2 ? 256u : 512u;
             sgrid = std::min(sgrid, resident);
