@@ -702,12 +702,38 @@ gossip_status upload_csr(gossip_ctx* c, const uint64_t* rp, const uint32_t* col,
 // five processes each: scatter 9.3-11.3 (mean 9.9) against 9.7-11.7 (mean 10.4) ms.  The trial words
 // are garbage: the first binned round rewrites every slot.
 BinArgs bin_args(const gossip_ctx* c, bool noskip, uint32_t src_side) {
+    // (field by field: a positional initializer put src_side into apply_pipe and the tuning keys one field
+    // off, unnoticed because every path it selected computes the same results)
     const BinState& s = c->bins;
-    return BinArgs{s.bins,      s.n_bins,   s.cb_src,    s.cb_run,   s.cb_grp,   s.n_binned, s.chunk_begin,
-                   s.n_chunks,  s.chunk,    s.units,     s.xcd_units, s.bdst,    s.val,      s.bin_words,
-                   s.dummy,     noskip ? 1u : 0u, s.n_runs ? s.n_runs - 1 : 0, s.ap_run, s.ap_grp,
-                   c->bin_stream ? 1u : 0u, s.deg, src_side, c->apply_pipe, c->scatter_direct && c->gather ? 1u : 0u,
-                   1u,          c->apply_persist && c->bin_stream ? c->d_work : nullptr, c->d_probe};
+    BinArgs b{};
+    b.bins = s.bins;
+    b.n_bins = s.n_bins;
+    b.cb_src = s.cb_src;
+    b.cb_run = s.cb_run;
+    b.cb_grp = s.cb_grp;
+    b.n_binned = s.n_binned;
+    b.chunk_begin = s.chunk_begin;
+    b.n_chunks = s.n_chunks;
+    b.chunk = s.chunk;
+    b.units = s.units;
+    b.xcd_units = s.xcd_units;
+    b.bdst = s.bdst;
+    b.val = s.val;
+    b.bin_words = s.bin_words;
+    b.dummy = s.dummy;
+    b.noskip = noskip ? 1u : 0u;
+    b.n_runs_m1 = s.n_runs ? s.n_runs - 1 : 0;
+    b.ap_run = s.ap_run;
+    b.ap_grp = s.ap_grp;
+    b.stream = c->bin_stream ? 1u : 0u;
+    b.deg = s.deg;
+    b.apply_pipe = c->apply_pipe;
+    b.direct = c->scatter_direct && c->gather ? 1u : 0u;
+    b.needy_check = 1u;
+    b.src_stats = src_side;
+    b.work = c->apply_persist && c->bin_stream ? c->d_work : nullptr;
+    b.probe = c->d_probe;
+    return b;
 }
 
 gossip_status tune_val(gossip_ctx* c) {
