@@ -214,7 +214,7 @@ struct gossip_ctx {
     bool cur_defer = false;       // this round defers: advance() folds nx into seen
     bool full_liveness = false;  // "full_liveness": ping every edge each ping round (A/B against closed form)
     uint64_t cur_missing = 0;    // (peer, message) pairs still missing at the round's push start (round_begin)
-    uint32_t apply_pipe = 0;     // "apply_pipe": the streamed apply's pipeline shape (0-3, A/B)
+    uint32_t apply_pipe = 2;     // "apply_pipe": the streamed apply's pipeline shape (0-3; 2 measured best)
     bool pb_clear_all = true;    // "blocked_clear_all": wide blocked rounds clear new words whole in level 2
     bool cur_clear_all = false;  // (the round in flight does)
     bool scatter_direct = false; // "scatter_direct": a vertex block's scatter reads other blocks' words directly
@@ -1378,6 +1378,8 @@ gossip_status round_compute(gossip_ctx* c) {
     if (c->last_bin) {
         if (c->apply_persist && c->bin_stream && !c->d_work)
             HIPCHK(hipMalloc((void**)&c->d_work, 8 * sizeof(uint32_t)));
+        if (c->apply_persist && c->bin_stream)  // the apply's bin counters, zeroed with the round's first launch
+            HIPCHK(queue_zero(c, c->d_work, 8 * sizeof(uint32_t)));
         BinArgs b = bin_args(c, c->bins_first, src_stats(c));
         // every bin is needy while more than one (peer, message) pair per peer is missing: no check pass
         b.needy_check = c->cur_missing > c->n_local && c->needy_skip ? 0u : 1u;
@@ -2458,8 +2460,7 @@ gossip_status gossip_kernel_bytes(gossip_ctx* c, const char* kernel, double* byt
     if (!c || !kernel || !bytes) return fail(GOSSIP_EINVAL, "null argument");
     if (c->d_probe && !strncmp(kernel, "#probe_", 7)) {  // apply_probe's clocks (a device read: syncs)
         static const char* const names[] = {"src",    "init",   "slots",  "finish", "bins",   "slots_n", "block", "blocks",
-                                            "xcd0",   "xcd1",   "xcd2",   "xcd3",   "xcd4",   "xcd5",    "xcd6",  "xcd7",
-                                            "sxcd0",  "sxcd1",  "sxcd2",  "sxcd3",  "sxcd4",  "sxcd5",   "sxcd6", "sxcd7"};
+                                            "xcd0",   "xcd1",   "xcd2",   "xcd3",   "xcd4",   "xcd5",    "xcd6",  "xcd7"};
         unsigned long long h[kProbeN];
         if (hipStreamSynchronize(c->stream) != hipSuccess ||
             hipMemcpy(h, c->d_probe, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess)

@@ -114,14 +114,13 @@ struct BinArgs {
                                   // does, for its bin's peers (bin_src_stats), and the scatter's staging is
                                   // one round trip
     uint32_t* work;               // persistent streamed apply ("apply_persist"): one bin counter per XCD group
-                                  // of workgroups, zeroed by the launch; null: one workgroup per bin
+                                  // of workgroups, zero at the launch; null: one workgroup per bin
     unsigned long long* probe;    // "apply_probe" (diagnostics): the streamed apply's per-phase wall-clock
                                   // ticks summed over bins (kProbe* slots); null otherwise
 };
 // apply_probe slots: wall-clock (100 MHz) ticks of the streamed apply's phases, summed over bins
 enum { kProbeSrc = 0, kProbeInit, kProbeSlots, kProbeFinish, kProbeBins, kProbeSlotsN, kProbeBlock, kProbeBlocks,
-       kProbeXcd, kProbeSXcd = kProbeXcd + 8, kProbeN = kProbeSXcd + 8 };
-// (kProbeXcd + x: lifetimes of the apply's blocks of XCD group x; kProbeSXcd + x: the streamed scatter's)
+       kProbeXcd, kProbeN = kProbeXcd + 8 };  // (kProbeXcd + x: lifetimes of the blocks of XCD group x)
 
 struct BinState {
     Bin* bins = nullptr;

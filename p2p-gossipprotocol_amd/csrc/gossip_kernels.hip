@@ -1384,7 +1384,6 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_stream(RoundArgs a, BinAr
         for (int i = threadIdx.x; i < 64 * W; i += kScatterBlock) cov_s[i] = 0;
     }
     Acc acc;
-    const uint64_t t_block = b.probe ? wall_clock64() : 0;  // apply_probe: the block's lifetime
     auto unit = [&](const uint64_t ui) {
         const BinUnit un = b.units[ui];
         if (un.p0 >= un.p1 && !un.first) return;  // padding of a row (block-uniform)
@@ -1478,8 +1477,6 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_stream(RoundArgs a, BinAr
         else pieces(std::false_type{});
     };
     scatter_rows(b, unit);
-    if (b.probe && threadIdx.x == 0)
-        atomicAdd(&b.probe[kProbeSXcd + (blockIdx.x & 7)], (unsigned long long)(wall_clock64() - t_block));
     flush<kWaves>(acc, a.st);
     if (COV) {
         __syncthreads();
@@ -1510,9 +1507,9 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_stream(RoundArgs a, BinAr
 template <int W, int kPipe> struct ApplyPipe { static constexpr int kG = W == 1 ? 4 : W == 2 ? 2 : 1, LA = 3, LB = 2, LC = 1; };
 template <> struct ApplyPipe<1, 1> { static constexpr int kG = 2, LA = 5, LB = 3, LC = 1; };
 template <> struct ApplyPipe<1, 2> { static constexpr int kG = 2, LA = 5, LB = 4, LC = 2; };
-template <> struct ApplyPipe<1, 3> { static constexpr int kG = 3, LA = 4, LB = 2, LC = 1; };
+template <> struct ApplyPipe<1, 3> { static constexpr int kG = 2, LA = 6, LB = 5, LC = 3; };
 
-template <int W, int kWords, int kB, int kPipe = 0>
+template <int W, int kWords, int kB, int kPipe = 0, bool kProbe = false>  // kProbe: apply_probe's clocks
 __global__ __launch_bounds__(kB) void k_bin_apply_runs(RoundArgs a, BinArgs b, uint32_t wd) {
     constexpr int kWaves = kB / 64;
     constexpr int kG = ApplyPipe<W, kPipe>::kG;                      // groups per stage
@@ -1527,16 +1524,16 @@ __global__ __launch_bounds__(kB) void k_bin_apply_runs(RoundArgs a, BinArgs b, u
         for (uint32_t i = threadIdx.x; i < 64 * W; i += kB) cov_s[i] = 0;
     const unsigned long long upto = lane == 63 ? ~0ull : (2ull << lane) - 1;  // lanes 0..lane
     const uint32_t run_max = (uint32_t)b.n_runs_m1;
-    const uint64_t t_block = b.probe ? wall_clock64() : 0;  // apply_probe: the block's lifetime
+    const uint64_t t_block = kProbe ? wall_clock64() : 0;  // apply_probe: the block's lifetime
     auto apply_bin = [&](const uint32_t bi) {
         const Bin bn = b.bins[bi];
         const uint32_t nv = bn.v1 - bn.v0;
         const uint64_t v0 = bn.v0;
         __syncthreads();  // the previous bin is done with acc_s (and cov_s is initialised)
         // apply_probe (diagnostics): thread 0 clocks the phases, with a barrier after each one
-        uint64_t tk = b.probe ? wall_clock64() : 0;
+        uint64_t tk = kProbe ? wall_clock64() : 0;
         auto tick = [&](int slot) {
-            if (!b.probe) return;
+            if (!kProbe) return;
             __syncthreads();
             if (threadIdx.x == 0) {
                 const uint64_t t = wall_clock64();
@@ -1555,7 +1552,7 @@ __global__ __launch_bounds__(kB) void k_bin_apply_runs(RoundArgs a, BinArgs b, u
             needy |= va && (injm(a, i % W) & ~(a.seen[v0 * W + i] | pend(i))) != 0;
         }
         tick(kProbeInit);
-        if (b.probe && threadIdx.x == 0) {
+        if (kProbe && threadIdx.x == 0) {
             atomicAdd(&b.probe[kProbeBins], 1ull);
             atomicAdd(&b.probe[kProbeSlotsN], (unsigned long long)(bn.s1 - bn.s0));
         }
@@ -1664,7 +1661,7 @@ __global__ __launch_bounds__(kB) void k_bin_apply_runs(RoundArgs a, BinArgs b, u
         const uint64_t bi = bin_of(blockIdx.x >> 3);
         if (bi < b.n_bins) apply_bin((uint32_t)bi);
     }
-    if (b.probe && threadIdx.x == 0) {
+    if (kProbe && threadIdx.x == 0) {
         const unsigned long long life = wall_clock64() - t_block;
         atomicAdd(&b.probe[kProbeBlock], life);
         atomicAdd(&b.probe[kProbeXcd + xg], life);
@@ -2769,13 +2766,17 @@ hipError_t launch_bin_apply(const RoundArgs& a, const BinArgs& b, uint32_t W_, h
         // one block per bin: every (row, member) of every group's rows (k_bin_apply_runs: bin_of)
         const uint64_t rows = (b.n_bins + kApplyRow - 1) / kApplyRow;
         unsigned sgrid = (unsigned)((rows + 7) / 8 * 8 * kApplyRow);
-        if (b.work) {  // persistent: the resident blocks (one per CU at either accumulator size's occupancy)
+        if (b.work) {  // persistent: the resident blocks; b.work was zeroed before the round's scatter
             const unsigned resident = b.bin_words > kBinWords / 2 ? 256u : 512u;
             sgrid = std::min(sgrid, resident);
-            if (hipError_t e = hipMemsetAsync(b.work, 0, 8 * sizeof(uint32_t), s)) return e;
         }
-        if (b.bin_words > kBinWords / 2 && wp_of(W_) == 1 && b.apply_pipe) {  // A/B pipeline shapes (one word)
-            if (b.apply_pipe == 1)
+        if (b.bin_words > kBinWords / 2 && wp_of(W_) == 1) {  // one word: the pipeline shapes (A/B), the probe
+            if (b.probe)
+                hipLaunchKernelGGL((k_bin_apply_runs<1, kBinWords, 1024, 2, true>), dim3(sgrid), dim3(1024), 0, s, a, b,
+                                   wd);
+            else if (b.apply_pipe == 0)
+                hipLaunchKernelGGL((k_bin_apply_runs<1, kBinWords, 1024, 0>), dim3(sgrid), dim3(1024), 0, s, a, b, wd);
+            else if (b.apply_pipe == 1)
                 hipLaunchKernelGGL((k_bin_apply_runs<1, kBinWords, 1024, 1>), dim3(sgrid), dim3(1024), 0, s, a, b, wd);
             else if (b.apply_pipe == 2)
                 hipLaunchKernelGGL((k_bin_apply_runs<1, kBinWords, 1024, 2>), dim3(sgrid), dim3(1024), 0, s, a, b, wd);

@@ -23,8 +23,7 @@ e.enable_timing(True)
 C = ("#atomics", "#trav", "#heavy_trav", "#pulled", "#gathers", "#needy_rows", "#exit_gathers")
 if tuning.get("apply_probe"):  # the streamed apply's phase clocks (100 MHz ticks summed over bins)
     C = C + ("#probe_src", "#probe_init", "#probe_slots", "#probe_finish", "#probe_bins", "#probe_slots_n",
-             "#probe_block", "#probe_blocks") + tuple(f"#probe_xcd{x}" for x in range(8)) + \
-        tuple(f"#probe_sxcd{x}" for x in range(8))
+             "#probe_block", "#probe_blocks") + tuple(f"#probe_xcd{x}" for x in range(8))
 prev = {k: e.kernel_time(k)[0] for k in K}
 prevc = {k: e.kernel_bytes(k) for k in C}
 while True:
@@ -42,8 +41,7 @@ while True:
                                 for k in ("probe_src", "probe_init", "probe_slots", "probe_finish")}) + \
             f" slots/bin {dc.get('probe_slots_n', 0) // nb}" + \
             f" blocks {dc.get('probe_blocks', 0)} block-lifetime ms@256CU {dc.get('probe_block', 0) / 1e5 / 256:.3f}" + \
-            " per XCD group ms@32CU " + str([round(dc.get(f"probe_xcd{x}", 0) / 1e5 / 32, 3) for x in range(8)]) + \
-            " scatter " + str([round(dc.get(f"probe_sxcd{x}", 0) / 1e5 / 32, 3) for x in range(8)])
+            " per XCD group ms@32CU " + str([round(dc.get(f"probe_xcd{x}", 0) / 1e5 / 32, 3) for x in range(8)])
         dc = {k: v for k, v in dc.items() if not k.startswith("probe")}
     print(st["round"], f"F={st['frontier'] / w.n:.4f}", d, dc, extra, flush=True)
     prev, prevc = cur, curc
