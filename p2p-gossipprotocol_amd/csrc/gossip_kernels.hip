@@ -492,6 +492,8 @@ __global__ __launch_bounds__(kBlock) void k_frontier_bits(RoundArgs a) {
 // already holds all of need.
 constexpr int kRowQ = 128;    // queue entries per wave
 template <int W, bool COV, bool FRONT, int kRowB>  // kRowB: edges per lane per step
+// (116 VGPRs, four waves per SIMD.  Launch bounds asking five or six spill to scratch and ran round 7 at
+// 5.9-6.1 and 8.3-8.6 ms against 4.8-5.1: the sweep and the row state do not fit 96 or 80 registers.)
 __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) {
     __shared__ unsigned int cov_s[COV ? 64 * W : 1];
     __shared__ uint32_t q_v[kWavesPerBlock][kRowQ];
