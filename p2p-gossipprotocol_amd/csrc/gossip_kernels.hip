@@ -570,6 +570,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
             nd[w] = va ? injm_full(a, w) & ~sv : 0ull;
             act |= m[w] != 0;
             needy |= (nd[w] & injm(a, w)) != 0;
+            if (vv) a.nx[v * W + w] = 0ull;  // nx is written whole in a pull round; rows that learn rewrite it
         }
         const uint64_t rb = d.r0, d_ = d.r1 - d.r0;
         const uint64_t dg = (act || needy) ? d_ : 0ull;
@@ -601,11 +602,6 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
             acc.undeliv += du;
         }
         const bool enq = needy && dg > 0 && dg <= a.heavy;  // heavy rows: k_pull_heavy
-        // nx is written whole in a pull round: here for the rows not queued (heavy rows too: k_pull_heavy ORs
-        // into it), by the row's finish for the queued ones (one store instead of a zero and a rewrite)
-        if (vv && !enq)
-#pragma unroll
-            for (int w = 0; w < W; ++w) a.nx[v * W + w] = 0ull;
         const unsigned long long bal = __ballot(enq);
         if (enq) {
             const uint32_t pos = (q_tail + (uint32_t)__builtin_amdgcn_mbcnt_hi(
@@ -710,9 +706,9 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
                 // still lacking a bit in flight: the only rows that can learn later (no injections: the next
                 // round's bits in flight are this round's receipts, a subset of this round's)
                 lacks |= (need[w] & injm(a, w) & ~fr) != 0;
-                a.nx[(uint64_t)rv * W + w] = fr;  // (the sweep left a queued row's nx to this store)
                 if (fr) {
                     a.seen[(uint64_t)rv * W + w] = (injm_full(a, w) & ~need[w]) | fr;  // within inj_mask
+                    a.nx[(uint64_t)rv * W + w] = fr;
                     pc += (uint32_t)__popcll(fr);
                     if (a.st_pre && w < (int)wd) pre.digest += digest_weight(((uint64_t)a.begin + rv) * wd + w) * fr;
                     any = true;
