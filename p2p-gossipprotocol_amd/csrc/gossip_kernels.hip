@@ -570,7 +570,10 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
             nd[w] = va ? injm_full(a, w) & ~sv : 0ull;
             act |= m[w] != 0;
             needy |= (nd[w] & injm(a, w)) != 0;
-            if (vv) a.nx[v * W + w] = 0ull;  // nx is written whole in a pull round; rows that learn rewrite it
+            // nx is written whole in a pull round; rows that learn rewrite it.  (Leaving a queued row's word to
+            // its finish alone turned these whole-line stores into partial ones: round 7 5.2-5.7 against
+            // 4.8-5.1 ms.)
+            if (vv) a.nx[v * W + w] = 0ull;
         }
         const uint64_t rb = d.r0, d_ = d.r1 - d.r0;
         const uint64_t dg = (act || needy) ? d_ : 0ull;
