@@ -2771,14 +2771,11 @@ hipError_t launch_bin_apply(const RoundArgs& a, const BinArgs& b, uint32_t W_, h
         // one block per bin: every (row, member) of every group's rows (k_bin_apply_runs: bin_of)
         const uint64_t rows = (b.n_bins + kApplyRow - 1) / kApplyRow;
         unsigned sgrid = (unsigned)((rows + 7) / 8 * 8 * kApplyRow);
-        // 16-wave workgroups for big bins, and for any bins when there are no more than one per CU (config 2:
-        // 256 bins of 4 K words); 8-wave ones, two per CU, otherwise
-        const bool wide = b.bin_words > kBinWords / 2 || b.n_bins <= 256;
         if (b.work) {  // persistent: the resident blocks; b.work was zeroed before the round's scatter
-            const unsigned resident = wide ? 256u : 512u;
+            const unsigned resident = b.bin_words > kBinWords / 2 ? 256u : 512u;
             sgrid = std::min(sgrid, resident);
         }
-        if (wide && wp_of(W_) == 1) {  // one word: the pipeline shapes (A/B), the probe
+        if (b.bin_words > kBinWords / 2 && wp_of(W_) == 1) {  // one word: the pipeline shapes (A/B), the probe
             if (b.probe)
                 hipLaunchKernelGGL((k_bin_apply_runs<1, kBinWords, 1024, 2, true>), dim3(sgrid), dim3(1024), 0, s, a, b,
                                    wd);
@@ -2790,7 +2787,7 @@ hipError_t launch_bin_apply(const RoundArgs& a, const BinArgs& b, uint32_t W_, h
                 hipLaunchKernelGGL((k_bin_apply_runs<1, kBinWords, 1024, 2>), dim3(sgrid), dim3(1024), 0, s, a, b, wd);
             else
                 hipLaunchKernelGGL((k_bin_apply_runs<1, kBinWords, 1024, 3>), dim3(sgrid), dim3(1024), 0, s, a, b, wd);
-        } else if (wide) {
+        } else if (b.bin_words > kBinWords / 2) {
             GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_apply_runs<W, kBinWords, 1024>),
                                                            dim3(sgrid), dim3(1024), 0, s, a, b, wd));
         } else {
