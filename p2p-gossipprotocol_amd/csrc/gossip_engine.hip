@@ -346,17 +346,18 @@ hipEvent_t take_event(gossip_ctx* c) {
 hipError_t flush_zero(gossip_ctx* c) {
     gossip::ZeroBatch& z = c->zq;
     if (!z.count) return hipSuccess;
-    hipError_t e = z.count == 1 ? hipMemsetAsync(z.p[0], 0, (size_t)z.n[0] * 4, c->stream)
-                                : gossip::launch_zero_batch(z, c->stream);
+    hipError_t e = z.count == 1 && !z.save[0] ? hipMemsetAsync(z.p[0], 0, (size_t)z.n[0] * 4, c->stream)
+                                              : gossip::launch_zero_batch(z, c->stream);
     z.count = 0;
     return e;
 }
 
-hipError_t queue_zero(gossip_ctx* c, void* p, uint64_t bytes) {
+hipError_t queue_zero(gossip_ctx* c, void* p, uint64_t bytes, void* save = nullptr) {
     if (c->zq.count == gossip::kZeroRanges)
         if (hipError_t e = flush_zero(c)) return e;
     c->zq.p[c->zq.count] = static_cast<uint32_t*>(p);
     c->zq.n[c->zq.count] = (uint32_t)(bytes / 4);
+    c->zq.save[c->zq.count] = static_cast<uint32_t*>(save);
     c->zq.count++;
     return hipSuccess;
 }
@@ -1414,10 +1415,10 @@ gossip_status round_compute(gossip_ctx* c) {
 
 gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative) {
     if (c->replaying && c->last_st_round != c->round) {  // the recorded sums; the lines go to the history
+        // copied to the history and cleared by the next round's first launch (the zero batch); whatever is
+        // queued before goes out first (a queued clear of these lines would run before their copy)
         HIPCHK(flush_zero(c));
-        HIPCHK(hipMemcpyAsync(c->d_hist + (uint64_t)c->rep_round * kStatLines, c->st, kStatLines * sizeof(DevStats),
-                              hipMemcpyDeviceToDevice, c->stream));
-        HIPCHK(queue_zero(c, c->st, kStatLines * sizeof(DevStats)));
+        HIPCHK(queue_zero(c, c->st, kStatLines * sizeof(DevStats), c->d_hist + (uint64_t)c->rep_round * kStatLines));
         c->last_st = c->rec_st[c->rep_round];
         c->lst_out_n = c->rec_lst[c->rep_round];
         c->last_st_round = c->round;
@@ -1637,6 +1638,7 @@ gossip_status replay_run(gossip_ctx* c, gossip_round_stats* per_round, uint32_t 
         return s;
     }
     std::vector<DevStats> h((uint64_t)R * kStatLines);
+    HIPCHK(flush_zero(c));  // (the last round's lines are still queued for the history)
     HIPCHK(hipMemcpyAsync(h.data(), c->d_hist, h.size() * sizeof(DevStats), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     bool same = k == R && c->finished;

@@ -399,7 +399,9 @@ hipError_t launch_zero_words(uint64_t* words, uint64_t n_words, hipStream_t s);
 constexpr int kZeroRanges = 8;
 struct ZeroBatch {
     uint32_t* p[kZeroRanges];
-    uint32_t n[kZeroRanges];  // words
+    uint32_t n[kZeroRanges];     // words
+    uint32_t* save[kZeroRanges];  // non-null: the range is copied here before it is cleared (a replayed run's
+                                  // stat lines into the history, without a copy launch per round)
     uint32_t count;
 };
 hipError_t launch_zero_batch(const ZeroBatch& z, hipStream_t s);

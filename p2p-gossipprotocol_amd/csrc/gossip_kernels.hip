@@ -2906,7 +2906,11 @@ hipError_t launch_commit_nx(uint64_t* seen, const uint64_t* nx, uint64_t n_words
 __global__ __launch_bounds__(kBlock) void k_zero_batch(ZeroBatch z) {
     for (uint32_t r = 0; r < z.count; ++r) {
         uint32_t* p = z.p[r];
-        for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < z.n[r]; i += gridDim.x * kBlock) p[i] = 0u;
+        uint32_t* save = z.save[r];
+        for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < z.n[r]; i += gridDim.x * kBlock) {
+            if (save) save[i] = p[i];
+            p[i] = 0u;
+        }
     }
 }
 
