@@ -1503,10 +1503,11 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_stream(RoundArgs a, BinAr
 // (loop unrolled by kS) so each wait is for loads issued an iteration earlier.
 // Lanes past the bin or its groups load clamped addresses and fold nothing.
 // The blocks that share an XCD (blockIdx % 8) apply consecutive bins, which read neighbouring runs of every
-// chunk.  (Measured at config 4: a persistent launch with rows of consecutive bins per XCD and a bounded
-// per-row sync, so that neighbouring bins walk their chunks together, was slower: 10.3-11.5 against
-// 9.6-9.8 ms per launch.)  The end of each bin is k_bin_apply's: test-and-set of its peers with plain
-// stores (and the fold of a deferred push round's words, a.fold).
+// chunk (rows of kApplyRow bins, dealt round-robin to the XCD groups; see the end of the kernel).  (Round 3
+// measured a persistent launch that also kept each row's bins in step with a bounded per-row sync: slower,
+// 10.3-11.5 against 9.6-9.8 ms.  The persistent launch here has no sync between blocks.)  The end of each
+// bin is k_bin_apply's: test-and-set of its peers with plain stores (and the fold of a deferred push
+// round's words, a.fold).
 // Pipeline shape (kPipe, W = 1 only; others use 0): groups per stage kG, and how many iterations ahead
 // each load is issued -- bdst + ap_grp LA, ap_run LB, val LC (LA > LB > LC >= 1), kS = LA + 1 register sets.
 template <int W, int kPipe> struct ApplyPipe { static constexpr int kG = W == 1 ? 4 : W == 2 ? 2 : 1, LA = 3, LB = 2, LC = 1; };
