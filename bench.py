@@ -34,6 +34,7 @@ REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO / "p2p-gossipprotocol_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+XGMI_LINK_GBS = 153.0  # one xGMI link, each direction; a GPU of the 8-GPU node has 7 (one to each other GPU)
 DENSE_KERNELS = ("bin_scatter", "bin_apply", "pull_heavy")  # the device work of a binned round
 
 
@@ -320,10 +321,14 @@ def per_round_profile(run, n_peers: int) -> list[dict]:
     a partitioned run on one GPU per part, the sum over the parts of one run
     emulating P parts on a single GPU, where they run one after another) and
     exchanges; and the round's fraction of the HBM
-    peak, frac = B_r / kernel time / peak.  Pull rounds (row, list and heavy
-    pulls) stop a row's scan once it holds every bit it can still learn, so
-    8(d)'s 20 B per traversal overstates what they touch: they are marked
-    work_avoiding (their frac can pass 1)."""
+    peak, frac = B_r / kernel time / peak.  A round whose kernels move fewer
+    bytes than 8(d) charges it is marked work_avoiding, with the reason: pull
+    rounds (row, list and heavy pulls) stop a row's scan once it holds every
+    bit it can still learn, so 8(d)'s 20 B per traversal overstates what they
+    touch ("pull"); a ping round's 6.125 B per ping are charged for every ping
+    pingLoop sends, while the closed-form liveness only walks the rows of the
+    peers whose miss count reaches the limit ("liveness").  Their frac can
+    pass 1."""
     from gossip_hip.engine import EXCHANGES, KERNELS
     names = KERNELS + EXCHANGES
     agg = part_agg(run)
@@ -348,14 +353,40 @@ def per_round_profile(run, n_peers: int) -> list[dict]:
         live_b = 6.125 * db["#pings"] + 16 * db["#pinging_peers"]
         alg = 32 * st["frontier"] + 20 * st["traversals"] + live_b
         frac = alg / (kms / 1e3) / 1e9 / HBM_PEAK_GBS if kms > 0 else 0.0
+        design = sum(db[k] for k in KERNELS)
+        why = "pull" if mode == "pull" else "liveness" if live_b and design < alg else None
         rows.append({"round": st["round"], "mode": mode, "frontier_frac": round(st["frontier"] / n_peers, 4),
                      "traversals": st["traversals"], "alg_bytes": round(alg), "liveness_bytes": round(live_b),
-                     "design_bytes": round(sum(db[k] for k in KERNELS)),
+                     "design_bytes": round(design),
                      "kernel_ms": round(kms, 3), "exchange_ms": round(xms, 3), "dense_ms": round(dense, 3),
-                     "frac": round(frac, 4), "work_avoiding": mode == "pull"})
+                     "frac": round(frac, 4), "work_avoiding": why is not None, "avoided": why})
         if fin:
             run.timing(False)
             return rows
+
+
+def link_projection(run, k_ms, k_b, timed_steps: int, dist) -> dict:
+    """What the partitioned run's exchange costs on the 8-GPU node's xGMI mesh:
+    per rank, the bytes it receives per step over its P - 1 links (one to each
+    other rank, XGMI_LINK_GBS each way) -- exchange_link_ms, the max over the
+    ranks.  For a rehearsal of P parts on one GPU (whose exchanges are device
+    copies) the projected P-GPU step is the slowest part's kernel time plus
+    that link time, with no overlap of the two and no host time:
+    projected_ms_per_step."""
+    from gossip_hip.engine import EXCHANGES, KERNELS
+    world = run.parts if dist is None else run.world
+    if world < 2:
+        return {}
+    link = max(sum(x[k] for k in EXCHANGES) for x in k_b) / timed_steps / ((world - 1) * XGMI_LINK_GBS * 1e9) * 1e3
+    out = {"exchange_link_ms_per_step": round(link, 3),
+           "exchange_link_model": f"max over ranks of the bytes a rank receives per step / ({world - 1} links x "
+                                  f"{XGMI_LINK_GBS:.0f} GB/s)"}
+    if run.parts > 1 and run.n_gpus == 1:
+        part_k = [sum(x[k][0] for k in KERNELS) / timed_steps for x in k_ms]
+        out.update({"part_kernel_ms_per_step": [round(v, 3) for v in part_k],
+                    "projected_ms_per_step": round(max(part_k) + link, 3),
+                    "projected_model": "slowest part's kernels + exchange_link_ms_per_step, no overlap, no host time"})
+    return out
 
 
 def main():
@@ -441,18 +472,24 @@ def main():
         # the dominant kernel by device time (part 0's; every part runs the same schedule)
         dom = max((k for k in KERNELS), key=lambda k: k_ms[0][k][0])
         ms, launches = k_ms[0][dom]
-        # without the work-avoiding (pull) rounds: their 8(d) bytes out of the numerator, their kernel time
-        # out of the step
+        # without the work-avoiding rounds: a pull round's 8(d) bytes out of the numerator and its kernel and
+        # exchange time out of the step; a ping round's liveness bytes out of the numerator (its push or binned
+        # work shares the round's time, which stays)
         step_ms = dt / args.steps * 1e3
         wa = [r for r in rounds_prof if r["work_avoiding"]]
-        rest_ms = step_ms - sum(r["kernel_ms"] + r["exchange_ms"] for r in wa)
-        rest_b = alg - sum(r["alg_bytes"] for r in wa)
-        roofline = {"bound": "hbm", "peak": HBM_PEAK_GBS * run.n_gpus, "unit": "GB/s",
-                    "step_frac": round(alg / (dt / args.steps) / 1e9 / (HBM_PEAK_GBS * run.n_gpus), 4),
-                    "step_frac_without_work_avoiding": round(rest_b / (rest_ms / 1e3) / 1e9 /
-                                                             (HBM_PEAK_GBS * run.n_gpus), 4) if rest_ms > 0 else None,
+        pulls = [r for r in wa if r["avoided"] == "pull"]
+        live_all = sum(r["liveness_bytes"] for r in rounds_prof)
+        rest_ms = step_ms - sum(r["kernel_ms"] + r["exchange_ms"] for r in pulls)
+        rest_b = alg - sum(r["alg_bytes"] for r in pulls) - sum(r["liveness_bytes"] for r in wa
+                                                                if r["avoided"] == "liveness")
+        peak_all = HBM_PEAK_GBS * run.n_gpus
+        roofline = {"bound": "hbm", "peak": peak_all, "unit": "GB/s",
+                    "step_frac": round(alg / (dt / args.steps) / 1e9 / peak_all, 4),
+                    "step_frac_without_liveness": round((alg - live_all) / (dt / args.steps) / 1e9 / peak_all, 4),
+                    "step_frac_without_work_avoiding": round(rest_b / (rest_ms / 1e3) / 1e9 / peak_all, 4)
+                    if rest_ms > 0 else None,
                     "work_avoiding_rounds": [r["round"] for r in wa],
-                    "step_alg_bytes": round(alg), "step_liveness_bytes": sum(r["liveness_bytes"] for r in rounds_prof),
+                    "step_alg_bytes": round(alg), "step_liveness_bytes": live_all,
                     "timed_steps": timed_steps,
                     "ms_per_step_with_events": round(dt_timed / timed_steps * 1e3, 3),
                     "kernel_ms_per_step": {k: round(agg(x[k][0] for x in k_ms) / timed_steps, 3)
@@ -461,6 +498,8 @@ def main():
                                              for k in EXCHANGES if k_ms[0][k][1]},
                     "exchange_gb_per_step": {k: round(sum(x[k] for x in k_b) / timed_steps / 1e9, 3)
                                              for k in EXCHANGES if k_ms[0][k][1]}}
+        if run.parts > 1 or dist is not None:
+            roofline.update(link_projection(run, k_ms, k_b, timed_steps, dist))
         if dense:
             # SURVEY 8(d)'s bytes of the binned rounds over the device time of their kernels
             # (bin_scatter + bin_apply + pull_heavy; part_agg over the parts): the honest dense-round fraction
@@ -520,6 +559,7 @@ def main():
             line["rounds"] = [{k: r[k] for k in ("round", "mode", "frontier_frac", "traversals", "alg_bytes",
                                                  "design_bytes", "kernel_ms", "frac", "work_avoiding")} |
                               ({"liveness_bytes": r["liveness_bytes"]} if r["liveness_bytes"] else {}) |
+                              ({"avoided": r["avoided"]} if r["avoided"] else {}) |
                               ({"exchange_ms": r["exchange_ms"]} if run.parts > 1 or dist is not None else {})
                               for r in rounds_prof]
         if roofline:

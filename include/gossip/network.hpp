@@ -95,7 +95,8 @@ private:
     SimOptions opt_;
     uint32_t M_ = 0, W_ = 0;
     gossip_ctx* ctx_ = nullptr;
-    uint64_t groupReportCount() const;
+    uint64_t groupReportCount() const;  // ~0: a part's count is unreadable (report buffer overflow)
+    uint64_t mergedReports_ = 0;        // reports behind the seed removals merged so far (partitioned runs)
     gossip_group* group_ = nullptr;
     bool started_ = false, finished_ = false, trace_ = false;
     std::atomic<bool> stop_{false};

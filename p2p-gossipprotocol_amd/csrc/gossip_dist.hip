@@ -271,19 +271,35 @@ int choose_mode(const DistDriver* d) {
 
 // Times one exchange on every local rank's stream (gossip_kernel_time(name)
 // of each part while timing is on) and books its bytes received per rank.
+// With one GPU per rank every rank's interval brackets the whole exchange on its
+// own stream.  An emulated group shares ONE stream: an interval opened on every
+// part before any copy would cover all parts' copies, so each part is timed only
+// around its own work (part(i, f): the copies into part i, or a kernel of part
+// i), and the intervals of the parts partition the exchange's time.
 struct ExchTimer {
     DistDriver* d;
     const char* name;
     std::vector<void*> tok;
     TraceRange tr;
     ExchTimer(DistDriver* d_, const char* n) : d(d_), name(n), tok(d_->ranks.size(), nullptr), tr("%s", n) {
+        if (d->emulate) return;
         for (size_t i = 0; i < d->ranks.size(); ++i) {
             hipSetDevice(d->ranks[i].device);
             ctx_timer_start(d->ranks[i].ctx, name, &tok[i]);
         }
     }
     void bytes(size_t i, double b) { ctx_add_bytes(d->ranks[i].ctx, name, b); }
+    template <class F>
+    gossip_status part(size_t i, F&& f) {
+        if (!d->emulate) return f();
+        void* t = nullptr;
+        ctx_timer_start(d->ranks[i].ctx, name, &t);
+        const gossip_status s = f();
+        ctx_timer_stop(d->ranks[i].ctx, name, t);
+        return s;
+    }
     ~ExchTimer() {
+        if (d->emulate) return;
         for (size_t i = 0; i < d->ranks.size(); ++i) {
             hipSetDevice(d->ranks[i].device);
             ctx_timer_stop(d->ranks[i].ctx, name, tok[i]);
@@ -297,11 +313,17 @@ gossip_status all_gather(DistDriver* d) {
     ExchTimer t(d, "all_gather");
     for (size_t i = 0; i < d->ranks.size(); ++i) t.bytes(i, 8.0 * words * (d->world - 1));
     if (d->emulate) {
-        for (auto& q : d->ranks)
-            for (auto& p : d->ranks)
-                if (p.rank != q.rank)
-                    DHIP(hipMemcpyAsync(q.gather + p.rank * words, p.gather + p.rank * words, words * 8,
-                                        hipMemcpyDeviceToDevice, q.stream));
+        for (size_t i = 0; i < d->ranks.size(); ++i) {
+            DistRank& q = d->ranks[i];
+            gossip_status s = t.part(i, [&]() -> gossip_status {
+                for (auto& p : d->ranks)
+                    if (p.rank != q.rank)
+                        DHIP(hipMemcpyAsync(q.gather + p.rank * words, p.gather + p.rank * words, words * 8,
+                                            hipMemcpyDeviceToDevice, q.stream));
+                return GOSSIP_OK;
+            });
+            if (s) return s;
+        }
         return GOSSIP_OK;
     }
     DNCCL(ncclGroupStart());
@@ -322,18 +344,31 @@ gossip_status compact_gather(DistDriver* d) {
     const uint32_t W = d->world;
     const uint64_t X = d->X, tpb = d->tpb, tiles = (uint64_t)W * tpb;
     ExchTimer t(d, "all_gather");
-    for (auto& r : d->ranks) {  // own tile bitmap
+    gossip_status s = GOSSIP_OK;
+    for (size_t i = 0; i < d->ranks.size(); ++i) {  // own tile bitmap
+        DistRank& r = d->ranks[i];
         DHIP(hipSetDevice(r.device));
-        hipLaunchKernelGGL(k_tile_bits, dim3((unsigned)std::min<uint64_t>((tpb + 3) / 4, 8192)), dim3(256), 0,
-                           r.stream, r.gather + r.rank * d->chunk * X, r.n_local, (uint32_t)X, r.bits + r.rank * tpb);
-        DHIP(hipGetLastError());
+        s = t.part(i, [&]() -> gossip_status {
+            hipLaunchKernelGGL(k_tile_bits, dim3((unsigned)std::min<uint64_t>((tpb + 3) / 4, 8192)), dim3(256), 0,
+                               r.stream, r.gather + r.rank * d->chunk * X, r.n_local, (uint32_t)X,
+                               r.bits + r.rank * tpb);
+            DHIP(hipGetLastError());
+            return GOSSIP_OK;
+        });
+        if (s) return s;
     }
     if (d->emulate) {
-        for (auto& q : d->ranks)
-            for (auto& p : d->ranks)
-                if (p.rank != q.rank)
-                    DHIP(hipMemcpyAsync(q.bits + p.rank * tpb, p.bits + p.rank * tpb, tpb * 8, hipMemcpyDeviceToDevice,
-                                        q.stream));
+        for (size_t i = 0; i < d->ranks.size(); ++i) {
+            DistRank& q = d->ranks[i];
+            s = t.part(i, [&]() -> gossip_status {
+                for (auto& p : d->ranks)
+                    if (p.rank != q.rank)
+                        DHIP(hipMemcpyAsync(q.bits + p.rank * tpb, p.bits + p.rank * tpb, tpb * 8,
+                                            hipMemcpyDeviceToDevice, q.stream));
+                return GOSSIP_OK;
+            });
+            if (s) return s;
+        }
     } else {
         DNCCL(ncclGroupStart());
         for (auto& r : d->ranks) {
@@ -343,31 +378,47 @@ gossip_status compact_gather(DistDriver* d) {
         DNCCL(ncclGroupEnd());
     }
     std::vector<uint64_t> off(W + 1);
-    for (auto& r : d->ranks) {
+    for (size_t i = 0; i < d->ranks.size(); ++i) {
+        DistRank& r = d->ranks[i];
         DHIP(hipSetDevice(r.device));
-        size_t tb = r.scan_bytes;
-        DHIP(hipcub::DeviceScan::ExclusiveSum(r.scan_tmp, tb, TilePop(r.bits, PopOp()), r.pos, (int)(tiles + 1), r.stream));
-        hipLaunchKernelGGL(k_pick_offsets, dim3(1), dim3(64 * ((W + 64) / 64)), 0, r.stream, r.pos, W, tpb, r.d_io);
-        DHIP(hipGetLastError());
-        DHIP(hipMemcpyAsync(r.h_io, r.d_io, (W + 1) * 8, hipMemcpyDeviceToHost, r.stream));
+        s = t.part(i, [&]() -> gossip_status {
+            size_t tb = r.scan_bytes;
+            DHIP(hipcub::DeviceScan::ExclusiveSum(r.scan_tmp, tb, TilePop(r.bits, PopOp()), r.pos, (int)(tiles + 1),
+                                                  r.stream));
+            hipLaunchKernelGGL(k_pick_offsets, dim3(1), dim3(64 * ((W + 64) / 64)), 0, r.stream, r.pos, W, tpb, r.d_io);
+            DHIP(hipGetLastError());
+            DHIP(hipMemcpyAsync(r.h_io, r.d_io, (W + 1) * 8, hipMemcpyDeviceToHost, r.stream));
+            return GOSSIP_OK;
+        });
+        if (s) return s;
         DHIP(hipStreamSynchronize(r.stream));
         std::memcpy(off.data(), r.h_io, (W + 1) * 8);  // (identical on every rank)
-        hipLaunchKernelGGL(k_tile_pack, dim3((unsigned)std::min<uint64_t>((tpb + 3) / 4, 8192)), dim3(256), 0,
-                           r.stream, r.gather + r.rank * d->chunk * X, r.n_local, (uint32_t)X, r.bits + r.rank * tpb,
-                           r.pos + r.rank * tpb, r.pk);
-        DHIP(hipGetLastError());
+        s = t.part(i, [&]() -> gossip_status {
+            hipLaunchKernelGGL(k_tile_pack, dim3((unsigned)std::min<uint64_t>((tpb + 3) / 4, 8192)), dim3(256), 0,
+                               r.stream, r.gather + r.rank * d->chunk * X, r.n_local, (uint32_t)X,
+                               r.bits + r.rank * tpb, r.pos + r.rank * tpb, r.pk);
+            DHIP(hipGetLastError());
+            return GOSSIP_OK;
+        });
+        if (s) return s;
     }
     for (size_t i = 0; i < d->ranks.size(); ++i)
         t.bytes(i, 8.0 * (double)((W - 1) * tpb) +
                        8.0 * X * (double)(off[W] - (off[d->ranks[i].rank + 1] - off[d->ranks[i].rank])));
     if (d->emulate) {
-        for (auto& q : d->ranks)
-            for (auto& p : d->ranks) {
-                const uint64_t c = off[p.rank + 1] - off[p.rank];
-                if (p.rank != q.rank && c)
-                    DHIP(hipMemcpyAsync(q.pk + off[p.rank] * X, p.pk + off[p.rank] * X, c * X * 8,
-                                        hipMemcpyDeviceToDevice, q.stream));
-            }
+        for (size_t i = 0; i < d->ranks.size(); ++i) {
+            DistRank& q = d->ranks[i];
+            s = t.part(i, [&]() -> gossip_status {
+                for (auto& p : d->ranks) {
+                    const uint64_t c = off[p.rank + 1] - off[p.rank];
+                    if (p.rank != q.rank && c)
+                        DHIP(hipMemcpyAsync(q.pk + off[p.rank] * X, p.pk + off[p.rank] * X, c * X * 8,
+                                            hipMemcpyDeviceToDevice, q.stream));
+                }
+                return GOSSIP_OK;
+            });
+            if (s) return s;
+        }
     } else {
         DNCCL(ncclGroupStart());
         for (auto& r : d->ranks) {
@@ -382,11 +433,16 @@ gossip_status compact_gather(DistDriver* d) {
         }
         DNCCL(ncclGroupEnd());
     }
-    for (auto& r : d->ranks) {
+    for (size_t i = 0; i < d->ranks.size(); ++i) {
+        DistRank& r = d->ranks[i];
         DHIP(hipSetDevice(r.device));
-        hipLaunchKernelGGL(k_tile_expand, dim3((unsigned)std::min<uint64_t>((tiles + 3) / 4, 16384)), dim3(256), 0,
-                           r.stream, r.gather, r.bits, r.pos, r.pk, (uint32_t)X, W, r.rank, d->chunk, d->n, tpb);
-        DHIP(hipGetLastError());
+        s = t.part(i, [&]() -> gossip_status {
+            hipLaunchKernelGGL(k_tile_expand, dim3((unsigned)std::min<uint64_t>((tiles + 3) / 4, 16384)), dim3(256), 0,
+                               r.stream, r.gather, r.bits, r.pos, r.pk, (uint32_t)X, W, r.rank, d->chunk, d->n, tpb);
+            DHIP(hipGetLastError());
+            return GOSSIP_OK;
+        });
+        if (s) return s;
     }
     return GOSSIP_OK;
 }
@@ -398,11 +454,17 @@ gossip_status all_to_all(DistDriver* d) {
     ExchTimer t(d, "all_to_all");
     for (size_t i = 0; i < d->ranks.size(); ++i) t.bytes(i, 8.0 * X * d->ranks[i].n_local * (d->world - 1));
     if (d->emulate) {
-        for (auto& q : d->ranks)
-            for (auto& p : d->ranks)
-                if (p.rank != q.rank)  // own pushes went straight to seen; the own slice of recv stays zero
-                    DHIP(hipMemcpyAsync(q.recv + p.rank * q.n_local * X, p.send + d->part[q.rank] * X,
-                                        q.n_local * X * 8, hipMemcpyDeviceToDevice, q.stream));
+        for (size_t i = 0; i < d->ranks.size(); ++i) {
+            DistRank& q = d->ranks[i];
+            gossip_status s = t.part(i, [&]() -> gossip_status {
+                for (auto& p : d->ranks)
+                    if (p.rank != q.rank)  // own pushes went straight to seen; the own slice of recv stays zero
+                        DHIP(hipMemcpyAsync(q.recv + p.rank * q.n_local * X, p.send + d->part[q.rank] * X,
+                                            q.n_local * X * 8, hipMemcpyDeviceToDevice, q.stream));
+                return GOSSIP_OK;
+            });
+            if (s) return s;
+        }
         return GOSSIP_OK;
     }
     DNCCL(ncclGroupStart());
@@ -464,13 +526,17 @@ gossip_status exchange_records(DistDriver* d, std::vector<uint64_t>& total_in) {
         for (size_t i = 0; i < d->ranks.size(); ++i) {
             DistRank& q = d->ranks[i];
             uint64_t off = 0;
-            for (auto& p : d->ranks) {
-                const uint64_t c = p.counts_out[q.rank];
-                if (c)
-                    DHIP(hipMemcpyAsync(q.rec_in + off * R, p.seg + (uint64_t)q.rank * chunk * R, c * R * 8,
-                                        hipMemcpyDeviceToDevice, q.stream));
-                off += c;
-            }
+            gossip_status s = t.part(i, [&]() -> gossip_status {
+                for (auto& p : d->ranks) {
+                    const uint64_t c = p.counts_out[q.rank];
+                    if (c)
+                        DHIP(hipMemcpyAsync(q.rec_in + off * R, p.seg + (uint64_t)q.rank * chunk * R, c * R * 8,
+                                            hipMemcpyDeviceToDevice, q.stream));
+                    off += c;
+                }
+                return GOSSIP_OK;
+            });
+            if (s) return s;
             total_in[i] = off;
         }
         return GOSSIP_OK;

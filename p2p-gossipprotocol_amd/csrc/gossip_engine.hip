@@ -1840,7 +1840,6 @@ gossip_status gossip_set_tuning(gossip_ctx* c, const char* key, int64_t value) {
                 return fail(GOSSIP_EHIP, "apply_probe buffer");
         } else if (!value && c->d_probe) {
             hipFree(c->d_probe);
-    hipFree(c->d_work);
             c->d_probe = nullptr;
         }
     }
@@ -1870,6 +1869,8 @@ void gossip_destroy(gossip_ctx* c) {
     hipFree(c->sx_bits);
     hipFree(c->smark);
     hipFree(c->d_probe);
+    hipFree(c->d_work);
+    hipFree(c->d_hist);
     hipFree(c->sx_pos);
     hipFree(c->sx_tmp);
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
@@ -2120,10 +2121,13 @@ gossip_status gossip_reset(gossip_ctx* c) {
         HIPCHK(hipMemsetAsync(c->n_reports, 0, sizeof(unsigned long long), s));
         HIPCHK(hipMemsetAsync(c->inj_live, 0, kMaxWords * sizeof(uint64_t), s));
         // per-edge miss counters: only the per-edge liveness scan uses them (the closed form, below, never
-        // does; config 5: a 0.5 GB clear per step saved)
+        // does; config 5: a 0.5 GB clear per step saved).  An overlay small enough for the one-launch run
+        // clears them anyway: that run scans every edge's counter, and it may run after this reset even
+        // though the reset itself did not take the tiny path ("tiny" turned on in between)
         const bool closed = c->n_local == c->n && c->symmetric && !c->cfg.rejoin_threshold &&
                             c->cfg.max_rounds < 0xFFFF && !c->full_liveness;
-        if (c->miss && !closed) HIPCHK(hipMemsetAsync(c->miss, 0, c->n_edges + 1, s));
+        const bool small = c->n <= kTinyPeers && c->n_edges <= kTinyEdges;
+        if (c->miss && (!closed || small)) HIPCHK(hipMemsetAsync(c->miss, 0, c->n_edges + 1, s));
         if (c->any_masked && c->col && c->n_edges) {
             hipLaunchKernelGGL(k_unmask, dim3(2048), dim3(256), 0, s, c->col, c->n_edges);
             HIPCHK(hipGetLastError());

@@ -88,7 +88,8 @@ struct BinArgs {
     const uint64_t* chunk_begin;  // n_chunks + 1 offsets into cb_*
     uint64_t n_chunks, chunk;     // source chunks of `chunk` peers
     const BinUnit* units;         // scatter work units, in chunk order
-    const uint64_t* xcd_units;    // 9 offsets: XCD x sweeps units [xcd_units[x], xcd_units[x+1])
+    const uint64_t* xcd_units;    // 9 words, only xcd_units[8] is meaningful: the unit count, a multiple of
+                                  // kScatterGrid / 8 (scatter_rows deals rows of units round-robin over the XCDs)
     const uint16_t* bdst;         // per slot: destination - bin.v0
     uint64_t* val;                // per slot: Wp words, the source's new words of this round
     uint32_t bin_words;           // LDS accumulator words of a bin (kBinWords or kBinWords / 2)

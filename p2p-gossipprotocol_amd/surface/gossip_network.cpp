@@ -246,8 +246,15 @@ int GossipNetwork::step() {
     if (trace_) captureRound(st.round);
     if (rc == 1) finished_ = true;
     // a partitioned run's seed removals come from the merged reports (single-partition stats carry them every
-    // round): every round while the reports are few (or traced), else once the run ends
-    if (group_ && (finished_ || trace_ || groupReportCount() < (1u << 20))) seedRemovalsFromReports();
+    // round): after a round that added reports while they are few (or traced), else once the run ends.  A
+    // round without new reports has no removals (its stats carry 0), so nothing is merged again for it.
+    if (group_) {
+        const uint64_t cnt = finished_ || trace_ ? ~0ull : groupReportCount();
+        if (finished_ || trace_ || (cnt < (1u << 20) && cnt != mergedReports_)) {
+            seedRemovalsFromReports();
+            mergedReports_ = cnt;
+        }
+    }
     return rc;
 }
 
@@ -274,13 +281,16 @@ std::vector<gossip_dead_report> GossipNetwork::reports() const {
     return out;
 }
 
-// Reports held by the parts of a group (their counters only: no merge)
+// Reports held by the parts of a group (their counters only: no merge); a part whose count cannot be read
+// (its report buffer overflowed: GOSSIP_EOVERFLOW) makes the total "many" (~0), so the merge waits for the
+// end of the run instead of dropping that part's reports
 uint64_t GossipNetwork::groupReportCount() const {
     uint64_t total = 0;
     gossip_ctx* part = nullptr;
     for (uint32_t p = 0; group_ && gossip_group_part(group_, p, &part) == GOSSIP_OK; ++p) {
         uint64_t n = 0;
-        if (gossip_read_reports(part, nullptr, 0, &n) == GOSSIP_OK) total += n;
+        if (gossip_read_reports(part, nullptr, 0, &n) != GOSSIP_OK) return ~0ull;
+        total += n;
     }
     return total;
 }

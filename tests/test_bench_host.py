@@ -58,7 +58,7 @@ def _rounds(parts):
          {p: {"push_light": 0.5, "push_heavy": 0.25} for p in range(parts)}, {}),
         ({"round": 1, "frontier": 1000, "traversals": 50_000},
          {p: {"bin_scatter": 1.0, "bin_apply": 2.0, "pull_heavy": 0.5 + p, "all_gather": 0.25} for p in range(parts)},
-         {p: {"#pings": 800.0, "#pinging_peers": 100.0, "bin_scatter": 1e6} for p in range(parts)}),
+         {p: {"#pings": 800.0, "#pinging_peers": 100.0, "bin_scatter": 1e7} for p in range(parts)}),
         ({"round": 2, "frontier": 900, "traversals": 40_000},
          {p: {"pull_light": 3.0} for p in range(parts)}, {}),
     ]
@@ -76,7 +76,7 @@ def test_per_round_profile_bytes_modes_and_part_times(parts, n_gpus):
     assert rows[0]["alg_bytes"] == 32 * 10 + 20 * 100
     assert rows[1]["alg_bytes"] == round(32 * 1000 + 20 * 50_000 + live)
     assert rows[1]["liveness_bytes"] == round(live)
-    assert rows[1]["design_bytes"] == parts * 1e6
+    assert rows[1]["design_bytes"] == parts * 1e7
     # device time: max over the parts on their own GPUs, their sum when they share one
     per_part = [1.0 + 2.0 + 0.5 + p for p in range(parts)]
     want = max(per_part) if parts == n_gpus else sum(per_part)
@@ -92,3 +92,37 @@ def test_part_agg():
     assert b.part_agg(FakeRun(1, 1, [])) is max
     assert b.part_agg(FakeRun(8, 8, [])) is max
     assert b.part_agg(FakeRun(8, 1, [])) is sum
+
+
+def test_liveness_round_is_flagged():
+    """A ping round whose kernels move fewer bytes than 8(d)'s liveness term
+    charges (the closed-form liveness walks only the dying peers' rows) is
+    marked work_avoiding ("liveness"); a binned ping round whose design bytes
+    exceed its 8(d) bytes is not."""
+    b = _bench()
+    rounds = _rounds(1) + [
+        ({"round": 3, "frontier": 10, "traversals": 100},
+         {0: {"push_light": 0.01, "liveness": 0.01}}, {0: {"#pings": 1e9, "#pinging_peers": 1e8, "push_light": 2320.0}}),
+    ]
+    rows = b.per_round_profile(FakeRun(1, 1, rounds), n_peers=10_000)
+    assert [r["avoided"] for r in rows] == [None, None, "pull", "liveness"]
+    assert rows[3]["work_avoiding"] and rows[3]["frac"] > 1
+
+
+def test_link_projection():
+    """exchange_link_ms: the bytes the busiest rank receives per step over its
+    P - 1 links; the projected P-GPU step adds it to the slowest part's kernels."""
+    from gossip_hip.engine import EXCHANGES, KERNELS
+    b = _bench()
+    run = FakeRun(4, 1, [])
+    k_ms = [{k: (0.0, 0) for k in KERNELS + EXCHANGES} for _ in range(4)]
+    k_b = [{k: 0.0 for k in KERNELS + EXCHANGES} for _ in range(4)]
+    for p in range(4):
+        k_ms[p]["bin_scatter"] = (2.0 * (p + 1), 2)  # 2 timed steps
+        k_b[p]["all_gather"] = 2 * 459e6 * (p + 1)
+    out = b.link_projection(run, k_ms, k_b, 2, None)
+    link = 4 * 459e6 / (3 * b.XGMI_LINK_GBS * 1e9) * 1e3
+    assert out["exchange_link_ms_per_step"] == pytest.approx(link, abs=1e-3)
+    assert out["part_kernel_ms_per_step"] == [1.0, 2.0, 3.0, 4.0]
+    assert out["projected_ms_per_step"] == pytest.approx(4.0 + link, abs=1e-3)
+    assert b.link_projection(FakeRun(1, 1, []), k_ms[:1], k_b[:1], 2, None) == {}

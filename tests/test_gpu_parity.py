@@ -371,6 +371,23 @@ def test_engine_variants_match_oracle(oracle, variant, idx, n, mode):
         _compare(e, ref, w)
 
 
+def test_apply_probe_toggle(oracle):
+    """apply_probe turned on, then off again, between runs of a streamed binned
+    workload: the persistent apply's bin counters must survive the toggle (the
+    probe-off branch once freed them and left the pointer dangling, so the next
+    binned round took bins from freed memory)."""
+    w = config(3, 1 << 18, pick=oracle.pick_origins)
+    rp, col = oracle.gen_workload(w)
+    ref = oracle.simulate_workload(w, rp, col)
+    with _engine(w, mode="bin") as e:
+        e.build_graph()
+        e.inject(w.origins, w.inject_rounds)
+        for probe in (1, 0, 1, 0):
+            e.set_tuning("apply_probe", probe)
+            e.reset()
+            _compare(e, ref, w)
+
+
 @pytest.mark.parametrize("variant", ["auto", "defer_10", "all_pull", "defer_10_all_pull", "defer_10_blocked",
                                      "defer_3_blocked"])
 @pytest.mark.parametrize("stop", [3, 4, 5, 6, 7, 8])
