@@ -115,27 +115,29 @@ __global__ void k_bin_assign(const unsigned long long* skeys, const uint32_t* sv
 }
 
 // (b) per position i of the slot order (sorted keys of (a)): key = chunk(source)
-// * n_bins + bin.  Sorted stably, so the entries of a (chunk, bin) pair stay
-// in slot order: consecutive cb entries of a pair have consecutive slots.
+// * n_bins + bin, chunk(u) = (u / seg) * cps + u % seg / chunk.  Sorted stably, so
+// the entries of a (chunk, bin) pair stay in slot order: consecutive cb entries
+// of a pair have consecutive slots.
 __global__ void k_cb_keys(const unsigned long long* skeys, uint64_t n_binned, uint32_t n_bins, uint32_t chunk,
-                          uint32_t* keys, uint32_t* vals) {
+                          uint32_t seg, uint32_t cps, uint32_t* keys, uint32_t* vals) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_binned;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t k = skeys[i];
-        keys[i] = (uint32_t)(k & 0xFFFFFFFFu) / chunk * n_bins + (uint32_t)(k >> 32);
+        const uint32_t u = (uint32_t)(k & 0xFFFFFFFFu);
+        keys[i] = (u / seg * cps + u % seg / chunk) * n_bins + (uint32_t)(k >> 32);
         vals[i] = (uint32_t)i;
     }
 }
 
 __global__ void k_cb_fill(const uint32_t* svals, uint64_t n_binned, const unsigned long long* skeys, const Bin* bins,
-                          uint32_t chunk, uint32_t* cb_slot, uint16_t* cb_src) {
+                          uint32_t chunk, uint32_t seg, uint32_t* cb_slot, uint16_t* cb_src) {
     for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n_binned;
          p += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t i = svals[p];
         const uint64_t k = skeys[i];
         const Bin bn = bins[k >> 32];
         cb_slot[p] = (uint32_t)(bn.s0 + (i - bn.u0));
-        cb_src[p] = (uint16_t)((uint32_t)(k & 0xFFFFFFFFu) % chunk);  // source, local to its chunk
+        cb_src[p] = (uint16_t)((uint32_t)(k & 0xFFFFFFFFu) % seg % chunk);  // source, local to its chunk
     }
 }
 
@@ -226,6 +228,7 @@ void free_bins(BinState* b) {
     hipFree(b->ap_grp);
     hipFree(b->chunk_begin);
     hipFree(b->units);
+    hipFree(b->stage_units);
     hipFree(b->xcd_units);
     hipFree(b->bdst);
     hipFree(b->val);
@@ -236,7 +239,7 @@ void free_bins(BinState* b) {
 
 hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local, uint64_t n_global, uint64_t m,
                       uint32_t heavy, uint32_t Wp, bool stream, uint32_t bin_words_req, uint32_t chunk_words_req,
-                      hipStream_t s, BinState* out, std::string* err) {
+                      uint64_t seg, hipStream_t s, BinState* out, std::string* err) {
     hipError_t rc = hipSuccess;
     const uint64_t n_tiles = (n_local + 63) / 64;
     // bigger bins -> longer slot runs per (source chunk, bin) in the scatter
@@ -311,7 +314,18 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
     if (chunk_words_req)
         chunk_words = std::max<uint64_t>(512, std::min<uint64_t>(kBinChunkWords, chunk_words_req / 512 * 512));
     chunk = std::max<uint64_t>(64, chunk_words / Wp);
-    n_chunks = (n_global + chunk - 1) / chunk;
+    // source segments: one (seg = n_global rounded to whole chunks) unless the caller cuts the ids (a vertex
+    // block: bin_segment), chunks never straddle a segment
+    if (!seg) seg = (n_global + chunk - 1) / chunk * chunk;
+    chunk = std::min<uint64_t>(chunk, seg);
+    st.seg = seg;
+    st.cps = (seg + chunk - 1) / chunk;
+    n_chunks = (n_global + seg - 1) / seg * st.cps;
+    if (seg >= (1ull << 32) || seg % 64) {
+        if (err) *err = "source segments must be whole 64-peer tiles below 2^32 peers";
+        rc = hipErrorInvalidValue;
+        goto done;
+    }
     if (n_chunks * h_bins.size() >= kNoSlot) {
         if (err) *err = "too many (chunk, bin) pairs for 32-bit keys";
         rc = hipErrorInvalidValue;
@@ -384,7 +398,7 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
     BCHECK(hipMalloc((void**)&keys_in, (upos + 1) * sizeof(uint32_t)));
     BCHECK(hipMalloc((void**)&keys_out, (upos + 1) * sizeof(uint32_t)));
     hipLaunchKernelGGL(k_cb_keys, dim3(gridn(upos)), dim3(256), 0, s, keys64_out, upos, (uint32_t)st.n_bins,
-                       (uint32_t)chunk, keys_in, vals_in);
+                       (uint32_t)chunk, (uint32_t)st.seg, (uint32_t)st.cps, keys_in, vals_in);
     BCHECK(hipGetLastError());
     temp_bytes = 0;
     BCHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, keys_in, keys_out, vals_in, vals_out, (size_t)upos,
@@ -402,7 +416,7 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
     BCHECK(hipMalloc((void**)&st.cb_src, (upos + 16) * sizeof(uint16_t)));  // k_bin_stream reads aligned 8-entry blocks
     BCHECK(hipMalloc((void**)&st.chunk_begin, (n_chunks + 1) * sizeof(uint64_t)));
     hipLaunchKernelGGL(k_cb_fill, dim3(gridn(upos)), dim3(256), 0, s, vals_out, upos, keys64_out, st.bins,
-                       (uint32_t)chunk, cb_slot, st.cb_src);
+                       (uint32_t)chunk, (uint32_t)st.seg, cb_slot, st.cb_src);
     BCHECK(hipGetLastError());
     hipLaunchKernelGGL(k_chunk_bounds, dim3(gridn(n_chunks + 1)), dim3(256), 0, s, keys_out, upos,
                        (uint32_t)st.n_bins, n_chunks, st.chunk_begin);
@@ -500,6 +514,7 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
             xu[8] = units.size();
         }
         st.n_units = units.size();
+        st.h_units = units;
         BCHECK(hipMalloc((void**)&st.units, units.size() * sizeof(BinUnit)));
         BCHECK(hipMemcpy(st.units, units.data(), units.size() * sizeof(BinUnit), hipMemcpyHostToDevice));
         BCHECK(hipMalloc((void**)&st.xcd_units, 9 * sizeof(uint64_t)));
@@ -526,6 +541,39 @@ done:
     }
     *out = st;
     return hipSuccess;
+}
+
+// The staged order of the units (a pipelined dense exchange, gossip_dist.hip): group 0 = the units whose
+// chunk lies inside the own block [begin, end) (their words are local when the exchange starts), group 1 + j
+// = the others of segments s = j (mod S) (stage j of the exchange delivers those segments' words from every
+// block); each group in chunk order, padded to whole rows of kScatterGrid / 8 units.  A chunk that straddles
+// the own block's edge waits for its segment's stage.
+hipError_t build_stage_units(BinState* b, uint32_t S, uint64_t begin, uint64_t end, uint64_t n_global) {
+    if (S < 1 || S > kMaxStages) return hipErrorInvalidValue;
+    if (b->stages == S) return hipSuccess;
+    const uint64_t members = kScatterGrid / 8;
+    std::vector<std::vector<BinUnit>> grp(S + 1);
+    for (const BinUnit& u : b->h_units) {
+        if (u.p0 >= u.p1 && !u.first) continue;  // row padding
+        const uint64_t vb = chunk_vb(u.c, b->seg, b->cps, b->chunk), ve = chunk_ve(u.c, b->seg, b->cps, b->chunk, n_global);
+        const bool own = vb >= begin && ve <= end;
+        grp[own ? 0 : 1 + (u.c / b->cps) % S].push_back(u);
+    }
+    std::vector<BinUnit> all;
+    for (uint32_t g = 0; g <= S; ++g) {
+        b->stage_lo[g] = all.size();
+        all.insert(all.end(), grp[g].begin(), grp[g].end());
+        while (all.size() % members) all.push_back(BinUnit{0u, 0u, 0, 0});
+    }
+    b->stage_lo[S + 1] = all.size();
+    hipFree(b->stage_units);
+    b->stage_units = nullptr;
+    b->stages = 0;
+    hipError_t e = hipMalloc((void**)&b->stage_units, std::max<size_t>(all.size(), 1) * sizeof(BinUnit));
+    if (e == hipSuccess && !all.empty())
+        e = hipMemcpy(b->stage_units, all.data(), all.size() * sizeof(BinUnit), hipMemcpyHostToDevice);
+    if (e == hipSuccess) b->stages = S;
+    return e;
 }
 
 }  // namespace gossip

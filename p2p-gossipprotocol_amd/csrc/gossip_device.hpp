@@ -14,6 +14,14 @@ constexpr unsigned kMaxGrid = 2048;  // 256 CUs x 8 blocks of 256 threads
 
 __device__ __forceinline__ bool bit_alive(const uint32_t* bits, uint32_t v) { return (bits[v >> 5] >> (v & 31)) & 1u; }
 
+// source chunk c of a bin layout: global peers [bin_chunk_vb, bin_chunk_ve) (BinArgs.seg / .cps)
+__device__ __forceinline__ uint64_t bin_chunk_vb(const BinArgs& b, uint64_t c) {
+    return (c / b.cps) * b.seg + (c % b.cps) * b.chunk;
+}
+__device__ __forceinline__ uint64_t bin_chunk_ve(const BinArgs& b, uint64_t c, uint64_t n) {
+    return min(min(bin_chunk_vb(b, c) + b.chunk, (c / b.cps + 1) * b.seg), n);
+}
+
 // the bits a peer can still learn: messages injected so far (at P = 1 the ones whose origin was alive to
 // inject them -- a never-injected message kept every row of config 5 scanning to its end)
 __device__ __forceinline__ uint64_t injm_full(const RoundArgs& a, int w) {

@@ -68,6 +68,11 @@ struct DistRank {
     size_t scan_bytes = 0;
     std::vector<uint64_t> counts_out, counts_in;
     gossip_round_stats local{};
+    // staged dense exchange: its stream (an emulated group shares one), the event after the own block's
+    // words are published, and one event per stage
+    hipStream_t xs = nullptr;
+    hipEvent_t ev_pub = nullptr;
+    hipEvent_t ev_stage[kMaxStages] = {};
 };
 
 }  // namespace
@@ -185,6 +190,11 @@ void free_rank(DistRank& r) {
     hipFree(r.pos);
     hipFree(r.pk);
     hipFree(r.scan_tmp);
+    if (r.ev_pub) hipEventDestroy(r.ev_pub);
+    for (hipEvent_t& e : r.ev_stage)
+        if (e) hipEventDestroy(e);
+    r.ev_pub = nullptr;
+    std::fill(std::begin(r.ev_stage), std::end(r.ev_stage), nullptr);
     if (r.h_io) hipHostFree(r.h_io);
     r.send = r.recv = r.gather = r.seg = r.rec_in = r.d_io = r.h_io = nullptr;
     r.bits = r.pos = r.pk = nullptr;
@@ -447,6 +457,90 @@ gossip_status compact_gather(DistDriver* d) {
     return GOSSIP_OK;
 }
 
+// The all-gather of a binned round in S stages: the global ids are cut into segments of
+// G peers (the bin layout's, bin_segment), stage j delivers every block's part of the segments s = j (mod S),
+// so every block sends in every stage, over every link at once.  The stages go out on the rank's exchange
+// stream after the own block's words are published; each ends with an event, and the rank's scatter stages
+// the own block's chunks first, then waits for each stage's event before the chunks of its segments
+// (ctx_arm_stages, round_compute).  The exchange of stage j + 1 runs under the scatter of stage j.
+// The ranges of block q in stage j, in the order both sides of a send / recv pair walk them
+void stage_ranges(const DistDriver* d, uint32_t q, uint32_t j, uint32_t S, uint64_t G,
+                  std::vector<std::pair<uint64_t, uint64_t>>& out) {
+    out.clear();
+    const uint64_t b = d->part[q], e = d->part[q + 1];
+    if (b >= e) return;
+    for (uint64_t sg = b / G; sg * G < e; ++sg)
+        if (sg % S == j) out.emplace_back(std::max(sg * G, b), std::min((sg + 1) * G, e));
+}
+
+gossip_status staged_gather(DistDriver* d, uint32_t S) {
+    const uint64_t X = d->X;
+    const uint64_t G = ctx_bin_seg(d->ranks[0].ctx);
+    for (size_t i = 0; i < d->ranks.size(); ++i) {
+        DistRank& r = d->ranks[i];
+        DHIP(hipSetDevice(r.device));
+        if (!r.xs) {
+            if (d->emulate && i) r.xs = d->ranks[0].xs;  // one exchange stream for the whole emulated group
+            else DHIP(hipStreamCreateWithFlags(&r.xs, hipStreamNonBlocking));
+        }
+        if (!r.ev_pub) DHIP(hipEventCreateWithFlags(&r.ev_pub, hipEventDisableTiming));
+        for (uint32_t j = 0; j < S; ++j)
+            if (!r.ev_stage[j]) DHIP(hipEventCreateWithFlags(&r.ev_stage[j], hipEventDisableTiming));
+        DHIP(hipEventRecord(r.ev_pub, r.stream));  // after round_begin's publish of the own words
+        DHIP(hipStreamWaitEvent(r.xs, r.ev_pub, 0));
+    }
+    // bytes received per rank: every other block's words, as in all_gather
+    std::vector<void*> tok(d->ranks.size(), nullptr);
+    for (size_t i = 0; i < d->ranks.size(); ++i) {
+        ctx_add_bytes(d->ranks[i].ctx, "all_gather", 8.0 * X * (double)(d->n - d->ranks[i].n_local));
+        if (!d->emulate) ctx_timer_start_on(d->ranks[i].ctx, d->ranks[i].xs, &tok[i]);
+    }
+    std::vector<std::pair<uint64_t, uint64_t>> rg, rg2;
+    for (uint32_t j = 0; j < S; ++j) {
+        if (d->emulate) {
+            for (size_t i = 0; i < d->ranks.size(); ++i) {
+                DistRank& q = d->ranks[i];
+                void* t = nullptr;
+                ctx_timer_start_on(q.ctx, q.xs, &t);
+                for (auto& p : d->ranks) {
+                    if (p.rank == q.rank) continue;
+                    stage_ranges(d, p.rank, j, S, G, rg);
+                    for (auto& x : rg)
+                        DHIP(hipMemcpyAsync(q.gather + x.first * X, p.gather + x.first * X, (x.second - x.first) * X * 8,
+                                            hipMemcpyDeviceToDevice, q.xs));
+                }
+                ctx_timer_stop_on(q.ctx, "all_gather", q.xs, t);
+            }
+        } else {
+            DNCCL(ncclGroupStart());
+            for (auto& r : d->ranks) {
+                hipSetDevice(r.device);
+                stage_ranges(d, r.rank, j, S, G, rg);
+                for (uint32_t q = 0; q < d->world; ++q) {
+                    if (q == r.rank) continue;
+                    for (auto& x : rg)
+                        DNCCL(ncclSend(r.gather + x.first * X, (x.second - x.first) * X, ncclUint64, (int)q, r.comm, r.xs));
+                    stage_ranges(d, q, j, S, G, rg2);
+                    for (auto& x : rg2)
+                        DNCCL(ncclRecv(r.gather + x.first * X, (x.second - x.first) * X, ncclUint64, (int)q, r.comm, r.xs));
+                }
+            }
+            DNCCL(ncclGroupEnd());
+        }
+        for (auto& r : d->ranks) {
+            DHIP(hipSetDevice(r.device));
+            DHIP(hipEventRecord(r.ev_stage[j], r.xs));
+        }
+    }
+    for (size_t i = 0; i < d->ranks.size(); ++i) {
+        DistRank& r = d->ranks[i];
+        DHIP(hipSetDevice(r.device));
+        if (!d->emulate) ctx_timer_stop_on(r.ctx, "all_gather", r.xs, tok[i]);
+        if (gossip_status s = ctx_arm_stages(r.ctx, S, r.ev_stage)) return s;
+    }
+    return GOSSIP_OK;
+}
+
 // dense push: rank p's staged masks for block q (send + begins[q] * X) to q,
 // received at recv + p * n_local(q) * X
 gossip_status all_to_all(DistDriver* d) {
@@ -617,7 +711,11 @@ gossip_status dist_step(DistDriver* d, gossip_round_stats* out) {
         // a narrow frontier exchanges its non-zero words only (the same gather buffer either way)
         const uint32_t gpm = ctx_gather_pm(d->ranks[0].ctx);
         const bool compact = d->world > 1 && d->front * 1000 < (uint64_t)gpm * d->n;
-        if ((s = compact ? compact_gather(d) : all_gather(d))) return s;
+        // a binned round with a whole-slice exchange goes out in stages under its scatter (every rank has a
+        // streamed bin layout and asks for the same number of stages)
+        uint32_t S = mode == GOSSIP_MODE_BIN && !compact && d->world > 1 ? ctx_stages(d->ranks[0].ctx) : 1u;
+        for (auto& r : d->ranks) S = ctx_stages(r.ctx) == S ? S : 1u;
+        if ((s = compact ? compact_gather(d) : S > 1 ? staged_gather(d, S) : all_gather(d))) return s;
         for (auto& r : d->ranks)
             if ((s = gossip_round_compute(r.ctx))) return s;
         for (auto& r : d->ranks)
@@ -769,13 +867,14 @@ void dist_reset(DistDriver* d) {
 void dist_free(DistDriver* d) {
     if (!d) return;
     for (auto& r : d->ranks) free_rank(r);
-    std::vector<hipStream_t> done;  // emulated groups share one stream
-    for (auto& r : d->ranks) {
-        if (!r.stream || std::find(done.begin(), done.end(), r.stream) != done.end()) continue;
-        hipSetDevice(r.device);
-        hipStreamDestroy(r.stream);
-        done.push_back(r.stream);
-    }
+    std::vector<hipStream_t> done;  // emulated groups share one stream (and one exchange stream)
+    for (auto& r : d->ranks)
+        for (hipStream_t st : {r.stream, r.xs}) {
+            if (!st || std::find(done.begin(), done.end(), st) != done.end()) continue;
+            hipSetDevice(r.device);
+            hipStreamDestroy(st);
+            done.push_back(st);
+        }
     delete d;
 }
 

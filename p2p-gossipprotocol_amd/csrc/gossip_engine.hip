@@ -194,6 +194,10 @@ struct gossip_ctx {
                                           // sparser dense rounds blocked
     uint64_t pb_direct_in = kPbFineIn;    // "blocked_direct_in": leading tiles of more in-degree are hubs
     uint32_t pb_lo_pm = kPbLoPermille;    // "blocked_push_permille": push rounds from this frontier run blocked
+    uint32_t stages_req = 4;     // "exchange_stages": a partitioned binned round's all-gather in this many stages,
+                                 // the scatter of each stage's chunks overlapping the next stage (1: one piece)
+    uint32_t stage_n = 0;        // armed by the driver for this round: the scatter waits stage_ev[j] ...
+    hipEvent_t stage_ev[gossip::kMaxStages] = {};  // ... before the chunks of stage j (gossip_dist.hip)
     uint32_t gather_pm = kGatherPermille; // "gather_permille": partitioned dense rounds below this frontier per-mille
                                           // exchange {tile bitmap, packed non-zero words} (gossip_dist.hip)
     uint32_t row_step = 1;                // "pull_step": k_pull_rows's neighbour words per row per step
@@ -302,6 +306,17 @@ DistDriver* ctx_dist(gossip_ctx* c) { return c->dist; }
 bool ctx_timing(gossip_ctx* c) { return c->timing; }
 uint64_t ctx_frontier_est(gossip_ctx* c) { return c->frontier_est; }
 uint32_t ctx_gather_pm(gossip_ctx* c) { return c->gather_pm; }
+uint32_t ctx_stages(gossip_ctx* c) {
+    return c->bins_ready && c->bin_stream && c->n_local != c->n ? std::min<uint32_t>(c->stages_req, kMaxStages) : 1u;
+}
+uint64_t ctx_bin_seg(gossip_ctx* c) { return c->bins.seg; }
+gossip_status ctx_arm_stages(gossip_ctx* c, uint32_t S, const hipEvent_t* ev) {  // (the caller set the device)
+    if (const hipError_t e = build_stage_units(&c->bins, S, c->begin, c->end, c->n))
+        return fail(GOSSIP_EHIP, std::string("staged scatter units: ") + hipGetErrorString(e));
+    std::copy(ev, ev + S, c->stage_ev);
+    c->stage_n = S;
+    return GOSSIP_OK;
+}
 void ctx_clear_exchange(gossip_ctx* c) {
     c->send = nullptr;
     c->recv = nullptr;
@@ -391,6 +406,20 @@ void ctx_timer_stop(gossip_ctx* c, const char* name, void* token) {
     if (!c->timing || !token) return;
     hipEvent_t b = take_event(c);
     hipEventRecord(b, c->stream);
+    c->timers[name].pending.emplace_back(static_cast<hipEvent_t>(token), b);
+}
+// the same on another stream of the ctx's device (the staged exchange's copy / collective stream)
+void ctx_timer_start_on(gossip_ctx* c, hipStream_t s, void** token) {
+    *token = nullptr;
+    if (!c->timing) return;
+    hipEvent_t a = take_event(c);
+    hipEventRecord(a, s);
+    *token = a;
+}
+void ctx_timer_stop_on(gossip_ctx* c, const char* name, hipStream_t s, void* token) {
+    if (!c->timing || !token) return;
+    hipEvent_t b = take_event(c);
+    hipEventRecord(b, s);
     c->timers[name].pending.emplace_back(static_cast<hipEvent_t>(token), b);
 }
 void ctx_add_bytes(gossip_ctx* c, const char* name, double bytes) {
@@ -520,7 +549,10 @@ RoundArgs make_args(gossip_ctx* c) {
     a.n_src = c->n_local;
     a.nx = c->nx;
     a.front = c->front;
-    if (c->tact[0] && c->n_local == c->n && c->world == 1) {  // single partition: remote applies keep no marks
+    // (a vertex block keeps marks of its own tiles: local deliveries, and the remote applies -- k_apply_records,
+    // k_apply_remote -- mark the tiles of the peers they activate; round 5, before which a block swept every
+    // tile in every push round: config 4 as 8 parts, ≈ 1.2 ms of kernels per near-empty round)
+    if (c->tact[0]) {
         a.tcur = c->tact[c->tcur];
         // the marked-tile sweep only for a nearly empty frontier (it walks 64 tiles per wave in turn;
         // at a 1.3 % frontier, 57 % of the tiles, the full sweep was faster: 3.1 against 4.4 ms)
@@ -716,6 +748,9 @@ BinArgs bin_args(const gossip_ctx* c, bool noskip, uint32_t src_side) {
     b.chunk_begin = s.chunk_begin;
     b.n_chunks = s.n_chunks;
     b.chunk = s.chunk;
+    b.seg = s.seg;
+    b.cps = s.cps;
+    b.n_units = s.n_units;
     b.units = s.units;
     b.xcd_units = s.xcd_units;
     b.bdst = s.bdst;
@@ -829,8 +864,10 @@ gossip_status prepare_bins(gossip_ctx* c) {
         // no partial-sector stores, no allocation trials).  "bin_stream" 0 keeps the slot layout (A/B, tests).
         c->bin_stream = c->bin_stream_req != 0;
         std::string err;
+        // a vertex block cuts the source ids into segments (the staged dense exchange delivers whole ones)
+        const uint64_t seg = c->n_local != c->n ? bin_segment(c->n) : 0;
         const hipError_t e = build_bins(c->rp, c->col, c->n_local, c->n, c->n_edges, c->heavy, c->Wp, c->bin_stream,
-                                        c->bin_words_req, c->bin_chunk_req, c->stream, &c->bins, &err);
+                                        c->bin_words_req, c->bin_chunk_req, seg, c->stream, &c->bins, &err);
         if (e == hipSuccess) {
             c->bins_ready = true;
             if (gossip_status ts = tune_val(c)) return ts;
@@ -1384,7 +1421,21 @@ gossip_status round_compute(gossip_ctx* c) {
         BinArgs b = bin_args(c, c->bins_first, src_stats(c));
         // every bin is needy while more than one (peer, message) pair per peer is missing: no check pass
         b.needy_check = c->cur_missing > c->n_local && c->needy_skip ? 0u : 1u;
-        HIPCHK(timed(c, "bin_scatter", [&] { return launch_bin_scatter(a, b, pw, c->stream); }));
+        if (c->stage_n && c->bins.stages == c->stage_n) {
+            // staged exchange (gossip_dist.hip): the own block's chunks first, then each stage's chunks once
+            // the driver's event says their words have landed in the gather buffer
+            const uint32_t S = c->stage_n;
+            c->stage_n = 0;
+            for (uint32_t g = 0; g <= S; ++g) {
+                if (g) HIPCHK(hipStreamWaitEvent(c->stream, c->stage_ev[g - 1], 0));
+                BinArgs bg = b;
+                bg.units = c->bins.stage_units + c->bins.stage_lo[g];
+                bg.n_units = c->bins.stage_lo[g + 1] - c->bins.stage_lo[g];
+                if (bg.n_units) HIPCHK(timed(c, "bin_scatter", [&] { return launch_bin_scatter(a, bg, pw, c->stream); }));
+            }
+        } else {
+            HIPCHK(timed(c, "bin_scatter", [&] { return launch_bin_scatter(a, b, pw, c->stream); }));
+        }
         HIPCHK(timed(c, "bin_apply", [&] { return launch_bin_apply(a, b, pw, c->stream); }));
         c->bins_first = false;
         HIPCHK(timed(c, "pull_heavy", [&] { return launch_pull_heavy(a, pw, c->stream, hz); }));
@@ -1844,6 +1895,10 @@ gossip_status gossip_set_tuning(gossip_ctx* c, const char* key, int64_t value) {
         }
     }
     else if (k == "gather_permille") c->gather_pm = value < 0 ? kGatherPermille : u;
+    else if (k == "exchange_stages") {
+        if (value < 1 || value > (int64_t)kMaxStages) return fail(GOSSIP_EINVAL, "exchange_stages must be 1..16");
+        c->stages_req = (uint32_t)value;
+    }
     else return fail(GOSSIP_EINVAL, "unknown tuning option: " + k);
     return GOSSIP_OK;
 }

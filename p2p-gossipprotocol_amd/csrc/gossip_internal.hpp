@@ -5,8 +5,10 @@
 
 #include <rocprofiler-sdk-roctx/roctx.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <string>
+#include <vector>
 
 #include "../../include/gossip/gossip.h"
 
@@ -66,6 +68,8 @@ constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 constexpr uint16_t kRunStart = 0x8000u;        // cb_src flag; chunk-local sources are < kBinChunkWords < 2^15
 static_assert(kBinChunkWords < kRunStart, "chunk-local sources fit 15 bits");
 
+constexpr uint32_t kMaxStages = 16;   // pipelined dense exchange: source segments delivered in at most this many stages
+
 struct Bin {
     uint32_t v0, v1;  // destination peers [v0, v1) (local ids, whole 64-peer tiles)
     uint64_t s0, s1;  // padded slot range
@@ -86,8 +90,13 @@ struct BinArgs {
     const uint32_t* cb_grp;       // per 64-entry group: the run of its first entry
     uint64_t n_binned;            // cb entries
     const uint64_t* chunk_begin;  // n_chunks + 1 offsets into cb_*
-    uint64_t n_chunks, chunk;     // source chunks of `chunk` peers
-    const BinUnit* units;         // scatter work units, in chunk order
+    uint64_t n_chunks, chunk;     // source chunks of `chunk` peers ...
+    uint64_t seg, cps;            // ... cut out of segments of `seg` peers, cps chunks each: chunk c covers
+                                  // [chunk_vb(c), chunk_ve(c)) (one segment at P = 1: c * chunk; a vertex block
+                                  // cuts the global ids into segments so a pipelined exchange can deliver the
+                                  // sources of whole chunks stage by stage, gossip_dist.hip)
+    const BinUnit* units;         // scatter work units, in chunk order (or a stage's units, staged exchange)
+    uint64_t n_units;             // units of this launch (a multiple of kScatterGrid / 8)
     const uint64_t* xcd_units;    // 9 words, only xcd_units[8] is meaningful: the unit count, a multiple of
                                   // kScatterGrid / 8 (scatter_rows deals rows of units round-robin over the XCDs)
     const uint16_t* bdst;         // per slot: destination - bin.v0
@@ -125,6 +134,7 @@ enum { kProbeSrc = 0, kProbeInit, kProbeSlots, kProbeFinish, kProbeBins, kProbeS
 
 struct BinState {
     Bin* bins = nullptr;
+    uint64_t seg = 0, cps = 0;    // BinArgs.seg, .cps
     uint64_t n_bins = 0;
     uint16_t* cb_src = nullptr;
     uint32_t* cb_run = nullptr;
@@ -137,6 +147,12 @@ struct BinState {
     BinUnit* units = nullptr;
     uint64_t* xcd_units = nullptr;
     uint64_t n_units = 0;
+    // staged exchange (P > 1, gossip_dist.hip): the units reordered -- the chunks of the own block first,
+    // then stage j = the chunks of segments s = j (mod S) -- each group padded to whole rows
+    BinUnit* stage_units = nullptr;
+    uint64_t stage_lo[kMaxStages + 2] = {};  // group g (0: own block, 1 + j: stage j) = [stage_lo[g], stage_lo[g + 1])
+    uint32_t stages = 0;                      // S the staged order was built for (0: none)
+    std::vector<BinUnit> h_units;             // the units (host copy)
     uint16_t* bdst = nullptr;
     uint64_t* val = nullptr;
     uint64_t* dummy = nullptr;
@@ -455,10 +471,21 @@ hipError_t build_powerlaw_device(uint64_t n_global, uint64_t begin, uint64_t end
 // hipErrorOutOfMemory (state untouched) when the layout does not fit next to
 // what is already resident.
 // bin_words / chunk_words: LDS words of a bin / a source chunk (0: chosen from the overlay's size)
+// seg: source segment size (0: one segment; a vertex block of a partitioned run passes bin_segment(n_global))
 hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local, uint64_t n_global, uint64_t n_edges,
-                      uint32_t heavy, uint32_t Wp, bool stream, uint32_t bin_words, uint32_t chunk_words, hipStream_t s,
-                      BinState* out, std::string* err);
+                      uint32_t heavy, uint32_t Wp, bool stream, uint32_t bin_words, uint32_t chunk_words, uint64_t seg,
+                      hipStream_t s, BinState* out, std::string* err);
 void free_bins(BinState* b);
+// a vertex block's source segments: 64 of them over the global ids (whole 64-peer tiles)
+inline uint64_t bin_segment(uint64_t n_global) { return ((n_global + 63) / 64 + 63) / 64 * 64; }
+// host side of BinArgs' chunk geometry
+inline uint64_t chunk_vb(uint64_t c, uint64_t seg, uint64_t cps, uint64_t chunk) { return (c / cps) * seg + (c % cps) * chunk; }
+inline uint64_t chunk_ve(uint64_t c, uint64_t seg, uint64_t cps, uint64_t chunk, uint64_t n) {
+    const uint64_t e = std::min(chunk_vb(c, seg, cps, chunk) + chunk, (c / cps + 1) * seg);
+    return std::min(e, n);
+}
+// the staged unit order for S stages of a vertex block [begin, end) (host side; BinState.stage_*)
+hipError_t build_stage_units(BinState* b, uint32_t S, uint64_t begin, uint64_t end, uint64_t n_global);
 
 // ---- library-driven multi-GPU rounds (gossip_dist.hip) ----
 struct DistDriver;
@@ -472,6 +499,13 @@ DistDriver* ctx_dist(gossip_ctx* c);
 bool ctx_timing(gossip_ctx* c);
 uint64_t ctx_frontier_est(gossip_ctx* c);  // peers the last round activated (this round's frontier)
 uint32_t ctx_gather_pm(gossip_ctx* c);     // "gather_permille"
+// staged dense exchange: the stages this ctx's binned rounds can take (1: none), its source segment size, and
+// the events the next binned round's scatter waits on before the chunks of each stage
+uint32_t ctx_stages(gossip_ctx* c);
+uint64_t ctx_bin_seg(gossip_ctx* c);
+gossip_status ctx_arm_stages(gossip_ctx* c, uint32_t S, const hipEvent_t* ev);
+void ctx_timer_start_on(gossip_ctx* c, hipStream_t s, void** token);
+void ctx_timer_stop_on(gossip_ctx* c, const char* name, hipStream_t s, void* token);
 // forget the exchange buffers registered by gossip_set_exchange / _gather / _sparse (they are being freed)
 void ctx_clear_exchange(gossip_ctx* c);
 // time device work issued on the ctx's stream under `name` (gossip_kernel_time) while timing is on

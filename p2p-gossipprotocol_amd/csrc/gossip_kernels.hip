@@ -114,6 +114,18 @@ __device__ __forceinline__ void mark_send(const RoundArgs& a, uint32_t c) {
     if (!(*w & bit)) atomicOr(w, bit);
 }
 
+// Owned peer lv was activated (its next-round new words were zero): its 64-peer tile joins the next round's
+// frontier tiles (a.tnx; read first: most tiles are already marked)
+__device__ __forceinline__ void mark_tile(const RoundArgs& a, uint64_t lv, Acc& acc) {
+    if (!a.tnx) return;
+    const unsigned long long tb = 1ull << ((lv >> 6) & 63);
+    unsigned long long* tw = reinterpret_cast<unsigned long long*>(a.tnx) + (lv >> 12);
+    if (!(*tw & tb)) {
+        atomicOr(tw, tb);
+        acc.atomics++;
+    }
+}
+
 // One delivery to global peer c (bit 31: masked edge): liveness, remote
 // staging or the local test-and-set.
 template <int W, bool CA, bool RM>
@@ -232,15 +244,7 @@ __device__ __forceinline__ void deliver_batch(const RoundArgs& a, const uint32_t
             if (!fr[j][w]) continue;
             acc.fresh += (unsigned long long)__popcll(fr[j][w]);
             acc.activated += onx[j][w] == 0;
-            if (a.tnx && onx[j][w] == 0) {  // the peer's tile joins the next round's frontier tiles
-                const uint64_t lv = (uint64_t)(c[j] - (uint32_t)a.begin);
-                const unsigned long long tb = 1ull << ((lv >> 6) & 63);
-                unsigned long long* tw = reinterpret_cast<unsigned long long*>(a.tnx) + (lv >> 12);
-                if (!(*tw & tb)) {  // read first: most tiles are already marked
-                    atomicOr(tw, tb);
-                    acc.atomics++;
-                }
-            }
+            if (onx[j][w] == 0) mark_tile(a, (uint64_t)(c[j] - (uint32_t)a.begin), acc);  // joins next round's tiles
         }
 }
 
@@ -964,7 +968,7 @@ __device__ __forceinline__ void scatter_stage(const RoundArgs& a, const BinArgs&
     static_assert(kBinChunkWords % kScatterBlock == 0, "slice split");
     const int lane = threadIdx.x & 63;
     // global source chunk; words from nw_src (own words at P = 1, the all-gathered ones at P > 1)
-    const uint64_t vb = (uint64_t)un.c * b.chunk, ve = min(vb + b.chunk, a.n_src);  // vb % 64 == 0
+    const uint64_t vb = bin_chunk_vb(b, un.c), ve = bin_chunk_ve(b, un.c, a.n_src);  // vb % 64 == 0
     const uint64_t nwords = (ve - vb) * W;
     // stage the slice (and the previous round's live bits): every load of
     // the lane in flight at once
@@ -1042,9 +1046,9 @@ __device__ __forceinline__ void scatter_stage(const RoundArgs& a, const BinArgs&
 // row barrier on top of that measured no gain: 71.4 against 71.3 ms per step).
 template <class F>
 __device__ __forceinline__ void scatter_rows(const BinArgs& b, F&& unit) {
-    // rows of `members` units, row r on XCD r % 8 (gossip_bins.hip; xcd_units[8]: the unit count)
+    // rows of `members` units, row r on XCD r % 8 (gossip_bins.hip; n_units: this launch's unit count)
     const uint32_t xcd = blockIdx.x & 7, member = blockIdx.x >> 3, members = gridDim.x >> 3;
-    const uint64_t rows = b.xcd_units[8] / members;
+    const uint64_t rows = b.n_units / members;
     for (uint64_t r = xcd; r < rows; r += 8) unit(r * members + member);
 }
 
@@ -1395,8 +1399,8 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_stream(RoundArgs a, BinAr
         // b.direct (a vertex block of a partitioned run): a chunk with no owned source books no stats, and
         // its few entries (1/P of a whole overlay's) read their words straight from the gather buffer (the
         // chunk's 144 KB stay in L2 after the first touch) instead of paying the chunk's staging
-        const uint64_t vb = (uint64_t)un.c * b.chunk;
-        const bool direct = b.direct && !(vb < a.end && vb + b.chunk > a.begin);  // block-uniform
+        const uint64_t vb = bin_chunk_vb(b, un.c);
+        const bool direct = b.direct && !(vb < a.end && bin_chunk_ve(b, un.c, a.n_src) > a.begin);  // block-uniform
         const uint64_t* src = a.nw_src + vb * W;
         if (!direct) {
             scatter_stage<W, COV>(a, b, un, wd, slice, live_s, cov_s, acc);
@@ -2337,7 +2341,8 @@ __global__ __launch_bounds__(kBlock) void k_inject(RoundArgs a, const uint32_t* 
 }
 
 // Partitioned rounds: OR the masks received from every rank into the owned
-// peers (test-and-set without atomics: this kernel is the only writer).
+// peers (test-and-set without atomics: this kernel is the only writer); an
+// activated peer marks its tile for the next round's marked-tile sweep.
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_apply_remote(RoundArgs a, const uint64_t* recv, uint32_t world,
                                                          uint64_t stride) {
@@ -2355,13 +2360,16 @@ __global__ __launch_bounds__(kBlock) void k_apply_remote(RoundArgs a, const uint
                 if (!fr) continue;
                 a.nx[v * W + w] = nxc | fr;
                 acc.fresh += (unsigned long long)__popcll(fr);
+                if (!nxc) mark_tile(a, v, acc);
                 continue;
             }
             const uint64_t fr = inc & ~cur;
             if (!fr) continue;
             a.seen[v * W + w] = cur | fr;
-            a.nx[v * W + w] |= fr;
+            const uint64_t nxc = a.nx[v * W + w];
+            a.nx[v * W + w] = nxc | fr;
             acc.fresh += (unsigned long long)__popcll(fr);
+            if (!nxc) mark_tile(a, v, acc);
         }
     }
     flush(acc, a.st);
@@ -2471,6 +2479,7 @@ __global__ __launch_bounds__(kBlock) void k_apply_records(RoundArgs a, const uin
                 const unsigned long long fr = u & ~old;
                 acc.activated += fr && old == 0;
                 acc.fresh += (unsigned long long)__popcll(fr);
+                if (fr && old == 0) mark_tile(a, lv, acc);
                 continue;
             }
             const unsigned long long fr = m & ~atomicOr(sp + w, m);
@@ -2479,6 +2488,7 @@ __global__ __launch_bounds__(kBlock) void k_apply_records(RoundArgs a, const uin
                 const unsigned long long onx = atomicOr(reinterpret_cast<unsigned long long*>(a.nx) + lv * W + w, fr);
                 acc.activated += onx == 0;
                 acc.fresh += (unsigned long long)__popcll(fr);
+                if (onx == 0) mark_tile(a, lv, acc);
             }
         }
     }

@@ -44,7 +44,7 @@ def test_group_on_one_device_equals_oracle(oracle, idx, n, P):
     assert again == stats
 
 
-@pytest.mark.parametrize("gather", ["compact", "whole", "direct"])
+@pytest.mark.parametrize("gather", ["compact", "whole", "whole_1_stage", "whole_3_stages", "direct"])
 @pytest.mark.parametrize("P", [2, 3, 5])
 @pytest.mark.parametrize("idx,n", [(3, 100_003), (5, 1 << 15), (2, 40_000)])
 def test_group_dense_exchange_forms_equal_oracle(oracle, idx, n, P, gather):
@@ -55,11 +55,18 @@ def test_group_dense_exchange_forms_equal_oracle(oracle, idx, n, P, gather):
     pairs, expansion into the gather buffer) -- on blocks that do not end on a
     tile boundary (n = 100,003) and a short last block (P = 3, 5).  Both forms
     give the oracle's run, as does the scatter reading other blocks' words
-    straight from the gather buffer ("direct": scatter_direct)."""
+    straight from the gather buffer ("direct": scatter_direct).  A binned
+    round's whole-slice exchange goes out in stages of source segments, the
+    scatter of each stage's chunks waiting for its event (4 by default; 1 =
+    one piece; 3 does not divide the 64 segments evenly)."""
     w = config(idx, n, pick=oracle.pick_origins)
     rp, col = oracle.gen_workload(w)
     ref = oracle.simulate_workload(w, rp, col)
-    tuning = {"gather_permille": 0 if gather == "whole" else 1000}
+    tuning = {"gather_permille": 0 if gather.startswith("whole") else 1000}
+    if gather == "whole_1_stage":
+        tuning["exchange_stages"] = 1
+    if gather == "whole_3_stages":
+        tuning["exchange_stages"] = 3
     if gather == "direct":
         tuning["scatter_direct"] = 1
     stats, seen, reps, again = _run_group(w, [0] * P, tuning=tuning)
