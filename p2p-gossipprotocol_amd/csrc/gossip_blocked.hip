@@ -153,16 +153,18 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_scatter(RoundArgs a, PbArgs p, 
         bool any = false;
 #pragma unroll
         for (int j = 0; j < kPbU; ++j) {
-            dir[j] = rec[j] && c[j] < p.direct_end;
+            dir[j] = rec[j] && c[j] >= p.dir_lo && c[j] < p.dir_hi;
             any |= dir[j];
         }
         if (!__ballot(any)) return;  // (most batches: no hub among the destinations)
         // a.fold: the hub's own new words (nw, left for the split to clear) are not yet in seen everywhere
         unsigned long long nwc[kPbU];
+        uint32_t lc[kPbU];  // local index of a direct destination
 #pragma unroll
         for (int j = 0; j < kPbU; ++j) {
-            cur[j] = a.seen[dir[j] ? c[j] : 0];
-            nwc[j] = a.fold && dir[j] ? a.nw[c[j]] : 0ull;
+            lc[j] = dir[j] ? c[j] - p.dir_base : 0u;
+            cur[j] = a.seen[lc[j]];
+            nwc[j] = a.fold && dir[j] ? a.nw[lc[j]] : 0ull;
         }
 #pragma unroll
         for (int j = 0; j < kPbU; ++j) {
@@ -170,17 +172,17 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_scatter(RoundArgs a, PbArgs p, 
             rec[j] = false;
             if (!(m[j] & ~(cur[j] | nwc[j]))) continue;  // all duplicates: dropped (peer.cpp:281)
             const unsigned long long fr =
-                m[j] & ~nwc[j] & ~atomicOr(reinterpret_cast<unsigned long long*>(a.seen) + c[j], m[j]);
+                m[j] & ~nwc[j] & ~atomicOr(reinterpret_cast<unsigned long long*>(a.seen) + lc[j], m[j]);
             acc.atomics++;
             acc.fresh_or[0] |= fr;
             if (!fr) continue;
-            const unsigned long long onx = atomicOr(reinterpret_cast<unsigned long long*>(a.nx) + c[j], fr);
+            const unsigned long long onx = atomicOr(reinterpret_cast<unsigned long long*>(a.nx) + lc[j], fr);
             acc.atomics++;
             acc.fresh += (unsigned long long)__popcll(fr);
             acc.activated += onx == 0;
             if (a.tnx && onx == 0) {  // the peer's tile joins the next round's frontier tiles
-                unsigned long long* tw = reinterpret_cast<unsigned long long*>(a.tnx) + (c[j] >> 12);
-                const unsigned long long tb = 1ull << ((c[j] >> 6) & 63);
+                unsigned long long* tw = reinterpret_cast<unsigned long long*>(a.tnx) + (lc[j] >> 12);
+                const unsigned long long tb = 1ull << ((lc[j] >> 6) & 63);
                 if (!(*tw & tb)) atomicOr(tw, tb);
             }
         }
@@ -254,7 +256,7 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_scatter(RoundArgs a, PbArgs p, 
                 deg = d <= a.heavy ? (uint32_t)d : 0u;  // heavy rows: (1)
                 // consumed: this buffer is the next round's accumulator (the hubs' words are read by
                 // direct(), heavy rows' by their chunks: the split clears those)
-                if (!p.clear_all && d <= a.heavy && v >= p.direct_end) a.nw[v] = 0ull;
+                if (!p.clear_all && d <= a.heavy && v >= p.keep_end) a.nw[v] = 0ull;
             }
             const uint32_t rest = n_pk - cnt;
             wave_sync();
@@ -312,7 +314,7 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_scatter(RoundArgs a, PbArgs p, 
                 acc.frontier++;
                 const uint32_t pc = (uint32_t)__popcll(m);
                 acc.covered += pc;
-                acc.digest += digest_weight(v * wd) * m;  // word 0 of wd
+                acc.digest += digest_weight((a.begin + v) * wd) * m;  // word 0 of wd
                 if (COV)
                     for (unsigned long long x = m; x; x &= x - 1) atomicAdd(&cov_s[__builtin_ctzll(x)], 1u);
                 const uint32_t pos = n_pk + lane_rank(bal);
@@ -701,6 +703,14 @@ PbArgs pb_args(const PbState& p) {
     a.err = p.err;
     a.direct_end = p.direct_end;
     a.map_shift = p.map_shift;
+    if (p.rank_mode) {  // the own block [c_lo[own], c_lo[own + 1]) is delivered at once (set by the caller)
+        a.keep_end = 0;
+    } else {
+        a.dir_lo = 0;
+        a.dir_hi = p.direct_end;
+        a.dir_base = 0;
+        a.keep_end = p.direct_end;
+    }
     return a;
 }
 
@@ -856,6 +866,149 @@ hipError_t build_pb(const uint64_t* rp, const uint32_t* col, uint64_t n_local, u
     return hipSuccess;
 }
 #undef PCHECK
+
+// ---- a vertex block's sparse push as records (P > 1) ----
+namespace {
+// every edge u -> v of the block into another block q: cnt[w][q]++ with w the level-1 workgroup that expands it
+__global__ __launch_bounds__(256) void k_px_count(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
+                                                  uint32_t heavy, const HeavyChunk* chunks, uint64_t n_chunks,
+                                                  const uint32_t* lo, uint32_t world, uint32_t own, uint32_t* cnt) {
+    __shared__ uint32_t lo_s[kPbCoarse + 1];
+    for (uint32_t i = threadIdx.x; i <= kPbCoarse; i += blockDim.x) lo_s[i] = i <= world ? lo[i] : 0xFFFFFFFFu;
+    __syncthreads();
+    auto edge = [&](uint32_t w, uint32_t v) {
+        const uint32_t q = find_bin<kPbCoarse>(lo_s, v);
+        if (q != own) atomicAdd(&cnt[(uint64_t)w * world + q], 1u);
+    };
+    for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < n_local; u += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t e0 = rp[u], e1 = rp[u + 1];
+        if (e1 - e0 > heavy) continue;
+        const uint32_t w = (uint32_t)((u >> 6) % kPbGrid);
+        for (uint64_t e = e0; e < e1; ++e) edge(w, col[e] & ~kMaskedEdge);
+    }
+    const int lane = threadIdx.x & 63;
+    for (uint64_t ci = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; ci < n_chunks;
+         ci += ((uint64_t)gridDim.x * blockDim.x) >> 6) {
+        const HeavyChunk ch = chunks[ci];
+        const uint32_t w = (uint32_t)(ci % kPbGrid);
+        for (uint64_t e = ch.e0 + lane; e < ch.e1; e += 64) edge(w, col[e] & ~kMaskedEdge);
+    }
+}
+
+// block (w, q): segment (w, q)'s records to seg + (q * stride + sum of the lengths of segments (w' < w, q)) * 2
+__global__ __launch_bounds__(256) void k_px_pack(PbArgs p, uint32_t world, uint32_t own, const uint64_t* part,
+                                                 uint64_t stride, uint64_t* seg, unsigned long long* counts,
+                                                 const HeavyChunk* chunks, uint64_t n_chunks, uint64_t* nw) {
+    const uint32_t w = blockIdx.x, q = blockIdx.y;
+    __shared__ unsigned long long off_s;
+    if (threadIdx.x < 64) {  // one wave: the lengths of the segments before this one (and the total, block 0)
+        const uint32_t n = w == 0 ? kPbGrid : w;
+        unsigned long long x = 0;
+        for (uint32_t i = threadIdx.x; i < n; i += 64) x += i < w || w == 0 ? p.s1_len[(uint64_t)i * world + q] : 0u;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+        if (threadIdx.x == 0) {
+            off_s = w == 0 ? 0ull : x;
+            if (w == 0) counts[q] = q == own ? 0ull : x;
+        }
+    }
+    __syncthreads();
+    if (q != own) {
+        const uint64_t len = p.s1_len[(uint64_t)w * world + q], base = p.s1_base[(uint64_t)w * world + q];
+        uint64_t* out = seg + (q * stride + off_s) * 2;
+        const uint64_t first = part[q];
+        for (uint64_t i = threadIdx.x; i < len; i += blockDim.x) {
+            const uint32_t d = p.r1_dst[base + i];
+            const bool pad = d == kPbPad;
+            out[2 * i] = pad ? first : (uint64_t)d;
+            out[2 * i + 1] = pad ? 0ull : p.r1_w[base + i];
+        }
+    }
+    if (q == 0)  // the heavy rows' words, read by every workgroup's chunks during level 1
+        for (uint64_t ci = (uint64_t)w * blockDim.x + threadIdx.x; ci < n_chunks; ci += (uint64_t)kPbGrid * blockDim.x)
+            nw[chunks[ci].v] = 0ull;
+}
+}  // namespace
+
+hipError_t build_px(const uint64_t* rp, const uint32_t* col, uint64_t n_local, uint64_t n_global, uint32_t heavy,
+                    const HeavyChunk* chunks, uint64_t n_chunks, const uint64_t* part, uint32_t world, uint32_t own,
+                    uint64_t cap_records, hipStream_t s, PbState* out, std::string* err) {
+    PbState st;
+    uint32_t* d_cnt = nullptr;
+    auto bail = [&](hipError_t e, const char* what) {
+        if (err) *err = std::string(what) + ": " + hipGetErrorString(e);
+        hipGetLastError();
+        hipFree(d_cnt);
+        free_pb(&st);
+        return e;
+    };
+    if (world < 2 || world > kPbCoarseMax || n_global >= (1ull << 32)) return hipErrorInvalidValue;
+    st.rank_mode = 1;
+    st.n_coarse = world;
+    while (((uint64_t)kPbMap << st.map_shift) < n_global) ++st.map_shift;
+    std::vector<uint32_t> lo(world + 1);
+    for (uint32_t q = 0; q <= world; ++q) lo[q] = (uint32_t)part[q];
+    hipError_t e = hipMalloc((void**)&st.c_lo, (world + 1) * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemcpyAsync(st.c_lo, lo.data(), (world + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, s);
+    const uint64_t n1s = (uint64_t)kPbGrid * world;
+    if (e == hipSuccess) e = hipMalloc((void**)&d_cnt, n1s * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemsetAsync(d_cnt, 0, n1s * sizeof(uint32_t), s);
+    if (e != hipSuccess) return bail(e, "record push tables");
+    hipLaunchKernelGGL(k_px_count, dim3(8192), dim3(256), 0, s, rp, col, n_local, heavy, chunks, n_chunks, st.c_lo,
+                       world, own, d_cnt);
+    if ((e = hipGetLastError()) != hipSuccess) return bail(e, "k_px_count");
+    std::vector<uint32_t> cnt(n1s), cap(n1s);
+    std::vector<uint64_t> base(n1s), per_q(world, 0);
+    if ((e = hipMemcpyAsync(cnt.data(), d_cnt, n1s * sizeof(uint32_t), hipMemcpyDeviceToHost, s)) != hipSuccess ||
+        (e = hipStreamSynchronize(s)) != hipSuccess)
+        return bail(e, "record push counts");
+    uint64_t n1 = 0;
+    for (uint64_t i = 0; i < n1s; ++i) {  // whole flushes (the last one padded)
+        cap[i] = (cnt[i] + kPbB1 - 1) / kPbB1 * kPbB1;
+        base[i] = n1;
+        n1 += cap[i];
+        per_q[i % world] += cap[i];
+    }
+    for (uint32_t q = 0; q < world; ++q)
+        if (per_q[q] > cap_records) {
+            if (err) *err = "a destination block's records could outgrow its exchange slot";
+            hipFree(d_cnt);
+            free_pb(&st);
+            return hipErrorInvalidValue;
+        }
+    st.n1 = n1;
+    size_t free_b = 0, total_b = 0;
+    if ((e = hipMemGetInfo(&free_b, &total_b)) != hipSuccess) return bail(e, "hipMemGetInfo");
+    if (n1 * 12 + (1ull << 30) > free_b) {
+        hipFree(d_cnt);
+        free_pb(&st);
+        if (err) *err = "record-push segments do not fit in free device memory";
+        return hipErrorOutOfMemory;
+    }
+    if ((e = hipMalloc((void**)&st.s1_base, n1s * sizeof(uint64_t))) != hipSuccess ||
+        (e = hipMalloc((void**)&st.s1_cap, n1s * sizeof(uint32_t))) != hipSuccess ||
+        (e = hipMalloc((void**)&st.s1_len, n1s * sizeof(uint32_t))) != hipSuccess ||
+        (e = hipMalloc((void**)&st.err, sizeof(uint32_t))) != hipSuccess ||
+        (e = hipMalloc((void**)&st.r1_dst, (n1 + 1) * sizeof(uint32_t))) != hipSuccess ||
+        (e = hipMalloc((void**)&st.r1_w, (n1 + 1) * sizeof(unsigned long long))) != hipSuccess ||
+        (e = hipMemcpyAsync(st.s1_base, base.data(), n1s * sizeof(uint64_t), hipMemcpyHostToDevice, s)) != hipSuccess ||
+        (e = hipMemcpyAsync(st.s1_cap, cap.data(), n1s * sizeof(uint32_t), hipMemcpyHostToDevice, s)) != hipSuccess ||
+        (e = hipMemsetAsync(st.s1_len, 0, n1s * sizeof(uint32_t), s)) != hipSuccess ||
+        (e = hipMemsetAsync(st.err, 0, sizeof(uint32_t), s)) != hipSuccess ||
+        (e = hipStreamSynchronize(s)) != hipSuccess)
+        return bail(e, "record push segments");
+    hipFree(d_cnt);
+    *out = st;
+    return hipSuccess;
+}
+
+hipError_t launch_px_pack(const PbArgs& p, uint32_t world, uint32_t own, const uint64_t* d_part, uint64_t stride,
+                          uint64_t* seg, unsigned long long* counts, const HeavyChunk* chunks, uint64_t n_chunks,
+                          uint64_t* nw, hipStream_t s) {
+    hipLaunchKernelGGL(k_px_pack, dim3(kPbGrid, world), dim3(256), 0, s, p, world, own, d_part, stride, seg, counts,
+                       chunks, n_chunks, nw);
+    return hipGetLastError();
+}
 
 hipError_t launch_pb_scatter(const RoundArgs& a, const PbArgs& p, bool check_alive, uint32_t wd, hipStream_t s) {
     const bool cov = a.cov != nullptr;

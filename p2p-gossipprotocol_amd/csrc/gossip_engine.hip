@@ -161,6 +161,12 @@ struct gossip_ctx {
     PbState pb;                  // propagation-blocked push rounds: record regions (gossip_blocked.hip)
     bool pb_ready = false;
     bool cur_pb = false;         // the round in flight runs propagation-blocked
+    // a vertex block's sparse push rounds as records (build_px; P > 1, one word per peer)
+    PbState px;
+    int px_state = 0;            // 0: not built yet, 1: ready, -1: not eligible (staging push)
+    uint64_t* d_part = nullptr;  // the partition's block bounds (device copy, the pack's)
+    int32_t px_pm = 2;           // "px_permille": record push from this frontier per-mille of the block (-1: never)
+    bool cur_px = false;         // the round in flight pushes records
     // late pull rounds over needy lists (k_pull_list)
     bool list_req = true;          // "list_rounds": 0 never
     uint32_t list_cap_req = 0;     // "list_cap": entries per list (0: n_local / 16, at least 2^16)
@@ -510,6 +516,8 @@ void free_graph(gossip_ctx* c) {
     c->bins_ready = false;
     free_pb(&c->pb);
     c->pb_ready = false;
+    free_pb(&c->px);
+    c->px_state = 0;
     hipFree(c->rp);
     hipFree(c->col);
     hipFree(c->chunks);
@@ -1173,6 +1181,35 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
         }
     }
     c->cur_sparse = !pull && remote && requested == GOSSIP_MODE_PUSH_SPARSE && c->seg != nullptr;
+    // a sparse push from a frontier the marked-tile sweep would not take (0.2 % of the block) writes records
+    // per destination block (gossip_blocked.hip build_px) instead of OR-ing into the staging buffer and
+    // compacting it: config 4 round 3 as 8 parts staged 47 M deliveries and then swept every part's whole
+    // 2 GB staging buffer for them (every 64-peer tile of it marked)
+    c->cur_px = false;
+    if (c->cur_sparse && c->Wp == 1 && c->px_pm >= 0 && !c->cfg.extra_cap && c->world <= kPbCoarseMax &&
+        (c->frontier_est + cnt) * 1000 >= c->n_local * (uint64_t)c->px_pm) {
+        if (c->px_state == 0) {
+            std::string err;
+            const hipError_t e =
+                build_px(c->rp, c->col, c->n_local, c->n, c->heavy, c->chunks, c->n_chunks, c->part_begins.data(),
+                         c->world, (uint32_t)(std::find(c->part_begins.begin(), c->part_begins.end(), c->begin) -
+                                              c->part_begins.begin()),
+                         c->part_begins[1], c->stream, &c->px, &err);
+            if (e == hipSuccess) {
+                hipFree(c->d_part);
+                c->d_part = nullptr;
+                HIPCHK(hipMalloc((void**)&c->d_part, (c->world + 1) * sizeof(uint64_t)));
+                HIPCHK(hipMemcpy(c->d_part, c->part_begins.data(), (c->world + 1) * sizeof(uint64_t),
+                                 hipMemcpyHostToDevice));
+                c->px_state = 1;
+            } else if (e == hipErrorOutOfMemory || e == hipErrorInvalidValue) {
+                c->px_state = -1;  // the staging push stays
+            } else {
+                return fail(GOSSIP_EHIP, "record push: " + err);
+            }
+        }
+        c->cur_px = c->px_state == 1;
+    }
     // a wide push round (the explosion before the dense rounds) is bound by memory-side atomics, two per
     // fresh delivery (seen, then nx); deferring the seen update halves them for one streamed pass
     // (k_commit_nx).  A per-rank choice: results do not depend on it.
@@ -1449,6 +1486,27 @@ gossip_status round_compute(gossip_ctx* c) {
         return GOSSIP_OK;
     }
     const bool remote = c->cur_remote;
+    if (c->cur_px) {  // records per destination block (level 1 of a blocked round, the own block delivered at once)
+        PbArgs p = pb_args(c->px);
+        const uint32_t own =
+            (uint32_t)(std::find(c->part_begins.begin(), c->part_begins.end(), c->begin) - c->part_begins.begin());
+        p.dir_lo = (uint32_t)c->begin;
+        p.dir_hi = (uint32_t)c->end;
+        p.dir_base = (uint32_t)c->begin;
+        p.chunks = c->chunks;
+        p.n_chunks = c->n_chunks;
+        p.nw = reinterpret_cast<unsigned long long*>(c->nw);
+        p.n_local = c->n_local;
+        p.clear_all = 0;
+        if (a.tcur) HIPCHK(queue_zero(c, a.tcur, tact_bytes(c)));  // unread marks go
+        HIPCHK(timed(c, "px_scatter", [&] { return launch_pb_scatter(a, p, c->any_dead, c->W, c->stream); }));
+        HIPCHK(timed(c, "compact_send", [&] {
+            return launch_px_pack(p, c->world, own, c->d_part, c->part_begins[1], c->seg, c->d_counts, c->chunks,
+                                  c->n_chunks, c->nw, c->stream);
+        }));
+        HIPCHK(hipMemcpyAsync(c->h_counts, c->d_counts, c->world * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+        return GOSSIP_OK;
+    }
     if (c->cfg.extra_cap)
         HIPCHK(timed(c, "push_extra", [&] { return launch_push_extra(a, pw, c->any_dead, remote, c->stream); }));
     HIPCHK(timed(c, "push_heavy", [&] { return launch_push_heavy(a, pw, c->any_dead, remote, c->stream); }));
@@ -1484,13 +1542,13 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
                                   c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         HIPCHK(queue_zero(c, c->st, kStatLines * sizeof(DevStats)));  // cleared with the next round's first launch
-        if (c->cur_pb) {
+        if (c->cur_pb || c->cur_px) {
             // bit 4: a wave gave up waiting for its staging generation (gossip_stage.hpp, kStageSpin: the
             // protocol always progresses, so this means a bug, not load); bits 1/2: a record region that
             // would have overflowed (cannot happen: capacities are in-degrees).  The round's results are
             // incomplete either way; the flags stay set until the next reset.
             uint32_t e = 0;
-            HIPCHK(hipMemcpy(&e, c->pb.err, sizeof(e), hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(&e, c->cur_px ? c->px.err : c->pb.err, sizeof(e), hipMemcpyDeviceToHost));
             if (e & 4u) return fail(GOSSIP_ESTALL, "blocked round: a record-staging wave stalled past its bound");
             if (e) return fail(GOSSIP_EOVERFLOW, "blocked round: a record region overflowed");
         }
@@ -1553,6 +1611,10 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
             if (c->last_front) c->kbytes["frontier_bits"] += 8.125 * (c->gather ? c->n : c->n_local);
             c->kbytes["pull_light"] += 40.0 * c->n_local + 4.0 * (double)d.pull_edges + 8.0 * (double)d.pull_gathers;
             c->kbytes["pull_heavy"] += 12.0 * (double)d.heavy_traversals;
+        } else if (c->cur_px) {  // as blocked level 1; the pack reads a 12-B record and writes 16 B per remote one
+            const double t = (double)d.traversals;
+            c->kbytes["px_scatter"] += 8.0 * c->n_local + 24.0 * d.frontier + 16.0 * t;
+            c->kbytes["compact_send"] += 28.0 * t;
         } else if (!c->cur_pb) {
             c->kbytes["push_light"] += 32.0 * d.frontier + 20.0 * (double)(d.traversals - d.heavy_traversals);
             c->kbytes["push_heavy"] += 20.0 * (double)d.heavy_traversals;
@@ -1895,6 +1957,7 @@ gossip_status gossip_set_tuning(gossip_ctx* c, const char* key, int64_t value) {
         }
     }
     else if (k == "gather_permille") c->gather_pm = value < 0 ? kGatherPermille : u;
+    else if (k == "px_permille") c->px_pm = value < 0 ? -1 : (int32_t)u;
     else if (k == "exchange_stages") {
         if (value < 1 || value > (int64_t)kMaxStages) return fail(GOSSIP_EINVAL, "exchange_stages must be 1..16");
         c->stages_req = (uint32_t)value;
@@ -1926,6 +1989,7 @@ void gossip_destroy(gossip_ctx* c) {
     hipFree(c->d_probe);
     hipFree(c->d_work);
     hipFree(c->d_hist);
+    hipFree(c->d_part);
     hipFree(c->sx_pos);
     hipFree(c->sx_tmp);
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
@@ -2204,6 +2268,7 @@ gossip_status gossip_reset(gossip_ctx* c) {
         HIPCHK(hipMemsetAsync(c->dmask, 0, c->n_local * 4 + 4, s));
     }
     if (c->pb_ready) HIPCHK(hipMemsetAsync(c->pb.err, 0, sizeof(uint32_t), s));  // error flags of the last run
+    if (c->px_state == 1) HIPCHK(hipMemsetAsync(c->px.err, 0, sizeof(uint32_t), s));
     c->n_rep_seen = 0;
     c->pre_booked = c->cur_list = c->cur_pre = false;
     c->lst_in = c->cur_lst_out = -1;

@@ -213,6 +213,9 @@ struct PbArgs {
     uint32_t direct_end;      // destinations below this (the hubs' tiles, each over kPbFineIn in-degree: one
                               // fine bin each, every record of a round into one LDS buffer) are delivered
                               // at once, as the push does (a read of seen, then an atomic if bits are new)
+    uint32_t dir_lo, dir_hi;  // level 1 delivers destinations in [dir_lo, dir_hi) at once (P = 1: [0, direct_end);
+    uint32_t dir_base;        //   a vertex block's record push: its own block), at local index c - dir_base
+    uint32_t keep_end;        // level 1 leaves the new words of sources below this (P = 1: the hubs, direct_end)
     const HeavyChunk* chunks; // the heavy rows' chunks (row order) ...
     uint64_t n_chunks;
     unsigned long long* nw;   // ... whose new words the split clears (set per round: the buffers rotate)
@@ -223,6 +226,7 @@ struct PbArgs {
 };
 
 struct PbState {
+    uint32_t rank_mode = 0;   // a vertex block's record push (build_px): the coarse bins are the destination blocks
     uint32_t n_coarse = 0;
     uint64_t n_fine = 0;
     uint32_t *c_lo = nullptr, *c_fine = nullptr, *f_lo = nullptr;
@@ -440,6 +444,18 @@ void free_pb(PbState* p);
 PbArgs pb_args(const PbState& p);
 // one blocked push round: level 1 (each workgroup's heavy rows, then its light rows), level 2, apply
 hipError_t launch_pb_scatter(const RoundArgs& a, const PbArgs& p, bool check_alive, uint32_t wd, hipStream_t s);
+// A vertex block's sparse push rounds as records (P > 1, one word per peer): level 1 with the destination
+// blocks as its coarse bins and the own block delivered at once; its segments' capacities from the block's
+// edge counts.  hipErrorInvalidValue: a destination's records could outgrow its slot of the exchange buffer
+// (cap_records each; the staging push stays).
+hipError_t build_px(const uint64_t* rp, const uint32_t* col, uint64_t n_local, uint64_t n_global, uint32_t heavy,
+                    const HeavyChunk* chunks, uint64_t n_chunks, const uint64_t* part, uint32_t world, uint32_t own,
+                    uint64_t cap_records, hipStream_t s, PbState* out, std::string* err);
+// after level 1: every destination block's records packed at seg + q * stride * 2 as {peer, word} (level 1's
+// padding as {first peer of q, 0}), counts[q] records; the heavy rows' new words cleared
+hipError_t launch_px_pack(const PbArgs& p, uint32_t world, uint32_t own, const uint64_t* d_part, uint64_t stride,
+                          uint64_t* seg, unsigned long long* counts, const HeavyChunk* chunks, uint64_t n_chunks,
+                          uint64_t* nw, hipStream_t s);
 hipError_t launch_pb_split(const PbArgs& p, hipStream_t s);
 hipError_t launch_pb_apply(const RoundArgs& a, const PbArgs& p, hipStream_t s);
 

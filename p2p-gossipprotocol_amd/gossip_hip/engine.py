@@ -18,7 +18,7 @@ from ._abi import DeadReport, GossipConfig, RoundStats, check
 _GRAPHS = {"powerlaw": _abi.GRAPH_POWERLAW, "ref_bootstrap": _abi.GRAPH_REF_BOOTSTRAP}
 KERNELS = ("push_light", "push_heavy", "push_extra", "src_count", "frontier_bits", "pull_light", "pull_heavy", "pull_list", "list_zero", "bin_scatter",
            "bin_apply", "pb_scatter", "pb_split", "pb_apply", "liveness", "rebootstrap", "rejoin", "churn", "kills",
-           "inject", "apply_remote", "commit", "compact_send", "tiny")
+           "inject", "apply_remote", "commit", "compact_send", "px_scatter", "tiny")
 # exchange steps of partitioned rounds, timed on each part's stream (gossip_dist.hip; bytes = received per part)
 EXCHANGES = ("all_gather", "all_to_all", "records")
 

@@ -76,6 +76,27 @@ def test_group_dense_exchange_forms_equal_oracle(oracle, idx, n, P, gather):
     assert again == stats
 
 
+@pytest.mark.parametrize("px", ["all", "off"])
+@pytest.mark.parametrize("P", [2, 3, 4])
+@pytest.mark.parametrize("idx,n", [(3, 100_003), (5, 1 << 15), (2, 40_000)])
+def test_group_record_push_equals_oracle(oracle, idx, n, P, px):
+    """Sparse push rounds at P > 1 as records per destination block
+    (gossip_blocked.hip build_px / k_px_pack: level 1 of a blocked round with
+    the destination blocks as its bins, the own block delivered at once, the
+    records packed per block and exchanged as {peer, word}) -- forced for
+    every sparse round ("all": px_permille 0), and the staging push with its
+    compaction ("off") -- both give the oracle's run, with dead peers and
+    masked edges (config 5) and short last blocks."""
+    w = config(idx, n, pick=oracle.pick_origins)
+    rp, col = oracle.gen_workload(w)
+    ref = oracle.simulate_workload(w, rp, col)
+    stats, seen, reps, again = _run_group(w, [0] * P, tuning={"px_permille": 0 if px == "all" else -1})
+    assert stats == ref["stats"]
+    assert np.array_equal(seen, ref["seen"])
+    assert np.array_equal(reps, ref["reports"])
+    assert again == stats
+
+
 @pytest.mark.parametrize("idx,n", [(2, 1 << 15), (5, 1 << 15)])
 def test_group_one_part_rccl_equals_oracle(oracle, idx, n):
     """ncclCommInitAll over device 0: every collective of the driver through RCCL."""
