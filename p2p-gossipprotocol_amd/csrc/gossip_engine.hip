@@ -228,6 +228,7 @@ struct gossip_ctx {
     bool pb_clear_all = true;    // "blocked_clear_all": wide blocked rounds clear new words whole in level 2
     bool cur_clear_all = false;  // (the round in flight does)
     bool scatter_direct = false; // "scatter_direct": a vertex block's scatter reads other blocks' words directly
+    bool scatter_small = false;  // "scatter_small": the streamed scatter's small-chunk instance where chunks fit it
     unsigned long long* d_probe = nullptr;  // "apply_probe": the streamed apply's phase clocks (kProbeN slots)
     bool apply_persist = true;   // "apply_persist": the streamed apply as 256 workgroups taking bins from
                                  // per-XCD counters (d_work), not one workgroup per bin
@@ -773,6 +774,7 @@ BinArgs bin_args(const gossip_ctx* c, bool noskip, uint32_t src_side) {
     b.deg = s.deg;
     b.apply_pipe = c->apply_pipe;
     b.direct = c->scatter_direct && c->gather ? 1u : 0u;
+    b.small = c->scatter_small ? 1u : 0u;
     b.needy_check = 1u;
     b.src_stats = src_side;
     b.work = c->apply_persist && c->bin_stream ? c->d_work : nullptr;
@@ -1939,6 +1941,7 @@ gossip_status gossip_set_tuning(gossip_ctx* c, const char* key, int64_t value) {
     else if (k == "bin_needy_skip") c->needy_skip = value != 0;
     else if (k == "replay") c->replay_req = value != 0;
     else if (k == "scatter_direct") c->scatter_direct = value != 0;
+    else if (k == "scatter_small") c->scatter_small = value != 0;
     else if (k == "blocked_clear_all") c->pb_clear_all = value != 0;
     else if (k == "apply_pipe") {
         if (value < 0 || value > 3) return fail(GOSSIP_EINVAL, "apply_pipe must be 0..3");

@@ -63,6 +63,9 @@ constexpr uint32_t kBinChunkWords = 18432;     // source chunk: its new words (1
 constexpr uint64_t kHubFactor = 4;             // chunks with more than 4x the mean cb entries are split into units
 constexpr int kScatterBlock = 1024;            // k_bin_scatter_lds: one 16-wave workgroup per CU
 constexpr int kScatterGrid = 256;              // one workgroup per CU
+constexpr uint32_t kSmallChunkWords = 4096;    // streamed scatter of chunks this small: 256-thread blocks ...
+constexpr int kSmallGrid = 1024;               // ... four per CU
+constexpr uint32_t kSmallBinWords = 2048;      // streamed apply of bins this small: 256-thread blocks, eight per CU
 constexpr uint32_t kApplyRow = 32;            // streamed apply: consecutive bins one XCD group applies together
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 constexpr uint16_t kRunStart = 0x8000u;        // cb_src flag; chunk-local sources are < kBinChunkWords < 2^15
@@ -112,6 +115,8 @@ struct BinArgs {
     uint32_t stream;              // 1: streamed layout, 0: val in slot order (k_bin_scatter_*)
     const uint32_t* deg;          // per owned peer: its row length (source-side stats booked by the apply)
     uint32_t apply_pipe;          // streamed apply's pipeline shape (k_bin_apply_runs, "apply_pipe"; 0 default)
+    uint32_t small;               // streamed scatter: the small-chunk instance (4096-word slices, 256 threads, four
+                                  // workgroups per CU) when the chunks fit it ("scatter_small")
     uint32_t direct;              // streamed scatter of a vertex block: chunks without owned sources read their
                                   // words from the gather buffer instead of staging them ("scatter_direct")
     uint32_t needy_check;         // 1: the apply first tests whether any peer of the bin can still learn

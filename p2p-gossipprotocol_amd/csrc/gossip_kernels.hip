@@ -960,12 +960,13 @@ __global__ __launch_bounds__(kBlock) void k_pull_list(RoundArgs a, const uint32_
 // staging is then one round trip instead of a chain of dependent row-bound
 // loads, ~40 us per unit).  Ends before the block barrier that publishes the
 // slice.
-template <int W, bool COV>
+// kCW / kSB: the slice's words and the block's threads (k_bin_stream's small-chunk instance: 4096 / 256)
+template <int W, bool COV, int kCW = (int)kBinChunkWords, int kSB = kScatterBlock>
 __device__ __forceinline__ void scatter_stage(const RoundArgs& a, const BinArgs& b, const BinUnit& un, uint32_t wd,
                                               unsigned long long* slice, unsigned long long* live_s,
                                               unsigned int* cov_s, Acc& acc) {
-    constexpr int kSliceIt = kBinChunkWords / kScatterBlock;  // slice words per lane
-    static_assert(kBinChunkWords % kScatterBlock == 0, "slice split");
+    constexpr int kSliceIt = kCW / kSB;  // slice words per lane
+    static_assert(kCW % kSB == 0, "slice split");
     const int lane = threadIdx.x & 63;
     // global source chunk; words from nw_src (own words at P = 1, the all-gathered ones at P > 1)
     const uint64_t vb = bin_chunk_vb(b, un.c), ve = bin_chunk_ve(b, un.c, a.n_src);  // vb % 64 == 0
@@ -976,25 +977,25 @@ __device__ __forceinline__ void scatter_stage(const RoundArgs& a, const BinArgs&
     uint64_t r[kSliceIt];
 #pragma unroll
     for (int k = 0; k < kSliceIt; ++k) {
-        const uint64_t i = threadIdx.x + (uint64_t)k * kScatterBlock;
+        const uint64_t i = threadIdx.x + (uint64_t)k * kSB;
         r[k] = i < nwords ? a.nw_src[vb * W + i] : 0ull;
     }
     __syncthreads();  // previous unit's readers are done with the slice
 #pragma unroll
-    for (int k = 0; k < kSliceIt; ++k) slice[threadIdx.x + k * kScatterBlock] = r[k];
-    if (threadIdx.x < kBinChunkWords / 64 / W) live_s[threadIdx.x] = b.noskip ? ~0ull : 0ull;
+    for (int k = 0; k < kSliceIt; ++k) slice[threadIdx.x + k * kSB] = r[k];
+    if (threadIdx.x < kCW / 64 / W) live_s[threadIdx.x] = b.noskip ? ~0ull : 0ull;
     __syncthreads();
     // per source (a wave covers 64 consecutive ones): live bits and, in the
     // chunk's first unit, the source side of its pushes (broadcastMessage,
     // peer.cpp:310-316) for the owned sources; row lengths loaded together
-    constexpr int kSrcIt = (kBinChunkWords / W + kScatterBlock - 1) / kScatterBlock;
+    constexpr int kSrcIt = (kCW / W + kSB - 1) / kSB;
     constexpr int kB = 5;  // sources whose row lengths are loaded together (register budget)
 #pragma unroll
     for (int k0 = 0; k0 < kSrcIt; k0 += kB) {
         uint32_t pcs[kB];
 #pragma unroll
         for (int kk = 0; kk < kB; ++kk) {
-            const uint64_t j = threadIdx.x + (uint64_t)(k0 + kk) * kScatterBlock;
+            const uint64_t j = threadIdx.x + (uint64_t)(k0 + kk) * kSB;
             pcs[kk] = 0;
             if (k0 + kk >= kSrcIt || j >= ((n_src + 63) & ~63ull)) continue;  // wave-uniform
             const uint64_t v = vb + j;
@@ -1019,7 +1020,7 @@ __device__ __forceinline__ void scatter_stage(const RoundArgs& a, const BinArgs&
         const bool cnt = a.dead_mode && a.dgone;
 #pragma unroll
         for (int kk = 0; kk < kB; ++kk) {
-            const uint64_t lv = vb + threadIdx.x + (uint64_t)(k0 + kk) * kScatterBlock - a.begin;
+            const uint64_t lv = vb + threadIdx.x + (uint64_t)(k0 + kk) * kSB - a.begin;
             d0[kk] = pcs[kk] ? a.rp[lv] : 0ull;
             d1[kk] = pcs[kk] ? a.rp[lv + 1] : 0ull;
             dg[kk] = pcs[kk] && cnt ? a.dgone[lv] : 0u;
@@ -1048,8 +1049,9 @@ template <class F>
 __device__ __forceinline__ void scatter_rows(const BinArgs& b, F&& unit) {
     // rows of `members` units, row r on XCD r % 8 (gossip_bins.hip; n_units: this launch's unit count)
     const uint32_t xcd = blockIdx.x & 7, member = blockIdx.x >> 3, members = gridDim.x >> 3;
-    const uint64_t rows = b.n_units / members;
-    for (uint64_t r = xcd; r < rows; r += 8) unit(r * members + member);
+    const uint64_t rows = (b.n_units + members - 1) / members;  // (units come in rows of kScatterGrid / 8)
+    for (uint64_t r = xcd; r < rows; r += 8)
+        if (r * members + member < b.n_units) unit(r * members + member);
 }
 
 // Producer/consumer scatter (slot layout).  Measured on the round-1 single-role kernel: a wave that both
@@ -1381,16 +1383,19 @@ __global__ __launch_bounds__(kB) void k_bin_apply(RoundArgs a, BinArgs b, uint32
 // as four 16-B stores 64 B apart -- sent every lane's store to L2 as a request
 // of its own (config 4: 9.7e8 write requests per launch, the TA ~92 % busy).
 // Every entry is written every binned round.
-template <int W, bool COV>
-__global__ __launch_bounds__(kScatterBlock) void k_bin_stream(RoundArgs a, BinArgs b, uint32_t wd) {
-    constexpr int kWaves = kScatterBlock / 64;
+// kCW / kSB: the LDS slice's words and the block's threads -- 18432 / 1024 (one workgroup per CU), or
+// 4096 / 256 for layouts of small chunks (several workgroups per CU: a unit's staging and its short entry
+// stream are a few dependent round trips, which one workgroup per CU leaves exposed)
+template <int W, bool COV, int kCW = (int)kBinChunkWords, int kSB = kScatterBlock>
+__global__ __launch_bounds__(kSB) void k_bin_stream(RoundArgs a, BinArgs b, uint32_t wd) {
+    constexpr int kWaves = kSB / 64;
     constexpr int kPW = W == 1 ? 1 : W / 2;  // pieces per entry (W >= 2)
     constexpr int kU = 4;                    // pieces per lane in flight
-    __shared__ unsigned long long slice[kBinChunkWords];
-    __shared__ unsigned long long live_s[kBinChunkWords / 64 / W];
+    __shared__ unsigned long long slice[kCW];
+    __shared__ unsigned long long live_s[kCW / 64 / W];
     __shared__ unsigned int cov_s[COV ? 64 * W : 1];
     if (COV) {
-        for (int i = threadIdx.x; i < 64 * W; i += kScatterBlock) cov_s[i] = 0;
+        for (int i = threadIdx.x; i < 64 * W; i += kSB) cov_s[i] = 0;
     }
     Acc acc;
     auto unit = [&](const uint64_t ui) {
@@ -1403,7 +1408,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_stream(RoundArgs a, BinAr
         const bool direct = b.direct && !(vb < a.end && bin_chunk_ve(b, un.c, a.n_src) > a.begin);  // block-uniform
         const uint64_t* src = a.nw_src + vb * W;
         if (!direct) {
-            scatter_stage<W, COV>(a, b, un, wd, slice, live_s, cov_s, acc);
+            scatter_stage<W, COV, kCW, kSB>(a, b, un, wd, slice, live_s, cov_s, acc);
             __syncthreads();
         }
         if (un.p0 >= un.p1) return;
@@ -1417,7 +1422,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_stream(RoundArgs a, BinAr
         // previous batch's stores waits for those stores' acknowledgements as well; issued one batch ahead,
         // the loads only wait behind one batch of stores.  (Unpipelined, and with the scheduler free to sink
         // the first piece's LDS read and its wait between the loads, a wave had about one batch in flight.)
-        constexpr uint64_t kStep = (uint64_t)kScatterBlock * kU;
+        constexpr uint64_t kStep = (uint64_t)kSB * kU;
         if (W == 1) {
             // piece k = entries 2k, 2k + 1 (cb_src read as one u32: 4-B aligned)
             const uint64_t k0 = un.p0 >> 1, k1 = (un.p1 + 1) >> 1;
@@ -1425,7 +1430,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_stream(RoundArgs a, BinAr
             auto load = [&](uint64_t kb, uint32_t (&o)[kU]) {
 #pragma unroll
                 for (int j = 0; j < kU; ++j)
-                    o[j] = __builtin_nontemporal_load(cb2 + min(kb + (uint64_t)j * kScatterBlock, k1 - 1));
+                    o[j] = __builtin_nontemporal_load(cb2 + min(kb + (uint64_t)j * kSB, k1 - 1));
             };
             uint32_t sv[kU], nv[kU];
             uint64_t kb = k0 + threadIdx.x;
@@ -1435,7 +1440,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_stream(RoundArgs a, BinAr
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int j = 0; j < kU; ++j) {
-                    const uint64_t k = kb + (uint64_t)j * kScatterBlock;
+                    const uint64_t k = kb + (uint64_t)j * kSB;
                     if (k >= k1) break;
                     const uint32_t u0 = sv[j] & (kRunStart - 1u), u1 = (sv[j] >> 16) & (kRunStart - 1u);
                     const uint64_t x0 = word(u0);
@@ -1458,7 +1463,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_stream(RoundArgs a, BinAr
             const uint64_t k0 = un.p0 * kPW, k1 = un.p1 * kPW;
             auto load = [&](uint64_t kb, uint32_t (&o)[kU]) {
 #pragma unroll
-                for (int j = 0; j < kU; ++j) o[j] = b.cb_src[min(kb + (uint64_t)j * kScatterBlock, k1 - 1) / kPW];
+                for (int j = 0; j < kU; ++j) o[j] = b.cb_src[min(kb + (uint64_t)j * kSB, k1 - 1) / kPW];
             };
             uint32_t sv[kU], nv[kU];
             uint64_t kb = k0 + threadIdx.x;
@@ -1468,7 +1473,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_stream(RoundArgs a, BinAr
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int j = 0; j < kU; ++j) {
-                    const uint64_t k = kb + (uint64_t)j * kScatterBlock;
+                    const uint64_t k = kb + (uint64_t)j * kSB;
                     if (k >= k1) break;
                     const uint32_t u = sv[j] & (kRunStart - 1u);
                     const uint32_t w0 = (uint32_t)(k % kPW) * 2;
@@ -1489,7 +1494,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_bin_stream(RoundArgs a, BinAr
     flush<kWaves>(acc, a.st);
     if (COV) {
         __syncthreads();
-        for (int i = threadIdx.x; i < 64 * W; i += kScatterBlock)
+        for (int i = threadIdx.x; i < 64 * W; i += kSB)
             if (cov_s[i]) atomicAdd(&a.cov[i], (unsigned long long)cov_s[i]);
     }
 }
@@ -2757,6 +2762,17 @@ hipError_t launch_apply_records(const RoundArgs& a, uint32_t W_, const uint64_t*
 hipError_t launch_bin_scatter(const RoundArgs& a, const BinArgs& b, uint32_t W_, hipStream_t s) {
     const uint32_t wd = wd_of(W_);
     if (b.stream) {
+        if (b.small && b.chunk * wp_of(W_) <= kSmallChunkWords) {  // small chunks: 256-thread blocks, kSmallGrid of them
+            GOSSIP_DISPATCH_W(wp_of(W_), {
+                if (a.cov)
+                    hipLaunchKernelGGL((k_bin_stream<W, true, kSmallChunkWords, 256>), dim3(kSmallGrid), dim3(256), 0,
+                                       s, a, b, wd);
+                else
+                    hipLaunchKernelGGL((k_bin_stream<W, false, kSmallChunkWords, 256>), dim3(kSmallGrid), dim3(256), 0,
+                                       s, a, b, wd);
+            });
+            return hipGetLastError();
+        }
         GOSSIP_DISPATCH_W(wp_of(W_), {
             if (a.cov) hipLaunchKernelGGL((k_bin_stream<W, true>), dim3(kScatterGrid), dim3(kScatterBlock), 0, s, a, b, wd);
             else hipLaunchKernelGGL((k_bin_stream<W, false>), dim3(kScatterGrid), dim3(kScatterBlock), 0, s, a, b, wd);
@@ -2783,7 +2799,7 @@ hipError_t launch_bin_apply(const RoundArgs& a, const BinArgs& b, uint32_t W_, h
         const uint64_t rows = (b.n_bins + kApplyRow - 1) / kApplyRow;
         unsigned sgrid = (unsigned)((rows + 7) / 8 * 8 * kApplyRow);
         if (b.work) {  // persistent: the resident blocks; b.work was zeroed before the round's scatter
-            const unsigned resident = b.bin_words > kBinWords / 2 ? 256u : 512u;
+            const unsigned resident = b.bin_words > kBinWords / 2 ? 256u : b.bin_words > kSmallBinWords ? 512u : 2048u;
             sgrid = std::min(sgrid, resident);
         }
         if (b.bin_words > kBinWords / 2 && wp_of(W_) == 1) {  // one word: the pipeline shapes (A/B), the probe
@@ -2801,6 +2817,10 @@ hipError_t launch_bin_apply(const RoundArgs& a, const BinArgs& b, uint32_t W_, h
         } else if (b.bin_words > kBinWords / 2) {
             GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_apply_runs<W, kBinWords, 1024>),
                                                            dim3(sgrid), dim3(1024), 0, s, a, b, wd));
+        } else if (b.bin_words <= kSmallBinWords) {
+            // 16 KB accumulators: eight 4-wave workgroups per CU (small bins of small overlays)
+            GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_apply_runs<W, kSmallBinWords, 256>),
+                                                           dim3(sgrid), dim3(256), 0, s, a, b, wd));
         } else {
             // 72 KB accumulators: two 8-wave workgroups per CU, one's per-bin phases under the other's slots
             GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_apply_runs<W, kBinWords / 2, 512>),

@@ -343,6 +343,8 @@ _VARIANTS = {"defer_1": ({"defer_permille": 1}, {"blocked": "off"}), "stream": (
              "stream_needy_test": ({"bin_stream": 1, "bin_needy_skip": 0}, {}),
              "apply_pipe_1": ({"apply_pipe": 1}, {}), "apply_pipe_2": ({"apply_pipe": 2}, {}),
              "apply_pipe_3": ({"apply_pipe": 3}, {}),
+             "scatter_small": ({"scatter_small": 1}, {}),
+             "small_kernels": ({"bin_words": 1024, "bin_chunk": 1024, "scatter_small": 1}, {}),
              "apply_probe": ({"apply_probe": 1}, {}), "apply_one_per_bin": ({"apply_persist": 0}, {}), "slots_needy_test": ({"bin_stream": 0, "bin_needy_skip": 0}, {}),
              "blocked_dense": ({"blocked_bin_slots": 0}, {"blocked_permille": 1000}),
              "blocked_dense_clear_peers": ({"blocked_bin_slots": 0, "blocked_clear_all": 0}, {"blocked_permille": 1000})}

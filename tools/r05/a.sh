@@ -4,7 +4,7 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/r05a; mkdir -p $O
-timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_group.py -m gpu -x -q -k "probe_toggle or variants or group or comm_init" --timeout 200 --timeout-method thread > $O/pytest.log 2>&1 || { grep -E "FAIL|Error|assert|Timeout" $O/pytest.log | head -30; tail -5 $O/pytest.log; exit 1; }
+timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_group.py -m gpu -x -q -k "probe_toggle or variants or group or comm_init or record_push" --timeout 200 --timeout-method thread > $O/pytest.log 2>&1 || { grep -E "FAIL|Error|assert|Timeout" $O/pytest.log | head -30; tail -5 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
 timeout -k 10 300 python -u tools/round_profile.py 4 > $O/rounds_c4.txt 2>&1 || { tail -20 $O/rounds_c4.txt; exit 1; }
 cut -c1-250 $O/rounds_c4.txt
