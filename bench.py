@@ -81,7 +81,7 @@ def pmc_traffic(workload: str, kernels, n_local: int):
     stores 1:1.  The binned kernels read coalesced streams (traffic = 2 x
     fetch + write); pull_heavy's gathers are counted 1:1."""
     cfg = workload.split("_")[0]  # "config4" ...
-    cands = [REPO / "profiles" / r / f"{cfg}_pmc_summary.json" for r in ("r04", "r03", "r02", "r01")]
+    cands = [REPO / "profiles" / r / f"{cfg}_pmc_summary.json" for r in ("r05", "r04", "r03", "r02", "r01")]
     path = next((p for p in cands if p.exists()), None)
     if path is None:
         return None, None
