@@ -680,6 +680,7 @@ void free_pb(PbState* p) {
     hipFree(p->r1_w);
     hipFree(p->r2_dst);
     hipFree(p->r2_w);
+    hipFree(p->rec_out);
     *p = PbState{};
 }
 
@@ -969,17 +970,25 @@ hipError_t build_px(const uint64_t* rp, const uint32_t* col, uint64_t n_local, u
         n1 += cap[i];
         per_q[i % world] += cap[i];
     }
-    for (uint32_t q = 0; q < world; ++q)
-        if (per_q[q] > cap_records) {
-            if (err) *err = "a destination block's records could outgrow its exchange slot";
-            hipFree(d_cnt);
-            free_pb(&st);
-            return hipErrorInvalidValue;
-        }
+    // the packed records of destination q at rec_out + q * stride; the block's remote records all together must
+    // fit what the receivers keep for them (cap_records: on a symmetric overlay a block receives as many as it
+    // sends)
+    uint64_t stride = 0, remote = 0;
+    for (uint32_t q = 0; q < world; ++q) {
+        stride = std::max(stride, per_q[q]);
+        remote += per_q[q];
+    }
+    if (remote > cap_records) {
+        if (err) *err = "the block's records could outgrow the receivers' buffers";
+        hipFree(d_cnt);
+        free_pb(&st);
+        return hipErrorInvalidValue;
+    }
+    st.rec_stride = std::max<uint64_t>(stride, 1);
     st.n1 = n1;
     size_t free_b = 0, total_b = 0;
     if ((e = hipMemGetInfo(&free_b, &total_b)) != hipSuccess) return bail(e, "hipMemGetInfo");
-    if (n1 * 12 + (1ull << 30) > free_b) {
+    if (n1 * 12 + (uint64_t)world * st.rec_stride * 16 + (1ull << 30) > free_b) {
         hipFree(d_cnt);
         free_pb(&st);
         if (err) *err = "record-push segments do not fit in free device memory";
@@ -991,6 +1000,7 @@ hipError_t build_px(const uint64_t* rp, const uint32_t* col, uint64_t n_local, u
         (e = hipMalloc((void**)&st.err, sizeof(uint32_t))) != hipSuccess ||
         (e = hipMalloc((void**)&st.r1_dst, (n1 + 1) * sizeof(uint32_t))) != hipSuccess ||
         (e = hipMalloc((void**)&st.r1_w, (n1 + 1) * sizeof(unsigned long long))) != hipSuccess ||
+        (e = hipMalloc((void**)&st.rec_out, (uint64_t)world * st.rec_stride * 16)) != hipSuccess ||
         (e = hipMemcpyAsync(st.s1_base, base.data(), n1s * sizeof(uint64_t), hipMemcpyHostToDevice, s)) != hipSuccess ||
         (e = hipMemcpyAsync(st.s1_cap, cap.data(), n1s * sizeof(uint32_t), hipMemcpyHostToDevice, s)) != hipSuccess ||
         (e = hipMemsetAsync(st.s1_len, 0, n1s * sizeof(uint32_t), s)) != hipSuccess ||

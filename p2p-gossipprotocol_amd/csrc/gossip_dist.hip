@@ -616,15 +616,28 @@ gossip_status exchange_records(DistDriver* d, std::vector<uint64_t>& total_in) {
         for (uint32_t q = 0; q < W; ++q) c += q == d->ranks[i].rank ? 0 : d->ranks[i].counts_in[q];
         t.bytes(i, 8.0 * R * c);
     }
+    // where each rank's records for destination q sit (the staging push's compaction, or the record push's own
+    // buffer), and how many each receiver can take
+    std::vector<const uint64_t*> src(d->ranks.size());
+    std::vector<uint64_t> stride(d->ranks.size());
+    for (size_t i = 0; i < d->ranks.size(); ++i) ctx_send_records(d->ranks[i].ctx, &src[i], &stride[i]);
+    for (size_t i = 0; i < d->ranks.size(); ++i) {
+        uint64_t c = 0;
+        for (uint32_t q = 0; q < W; ++q) c += d->ranks[i].counts_in[q];
+        if (c > (uint64_t)W * d->ranks[i].n_local)
+            return set_error(GOSSIP_EOVERFLOW, "sparse exchange: more records than the receive buffer holds");
+    }
+    (void)chunk;
     if (d->emulate) {
         for (size_t i = 0; i < d->ranks.size(); ++i) {
             DistRank& q = d->ranks[i];
             uint64_t off = 0;
             gossip_status s = t.part(i, [&]() -> gossip_status {
-                for (auto& p : d->ranks) {
+                for (size_t k = 0; k < d->ranks.size(); ++k) {
+                    const DistRank& p = d->ranks[k];
                     const uint64_t c = p.counts_out[q.rank];
                     if (c)
-                        DHIP(hipMemcpyAsync(q.rec_in + off * R, p.seg + (uint64_t)q.rank * chunk * R, c * R * 8,
+                        DHIP(hipMemcpyAsync(q.rec_in + off * R, src[k] + (uint64_t)q.rank * stride[k] * R, c * R * 8,
                                             hipMemcpyDeviceToDevice, q.stream));
                     off += c;
                 }
@@ -642,7 +655,8 @@ gossip_status exchange_records(DistDriver* d, std::vector<uint64_t>& total_in) {
         uint64_t off = 0;
         for (uint32_t q = 0; q < W; ++q) {  // both sides know every count: zero-length pairs are skipped on both
             if (r.counts_out[q])
-                DNCCL(ncclSend(r.seg + (uint64_t)q * chunk * R, r.counts_out[q] * R, ncclUint64, (int)q, r.comm, r.stream));
+                DNCCL(ncclSend(src[i] + (uint64_t)q * stride[i] * R, r.counts_out[q] * R, ncclUint64, (int)q, r.comm,
+                               r.stream));
             if (r.counts_in[q])
                 DNCCL(ncclRecv(r.rec_in + off * R, r.counts_in[q] * R, ncclUint64, (int)q, r.comm, r.stream));
             off += r.counts_in[q];

@@ -317,6 +317,10 @@ uint32_t ctx_stages(gossip_ctx* c) {
     return c->bins_ready && c->bin_stream && c->n_local != c->n ? std::min<uint32_t>(c->stages_req, kMaxStages) : 1u;
 }
 uint64_t ctx_bin_seg(gossip_ctx* c) { return c->bins.seg; }
+void ctx_send_records(gossip_ctx* c, const uint64_t** base, uint64_t* stride) {
+    *base = c->cur_px ? c->px.rec_out : c->seg;
+    *stride = c->cur_px ? c->px.rec_stride : c->part_begins[1];
+}
 gossip_status ctx_arm_stages(gossip_ctx* c, uint32_t S, const hipEvent_t* ev) {  // (the caller set the device)
     if (const hipError_t e = build_stage_units(&c->bins, S, c->begin, c->end, c->n))
         return fail(GOSSIP_EHIP, std::string("staged scatter units: ") + hipGetErrorString(e));
@@ -1188,7 +1192,7 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
     // compacting it: config 4 round 3 as 8 parts staged 47 M deliveries and then swept every part's whole
     // 2 GB staging buffer for them (every 64-peer tile of it marked)
     c->cur_px = false;
-    if (c->cur_sparse && c->Wp == 1 && c->px_pm >= 0 && !c->cfg.extra_cap && c->world <= kPbCoarseMax &&
+    if (c->cur_sparse && c->Wp == 1 && c->px_pm >= 0 && !c->cfg.extra_cap && c->symmetric && c->world <= kPbCoarseMax &&
         (c->frontier_est + cnt) * 1000 >= c->n_local * (uint64_t)c->px_pm) {
         if (c->px_state == 0) {
             std::string err;
@@ -1196,7 +1200,7 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
                 build_px(c->rp, c->col, c->n_local, c->n, c->heavy, c->chunks, c->n_chunks, c->part_begins.data(),
                          c->world, (uint32_t)(std::find(c->part_begins.begin(), c->part_begins.end(), c->begin) -
                                               c->part_begins.begin()),
-                         c->part_begins[1], c->stream, &c->px, &err);
+                         (uint64_t)c->world * c->n_local, c->stream, &c->px, &err);
             if (e == hipSuccess) {
                 hipFree(c->d_part);
                 c->d_part = nullptr;
@@ -1503,7 +1507,7 @@ gossip_status round_compute(gossip_ctx* c) {
         if (a.tcur) HIPCHK(queue_zero(c, a.tcur, tact_bytes(c)));  // unread marks go
         HIPCHK(timed(c, "px_scatter", [&] { return launch_pb_scatter(a, p, c->any_dead, c->W, c->stream); }));
         HIPCHK(timed(c, "compact_send", [&] {
-            return launch_px_pack(p, c->world, own, c->d_part, c->part_begins[1], c->seg, c->d_counts, c->chunks,
+            return launch_px_pack(p, c->world, own, c->d_part, c->px.rec_stride, c->px.rec_out, c->d_counts, c->chunks,
                                   c->n_chunks, c->nw, c->stream);
         }));
         HIPCHK(hipMemcpyAsync(c->h_counts, c->d_counts, c->world * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
@@ -2292,7 +2296,9 @@ gossip_status gossip_reset(gossip_ctx* c) {
     c->cum_digest = c->cum_covered = 0;
     c->cum_dead_cov = c->cum_died = c->cum_injected = 0;
     if (c->dist) gossip::dist_reset(c->dist);
-    if (!tiny) HIPCHK(hipStreamSynchronize(s));  // (every read of device state synchronises the stream first)
+    // no host wait: the clears above are ordered before the run's kernels on the stream, and every host read of
+    // device state synchronises the stream first (a wait here left the GPU idle while the host issued the run's
+    // first round)
     return GOSSIP_OK;
 }
 

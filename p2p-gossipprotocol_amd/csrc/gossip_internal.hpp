@@ -243,6 +243,8 @@ struct PbState {
     uint16_t* r2_dst = nullptr;
     unsigned long long* r2_w = nullptr;
     uint64_t n1 = 0, n2 = 0;  // record capacities of the two levels
+    uint64_t* rec_out = nullptr;  // rank mode: the packed {peer, word} records, rec_stride per destination block
+    uint64_t rec_stride = 0;
 };
 
 struct DeadReport {
@@ -456,6 +458,9 @@ hipError_t launch_pb_scatter(const RoundArgs& a, const PbArgs& p, bool check_ali
 hipError_t build_px(const uint64_t* rp, const uint32_t* col, uint64_t n_local, uint64_t n_global, uint32_t heavy,
                     const HeavyChunk* chunks, uint64_t n_chunks, const uint64_t* part, uint32_t world, uint32_t own,
                     uint64_t cap_records, hipStream_t s, PbState* out, std::string* err);
+// the record buffer of the sparse push round in flight ({peer, words} per record, stride records per destination
+// block): the staging push's compaction (the exchange's seg buffer) or the record push's own (gossip_dist.hip)
+void ctx_send_records(gossip_ctx* c, const uint64_t** base, uint64_t* stride);
 // after level 1: every destination block's records packed at seg + q * stride * 2 as {peer, word} (level 1's
 // padding as {first peer of q, 0}), counts[q] records; the heavy rows' new words cleared
 hipError_t launch_px_pack(const PbArgs& p, uint32_t world, uint32_t own, const uint64_t* d_part, uint64_t stride,

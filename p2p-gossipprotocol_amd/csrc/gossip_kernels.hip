@@ -2642,17 +2642,28 @@ hipError_t launch_push_light(const RoundArgs& a, uint32_t W_, bool check_alive, 
     const bool cov = a.cov != nullptr;
 #define GOSSIP_LIGHT(CA, RM, COV) \
     hipLaunchKernelGGL((k_push_light<W, CA, RM, COV, false>), dim3(g), dim3(kBlock), 0, s, a, wd)
-    if (a.tsparse && !remote) {  // a nearly empty frontier: only the marked tiles
+    if (a.tsparse) {  // a nearly empty frontier: only the marked tiles (a vertex block's too, round 5)
         const unsigned gs = grid_for((tiles + 63) / 64, kWavesPerBlock);
+#define GOSSIP_SP(CA, RM, COV) \
+    hipLaunchKernelGGL((k_push_light<W, CA, RM, COV, true>), dim3(gs), dim3(kBlock), 0, s, a, wd)
         GOSSIP_DISPATCH_W(wp_of(W_), {
-            if (cov) {
-                if (check_alive) hipLaunchKernelGGL((k_push_light<W, true, false, true, true>), dim3(gs), dim3(kBlock), 0, s, a, wd);
-                else hipLaunchKernelGGL((k_push_light<W, false, false, true, true>), dim3(gs), dim3(kBlock), 0, s, a, wd);
+            if (remote) {
+                if (cov) {
+                    if (check_alive) GOSSIP_SP(true, true, true);
+                    else GOSSIP_SP(false, true, true);
+                } else {
+                    if (check_alive) GOSSIP_SP(true, true, false);
+                    else GOSSIP_SP(false, true, false);
+                }
+            } else if (cov) {
+                if (check_alive) GOSSIP_SP(true, false, true);
+                else GOSSIP_SP(false, false, true);
             } else {
-                if (check_alive) hipLaunchKernelGGL((k_push_light<W, true, false, false, true>), dim3(gs), dim3(kBlock), 0, s, a, wd);
-                else hipLaunchKernelGGL((k_push_light<W, false, false, false, true>), dim3(gs), dim3(kBlock), 0, s, a, wd);
+                if (check_alive) GOSSIP_SP(true, false, false);
+                else GOSSIP_SP(false, false, false);
             }
         });
+#undef GOSSIP_SP
         return hipGetLastError();
     }
     GOSSIP_DISPATCH_W(wp_of(W_), {
