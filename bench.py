@@ -278,9 +278,11 @@ class Ranked(Single):
     def __init__(self, w, dev, tune, world, rank):
         import torch.distributed as dist
 
-        from gossip_hip import Engine, comm_unique_id, partition
+        from gossip_hip import Engine, comm_unique_id, partition_edges
         self.dist, self.world, self.rank = dist, world, rank
-        part = partition(w.n, world)
+        # blocks of about equal work (the powerlaw overlay's edges sit at the low ids), as gossip_group_create
+        part = partition_edges(w.n, w.n_msgs, world, **{k: v for k, v in tune.items() if k != "tuning"},
+                               **w.engine_kwargs())
         self.eng = Engine(w.n, w.n_msgs, device=dev, part=(part[rank], part[rank + 1]), **tune, **w.engine_kwargs())
         self.eng.build_graph()
         self.eng.inject(w.origins, w.inject_rounds)

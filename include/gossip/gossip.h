@@ -49,6 +49,8 @@ typedef int gossip_status;
 #define GOSSIP_FLAG_NO_BLOCKED 32u      /* no propagation-blocked push rounds (saves ~22 B per edge of records) */
 #define GOSSIP_FLAG_FORCE_BLOCKED 64u   /* every push or binned round runs propagation-blocked where it can
                                            (single partition, one word per peer, slot layout) */
+#define GOSSIP_FLAG_UNIFORM_PARTITION 128u /* gossip_group_create: blocks of ceil(n/parts) peers instead of
+                                              gossip_partition_edges */
 
 /*
  * Replaces: NetworkConfig's parsed values (config.cpp:31-42,93-96) plus the
@@ -230,11 +232,16 @@ gossip_status gossip_round_commit(gossip_ctx* ctx, uint64_t global_new_receipts,
  * rank runs the same one; results equal the single-partition run. */
 #define GOSSIP_ECOMM (-7)           /* RCCL error */
 #define GOSSIP_COMM_ID_BYTES 128    /* ncclUniqueId */
-/* begins[world+1]: rank p owns peers [begins[p], begins[p+1]) */
+/* begins[world+1]: rank p owns peers [begins[p], begins[p+1]) -- blocks of ceil(n/world) peers */
 gossip_status gossip_partition(uint64_t n_peers, uint32_t world, uint64_t* begins);
+/* The same for cfg's overlay, blocks of about equal work (edges plus a per-peer share; whole 64-peer tiles):
+ * the powerlaw overlay's degree mass sits at the low ids (config 4 as 8 blocks of ceil(n/8): the first holds
+ * 3.2x the edges of any other).  Other overlays: gossip_partition.  gossip_group_create uses it (unless
+ * GOSSIP_FLAG_UNIFORM_PARTITION); with gossip_comm_init any contiguous partition in rank order works. */
+gossip_status gossip_partition_edges(const gossip_config* cfg, uint32_t world, uint64_t* begins);
 /* One process per GPU: rank 0 creates the id, every rank receives it out of band. */
 gossip_status gossip_comm_unique_id(uint8_t* id /* GOSSIP_COMM_ID_BYTES */);
-/* Makes ctx (created with the rank's block of gossip_partition as its part range)
+/* Makes ctx (created with the rank's block of gossip_partition[_edges] as its part range)
  * rank `rank` of `world`: allocates the exchange buffers, joins the RCCL
  * communicator (collective: every rank calls it), after which gossip_step /
  * gossip_run issue the collectives themselves (call them in lockstep on every

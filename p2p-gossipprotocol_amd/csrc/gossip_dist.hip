@@ -2,11 +2,12 @@
 //
 // The reference sends every gossip message to another PeerNode process over
 // TCP (broadcastMessage peer.cpp:310-316 -> handleClient peer.cpp:255-295).
-// Here peers are 1D vertex-partitioned into blocks of ceil(n/P) (SURVEY.md
-// 8(e)) and one round's cross-block traffic is ONE exchange, issued by this
-// driver on the block's HIP stream:
-//   dense rounds (PULL / BIN): in-place ncclAllGather of every block's new
-//     words into a buffer indexed by global peer; each block then pulls or
+// Here peers are 1D vertex-partitioned into contiguous blocks (SURVEY.md
+// 8(e); gossip_partition: ceil(n/P) peers each, gossip_partition_edges: about
+// equal edge counts, round 5) and one round's cross-block traffic is ONE
+// exchange, issued by this driver on the block's HIP stream:
+//   dense rounds (PULL / BIN): an all-gather (send / recv pairs of the blocks'
+//     slices) of every block's new words into a buffer indexed by global peer; each block then pulls or
 //     streams its in-edges from it (no second exchange, no atomics).  Below
 //     gather_permille of frontier the blocks exchange a bitmap of their
 //     64-peer tiles' non-zero words and those words packed instead (an
@@ -38,6 +39,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -61,9 +63,10 @@ struct DistRank {
     uint64_t *send = nullptr, *recv = nullptr, *gather = nullptr, *seg = nullptr, *rec_in = nullptr;
     uint64_t* d_io = nullptr;  // device scratch: stats all-reduce, record counts
     uint64_t* h_io = nullptr;  // pinned mirror
-    // compact dense exchange: every block's tile bitmap (tpb words per block, block order), the exclusive
-    // prefix of their popcounts (a tile's first packed word), the packed words of all blocks (block order)
+    // compact dense exchange: every block's tile bitmap (block q's tiles from toff[q], block order), the
+    // exclusive prefix of their popcounts (a tile's first packed word), the packed words of all blocks
     uint64_t *bits = nullptr, *pos = nullptr, *pk = nullptr;
+    uint64_t *d_part = nullptr, *d_toff = nullptr;  // the partition's block bounds and tile offsets (device)
     void* scan_tmp = nullptr;
     size_t scan_bytes = 0;
     std::vector<uint64_t> counts_out, counts_in;
@@ -81,9 +84,10 @@ struct DistDriver {
     std::vector<DistRank> ranks;  // the ranks this process drives
     uint32_t world = 1;
     bool emulate = false;         // every rank local on one device: device copies, one stream
-    std::vector<uint64_t> part;
-    uint64_t n = 0, chunk = 0;
-    uint64_t tpb = 0;  // 64-peer tiles per block (compact exchange)
+    std::vector<uint64_t> part;  // begins[world + 1]: any contiguous partition (every block non-empty)
+    std::vector<uint64_t> toff;  // toff[q]: the 64-peer tiles of the blocks before q (compact exchange)
+    uint64_t n = 0;
+    uint64_t maxb = 0;           // the largest block (a staging push's records per destination stay below it)
     uint32_t X = 1, R = 2;
     uint32_t pull_pm = kPullPermille, sparse_pm = 250, bin_pm = 4000, bin_front_pm = 100;
     // schedule state, from global stats (identical on every rank)
@@ -135,6 +139,13 @@ __global__ __launch_bounds__(256) void k_tile_bits(const uint64_t* words, uint64
     }
 }
 
+// block q of tile T (toff: the tile offsets of the world + 1 block bounds; world is small)
+__device__ __forceinline__ uint32_t tile_block(const uint64_t* toff, uint32_t world, uint64_t T) {
+    uint32_t q = 0;
+    while (q + 1 < world && toff[q + 1] <= T) ++q;
+    return q;
+}
+
 // the block's non-zero words, packed in peer order at out[pos[t] + rank of the peer in its tile]
 __global__ __launch_bounds__(256) void k_tile_pack(const uint64_t* words, uint64_t n, uint32_t X, const uint64_t* bits,
                                                    const uint64_t* pos, uint64_t* out) {
@@ -153,15 +164,16 @@ __global__ __launch_bounds__(256) void k_tile_pack(const uint64_t* words, uint64
 // every other block's words back into the gather buffer (zeros where the bitmap has none)
 __global__ __launch_bounds__(256) void k_tile_expand(uint64_t* gather, const uint64_t* bits, const uint64_t* pos,
                                                      const uint64_t* pk, uint32_t X, uint32_t world, uint32_t own,
-                                                     uint64_t chunk, uint64_t n, uint64_t tpb) {
+                                                     const uint64_t* part, const uint64_t* toff) {
     const int lane = threadIdx.x & 63;
-    const uint64_t tiles = (uint64_t)world * tpb;
+    const uint64_t tiles = toff[world];
     for (uint64_t T = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; T < tiles;
          T += ((uint64_t)gridDim.x * blockDim.x) >> 6) {
-        const uint64_t q = T / tpb, t = T % tpb;
-        const uint64_t v = q * chunk + t * 64 + lane;
-        const uint64_t end = std::min<uint64_t>((q + 1) * chunk, n);
-        if (q == own || q * chunk + t * 64 >= end) continue;  // wave-uniform
+        const uint32_t q = tile_block(toff, world, T);
+        const uint64_t t = T - toff[q];
+        const uint64_t v = part[q] + t * 64 + lane;
+        const uint64_t end = part[q + 1];
+        if (q == own) continue;  // wave-uniform
         const uint64_t b = bits[T];
         const bool set = (b >> lane) & 1;
         const uint64_t at = pos[T] + (uint64_t)__builtin_popcountll(b & ((1ull << lane) - 1));
@@ -170,9 +182,9 @@ __global__ __launch_bounds__(256) void k_tile_expand(uint64_t* gather, const uin
     }
 }
 
-__global__ void k_pick_offsets(const uint64_t* pos, uint32_t world, uint64_t tpb, uint64_t* out) {
+__global__ void k_pick_offsets(const uint64_t* pos, uint32_t world, const uint64_t* toff, uint64_t* out) {
     const uint32_t q = threadIdx.x;
-    if (q <= world) out[q] = pos[(uint64_t)q * tpb];
+    if (q <= world) out[q] = pos[toff[q]];
 }
 
 // Buffers and communicator of one rank (its stream is released by dist_free).
@@ -190,6 +202,9 @@ void free_rank(DistRank& r) {
     hipFree(r.pos);
     hipFree(r.pk);
     hipFree(r.scan_tmp);
+    hipFree(r.d_part);
+    hipFree(r.d_toff);
+    r.d_part = r.d_toff = nullptr;
     if (r.ev_pub) hipEventDestroy(r.ev_pub);
     for (hipEvent_t& e : r.ev_stage)
         if (e) hipEventDestroy(e);
@@ -213,16 +228,20 @@ gossip_status setup_rank(DistDriver* d, DistRank& r) {
     };
     DHIP(alloc(&r.send, d->n * X));
     DHIP(alloc(&r.recv, W * r.n_local * X));
-    DHIP(alloc(&r.gather, W * d->chunk * X));
-    DHIP(alloc(&r.seg, W * d->chunk * R));
+    DHIP(alloc(&r.gather, d->n * X));  // indexed by global peer: block q's words at part[q]
+    DHIP(alloc(&r.seg, W * d->maxb * R));
     DHIP(alloc(&r.rec_in, W * r.n_local * R));
     DHIP(alloc(&r.d_io, 2 * std::max<uint64_t>(W + 1, kStatSlots)));
     DHIP(hipHostMalloc((void**)&r.h_io, 2 * std::max<uint64_t>(W + 1, kStatSlots) * 8));
-    if (W > 1) {  // compact dense exchange (a short last block's unused tiles stay zero)
-        const uint64_t tiles = W * d->tpb;
+    DHIP(alloc(&r.d_part, W + 1));
+    DHIP(alloc(&r.d_toff, W + 1));
+    DHIP(hipMemcpyAsync(r.d_part, d->part.data(), (W + 1) * 8, hipMemcpyHostToDevice, r.stream));
+    DHIP(hipMemcpyAsync(r.d_toff, d->toff.data(), (W + 1) * 8, hipMemcpyHostToDevice, r.stream));
+    if (W > 1) {  // compact dense exchange
+        const uint64_t tiles = d->toff[W];
         DHIP(alloc(&r.bits, tiles + 1));  // (+1: a zero past the last tile, so the scan yields the total)
         DHIP(alloc(&r.pos, tiles + 1));
-        DHIP(alloc(&r.pk, W * d->chunk * X));
+        DHIP(alloc(&r.pk, d->n * X));
         DHIP(hipcub::DeviceScan::ExclusiveSum(nullptr, r.scan_bytes, TilePop(r.bits, PopOp()), r.pos, (int)(tiles + 1),
                                               r.stream));
         DHIP(hipMalloc(&r.scan_tmp, r.scan_bytes + 16));
@@ -255,11 +274,16 @@ gossip_status bind_rank(DistDriver* d, DistRank& r) {
     return GOSSIP_OK;
 }
 
-void init_schedule(DistDriver* d, const gossip_config& cfg) {
+// part: the blocks' bounds (world + 1, from 0 to n, every block non-empty)
+void init_schedule(DistDriver* d, const gossip_config& cfg, const std::vector<uint64_t>& part) {
     d->n = cfg.n_peers;
-    d->part = blocks(d->n, d->world);
-    d->chunk = d->part[1];
-    d->tpb = (d->chunk + 63) / 64;
+    d->part = part;
+    d->toff.assign(d->world + 1, 0);
+    d->maxb = 0;
+    for (uint32_t q = 0; q < d->world; ++q) {
+        d->toff[q + 1] = d->toff[q] + (part[q + 1] - part[q] + 63) / 64;
+        d->maxb = std::max(d->maxb, part[q + 1] - part[q]);
+    }
     if (cfg.pull_permille) d->pull_pm = cfg.pull_permille;
     if (cfg.bin_permille) d->bin_pm = cfg.bin_permille;
 }
@@ -317,19 +341,21 @@ struct ExchTimer {
     }
 };
 
-// every block's new words (published at gather + rank * chunk * X) to every rank
+// every block's new words (published at gather + part[rank] * X) to every rank: send / recv pairs of the
+// blocks' slices (the blocks may differ in size), every link at once
 gossip_status all_gather(DistDriver* d) {
-    const uint64_t words = d->chunk * d->X;
+    const uint64_t X = d->X;
+    auto size = [&](uint32_t q) { return (d->part[q + 1] - d->part[q]) * X; };
     ExchTimer t(d, "all_gather");
-    for (size_t i = 0; i < d->ranks.size(); ++i) t.bytes(i, 8.0 * words * (d->world - 1));
+    for (size_t i = 0; i < d->ranks.size(); ++i) t.bytes(i, 8.0 * X * (double)(d->n - d->ranks[i].n_local));
     if (d->emulate) {
         for (size_t i = 0; i < d->ranks.size(); ++i) {
             DistRank& q = d->ranks[i];
             gossip_status s = t.part(i, [&]() -> gossip_status {
                 for (auto& p : d->ranks)
                     if (p.rank != q.rank)
-                        DHIP(hipMemcpyAsync(q.gather + p.rank * words, p.gather + p.rank * words, words * 8,
-                                            hipMemcpyDeviceToDevice, q.stream));
+                        DHIP(hipMemcpyAsync(q.gather + d->part[p.rank] * X, p.gather + d->part[p.rank] * X,
+                                            size(p.rank) * 8, hipMemcpyDeviceToDevice, q.stream));
                 return GOSSIP_OK;
             });
             if (s) return s;
@@ -339,7 +365,11 @@ gossip_status all_gather(DistDriver* d) {
     DNCCL(ncclGroupStart());
     for (auto& r : d->ranks) {
         hipSetDevice(r.device);
-        DNCCL(ncclAllGather(r.gather + r.rank * words, r.gather, words, ncclUint64, r.comm, r.stream));
+        for (uint32_t q = 0; q < d->world; ++q) {
+            if (q == r.rank) continue;
+            DNCCL(ncclSend(r.gather + d->part[r.rank] * X, size(r.rank), ncclUint64, (int)q, r.comm, r.stream));
+            DNCCL(ncclRecv(r.gather + d->part[q] * X, size(q), ncclUint64, (int)q, r.comm, r.stream));
+        }
     }
     DNCCL(ncclGroupEnd());
     return GOSSIP_OK;
@@ -352,16 +382,17 @@ gossip_status all_gather(DistDriver* d) {
 // non-zero peer of the other blocks, against 8 X B per peer of them.
 gossip_status compact_gather(DistDriver* d) {
     const uint32_t W = d->world;
-    const uint64_t X = d->X, tpb = d->tpb, tiles = (uint64_t)W * tpb;
+    const uint64_t X = d->X, tiles = d->toff[W];
+    auto ntl = [&](uint32_t q) { return d->toff[q + 1] - d->toff[q]; };
     ExchTimer t(d, "all_gather");
     gossip_status s = GOSSIP_OK;
     for (size_t i = 0; i < d->ranks.size(); ++i) {  // own tile bitmap
         DistRank& r = d->ranks[i];
         DHIP(hipSetDevice(r.device));
         s = t.part(i, [&]() -> gossip_status {
-            hipLaunchKernelGGL(k_tile_bits, dim3((unsigned)std::min<uint64_t>((tpb + 3) / 4, 8192)), dim3(256), 0,
-                               r.stream, r.gather + r.rank * d->chunk * X, r.n_local, (uint32_t)X,
-                               r.bits + r.rank * tpb);
+            hipLaunchKernelGGL(k_tile_bits, dim3((unsigned)std::min<uint64_t>((ntl(r.rank) + 3) / 4, 8192)), dim3(256),
+                               0, r.stream, r.gather + d->part[r.rank] * X, r.n_local, (uint32_t)X,
+                               r.bits + d->toff[r.rank]);
             DHIP(hipGetLastError());
             return GOSSIP_OK;
         });
@@ -373,7 +404,7 @@ gossip_status compact_gather(DistDriver* d) {
             s = t.part(i, [&]() -> gossip_status {
                 for (auto& p : d->ranks)
                     if (p.rank != q.rank)
-                        DHIP(hipMemcpyAsync(q.bits + p.rank * tpb, p.bits + p.rank * tpb, tpb * 8,
+                        DHIP(hipMemcpyAsync(q.bits + d->toff[p.rank], p.bits + d->toff[p.rank], ntl(p.rank) * 8,
                                             hipMemcpyDeviceToDevice, q.stream));
                 return GOSSIP_OK;
             });
@@ -383,7 +414,11 @@ gossip_status compact_gather(DistDriver* d) {
         DNCCL(ncclGroupStart());
         for (auto& r : d->ranks) {
             hipSetDevice(r.device);
-            DNCCL(ncclAllGather(r.bits + r.rank * tpb, r.bits, tpb, ncclUint64, r.comm, r.stream));
+            for (uint32_t q = 0; q < W; ++q) {
+                if (q == r.rank) continue;
+                DNCCL(ncclSend(r.bits + d->toff[r.rank], ntl(r.rank), ncclUint64, (int)q, r.comm, r.stream));
+                DNCCL(ncclRecv(r.bits + d->toff[q], ntl(q), ncclUint64, (int)q, r.comm, r.stream));
+            }
         }
         DNCCL(ncclGroupEnd());
     }
@@ -395,7 +430,8 @@ gossip_status compact_gather(DistDriver* d) {
             size_t tb = r.scan_bytes;
             DHIP(hipcub::DeviceScan::ExclusiveSum(r.scan_tmp, tb, TilePop(r.bits, PopOp()), r.pos, (int)(tiles + 1),
                                                   r.stream));
-            hipLaunchKernelGGL(k_pick_offsets, dim3(1), dim3(64 * ((W + 64) / 64)), 0, r.stream, r.pos, W, tpb, r.d_io);
+            hipLaunchKernelGGL(k_pick_offsets, dim3(1), dim3(64 * ((W + 64) / 64)), 0, r.stream, r.pos, W, r.d_toff,
+                               r.d_io);
             DHIP(hipGetLastError());
             DHIP(hipMemcpyAsync(r.h_io, r.d_io, (W + 1) * 8, hipMemcpyDeviceToHost, r.stream));
             return GOSSIP_OK;
@@ -404,16 +440,16 @@ gossip_status compact_gather(DistDriver* d) {
         DHIP(hipStreamSynchronize(r.stream));
         std::memcpy(off.data(), r.h_io, (W + 1) * 8);  // (identical on every rank)
         s = t.part(i, [&]() -> gossip_status {
-            hipLaunchKernelGGL(k_tile_pack, dim3((unsigned)std::min<uint64_t>((tpb + 3) / 4, 8192)), dim3(256), 0,
-                               r.stream, r.gather + r.rank * d->chunk * X, r.n_local, (uint32_t)X,
-                               r.bits + r.rank * tpb, r.pos + r.rank * tpb, r.pk);
+            hipLaunchKernelGGL(k_tile_pack, dim3((unsigned)std::min<uint64_t>((ntl(r.rank) + 3) / 4, 8192)), dim3(256),
+                               0, r.stream, r.gather + d->part[r.rank] * X, r.n_local, (uint32_t)X,
+                               r.bits + d->toff[r.rank], r.pos + d->toff[r.rank], r.pk);
             DHIP(hipGetLastError());
             return GOSSIP_OK;
         });
         if (s) return s;
     }
     for (size_t i = 0; i < d->ranks.size(); ++i)
-        t.bytes(i, 8.0 * (double)((W - 1) * tpb) +
+        t.bytes(i, 8.0 * (double)(tiles - ntl(d->ranks[i].rank)) +
                        8.0 * X * (double)(off[W] - (off[d->ranks[i].rank + 1] - off[d->ranks[i].rank])));
     if (d->emulate) {
         for (size_t i = 0; i < d->ranks.size(); ++i) {
@@ -448,7 +484,7 @@ gossip_status compact_gather(DistDriver* d) {
         DHIP(hipSetDevice(r.device));
         s = t.part(i, [&]() -> gossip_status {
             hipLaunchKernelGGL(k_tile_expand, dim3((unsigned)std::min<uint64_t>((tiles + 3) / 4, 16384)), dim3(256), 0,
-                               r.stream, r.gather, r.bits, r.pos, r.pk, (uint32_t)X, W, r.rank, d->chunk, d->n, tpb);
+                               r.stream, r.gather, r.bits, r.pos, r.pk, (uint32_t)X, W, r.rank, r.d_part, r.d_toff);
             DHIP(hipGetLastError());
             return GOSSIP_OK;
         });
@@ -579,7 +615,7 @@ gossip_status all_to_all(DistDriver* d) {
 // rank q receives sender p's records after those of senders < p
 gossip_status exchange_records(DistDriver* d, std::vector<uint64_t>& total_in) {
     const uint32_t W = d->world;
-    const uint64_t R = d->R, chunk = d->chunk;
+    const uint64_t R = d->R;
     for (auto& r : d->ranks) {
         gossip_status s = gossip_sparse_counts(r.ctx, r.counts_out.data());
         if (s) return s;
@@ -627,7 +663,6 @@ gossip_status exchange_records(DistDriver* d, std::vector<uint64_t>& total_in) {
         if (c > (uint64_t)W * d->ranks[i].n_local)
             return set_error(GOSSIP_EOVERFLOW, "sparse exchange: more records than the receive buffer holds");
     }
-    (void)chunk;
     if (d->emulate) {
         for (size_t i = 0; i < d->ranks.size(); ++i) {
             DistRank& q = d->ranks[i];
@@ -914,6 +949,44 @@ gossip_status gossip_partition(uint64_t n_peers, uint32_t world, uint64_t* begin
     return GOSSIP_OK;
 }
 
+// Blocks of about equal work on the powerlaw overlay.  Its degree mass is skewed to the
+// low ids: every peer draws k picks from one seed response of L candidates (E[k] = sum over j < L of
+// 1 - (j/L)^2.5, 3.75 at L = 6) and candidate c = floor(n V^3), so P(c < x) = (x/n)^(1/3).  Symmetrised, the
+// edges with an end in [0, x) are about E[k] (x + n (x/n)^(1/3)): at P = 8 the first eighth of the ids holds
+// 3.2 times the edges of any other eighth (config 4 as 8 ceil(n/P) parts: part 0's kernels 18.9 ms per step,
+// the others' 8.8-9.8).  A block's cost is its edges plus kPeerCost edge-equivalents per peer (its O(peers)
+// sweeps and finishes); boundaries are whole 64-peer tiles.  A pure function of the config, so every rank
+// computes the same blocks.
+gossip_status gossip_partition_edges(const gossip_config* cfg, uint32_t world, uint64_t* begins) {
+    if (!cfg || !begins || world < 1 || cfg->n_peers < (uint64_t)world * 64)
+        return cfg ? gossip_partition(cfg->n_peers, world, begins) : set_error(GOSSIP_EINVAL, "null config");
+    if (cfg->graph_model != GOSSIP_GRAPH_POWERLAW) return gossip_partition(cfg->n_peers, world, begins);
+    constexpr double kPeerCost = 2.0;
+    const uint64_t n = cfg->n_peers;
+    const uint32_t L = cfg->list_len ? cfg->list_len : 6;
+    double ek = 0.0;
+    for (uint32_t j = 1; j < L; ++j) ek += 1.0 - std::pow((double)j / L, 2.5);
+    auto cost = [&](double u) { return ek * (u + std::cbrt(u)) + kPeerCost * u; };
+    const double total = cost(1.0);
+    begins[0] = 0;
+    for (uint32_t q = 1; q < world; ++q) {
+        const double want = total * q / world;
+        double lo = 0.0, hi = 1.0;
+        for (int it = 0; it < 200; ++it) {
+            const double mid = 0.5 * (lo + hi);
+            (cost(mid) < want ? lo : hi) = mid;
+        }
+        uint64_t x = ((uint64_t)(hi * (double)n) + 63) / 64 * 64;
+        x = std::max<uint64_t>(x, begins[q - 1] + 64);                  // non-empty, whole tiles
+        x = std::min<uint64_t>(x, n - (uint64_t)(world - q) * 64 / 64 * 64);  // room for the blocks after it
+        begins[q] = x;
+    }
+    begins[world] = n;
+    for (uint32_t q = 0; q < world; ++q)
+        if (begins[q + 1] <= begins[q]) return gossip_partition(n, world, begins);
+    return GOSSIP_OK;
+}
+
 gossip_status gossip_comm_unique_id(uint8_t* id) {
     if (!id) return set_error(GOSSIP_EINVAL, "null argument");
     ncclUniqueId u;
@@ -930,24 +1003,49 @@ gossip_status gossip_comm_init(gossip_ctx* ctx, const uint8_t* id, uint32_t worl
     if (cfg.rejoin_threshold) return set_error(GOSSIP_EINVAL, "rejoin_threshold needs a single partition");
     DistDriver* d = new DistDriver();
     d->world = world;
-    init_schedule(d, cfg);
     d->ranks.resize(1);
     DistRank& r = d->ranks[0];
     r.ctx = ctx;
     r.rank = rank;
-    gossip_status s = bind_rank(d, r);
-    if (!s) {
-        hipSetDevice(r.device);
-        if (hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking) != hipSuccess)
-            s = set_error(GOSSIP_EHIP, "stream");
-    }
-    if (!s) s = setup_rank(d, r);
+    r.device = ctx_device(ctx);
+    gossip_status s = GOSSIP_OK;
+    hipSetDevice(r.device);
+    if (hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking) != hipSuccess) s = set_error(GOSSIP_EHIP, "stream");
     if (!s) {
         ncclUniqueId u;
         std::memcpy(&u, id, sizeof(u));
         const ncclResult_t nr = ncclCommInitRank(&r.comm, (int)world, u, (int)rank);
         if (nr != ncclSuccess) s = set_error(GOSSIP_ECOMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(nr));
     }
+    if (!s) {  // every rank's block (any contiguous partition: gossip_partition or gossip_partition_edges)
+        uint64_t b = 0, e = 0;
+        ctx_range(ctx, &b, &e);
+        uint64_t* dv = nullptr;
+        std::vector<uint64_t> h(2 * (size_t)world + 2);
+        hipError_t he = hipMalloc((void**)&dv, h.size() * 8);
+        h[0] = b;
+        h[1] = e;
+        if (he == hipSuccess) he = hipMemcpyAsync(dv, h.data(), 16, hipMemcpyHostToDevice, r.stream);
+        ncclResult_t nr = he == hipSuccess ? ncclAllGather(dv, dv + 2, 2, ncclUint64, r.comm, r.stream) : ncclSuccess;
+        if (he == hipSuccess && nr == ncclSuccess)
+            he = hipMemcpyAsync(h.data() + 2, dv + 2, 16 * (size_t)world, hipMemcpyDeviceToHost, r.stream);
+        if (he == hipSuccess) he = hipStreamSynchronize(r.stream);
+        hipFree(dv);
+        if (he != hipSuccess) s = set_error(GOSSIP_EHIP, std::string("block table: ") + hipGetErrorString(he));
+        else if (nr != ncclSuccess) s = set_error(GOSSIP_ECOMM, std::string("block table: ") + ncclGetErrorString(nr));
+        std::vector<uint64_t> part(world + 1);
+        for (uint32_t q = 0; !s && q < world; ++q) {
+            part[q] = h[2 + 2 * q];
+            part[q + 1] = h[3 + 2 * q];
+            if (part[q + 1] <= part[q] || (q && h[1 + 2 * q] != part[q]))
+                s = set_error(GOSSIP_EINVAL, "the ranks' part ranges are not contiguous non-empty blocks in rank order");
+        }
+        if (!s && (part[0] != 0 || part[world] != cfg.n_peers))
+            s = set_error(GOSSIP_EINVAL, "the ranks' part ranges do not cover [0, n_peers)");
+        if (!s) init_schedule(d, cfg, part);
+    }
+    if (!s) s = bind_rank(d, r);
+    if (!s) s = setup_rank(d, r);
     if (s) {
         // the ctx must not keep pointers into the buffers dist_free releases: it stays a
         // single-partition ctx on the null stream, usable with gossip_step
@@ -996,7 +1094,8 @@ gossip_status gossip_group_create(const gossip_config* cfg, uint32_t n_parts, co
     same &= devices[0] == devices[n_parts - 1];
     if (!same && !distinct) return set_error(GOSSIP_EINVAL, "devices must be all distinct or all the same");
     std::vector<uint64_t> part(n_parts + 1);
-    gossip_status s = gossip_partition(cfg->n_peers, n_parts, part.data());
+    gossip_status s = cfg->flags & GOSSIP_FLAG_UNIFORM_PARTITION ? gossip_partition(cfg->n_peers, n_parts, part.data())
+                                                                 : gossip_partition_edges(cfg, n_parts, part.data());
     if (s) return s;
     gossip_group* g = new gossip_group();
     g->n = cfg->n_peers;
@@ -1005,7 +1104,7 @@ gossip_status gossip_group_create(const gossip_config* cfg, uint32_t n_parts, co
     g->d = d;
     d->world = n_parts;
     d->emulate = same && n_parts > 1;
-    init_schedule(d, *cfg);
+    init_schedule(d, *cfg, part);
     d->ranks.resize(n_parts);
     auto bail = [&](gossip_status st) {
         for (auto& r : d->ranks)

@@ -164,7 +164,10 @@ struct gossip_ctx {
     // a vertex block's sparse push rounds as records (build_px; P > 1, one word per peer)
     PbState px;
     int px_state = 0;            // 0: not built yet, 1: ready, -1: not eligible (staging push)
-    uint64_t* d_part = nullptr;  // the partition's block bounds (device copy, the pack's)
+    uint64_t* d_part = nullptr;  // the partition's block bounds (device copy: the record pack's, the compaction's)
+    uint64_t* d_toff = nullptr;  // the 64-peer tiles of the blocks before each block (device; the compaction's)
+    uint64_t n_tiles_all = 0;    // ... all of them
+    uint64_t blk_stride = 0;     // the largest block: a destination's staged records in the compaction's output
     int32_t px_pm = 2;           // "px_permille": record push from this frontier per-mille of the block (-1: never)
     bool cur_px = false;         // the round in flight pushes records
     // late pull rounds over needy lists (k_pull_list)
@@ -319,7 +322,7 @@ uint32_t ctx_stages(gossip_ctx* c) {
 uint64_t ctx_bin_seg(gossip_ctx* c) { return c->bins.seg; }
 void ctx_send_records(gossip_ctx* c, const uint64_t** base, uint64_t* stride) {
     *base = c->cur_px ? c->px.rec_out : c->seg;
-    *stride = c->cur_px ? c->px.rec_stride : c->part_begins[1];
+    *stride = c->cur_px ? c->px.rec_stride : c->blk_stride;
 }
 gossip_status ctx_arm_stages(gossip_ctx* c, uint32_t S, const hipEvent_t* ev) {  // (the caller set the device)
     if (const hipError_t e = build_stage_units(&c->bins, S, c->begin, c->end, c->n))
@@ -1202,12 +1205,7 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
                                               c->part_begins.begin()),
                          (uint64_t)c->world * c->n_local, c->stream, &c->px, &err);
             if (e == hipSuccess) {
-                hipFree(c->d_part);
-                c->d_part = nullptr;
-                HIPCHK(hipMalloc((void**)&c->d_part, (c->world + 1) * sizeof(uint64_t)));
-                HIPCHK(hipMemcpy(c->d_part, c->part_begins.data(), (c->world + 1) * sizeof(uint64_t),
-                                 hipMemcpyHostToDevice));
-                c->px_state = 1;
+                c->px_state = 1;  // (d_part: set with the sparse exchange, gossip_set_sparse)
             } else if (e == hipErrorOutOfMemory || e == hipErrorInvalidValue) {
                 c->px_state = -1;  // the staging push stays
             } else {
@@ -1520,8 +1518,8 @@ gossip_status round_compute(gossip_ctx* c) {
     HIPCHK(timed(c, "push_light", [&] { return launch_push_light(a, pw, c->any_dead, remote, c->stream); }));
     if (c->cur_sparse) {
         HIPCHK(timed(c, "compact_send", [&] {
-            return launch_compact_send(a, pw, c->part_begins[1], c->world, c->d_counts, c->seg, c->sx_bits, c->sx_pos,
-                                       c->sx_tmp, c->sx_bytes, c->stream);
+            return launch_compact_send(a, pw, c->d_part, c->d_toff, c->n_tiles_all, c->world, c->blk_stride, c->d_counts,
+                                       c->seg, c->sx_bits, c->sx_pos, c->sx_tmp, c->sx_bytes, c->stream);
         }));
         HIPCHK(hipMemcpyAsync(c->h_counts, c->d_counts, c->world * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
     }
@@ -1997,6 +1995,7 @@ void gossip_destroy(gossip_ctx* c) {
     hipFree(c->d_work);
     hipFree(c->d_hist);
     hipFree(c->d_part);
+    hipFree(c->d_toff);
     hipFree(c->sx_pos);
     hipFree(c->sx_tmp);
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
@@ -2389,10 +2388,6 @@ gossip_status gossip_set_exchange(gossip_ctx* c, void* send, void* recv, uint32_
 gossip_status gossip_set_gather(gossip_ctx* c, void* gather) {
     if (!c || !gather) return fail(GOSSIP_EINVAL, "null argument");
     if (c->part_begins.size() < 2) return fail(GOSSIP_ESTATE, "call gossip_set_exchange first");
-    const uint64_t chunk = c->part_begins[1];
-    for (uint32_t p = 0; p <= c->world; ++p)
-        if (c->part_begins[p] != std::min<uint64_t>((uint64_t)p * chunk, c->n))
-            return fail(GOSSIP_EINVAL, "gather needs blocks of ceil(n/world) peers (begins[p] = p*chunk)");
     if (set_dev(c)) return GOSSIP_EHIP;
     hipFree(c->front);
     c->front = nullptr;
@@ -2408,7 +2403,22 @@ gossip_status gossip_set_sparse(gossip_ctx* c, void* seg) {
     if (!c->d_counts) {
         HIPCHK(hipMalloc((void**)&c->d_counts, (c->world + 1) * sizeof(unsigned long long)));
         HIPCHK(hipHostMalloc((void**)&c->h_counts, (c->world + 1) * sizeof(uint64_t)));
-        const uint64_t tiles = (uint64_t)c->world * ((c->part_begins[1] + 63) / 64);
+        // the blocks (any contiguous partition): bounds and tile offsets on the device, the largest block
+        std::vector<uint64_t> toff(c->world + 1, 0);
+        c->blk_stride = 0;
+        for (uint32_t q = 0; q < c->world; ++q) {
+            toff[q + 1] = toff[q] + (c->part_begins[q + 1] - c->part_begins[q] + 63) / 64;
+            c->blk_stride = std::max(c->blk_stride, c->part_begins[q + 1] - c->part_begins[q]);
+        }
+        c->n_tiles_all = toff[c->world];
+        hipFree(c->d_part);
+        hipFree(c->d_toff);
+        c->d_part = c->d_toff = nullptr;
+        HIPCHK(hipMalloc((void**)&c->d_part, (c->world + 1) * sizeof(uint64_t)));
+        HIPCHK(hipMalloc((void**)&c->d_toff, (c->world + 1) * sizeof(uint64_t)));
+        HIPCHK(hipMemcpy(c->d_part, c->part_begins.data(), (c->world + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(c->d_toff, toff.data(), (c->world + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
+        const uint64_t tiles = c->n_tiles_all;
         HIPCHK(hipMalloc((void**)&c->sx_bits, (tiles + 1) * sizeof(uint64_t)));
         HIPCHK(hipMemset(c->sx_bits, 0, (tiles + 1) * sizeof(uint64_t)));
         HIPCHK(hipMalloc((void**)&c->sx_pos, (tiles + 1) * sizeof(uint64_t)));

@@ -378,15 +378,17 @@ hipError_t launch_list_zero(const RoundArgs& a, const uint32_t* lst, uint32_t n,
 hipError_t launch_pull_list(const RoundArgs& a, const uint32_t* lst, uint32_t n, hipStream_t s);
 hipError_t launch_apply_remote(const RoundArgs& a, uint32_t W, const uint64_t* recv, uint32_t world,
                                uint64_t part_stride, hipStream_t s);
-// sparse push exchange: send -> per-destination {peer, words} records at seg + q * chunk, counts[q] of them
-// (bits: world * ceil(chunk / 64) + 1 words, the last kept zero; pos: as many; scan_tmp: compact_send_scratch)
+// sparse push exchange: send -> per-destination {peer, words} records at seg + q * stride, counts[q] of them
+// (part / toff: the blocks' bounds and tile offsets on the device, tiles = toff[world]; bits: tiles + 1 words,
+// the last kept zero; pos: as many; scan_tmp: compact_send_scratch)
 hipError_t compact_send_scratch(uint64_t tiles, size_t* scan_bytes);
 // a sparse round's staging marks: 1 bit per 64 global peers (+ a word of slack)
 inline uint64_t smark_bytes(uint64_t n_global) { return ((n_global + 4095) / 4096 + 1) * 8; }
 // (smark: the round's staging marks, cleared here for the next sparse round)
-hipError_t launch_compact_send(const RoundArgs& a, uint32_t W, uint64_t chunk, uint32_t world,
-                               unsigned long long* counts, uint64_t* seg, uint64_t* bits, uint64_t* pos,
-                               void* scan_tmp, size_t scan_bytes, hipStream_t s);
+hipError_t launch_compact_send(const RoundArgs& a, uint32_t W, const uint64_t* part, const uint64_t* toff,
+                               uint64_t tiles, uint32_t world, uint64_t stride, unsigned long long* counts,
+                               uint64_t* seg, uint64_t* bits, uint64_t* pos, void* scan_tmp, size_t scan_bytes,
+                               hipStream_t s);
 hipError_t launch_apply_records(const RoundArgs& a, uint32_t W, const uint64_t* rec, uint64_t n_rec, hipStream_t s);
 hipError_t launch_bin_scatter(const RoundArgs& a, const BinArgs& b, uint32_t W, hipStream_t s);
 hipError_t launch_bin_apply(const RoundArgs& a, const BinArgs& b, uint32_t W, hipStream_t s);

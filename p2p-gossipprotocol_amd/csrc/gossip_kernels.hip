@@ -2393,22 +2393,29 @@ __global__ __launch_bounds__(kBlock) void k_apply_remote(RoundArgs a, const uint
 // destination: millions of same-address atomics per round -- config 4 at
 // P = 8, 69 ms of compaction per step.)
 // ---------------------------------------------------------------------------
+// block q of tile T (toff: the tiles of the blocks before each block; world is small)
+__device__ __forceinline__ uint32_t send_block(const uint64_t* toff, uint32_t world, uint64_t T) {
+    uint32_t q = 0;
+    while (q + 1 < world && toff[q + 1] <= T) ++q;
+    return q;
+}
+
 template <int W>
-__global__ __launch_bounds__(kBlock) void k_send_bits(RoundArgs a, uint64_t chunk, uint64_t tpb, uint32_t world,
-                                                      uint64_t* bits) {
+__global__ __launch_bounds__(kBlock) void k_send_bits(RoundArgs a, const uint64_t* part, const uint64_t* toff,
+                                                      uint32_t world, uint64_t* bits) {
     // a wave per 64 tiles: lane l tests tile T0 + l against the round's marks (its peers span at most two
     // marked 64-peer tiles), unmarked tiles get a zero bitmap word, and the wave reads the staging words of
     // the marked ones in turn (a sparse round's send buffer is 2 GB at config 4; the marked tiles are few)
     const int lane = threadIdx.x & 63;
-    const uint64_t tiles = (uint64_t)world * tpb;
+    const uint64_t tiles = toff[world];
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
     for (uint64_t T0 = ((uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * 64; T0 < tiles;
          T0 += nwaves * 64) {
         const uint64_t T = T0 + lane;
         bool mk = false;
         if (T < tiles) {
-            const uint64_t q = T / tpb, t = T % tpb;
-            const uint64_t v0 = q * chunk + t * 64, end = min((q + 1) * chunk, a.n_global);
+            const uint32_t q = send_block(toff, world, T);
+            const uint64_t v0 = part[q] + (T - toff[q]) * 64, end = part[q + 1];
             if (v0 < end) {
                 const uint64_t g0 = v0 >> 6, g1 = (min(v0 + 64, end) - 1) >> 6;
                 mk = ((a.smark[g0 >> 6] >> (g0 & 63)) | (a.smark[g1 >> 6] >> (g1 & 63))) & 1ull;
@@ -2417,9 +2424,9 @@ __global__ __launch_bounds__(kBlock) void k_send_bits(RoundArgs a, uint64_t chun
         }
         for (unsigned long long todo = __ballot(mk); todo; todo &= todo - 1) {  // wave-uniform
             const uint64_t Tm = T0 + (uint64_t)__builtin_ctzll(todo);
-            const uint64_t q = Tm / tpb, t = Tm % tpb;
-            const uint64_t end = min((q + 1) * chunk, a.n_global);
-            const uint64_t v = q * chunk + t * 64 + lane;
+            const uint32_t q = send_block(toff, world, Tm);
+            const uint64_t end = part[q + 1];
+            const uint64_t v = part[q] + (Tm - toff[q]) * 64 + lane;
             bool any = false;
             if (v < end) {
 #pragma unroll
@@ -2432,14 +2439,14 @@ __global__ __launch_bounds__(kBlock) void k_send_bits(RoundArgs a, uint64_t chun
 }
 
 template <int W>
-__global__ __launch_bounds__(kBlock) void k_send_pack(RoundArgs a, uint64_t chunk, uint64_t tpb, uint32_t world,
-                                                      const uint64_t* bits, const uint64_t* pos,
-                                                      unsigned long long* counts, uint64_t* seg) {
+__global__ __launch_bounds__(kBlock) void k_send_pack(RoundArgs a, const uint64_t* part, const uint64_t* toff,
+                                                      uint32_t world, uint64_t stride, const uint64_t* bits,
+                                                      const uint64_t* pos, unsigned long long* counts, uint64_t* seg) {
     const int lane = threadIdx.x & 63;
-    const uint64_t tiles = (uint64_t)world * tpb;
+    const uint64_t tiles = toff[world];
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
     const uint64_t gid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (gid < world) counts[gid] = pos[(gid + 1) * tpb] - pos[gid * tpb];  // records per destination
+    if (gid < world) counts[gid] = pos[toff[gid + 1]] - pos[toff[gid]];  // records per destination
     // a wave per 64 tiles: one coalesced read of their bitmap words, then the tiles with records in turn
     // (a wave per tile waited on one bitmap word per tile: 64 round trips per wave at config 4, P = 8)
     for (uint64_t T0 = ((uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * 64; T0 < tiles;
@@ -2451,10 +2458,10 @@ __global__ __launch_bounds__(kBlock) void k_send_pack(RoundArgs a, uint64_t chun
             const uint64_t b = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(bl >> 32), src) << 32) |
                                (uint32_t)__shfl((int)(uint32_t)bl, src);
             if ((b >> lane) & 1) {
-                const uint64_t q = T / tpb, t = T % tpb;
-                const uint64_t v = q * chunk + t * 64 + lane;
-                const uint64_t idx = pos[T] - pos[q * tpb] + (uint64_t)__popcll(b & ((1ull << lane) - 1));
-                uint64_t* rec = seg + (q * chunk + idx) * (1 + W);
+                const uint32_t q = send_block(toff, world, T);
+                const uint64_t v = part[q] + (T - toff[q]) * 64 + lane;
+                const uint64_t idx = pos[T] - pos[toff[q]] + (uint64_t)__popcll(b & ((1ull << lane) - 1));
+                uint64_t* rec = seg + (q * stride + idx) * (1 + W);
                 rec[0] = v;
 #pragma unroll
                 for (int w = 0; w < W; ++w) {
@@ -2744,13 +2751,13 @@ hipError_t compact_send_scratch(uint64_t tiles, size_t* scan_bytes) {
     return hipcub::DeviceScan::ExclusiveSum(nullptr, *scan_bytes, it, (uint64_t*)nullptr, (int)(tiles + 1));
 }
 
-hipError_t launch_compact_send(const RoundArgs& a, uint32_t W_, uint64_t chunk, uint32_t world,
-                               unsigned long long* counts, uint64_t* seg, uint64_t* bits, uint64_t* pos,
-                               void* scan_tmp, size_t scan_bytes, hipStream_t s) {
+hipError_t launch_compact_send(const RoundArgs& a, uint32_t W_, const uint64_t* part, const uint64_t* toff,
+                               uint64_t tiles, uint32_t world, uint64_t stride, unsigned long long* counts,
+                               uint64_t* seg, uint64_t* bits, uint64_t* pos, void* scan_tmp, size_t scan_bytes,
+                               hipStream_t s) {
     if (!a.smark) return hipErrorInvalidValue;
-    const uint64_t tpb = (chunk + 63) / 64, tiles = (uint64_t)world * tpb;
     const unsigned grid_b = (unsigned)std::min<uint64_t>(grid_for((tiles + 63) / 64, kWavesPerBlock), 4096);
-    GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_send_bits<W>, dim3(grid_b), dim3(kBlock), 0, s, a, chunk, tpb,
+    GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_send_bits<W>, dim3(grid_b), dim3(kBlock), 0, s, a, part, toff,
                                                    world, bits));
     if (hipError_t e = hipGetLastError()) return e;
     // (bits[tiles] is zero from the allocation: the scan's last element is the total)
@@ -2758,7 +2765,8 @@ hipError_t launch_compact_send(const RoundArgs& a, uint32_t W_, uint64_t chunk, 
     size_t tb = scan_bytes;
     if (hipError_t e = hipcub::DeviceScan::ExclusiveSum(scan_tmp, tb, it, pos, (int)(tiles + 1), s)) return e;
     GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_send_pack<W>, dim3(std::max(grid_b, grid_for(world, kBlock))),
-                                                   dim3(kBlock), 0, s, a, chunk, tpb, world, bits, pos, counts, seg));
+                                                   dim3(kBlock), 0, s, a, part, toff, world, stride, bits, pos,
+                                                   counts, seg));
     if (hipError_t e = hipGetLastError()) return e;
     return hipMemsetAsync(a.smark, 0, smark_bytes(a.n_global), s);
 }

@@ -6,5 +6,5 @@ over RCCL (Engine.comm_init, Group); distributed.py is the torch.distributed
 mirror of the same driver, kept as the gloo test harness.
 """
 from ._abi import GossipError, declared_symbols, lib  # noqa: F401
-from .engine import EXCHANGES, KERNELS, Engine, Group, comm_unique_id, device_count, partition, pick_origins  # noqa: F401
+from .engine import EXCHANGES, KERNELS, Engine, Group, comm_unique_id, device_count, partition, partition_edges, pick_origins  # noqa: F401
 from .workloads import Workload, config, ping_every_rounds, run_engine  # noqa: F401

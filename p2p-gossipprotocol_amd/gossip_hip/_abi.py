@@ -145,6 +145,7 @@ def lib() -> C.CDLL:
         "gossip_set_tuning": (i32, [P, C.c_char_p, C.c_int64]),
         # library-driven multi-GPU rounds (gossip_dist.hip)
         "gossip_partition": (i32, [u64, u32, pu64]),
+        "gossip_partition_edges": (i32, [C.POINTER(GossipConfig), u32, pu64]),
         "gossip_comm_unique_id": (i32, [pu8]),
         "gossip_comm_init": (i32, [P, pu8, u32, u32]),
         "gossip_comm_finalize": (i32, [P, C.POINTER(RoundStats), u32, C.POINTER(DeadReport), u64, pu64]),

@@ -45,6 +45,15 @@ def partition(n_peers: int, world: int) -> list[int]:
     return [int(x) for x in out]
 
 
+def partition_edges(n_peers: int, n_msgs: int, world: int, **kw) -> list[int]:
+    """Blocks of about equal work for this overlay (gossip_partition_edges: the
+    powerlaw overlay's edges sit at the low ids; others get partition())."""
+    cfg = make_config(n_peers, n_msgs, **kw)
+    out = np.zeros(world + 1, dtype=np.uint64)
+    check(_abi.lib().gossip_partition_edges(C.byref(cfg), world, _ptr(out, C.c_uint64)), "gossip_partition_edges")
+    return [int(x) for x in out]
+
+
 def device_count() -> int:
     """HIP devices visible to this process (gossip_device_count)."""
     n = C.c_int32()

@@ -1,0 +1,39 @@
+"""gossip_partition_edges (host code of libgossip_hip, no GPU): blocks of
+about equal work for the powerlaw overlay -- contiguous, whole 64-peer tiles,
+covering [0, n) -- checked against the oracle's own overlay: every block's
+edges plus 2 edge-equivalents per peer within a few per cent of the mean,
+where blocks of ceil(n/P) peers put 2.5x the mean edges on the first one."""
+import numpy as np
+import pytest
+
+from gossip_hip import partition, partition_edges
+from gossip_hip.workloads import config
+
+
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 8])
+def test_blocks_are_contiguous_tiles(P):
+    n = 1 << 20
+    b = partition_edges(n, 64, P)
+    assert b[0] == 0 and b[-1] == n and len(b) == P + 1
+    assert all(b[q + 1] > b[q] for q in range(P))
+    assert all(x % 64 == 0 for x in b[:-1])
+
+
+def test_other_overlays_and_tiny_ones_get_uniform_blocks():
+    assert partition_edges(4096, 64, 4, graph="ref_bootstrap") == partition(4096, 4)
+    assert partition_edges(100, 64, 3) == partition(100, 3)  # fewer than 64 peers per block
+
+
+@pytest.mark.parametrize("P", [2, 4, 8])
+def test_blocks_balance_the_oracles_overlay(oracle, P):
+    w = config(4, 1 << 20, pick=oracle.pick_origins)
+    rp, col = oracle.gen_workload(w)
+    rp = np.asarray(rp, dtype=np.int64)
+
+    def costs(b):
+        return np.array([rp[b[q + 1]] - rp[b[q]] + 2 * (b[q + 1] - b[q]) for q in range(P)], dtype=np.float64)
+
+    bal = costs(partition_edges(w.n, w.n_msgs, P, **w.engine_kwargs()))
+    uni = costs(partition(w.n, P))
+    assert bal.max() / bal.mean() < 1.05
+    assert uni.max() / uni.mean() > 1.2  # what the uniform blocks did
