@@ -61,6 +61,8 @@ struct DistRank {
     ncclComm_t comm = nullptr;
     uint64_t begin = 0, n_local = 0;
     uint64_t *send = nullptr, *recv = nullptr, *gather = nullptr, *seg = nullptr, *rec_in = nullptr;
+    uint64_t rec_cap = 0;  // records rec_in holds (grown when a round's records do not fit: a record push
+                           // sends one per remote delivery, a small block of hubs receives many)
     uint64_t* d_io = nullptr;  // device scratch: stats all-reduce, record counts
     uint64_t* h_io = nullptr;  // pinned mirror
     // compact dense exchange: every block's tile bitmap (block q's tiles from toff[q], block order), the
@@ -231,6 +233,7 @@ gossip_status setup_rank(DistDriver* d, DistRank& r) {
     DHIP(alloc(&r.gather, d->n * X));  // indexed by global peer: block q's words at part[q]
     DHIP(alloc(&r.seg, W * d->maxb * R));
     DHIP(alloc(&r.rec_in, W * r.n_local * R));
+    r.rec_cap = W * r.n_local;
     DHIP(alloc(&r.d_io, 2 * std::max<uint64_t>(W + 1, kStatSlots)));
     DHIP(hipHostMalloc((void**)&r.h_io, 2 * std::max<uint64_t>(W + 1, kStatSlots) * 8));
     DHIP(alloc(&r.d_part, W + 1));
@@ -658,10 +661,18 @@ gossip_status exchange_records(DistDriver* d, std::vector<uint64_t>& total_in) {
     std::vector<uint64_t> stride(d->ranks.size());
     for (size_t i = 0; i < d->ranks.size(); ++i) ctx_send_records(d->ranks[i].ctx, &src[i], &stride[i]);
     for (size_t i = 0; i < d->ranks.size(); ++i) {
+        DistRank& r = d->ranks[i];
         uint64_t c = 0;
-        for (uint32_t q = 0; q < W; ++q) c += d->ranks[i].counts_in[q];
-        if (c > (uint64_t)W * d->ranks[i].n_local)
-            return set_error(GOSSIP_EOVERFLOW, "sparse exchange: more records than the receive buffer holds");
+        for (uint32_t q = 0; q < W; ++q) c += r.counts_in[q];
+        if (c > r.rec_cap) {  // (once, on the first round with that many records; hipFree waits for the device)
+            DHIP(hipSetDevice(r.device));
+            DHIP(hipStreamSynchronize(r.stream));
+            hipFree(r.rec_in);
+            r.rec_in = nullptr;
+            r.rec_cap = 0;
+            DHIP(hipMalloc((void**)&r.rec_in, c * R * 8));
+            r.rec_cap = c;
+        }
     }
     if (d->emulate) {
         for (size_t i = 0; i < d->ranks.size(); ++i) {

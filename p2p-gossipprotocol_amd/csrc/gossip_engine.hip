@@ -169,7 +169,8 @@ struct gossip_ctx {
     uint64_t n_tiles_all = 0;    // ... all of them
     uint64_t blk_stride = 0;     // the largest block: a destination's staged records in the compaction's output
     int32_t px_pm = 2;           // "px_permille": record push from this frontier per-mille of the block (-1: never)
-    bool cur_px = false;         // the round in flight pushes records
+    bool cur_px = false;         // the round in flight pushes records (level 1)
+    bool cur_arec = false;       // ... or appends them from the push (a near-empty frontier)
     // late pull rounds over needy lists (k_pull_list)
     bool list_req = true;          // "list_rounds": 0 never
     uint32_t list_cap_req = 0;     // "list_cap": entries per list (0: n_local / 16, at least 2^16)
@@ -321,8 +322,8 @@ uint32_t ctx_stages(gossip_ctx* c) {
 }
 uint64_t ctx_bin_seg(gossip_ctx* c) { return c->bins.seg; }
 void ctx_send_records(gossip_ctx* c, const uint64_t** base, uint64_t* stride) {
-    *base = c->cur_px ? c->px.rec_out : c->seg;
-    *stride = c->cur_px ? c->px.rec_stride : c->blk_stride;
+    *base = c->cur_px || c->cur_arec ? c->px.rec_out : c->seg;
+    *stride = c->cur_px || c->cur_arec ? c->px.rec_stride : c->blk_stride;
 }
 gossip_status ctx_arm_stages(gossip_ctx* c, uint32_t S, const hipEvent_t* ev) {  // (the caller set the device)
     if (const hipError_t e = build_stage_units(&c->bins, S, c->begin, c->end, c->n))
@@ -1194,9 +1195,11 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
     // per destination block (gossip_blocked.hip build_px) instead of OR-ing into the staging buffer and
     // compacting it: config 4 round 3 as 8 parts staged 47 M deliveries and then swept every part's whole
     // 2 GB staging buffer for them (every 64-peer tile of it marked)
-    c->cur_px = false;
-    if (c->cur_sparse && c->Wp == 1 && c->px_pm >= 0 && !c->cfg.extra_cap && c->symmetric && c->world <= kPbCoarseMax &&
-        (c->frontier_est + cnt) * 1000 >= c->n_local * (uint64_t)c->px_pm) {
+    // Below that frontier the push appends its remote deliveries as records to the same buffer (one counter
+    // atomic per wave and destination block): the staging buffer's compaction swept every tile of every
+    // destination block whatever the round's size (config 4 at P = 8: ≈ 90 us per part in near-empty rounds)
+    c->cur_px = c->cur_arec = false;
+    if (c->cur_sparse && c->Wp == 1 && c->px_pm >= 0 && !c->cfg.extra_cap && c->symmetric && c->world <= kPbCoarseMax) {
         if (c->px_state == 0) {
             std::string err;
             const hipError_t e =
@@ -1212,7 +1215,9 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
                 return fail(GOSSIP_EHIP, "record push: " + err);
             }
         }
-        c->cur_px = c->px_state == 1;
+        const bool wide = (c->frontier_est + cnt) * 1000 >= c->n_local * (uint64_t)c->px_pm;
+        c->cur_px = c->px_state == 1 && wide;
+        c->cur_arec = c->px_state == 1 && !wide;
     }
     // a wide push round (the explosion before the dense rounds) is bound by memory-side atomics, two per
     // fresh delivery (seen, then nx); deferring the seen update halves them for one streamed pass
@@ -1294,7 +1299,14 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
         }
         if (remote && !c->cur_sparse) c->send_dirty = true;
     }
-    a.smark = remote && c->cur_sparse ? c->smark : nullptr;
+    a.smark = remote && c->cur_sparse && !c->cur_arec ? c->smark : nullptr;
+    if (c->cur_arec) {
+        a.rec_out = c->px.rec_out;
+        a.rec_cnt = c->d_counts;
+        a.rec_stride = c->px.rec_stride;
+        a.part = c->d_part;
+        a.world = c->world;
+    }
     if (c->cur_pb) a.tsparse = 0;  // the blocked round sweeps every tile (round_compute clears the marks)
     c->cur = a;
     c->cur_remote = remote;
@@ -1490,6 +1502,7 @@ gossip_status round_compute(gossip_ctx* c) {
         return GOSSIP_OK;
     }
     const bool remote = c->cur_remote;
+    if (c->cur_arec) HIPCHK(queue_zero(c, c->d_counts, c->world * sizeof(unsigned long long)));  // append counters
     if (c->cur_px) {  // records per destination block (level 1 of a blocked round, the own block delivered at once)
         PbArgs p = pb_args(c->px);
         const uint32_t own =
@@ -1516,7 +1529,9 @@ gossip_status round_compute(gossip_ctx* c) {
     HIPCHK(timed(c, "push_heavy", [&] { return launch_push_heavy(a, pw, c->any_dead, remote, c->stream); }));
     if (a.tcur && !a.tsparse) HIPCHK(queue_zero(c, a.tcur, tact_bytes(c)));  // unread marks go
     HIPCHK(timed(c, "push_light", [&] { return launch_push_light(a, pw, c->any_dead, remote, c->stream); }));
-    if (c->cur_sparse) {
+    if (c->cur_arec) {
+        HIPCHK(hipMemcpyAsync(c->h_counts, c->d_counts, c->world * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    } else if (c->cur_sparse) {
         HIPCHK(timed(c, "compact_send", [&] {
             return launch_compact_send(a, pw, c->d_part, c->d_toff, c->n_tiles_all, c->world, c->blk_stride, c->d_counts,
                                        c->seg, c->sx_bits, c->sx_pos, c->sx_tmp, c->sx_bytes, c->stream);

@@ -261,6 +261,15 @@ struct RoundArgs {
     uint64_t* nw;           // this round's new words (sources); cleared by push_light
     uint64_t* nx;           // next round's new words (fresh)
     uint64_t* send;         // dense remote staging (n_global * W) or null
+    // near-empty sparse push rounds of a vertex block (one word per peer): a remote delivery appends a record
+    // {peer, word} to its destination block's slice of rec_out (rec_stride records each: the record push's
+    // buffer, sized by the block's edges into each block), its place from rec_cnt[q] (one atomic per wave and
+    // destination); no staging, no compaction
+    uint64_t* rec_out;
+    unsigned long long* rec_cnt;
+    uint64_t rec_stride;
+    const uint64_t* part;          // the blocks' bounds (world + 1)
+    uint32_t world;
     unsigned long long* smark;  // sparse push rounds: 1 bit per 64 global peers whose staging words this round
                                 // wrote (the compaction reads only those tiles); null otherwise
     uint8_t* miss;          // per-edge miss counters

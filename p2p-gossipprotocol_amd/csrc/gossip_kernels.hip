@@ -126,6 +126,30 @@ __device__ __forceinline__ void mark_tile(const RoundArgs& a, uint64_t lv, Acc& 
     }
 }
 
+// Appends {c, m} to destination block q's records (RoundArgs.rec_out) for every lane with want set: one
+// counter atomic per wave and destination block (one word per peer)
+__device__ __forceinline__ void append_records(const RoundArgs& a, bool want, uint32_t c, uint64_t m) {
+    const int lane = threadIdx.x & 63;
+    uint32_t q = 0;
+    if (want)
+        while (q + 1 < a.world && a.part[q + 1] <= c) ++q;
+    for (unsigned long long todo = __ballot(want); todo;) {  // wave-uniform
+        const int lead = __builtin_ctzll(todo);
+        const uint32_t qq = (uint32_t)__shfl((int)q, lead);
+        const unsigned long long grp = __ballot(want && q == qq);
+        unsigned long long base = 0;
+        if (lane == lead) base = atomicAdd(a.rec_cnt + qq, (unsigned long long)__popcll(grp));
+        base = ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(base >> 32), lead) << 32) |
+               (uint32_t)__shfl((int)(uint32_t)base, lead);
+        if (want && q == qq) {
+            uint64_t* rec = a.rec_out + (qq * a.rec_stride + base + (uint64_t)__popcll(grp & ((1ull << lane) - 1))) * 2;
+            rec[0] = c;
+            rec[1] = m;
+        }
+        todo &= ~grp;
+    }
+}
+
 // One delivery to global peer c (bit 31: masked edge): liveness, remote
 // staging or the local test-and-set.
 template <int W, bool CA, bool RM>
@@ -139,6 +163,14 @@ __device__ __forceinline__ void deliver(const RoundArgs& a, uint32_t c, const ui
     }
     acc.deliv += pc;  // sentTo.insert (peer.cpp:314)
     if (RM && (c < a.begin || c >= a.end)) {
+        if (W == 1 && a.rec_out) {  // a record of its own (deliver_batch appends them a wave at a time)
+            uint32_t q = 0;
+            while (q + 1 < a.world && a.part[q + 1] <= c) ++q;
+            uint64_t* rec = a.rec_out + (q * a.rec_stride + atomicAdd(a.rec_cnt + q, 1ull)) * 2;
+            rec[0] = c;
+            rec[1] = m[0];
+            return;
+        }
         unsigned long long* dst = reinterpret_cast<unsigned long long*>(a.send) + (uint64_t)c * W;
         bool wrote = false;
 #pragma unroll
@@ -168,10 +200,11 @@ __device__ __forceinline__ void deliver(const RoundArgs& a, uint32_t c, const ui
 template <int W, bool CA, bool RM, int kU>
 __device__ __forceinline__ void deliver_batch(const RoundArgs& a, const uint32_t (&c)[kU],
                                               const uint64_t (&m)[kU][W], const uint32_t (&pc)[kU], Acc& acc) {
-    bool loc[kU];
+    bool loc[kU], rem[kU];
     uint32_t al[kU];
 #pragma unroll
     for (int j = 0; j < kU; ++j) {
+        rem[j] = false;
         const bool ok = !(c[j] & kMaskedEdge);  // invalid lanes carry a masked id
         acc.trav += ok;
         loc[j] = ok;
@@ -185,7 +218,10 @@ __device__ __forceinline__ void deliver_batch(const RoundArgs& a, const uint32_t
         } else if (loc[j]) {
             acc.deliv += pc[j];  // sentTo.insert (peer.cpp:314)
         }
-        if (RM && loc[j] && (c[j] < a.begin || c[j] >= a.end)) {
+        if (RM && loc[j] && (c[j] < a.begin || c[j] >= a.end) && W == 1 && a.rec_out) {
+            rem[j] = true;  // a record, appended below
+            loc[j] = false;
+        } else if (RM && loc[j] && (c[j] < a.begin || c[j] >= a.end)) {
             unsigned long long* dst = reinterpret_cast<unsigned long long*>(a.send) + (uint64_t)c[j] * W;
             bool wrote = false;
 #pragma unroll
@@ -200,6 +236,10 @@ __device__ __forceinline__ void deliver_batch(const RoundArgs& a, const uint32_t
             if (wrote) mark_send(a, c[j]);
             loc[j] = false;
         }
+    }
+    if (RM && W == 1 && a.rec_out) {
+#pragma unroll
+        for (int j = 0; j < kU; ++j) append_records(a, rem[j], c[j], m[j][0]);
     }
     // unconditional loads (lanes without a delivery read word 0): a load under a branch gets its own wait
     uint64_t cur[kU][W];

@@ -76,7 +76,7 @@ def test_group_dense_exchange_forms_equal_oracle(oracle, idx, n, P, gather):
     assert again == stats
 
 
-@pytest.mark.parametrize("px", ["all", "off"])
+@pytest.mark.parametrize("px", ["all", "off", "append"])
 @pytest.mark.parametrize("P", [2, 3, 4])
 @pytest.mark.parametrize("idx,n", [(3, 100_003), (5, 1 << 15), (2, 40_000)])
 def test_group_record_push_equals_oracle(oracle, idx, n, P, px):
@@ -84,13 +84,16 @@ def test_group_record_push_equals_oracle(oracle, idx, n, P, px):
     (gossip_blocked.hip build_px / k_px_pack: level 1 of a blocked round with
     the destination blocks as its bins, the own block delivered at once, the
     records packed per block and exchanged as {peer, word}) -- forced for
-    every sparse round ("all": px_permille 0), and the staging push with its
-    compaction ("off") -- both give the oracle's run, with dead peers and
-    masked edges (config 5) and short last blocks."""
+    every sparse round ("all": px_permille 0), the push appending its remote
+    deliveries as records itself, one counter atomic per wave and destination
+    ("append": every sparse round under the record push's frontier), and the
+    staging push with its compaction ("off") -- all give the oracle's run,
+    with dead peers and masked edges (config 5) and short last blocks."""
     w = config(idx, n, pick=oracle.pick_origins)
     rp, col = oracle.gen_workload(w)
     ref = oracle.simulate_workload(w, rp, col)
-    stats, seen, reps, again = _run_group(w, [0] * P, tuning={"px_permille": 0 if px == "all" else -1})
+    pm = {"all": 0, "off": -1, "append": 1 << 30}[px]
+    stats, seen, reps, again = _run_group(w, [0] * P, tuning={"px_permille": pm})
     assert stats == ref["stats"]
     assert np.array_equal(seen, ref["seen"])
     assert np.array_equal(reps, ref["reports"])
