@@ -244,10 +244,11 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
     const uint64_t n_tiles = (n_local + 63) / 64;
     // bigger bins -> longer slot runs per (source chunk, bin) in the scatter
     // (measured: 16 K-word bins 86 ms/step at config 4, 8 K-word bins 101 ms)
-    // ... and at least one bin per CU on small overlays (config 2, 2^20 peers: 57 bins of 18 K left most CUs
-    // idle in the apply; 256 bins of 4 K: kernels 9.2-9.3 -> 7.9 ms per step; config 3 keeps whole bins:
-    // 4 K bins cost it 0.5 ms)
-    uint32_t bin_words = (uint32_t)std::min<uint64_t>(kBinWords, std::max<uint64_t>(2048, n_local * Wp / 256 / 512 * 512));
+    // ... and several bins per CU on small overlays (config 2, 2^20 peers: 57 bins of 18 K left most CUs
+    // idle in the apply; 256 bins of 4 K: kernels 9.2-9.3 -> 7.9 ms per step; round 5: 512 bins of 2 K with
+    // the small-bin apply, eight workgroups per CU, 5.06 -> 4.68 ms per step, profiles/r05/ab/r05b/sweep_c2.txt;
+    // config 3 keeps whole bins: 4 K bins cost it 0.5 ms)
+    uint32_t bin_words = (uint32_t)std::min<uint64_t>(kBinWords, std::max<uint64_t>(2048, n_local * Wp / 512 / 512 * 512));
     if (bin_words_req) bin_words = std::max<uint32_t>(512, std::min<uint32_t>(kBinWords, bin_words_req / 512 * 512));
     const uint32_t max_peers = bin_words / Wp;  // a multiple of 64 for Wp <= 8
     const uint64_t slot_cap = kBinSlotCap * bin_words / kBinWords;
