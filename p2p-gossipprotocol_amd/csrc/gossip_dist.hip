@@ -166,7 +166,13 @@ __global__ __launch_bounds__(256) void k_tile_pack(const uint64_t* words, uint64
 // every other block's words back into the gather buffer (zeros where the bitmap has none)
 __global__ __launch_bounds__(256) void k_tile_expand(uint64_t* gather, const uint64_t* bits, const uint64_t* pos,
                                                      const uint64_t* pk, uint32_t X, uint32_t world, uint32_t own,
-                                                     const uint64_t* part, const uint64_t* toff) {
+                                                     const uint64_t* part_g, const uint64_t* toff_g) {
+    __shared__ uint64_t part[kMaxWorld + 1], toff[kMaxWorld + 1];  // (a dependent global load per lookup step)
+    for (uint32_t i = threadIdx.x; i <= world; i += blockDim.x) {
+        part[i] = part_g[i];
+        toff[i] = toff_g[i];
+    }
+    __syncthreads();
     const int lane = threadIdx.x & 63;
     const uint64_t tiles = toff[world];
     for (uint64_t T = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; T < tiles;

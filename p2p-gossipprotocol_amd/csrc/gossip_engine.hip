@@ -2393,6 +2393,7 @@ gossip_status gossip_set_exchange(gossip_ctx* c, void* send, void* recv, uint32_
         found |= (pb[p] == c->begin && pb[p + 1] == c->end);
     }
     if (pb[0] != 0 || pb[world] != c->n || !found) return fail(GOSSIP_EINVAL, "partition table does not match ctx");
+    if (world > gossip::kMaxWorld) return fail(GOSSIP_EINVAL, "at most 64 blocks");
     c->send = (uint64_t*)send;
     c->recv = (const uint64_t*)recv;
     c->world = world;

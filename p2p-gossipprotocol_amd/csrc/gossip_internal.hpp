@@ -72,6 +72,7 @@ constexpr uint16_t kRunStart = 0x8000u;        // cb_src flag; chunk-local sourc
 static_assert(kBinChunkWords < kRunStart, "chunk-local sources fit 15 bits");
 
 constexpr uint32_t kMaxStages = 16;   // pipelined dense exchange: source segments delivered in at most this many stages
+constexpr uint32_t kMaxWorld = 64;    // blocks of a partitioned run (their bounds are staged in LDS by the exchange kernels)
 
 struct Bin {
     uint32_t v0, v1;  // destination peers [v0, v1) (local ids, whole 64-peer tiles)

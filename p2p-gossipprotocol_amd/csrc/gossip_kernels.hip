@@ -2441,8 +2441,14 @@ __device__ __forceinline__ uint32_t send_block(const uint64_t* toff, uint32_t wo
 }
 
 template <int W>
-__global__ __launch_bounds__(kBlock) void k_send_bits(RoundArgs a, const uint64_t* part, const uint64_t* toff,
+__global__ __launch_bounds__(kBlock) void k_send_bits(RoundArgs a, const uint64_t* part_g, const uint64_t* toff_g,
                                                       uint32_t world, uint64_t* bits) {
+    __shared__ uint64_t part[kMaxWorld + 1], toff[kMaxWorld + 1];  // (a dependent global load per lookup step)
+    for (uint32_t i = threadIdx.x; i <= world; i += kBlock) {
+        part[i] = part_g[i];
+        toff[i] = toff_g[i];
+    }
+    __syncthreads();
     // a wave per 64 tiles: lane l tests tile T0 + l against the round's marks (its peers span at most two
     // marked 64-peer tiles), unmarked tiles get a zero bitmap word, and the wave reads the staging words of
     // the marked ones in turn (a sparse round's send buffer is 2 GB at config 4; the marked tiles are few)
@@ -2479,9 +2485,15 @@ __global__ __launch_bounds__(kBlock) void k_send_bits(RoundArgs a, const uint64_
 }
 
 template <int W>
-__global__ __launch_bounds__(kBlock) void k_send_pack(RoundArgs a, const uint64_t* part, const uint64_t* toff,
+__global__ __launch_bounds__(kBlock) void k_send_pack(RoundArgs a, const uint64_t* part_g, const uint64_t* toff_g,
                                                       uint32_t world, uint64_t stride, const uint64_t* bits,
                                                       const uint64_t* pos, unsigned long long* counts, uint64_t* seg) {
+    __shared__ uint64_t part[kMaxWorld + 1], toff[kMaxWorld + 1];
+    for (uint32_t i = threadIdx.x; i <= world; i += kBlock) {
+        part[i] = part_g[i];
+        toff[i] = toff_g[i];
+    }
+    __syncthreads();
     const int lane = threadIdx.x & 63;
     const uint64_t tiles = toff[world];
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
