@@ -506,6 +506,9 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
             const uint64_t mean = std::max<uint64_t>(1024, upos / std::max<uint64_t>(1, n_chunks));
             for (uint64_t c = 0; c < n_chunks; ++c) {
                 const uint64_t len = cbeg[c + 1] - cbeg[c];
+                // a chunk of the last segment that starts past the ids has no sources (n = 100000 in segments
+                // of 1600 and chunks of 1024: chunk 125 starts at 100224; its staging read past the gather buffer)
+                if (chunk_vb(c, st.seg, st.cps, chunk) >= n_global) continue;
                 const uint64_t k = len > kHubFactor * mean ? (len + mean - 1) / mean : 1;
                 for (uint64_t j = 0; j < k; ++j)
                     units.push_back(

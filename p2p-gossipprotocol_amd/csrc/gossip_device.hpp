@@ -18,8 +18,10 @@ __device__ __forceinline__ bool bit_alive(const uint32_t* bits, uint32_t v) { re
 __device__ __forceinline__ uint64_t bin_chunk_vb(const BinArgs& b, uint64_t c) {
     return (c / b.cps) * b.seg + (c % b.cps) * b.chunk;
 }
+// (a chunk of the last segment can start past n: empty, not negative)
 __device__ __forceinline__ uint64_t bin_chunk_ve(const BinArgs& b, uint64_t c, uint64_t n) {
-    return min(min(bin_chunk_vb(b, c) + b.chunk, (c / b.cps + 1) * b.seg), n);
+    const uint64_t vb = bin_chunk_vb(b, c);
+    return max(vb, min(min(vb + b.chunk, (c / b.cps + 1) * b.seg), n));
 }
 
 // the bits a peer can still learn: messages injected so far (at P = 1 the ones whose origin was alive to

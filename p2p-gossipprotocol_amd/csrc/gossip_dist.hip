@@ -40,6 +40,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -758,6 +760,24 @@ gossip_status all_reduce_stats(DistDriver* d, uint64_t* g) {
     return GOSSIP_OK;
 }
 
+// GOSSIP_SYNC_DEBUG (diagnostics): each exchange waited for, a device fault named on stderr
+const bool kDistSyncDebug = std::getenv("GOSSIP_SYNC_DEBUG") != nullptr;
+
+gossip_status dbg_sync(DistDriver* d, const char* what, gossip_status s) {
+    if (s || !kDistSyncDebug) return s;
+    for (auto& r : d->ranks) {
+        hipSetDevice(r.device);
+        hipError_t e = hipStreamSynchronize(r.stream);
+        if (e == hipSuccess && r.xs) e = hipStreamSynchronize(r.xs);
+        if (e != hipSuccess) {
+            std::fprintf(stderr, "[gossip] exchange %s (round %zu, rank %u): %s\n", what, d->modes.size(), r.rank,
+                         hipGetErrorString(e));
+            return set_error(GOSSIP_EHIP, std::string("exchange ") + what + ": " + hipGetErrorString(e));
+        }
+    }
+    return GOSSIP_OK;
+}
+
 // One round on every local rank, lockstep phases.
 gossip_status dist_step(DistDriver* d, gossip_round_stats* out) {
     if (d->finished) return set_error(GOSSIP_ESTATE, "run finished: call gossip_reset");
@@ -781,7 +801,9 @@ gossip_status dist_step(DistDriver* d, gossip_round_stats* out) {
         // streamed bin layout and asks for the same number of stages)
         uint32_t S = mode == GOSSIP_MODE_BIN && !compact && d->world > 1 ? ctx_stages(d->ranks[0].ctx) : 1u;
         for (auto& r : d->ranks) S = ctx_stages(r.ctx) == S ? S : 1u;
-        if ((s = compact ? compact_gather(d) : S > 1 ? staged_gather(d, S) : all_gather(d))) return s;
+        if ((s = dbg_sync(d, compact ? "compact_gather" : S > 1 ? "staged_gather" : "all_gather",
+                          compact ? compact_gather(d) : S > 1 ? staged_gather(d, S) : all_gather(d))))
+            return s;
         for (auto& r : d->ranks)
             if ((s = gossip_round_compute(r.ctx))) return s;
         for (auto& r : d->ranks)
@@ -790,14 +812,14 @@ gossip_status dist_step(DistDriver* d, gossip_round_stats* out) {
         for (auto& r : d->ranks)
             if ((s = gossip_round_compute(r.ctx))) return s;
         std::vector<uint64_t> total_in;
-        if ((s = exchange_records(d, total_in))) return s;
+        if ((s = dbg_sync(d, "records", exchange_records(d, total_in)))) return s;
         for (size_t i = 0; i < d->ranks.size(); ++i)
             if ((s = gossip_round_finish_sparse(d->ranks[i].ctx, d->ranks[i].rec_in, total_in[i], &d->ranks[i].local)))
                 return s;
     } else {
         for (auto& r : d->ranks)
             if ((s = gossip_round_compute(r.ctx))) return s;
-        if ((s = all_to_all(d))) return s;
+        if ((s = dbg_sync(d, "all_to_all", all_to_all(d)))) return s;
         for (auto& r : d->ranks)
             if ((s = gossip_round_finish(r.ctx, &r.local))) return s;
     }

@@ -392,16 +392,30 @@ hipError_t queue_zero(gossip_ctx* c, void* p, uint64_t bytes, void* save = nullp
     return hipSuccess;
 }
 
+// GOSSIP_SYNC_DEBUG (diagnostics): every launch waited for, a device fault named by its kernel on stderr
+const bool kSyncDebug = std::getenv("GOSSIP_SYNC_DEBUG") != nullptr;
+
+hipError_t sync_debug(gossip_ctx* c, const char* name) {
+    const hipError_t e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess)
+        std::fprintf(stderr, "[gossip] %s (round %u, block at %llu): %s\n", name, c->round,
+                     (unsigned long long)c->begin, hipGetErrorString(e));
+    return e;
+}
+
 template <class F>
 hipError_t timed(gossip_ctx* c, const char* name, F&& launch) {
     if (hipError_t e = flush_zero(c)) return e;
-    if (!c->timing) return launch();
+    if (!c->timing) {
+        const hipError_t e = launch();
+        return e == hipSuccess && kSyncDebug ? sync_debug(c, name) : e;
+    }
     hipEvent_t a = take_event(c), b = take_event(c);
     hipEventRecord(a, c->stream);
     hipError_t e = launch();
     hipEventRecord(b, c->stream);
     c->timers[name].pending.emplace_back(a, b);
-    return e;
+    return e == hipSuccess && kSyncDebug ? sync_debug(c, name) : e;
 }
 
 }  // namespace
@@ -1198,8 +1212,10 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
     // Below that frontier the push appends its remote deliveries as records to the same buffer (one counter
     // atomic per wave and destination block): the staging buffer's compaction swept every tile of every
     // destination block whatever the round's size (config 4 at P = 8: ≈ 90 us per part in near-empty rounds)
+    // (only under the library's own driver, which reads the records where ctx_send_records says: a caller of
+    // the phase API takes them from its gossip_set_sparse buffer)
     c->cur_px = c->cur_arec = false;
-    if (c->cur_sparse && c->Wp == 1 && c->px_pm >= 0 && !c->cfg.extra_cap && c->symmetric && c->world <= kPbCoarseMax) {
+    if (c->dist && c->cur_sparse && c->Wp == 1 && c->px_pm >= 0 && !c->cfg.extra_cap && c->symmetric && c->world <= kPbCoarseMax) {
         if (c->px_state == 0) {
             std::string err;
             const hipError_t e =

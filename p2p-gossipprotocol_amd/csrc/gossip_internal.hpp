@@ -519,8 +519,8 @@ inline uint64_t bin_segment(uint64_t n_global) { return ((n_global + 63) / 64 + 
 // host side of BinArgs' chunk geometry
 inline uint64_t chunk_vb(uint64_t c, uint64_t seg, uint64_t cps, uint64_t chunk) { return (c / cps) * seg + (c % cps) * chunk; }
 inline uint64_t chunk_ve(uint64_t c, uint64_t seg, uint64_t cps, uint64_t chunk, uint64_t n) {
-    const uint64_t e = std::min(chunk_vb(c, seg, cps, chunk) + chunk, (c / cps + 1) * seg);
-    return std::min(e, n);
+    const uint64_t vb = chunk_vb(c, seg, cps, chunk);
+    return std::max(vb, std::min(std::min(vb + chunk, (c / cps + 1) * seg), n));  // (empty past n)
 }
 // the staged unit order for S stages of a vertex block [begin, end) (host side; BinState.stage_*)
 hipError_t build_stage_units(BinState* b, uint32_t S, uint64_t begin, uint64_t end, uint64_t n_global);
