@@ -263,6 +263,11 @@ gossip_status gossip_comm_modes(gossip_ctx* ctx, int32_t* modes, uint32_t cap, u
 typedef struct gossip_group gossip_group;
 gossip_status gossip_group_create(const gossip_config* cfg, uint32_t n_parts, const int32_t* devices,
                                   gossip_group** out);
+/* The same with the caller's partition: begins[0] = 0 < begins[1] < ... < begins[n_parts] = n_peers, every
+ * block starting on a whole 64-peer tile (gossip_group_create: gossip_partition_edges, or gossip_partition
+ * under GOSSIP_FLAG_UNIFORM_PARTITION). */
+gossip_status gossip_group_create_parts(const gossip_config* cfg, uint32_t n_parts, const int32_t* devices,
+                                        const uint64_t* begins, gossip_group** out);
 void gossip_group_destroy(gossip_group* g);
 gossip_status gossip_group_part(gossip_group* g, uint32_t p, gossip_ctx** ctx);
 gossip_status gossip_group_build_graph(gossip_group* g);

@@ -239,7 +239,7 @@ void free_bins(BinState* b) {
 
 hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local, uint64_t n_global, uint64_t m,
                       uint32_t heavy, uint32_t Wp, bool stream, uint32_t bin_words_req, uint32_t chunk_words_req,
-                      uint64_t seg, hipStream_t s, BinState* out, std::string* err) {
+                      uint64_t seg, uint64_t min_units, hipStream_t s, BinState* out, std::string* err) {
     hipError_t rc = hipSuccess;
     const uint64_t n_tiles = (n_local + 63) / 64;
     // bigger bins -> longer slot runs per (source chunk, bin) in the scatter
@@ -504,12 +504,17 @@ hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local,
         const uint64_t members = kScatterGrid / 8;
         {
             const uint64_t mean = std::max<uint64_t>(1024, upos / std::max<uint64_t>(1, n_chunks));
+            // min_units ("scatter_units"): chunks split into units of at most upos / min_units entries, so a
+            // small overlay's few chunks still spread over the grid (config 2: 410 chunks of about 18 K entries
+            // for 256 workgroups, each unit a chain of dependent round trips)
+            const uint64_t cap = min_units ? std::max<uint64_t>(256, (upos + min_units - 1) / min_units) : ~0ull;
             for (uint64_t c = 0; c < n_chunks; ++c) {
                 const uint64_t len = cbeg[c + 1] - cbeg[c];
                 // a chunk of the last segment that starts past the ids has no sources (n = 100000 in segments
                 // of 1600 and chunks of 1024: chunk 125 starts at 100224; its staging read past the gather buffer)
                 if (chunk_vb(c, st.seg, st.cps, chunk) >= n_global) continue;
-                const uint64_t k = len > kHubFactor * mean ? (len + mean - 1) / mean : 1;
+                uint64_t k = len > kHubFactor * mean ? (len + mean - 1) / mean : 1;
+                if (len > cap) k = std::max<uint64_t>(k, (len + cap - 1) / cap);
                 for (uint64_t j = 0; j < k; ++j)
                     units.push_back(
                         BinUnit{(uint32_t)c, j == 0 ? 1u : 0u, cbeg[c] + len * j / k, cbeg[c] + len * (j + 1) / k});

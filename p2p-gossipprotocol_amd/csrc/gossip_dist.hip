@@ -1123,6 +1123,24 @@ gossip_status gossip_group_create(const gossip_config* cfg, uint32_t n_parts, co
                                   gossip_group** out) {
     if (!cfg || !devices || !out || n_parts < 1) return set_error(GOSSIP_EINVAL, "bad argument");
     *out = nullptr;
+    std::vector<uint64_t> part(n_parts + 1);
+    gossip_status s = cfg->flags & GOSSIP_FLAG_UNIFORM_PARTITION ? gossip_partition(cfg->n_peers, n_parts, part.data())
+                                                                 : gossip_partition_edges(cfg, n_parts, part.data());
+    if (s) return s;
+    return gossip_group_create_parts(cfg, n_parts, devices, part.data(), out);
+}
+
+gossip_status gossip_group_create_parts(const gossip_config* cfg, uint32_t n_parts, const int32_t* devices,
+                                        const uint64_t* begins, gossip_group** out) {
+    if (!cfg || !devices || !out || !begins || n_parts < 1) return set_error(GOSSIP_EINVAL, "bad argument");
+    *out = nullptr;
+    if (begins[0] != 0 || begins[n_parts] != cfg->n_peers)
+        return set_error(GOSSIP_EINVAL, "part begins must run from 0 to n_peers");
+    for (uint32_t q = 0; q < n_parts; ++q)
+        if (begins[q + 1] <= begins[q] || begins[q] % 64)
+            return set_error(GOSSIP_EINVAL, "parts must be non-empty and start on whole 64-peer tiles");
+    const std::vector<uint64_t> part(begins, begins + n_parts + 1);
+    gossip_status s = GOSSIP_OK;
     if (cfg->rejoin_threshold && n_parts > 1) return set_error(GOSSIP_EINVAL, "rejoin_threshold needs a single partition");
     bool same = true, distinct = true;
     for (uint32_t p = 0; p < n_parts; ++p)
@@ -1132,10 +1150,6 @@ gossip_status gossip_group_create(const gossip_config* cfg, uint32_t n_parts, co
         }
     same &= devices[0] == devices[n_parts - 1];
     if (!same && !distinct) return set_error(GOSSIP_EINVAL, "devices must be all distinct or all the same");
-    std::vector<uint64_t> part(n_parts + 1);
-    gossip_status s = cfg->flags & GOSSIP_FLAG_UNIFORM_PARTITION ? gossip_partition(cfg->n_peers, n_parts, part.data())
-                                                                 : gossip_partition_edges(cfg, n_parts, part.data());
-    if (s) return s;
     gossip_group* g = new gossip_group();
     g->n = cfg->n_peers;
     g->W = (cfg->n_msgs + 63) / 64;

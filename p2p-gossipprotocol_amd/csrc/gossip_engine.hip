@@ -168,7 +168,11 @@ struct gossip_ctx {
     uint64_t* d_toff = nullptr;  // the 64-peer tiles of the blocks before each block (device; the compaction's)
     uint64_t n_tiles_all = 0;    // ... all of them
     uint64_t blk_stride = 0;     // the largest block: a destination's staged records in the compaction's output
-    int32_t px_pm = 2;           // "px_permille": record push from this frontier per-mille of the block (-1: never)
+    // "px_per100k" ("px_permille": x 100): record push from this frontier, per 100 000 peers of the block (-1:
+    // never).  5: config 4 as 8 parts pushes round 2 (6.7 K frontier peers per block, 3.4 M traversals, most
+    // from hubs) as records, 1.3 against 3.7 ms of kernels summed with appended records, whose counters every
+    // wave of the block hits; rounds 0, 1, 10 and 11 (tens of frontier peers) append (0.4 against 0.7 ms)
+    int32_t px_pm = 5;
     bool cur_px = false;         // the round in flight pushes records (level 1)
     bool cur_arec = false;       // ... or appends them from the push (a near-empty frontier)
     // late pull rounds over needy lists (k_pull_list)
@@ -233,6 +237,9 @@ struct gossip_ctx {
     bool cur_clear_all = false;  // (the round in flight does)
     bool scatter_direct = false; // "scatter_direct": a vertex block's scatter reads other blocks' words directly
     bool scatter_small = false;  // "scatter_small": the streamed scatter's small-chunk instance where chunks fit it
+    uint32_t scatter_units = 0;  // "scatter_units": at least this many scatter units (chunks split; 0: hubs only)
+    bool split_direct = false;   // "scatter_split_direct": a split chunk's later units read words from nw_src
+    bool apply_wide = false;     // "apply_wide": small bins applied by 16-wave workgroups
     unsigned long long* d_probe = nullptr;  // "apply_probe": the streamed apply's phase clocks (kProbeN slots)
     bool apply_persist = true;   // "apply_persist": the streamed apply as 256 workgroups taking bins from
                                  // per-XCD counters (d_work), not one workgroup per bin
@@ -797,6 +804,8 @@ BinArgs bin_args(const gossip_ctx* c, bool noskip, uint32_t src_side) {
     b.apply_pipe = c->apply_pipe;
     b.direct = c->scatter_direct && c->gather ? 1u : 0u;
     b.small = c->scatter_small ? 1u : 0u;
+    b.split_direct = c->split_direct ? 1u : 0u;
+    b.wide = c->apply_wide ? 1u : 0u;
     b.needy_check = 1u;
     b.src_stats = src_side;
     b.work = c->apply_persist && c->bin_stream ? c->d_work : nullptr;
@@ -899,7 +908,8 @@ gossip_status prepare_bins(gossip_ctx* c) {
         // a vertex block cuts the source ids into segments (the staged dense exchange delivers whole ones)
         const uint64_t seg = c->n_local != c->n ? bin_segment(c->n) : 0;
         const hipError_t e = build_bins(c->rp, c->col, c->n_local, c->n, c->n_edges, c->heavy, c->Wp, c->bin_stream,
-                                        c->bin_words_req, c->bin_chunk_req, seg, c->stream, &c->bins, &err);
+                                        c->bin_words_req, c->bin_chunk_req, seg, c->scatter_units, c->stream, &c->bins,
+                                        &err);
         if (e == hipSuccess) {
             c->bins_ready = true;
             if (gossip_status ts = tune_val(c)) return ts;
@@ -1231,7 +1241,7 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
                 return fail(GOSSIP_EHIP, "record push: " + err);
             }
         }
-        const bool wide = (c->frontier_est + cnt) * 1000 >= c->n_local * (uint64_t)c->px_pm;
+        const bool wide = (c->frontier_est + cnt) * 100000 >= c->n_local * (uint64_t)c->px_pm;
         c->cur_px = c->px_state == 1 && wide;
         c->cur_arec = c->px_state == 1 && !wide;
     }
@@ -1974,6 +1984,9 @@ gossip_status gossip_set_tuning(gossip_ctx* c, const char* key, int64_t value) {
     else if (k == "bin_needy_skip") c->needy_skip = value != 0;
     else if (k == "replay") c->replay_req = value != 0;
     else if (k == "scatter_direct") c->scatter_direct = value != 0;
+    else if (k == "scatter_units") c->scatter_units = u;
+    else if (k == "scatter_split_direct") c->split_direct = value != 0;
+    else if (k == "apply_wide") c->apply_wide = value != 0;
     else if (k == "scatter_small") c->scatter_small = value != 0;
     else if (k == "blocked_clear_all") c->pb_clear_all = value != 0;
     else if (k == "apply_pipe") {
@@ -1993,7 +2006,8 @@ gossip_status gossip_set_tuning(gossip_ctx* c, const char* key, int64_t value) {
         }
     }
     else if (k == "gather_permille") c->gather_pm = value < 0 ? kGatherPermille : u;
-    else if (k == "px_permille") c->px_pm = value < 0 ? -1 : (int32_t)u;
+    else if (k == "px_permille") c->px_pm = value < 0 ? -1 : (int32_t)std::min<int64_t>(value * 100, 1 << 30);
+    else if (k == "px_per100k") c->px_pm = value < 0 ? -1 : (int32_t)std::min<int64_t>(value, 1 << 30);
     else if (k == "exchange_stages") {
         if (value < 1 || value > (int64_t)kMaxStages) return fail(GOSSIP_EINVAL, "exchange_stages must be 1..16");
         c->stages_req = (uint32_t)value;

@@ -120,6 +120,9 @@ struct BinArgs {
                                   // workgroups per CU) when the chunks fit it ("scatter_small")
     uint32_t direct;              // streamed scatter of a vertex block: chunks without owned sources read their
                                   // words from the gather buffer instead of staging them ("scatter_direct")
+    uint32_t split_direct;        // streamed scatter: the units of a split chunk after its first read their words
+                                  // from nw_src instead of staging the chunk again ("scatter_split_direct")
+    uint32_t wide;                // streamed apply of small bins: 16-wave workgroups ("apply_wide")
     uint32_t needy_check;         // 1: the apply first tests whether any peer of the bin can still learn
                                   // something (a pass over the bin's seen words) and skips its slots if not;
                                   // 0 on rounds with more than one missing pair per peer, where every bin is
@@ -512,7 +515,7 @@ hipError_t build_powerlaw_device(uint64_t n_global, uint64_t begin, uint64_t end
 // seg: source segment size (0: one segment; a vertex block of a partitioned run passes bin_segment(n_global))
 hipError_t build_bins(const uint64_t* rp, const uint32_t* col, uint64_t n_local, uint64_t n_global, uint64_t n_edges,
                       uint32_t heavy, uint32_t Wp, bool stream, uint32_t bin_words, uint32_t chunk_words, uint64_t seg,
-                      hipStream_t s, BinState* out, std::string* err);
+                      uint64_t min_units, hipStream_t s, BinState* out, std::string* err);
 void free_bins(BinState* b);
 // a vertex block's source segments: 64 of them over the global ids (whole 64-peer tiles)
 inline uint64_t bin_segment(uint64_t n_global) { return ((n_global + 63) / 64 + 63) / 64 * 64; }

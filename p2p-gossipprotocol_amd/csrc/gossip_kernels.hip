@@ -1445,7 +1445,9 @@ __global__ __launch_bounds__(kSB) void k_bin_stream(RoundArgs a, BinArgs b, uint
         // its few entries (1/P of a whole overlay's) read their words straight from the gather buffer (the
         // chunk's 144 KB stay in L2 after the first touch) instead of paying the chunk's staging
         const uint64_t vb = bin_chunk_vb(b, un.c);
-        const bool direct = b.direct && !(vb < a.end && bin_chunk_ve(b, un.c, a.n_src) > a.begin);  // block-uniform
+        // (b.split_direct: a split chunk's later units, whose first unit stages the chunk and books its stats)
+        const bool direct = (b.direct && !(vb < a.end && bin_chunk_ve(b, un.c, a.n_src) > a.begin)) ||
+                            (b.split_direct && !un.first);  // block-uniform
         const uint64_t* src = a.nw_src + vb * W;
         if (!direct) {
             scatter_stage<W, COV, kCW, kSB>(a, b, un, wd, slice, live_s, cov_s, acc);
@@ -2870,7 +2872,10 @@ hipError_t launch_bin_apply(const RoundArgs& a, const BinArgs& b, uint32_t W_, h
         const uint64_t rows = (b.n_bins + kApplyRow - 1) / kApplyRow;
         unsigned sgrid = (unsigned)((rows + 7) / 8 * 8 * kApplyRow);
         if (b.work) {  // persistent: the resident blocks; b.work was zeroed before the round's scatter
-            const unsigned resident = b.bin_words > kBinWords / 2 ? 256u : b.bin_words > kSmallBinWords ? 512u : 2048u;
+            const bool wide = b.wide && b.bin_words <= kSmallBinWords;
+            const unsigned resident = b.bin_words > kBinWords / 2 ? 256u
+                                      : b.bin_words > kSmallBinWords || wide ? 512u
+                                                                           : 2048u;
             sgrid = std::min(sgrid, resident);
         }
         if (b.bin_words > kBinWords / 2 && wp_of(W_) == 1) {  // one word: the pipeline shapes (A/B), the probe
@@ -2887,6 +2892,11 @@ hipError_t launch_bin_apply(const RoundArgs& a, const BinArgs& b, uint32_t W_, h
                 hipLaunchKernelGGL((k_bin_apply_runs<1, kBinWords, 1024, 3>), dim3(sgrid), dim3(1024), 0, s, a, b, wd);
         } else if (b.bin_words > kBinWords / 2) {
             GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_apply_runs<W, kBinWords, 1024>),
+                                                           dim3(sgrid), dim3(1024), 0, s, a, b, wd));
+        } else if (b.bin_words <= kSmallBinWords && b.wide) {
+            // 16 KB accumulators, 16 waves each: a bin's slots in a quarter of the iterations (small overlays,
+            // fewer bins than the chip holds workgroups)
+            GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_apply_runs<W, kSmallBinWords, 1024>),
                                                            dim3(sgrid), dim3(1024), 0, s, a, b, wd));
         } else if (b.bin_words <= kSmallBinWords) {
             // 16 KB accumulators: eight 4-wave workgroups per CU (small bins of small overlays)

@@ -151,6 +151,8 @@ def lib() -> C.CDLL:
         "gossip_comm_finalize": (i32, [P, C.POINTER(RoundStats), u32, C.POINTER(DeadReport), u64, pu64]),
         "gossip_comm_modes": (i32, [P, C.POINTER(C.c_int32), u32, pu32]),
         "gossip_group_create": (i32, [C.POINTER(GossipConfig), u32, C.POINTER(C.c_int32), C.POINTER(P)]),
+        "gossip_group_create_parts": (i32, [C.POINTER(GossipConfig), u32, C.POINTER(C.c_int32),
+                                            C.POINTER(C.c_uint64), C.POINTER(P)]),
         "gossip_group_destroy": (None, [P]),
         "gossip_group_part": (i32, [P, u32, C.POINTER(P)]),
         "gossip_group_build_graph": (i32, [P]),

@@ -340,14 +340,20 @@ class Group:
     """One process driving several vertex blocks (gossip_group_*): one part
     per entry of `devices` (distinct GPUs: RCCL communicators from
     ncclCommInitAll; all the same GPU: device-copy exchange).  Takes the
-    Engine's keyword arguments (except part/device)."""
+    Engine's keyword arguments (except part/device); `begins` (n_parts + 1
+    block bounds) replaces the default partition (gossip_group_create_parts)."""
 
-    def __init__(self, n_peers: int, n_msgs: int, devices, tuning: dict | None = None, **kw):
+    def __init__(self, n_peers: int, n_msgs: int, devices, tuning: dict | None = None, begins=None, **kw):
         self._L = _abi.lib()
         cfg = make_config(n_peers, n_msgs, **kw)
         devs = (C.c_int32 * len(devices))(*devices)
         g = C.c_void_p()
-        check(self._L.gossip_group_create(C.byref(cfg), len(devices), devs, C.byref(g)), "gossip_group_create")
+        if begins is None:
+            check(self._L.gossip_group_create(C.byref(cfg), len(devices), devs, C.byref(g)), "gossip_group_create")
+        else:
+            b = (C.c_uint64 * (len(devices) + 1))(*[int(x) for x in begins])
+            check(self._L.gossip_group_create_parts(C.byref(cfg), len(devices), devs, b, C.byref(g)),
+                  "gossip_group_create_parts")
         self._g = g
         self.n_peers, self.n_msgs = n_peers, n_msgs
         self.W = (n_msgs + 63) // 64

@@ -345,6 +345,9 @@ _VARIANTS = {"defer_1": ({"defer_permille": 1}, {"blocked": "off"}), "stream": (
              "apply_pipe_3": ({"apply_pipe": 3}, {}),
              "scatter_small": ({"scatter_small": 1}, {}),
              "small_kernels": ({"bin_words": 1024, "bin_chunk": 1024, "scatter_small": 1}, {}),
+             "split_units": ({"scatter_units": 4096}, {}),
+             "split_units_direct": ({"scatter_units": 4096, "scatter_split_direct": 1, "scatter_small": 1}, {}),
+             "apply_wide": ({"bin_words": 2048, "apply_wide": 1}, {}),
              "apply_probe": ({"apply_probe": 1}, {}), "apply_one_per_bin": ({"apply_persist": 0}, {}), "slots_needy_test": ({"bin_stream": 0, "bin_needy_skip": 0}, {}),
              "blocked_dense": ({"blocked_bin_slots": 0}, {"blocked_permille": 1000}),
              "blocked_dense_clear_peers": ({"blocked_bin_slots": 0, "blocked_clear_all": 0}, {"blocked_permille": 1000})}

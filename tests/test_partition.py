@@ -37,3 +37,13 @@ def test_blocks_balance_the_oracles_overlay(oracle, P):
     uni = costs(partition(w.n, P))
     assert bal.max() / bal.mean() < 1.05
     assert uni.max() / uni.mean() > 1.2  # what the uniform blocks did
+
+
+@pytest.mark.parametrize("begins", [[1, 64, 128], [0, 64, 100], [0, 100, 128], [0, 64, 64, 128]])
+def test_group_create_parts_rejects_bad_blocks(begins):
+    """gossip_group_create_parts checks the caller's partition before touching a device: blocks must cover
+    [0, n_peers), be non-empty and start on whole 64-peer tiles."""
+    from gossip_hip import Group
+    from gossip_hip._abi import GossipError
+    with pytest.raises(GossipError, match="part"):
+        Group(128, 64, [0] * (len(begins) - 1), begins=begins)
