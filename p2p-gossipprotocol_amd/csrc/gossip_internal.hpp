@@ -342,6 +342,8 @@ struct RoundArgs {
     uint32_t lst_cap;
     uint32_t src_booked;           // k_pull_rows: the sweep books no source side
     uint32_t row_step;             // k_pull_rows: neighbour words gathered per row per step (1 or 2)
+    uint32_t row_q;                // k_pull_rows: queue entries per wave (128; 256: "row_queue", A/B)
+    uint32_t row_grid;             // k_pull_rows: workgroups (0: kMaxGrid; "row_grid", A/B)
 };
 
 // Re-bootstrap draw (handleDeadPeer peer.cpp:398-404 -> selectAndConnectPeers

@@ -534,8 +534,7 @@ __global__ __launch_bounds__(kBlock) void k_frontier_bits(RoundArgs a) {
 // for whole rows) -- or at its end.  Finished lanes take the next row:
 // fr = (OR of the scanned neighbours) & need, and a row that stops early
 // already holds all of need.
-constexpr int kRowQ = 128;    // queue entries per wave
-template <int W, bool COV, bool FRONT, int kRowB>  // kRowB: edges per lane per step
+template <int W, bool COV, bool FRONT, int kRowB, int kRowQ = 128>  // kRowB: edges per lane per step; kRowQ: queue entries per wave
 // (116 VGPRs, four waves per SIMD.  Launch bounds asking five or six spill to scratch and ran round 7 at
 // 5.9-6.1 and 8.3-8.6 ms against 4.8-5.1: the sweep and the row state do not fit 96 or 80 registers.)
 __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) {
@@ -2747,14 +2746,46 @@ hipError_t launch_frontier_bits(const RoundArgs& a, uint32_t W_, hipStream_t s) 
     return hipGetLastError();
 }
 
+// the workgroups of kernel f resident on the device at once (occupancy at its registers and LDS x CUs)
+template <class K>
+unsigned resident_blocks(K f, int block) {
+    int dev = 0, cus = 0, nb = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, block, 0) != hipSuccess || nb < 1 || cus < 1) {
+        hipGetLastError();
+        return kMaxGrid;
+    }
+    return (unsigned)(nb * cus);
+}
+
 hipError_t launch_pull_rows(const RoundArgs& a, uint32_t W_, hipStream_t s) {
-    // a row queue per wave: every wave resident at once (its queue carries its work)
-    const unsigned g = std::min(grid_for((a.n_local + 63) / 64, kWavesPerBlock), (unsigned)kMaxGrid);
+    // a row queue per wave: every wave resident at once (its queue carries its work).  The grid is the
+    // resident workgroups (1024 at 116 VGPRs: four per CU): kMaxGrid (2048) left half the waves to start
+    // after the first half had swept its tiles -- arms alternated in one process, config 4 round 7 5.16
+    // against 5.02 ms, config 5 2.36 against 2.19 (profiles/r05/ab/r05u); "row_grid" overrides it (A/B)
+    const unsigned want = grid_for((a.n_local + 63) / 64, kWavesPerBlock);
     const uint32_t wd = wd_of(W_);
+    auto go = [&](void (*kern)(RoundArgs, uint32_t)) {
+        static std::pair<const void*, unsigned> cache[16] = {};  // (instances share the pointer type)
+        unsigned res = 0;
+        for (auto& e : cache) {
+            if (e.first == (const void*)kern) { res = e.second; break; }
+            if (!e.first) {
+                e = {(const void*)kern, resident_blocks(kern, kBlock)};
+                res = e.second;
+                break;
+            }
+        }
+        if (!res) res = resident_blocks(kern, kBlock);
+        const unsigned g = std::min(want, a.row_grid ? a.row_grid : res);
+        hipLaunchKernelGGL(kern, dim3(g), dim3(kBlock), 0, s, a, wd);
+    };
 #define GOSSIP_ROWS(COV, FR)                                                                        \
     do {                                                                                            \
-        if (a.row_step == 1) hipLaunchKernelGGL((k_pull_rows<W, COV, FR, 1>), dim3(g), dim3(kBlock), 0, s, a, wd); \
-        else hipLaunchKernelGGL((k_pull_rows<W, COV, FR, 2>), dim3(g), dim3(kBlock), 0, s, a, wd);              \
+        if (a.row_step == 1 && a.row_q == 256 && W == 1 && !COV && !FR) go(k_pull_rows<W, COV, FR, 1, 256>); \
+        else if (a.row_step == 1) go(k_pull_rows<W, COV, FR, 1>);                                   \
+        else go(k_pull_rows<W, COV, FR, 2>);                                                        \
     } while (0)
     GOSSIP_DISPATCH_W(wp_of(W_), {
         if (a.cov) { if (a.front) GOSSIP_ROWS(true, true); else GOSSIP_ROWS(true, false); }
