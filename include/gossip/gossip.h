@@ -354,7 +354,19 @@ gossip_status gossip_kernel_bytes(gossip_ctx* ctx, const char* kernel, double* b
  * "#probe_init", "#probe_slots", "#probe_finish" give 100 MHz ticks summed
  * over bins, "#probe_bins" and "#probe_slots_n" the bins and slots,
  * "#probe_block" and "#probe_blocks" the workgroups' lifetimes and count;
- * 0 off).
+ * 0 off), "scatter_small" (the streamed scatter's 4096-word, 256-thread
+ * instance where chunks fit it; 0 default), "scatter_units" (layout: split
+ * chunks into at least this many scatter units; 0 default),
+ * "scatter_split_direct" (a split chunk's later units read their words
+ * instead of staging them; 0 default), "apply_wide" (small bins applied by
+ * 16-wave workgroups; 0 default), "exchange_stages" (partitioned binned
+ * rounds: the all-gather in this many stages under the scatter, 1-16; 4
+ * default), "px_per100k" / "px_permille" (partitioned sparse push rounds
+ * from this frontier per 100 000 / per 1000 of the block send records made
+ * by the record push, below it records appended by the push; -1 never; 5
+ * per 100 000 default), "row_queue" (128 default or 256: the row pull's
+ * queue entries per wave), "row_grid" (the row pull's workgroups; 0 default:
+ * those resident at once).
  * Layout keys
  * apply at the next gossip_build_graph / gossip_load_csr ("list_cap": at the
  * next chain of needy-list rounds, never inside one).  GOSSIP_EINVAL: unknown key. */
