@@ -299,8 +299,13 @@ struct gossip_ctx {
     bool recording = false, replaying = false, rec_valid = false;
     std::vector<DevStats> rec_st;          // per round: the decoded stat sums
     std::vector<uint32_t> rec_lst;         // per round: entries its needy list received
-    DevStats* d_hist = nullptr;            // replay: every round's kStatLines stat lines
+    DevStats* d_hist = nullptr;            // replay: every round's kStatLines stat lines (and one more row)
     uint32_t hist_cap = 0, rep_round = 0;
+    // replay: per-round copies of the state a round otherwise clears for the next (tile marks, heavy-row
+    // accumulators, the apply's counters, needy-list counters), zeroed once per replayed run with the history,
+    // so a replayed round queues no clears (config 2: one 5 us launch per round of 55)
+    uint64_t* rep_aux = nullptr;
+    uint64_t rep_aux_words = 0, rep_tw = 0, rep_hw = 0;
 
     // library-driven multi-GPU rounds (gossip_dist.hip): the driver that issues
     // this ctx's collectives; owned here for gossip_comm_init, by the group otherwise
@@ -576,6 +581,16 @@ void rec_drop(gossip_ctx* c);  // forget a recorded schedule (gossip_run)
 
 uint64_t tact_bytes(const gossip_ctx* c) { return (((c->n_local + 63) / 64 + 63) / 64 + 1) * 8; }
 
+// replay: round r's rows of the per-round state (gossip_ctx.rep_aux, laid out for hist_cap rounds)
+uint64_t* rep_tact(gossip_ctx* c, uint32_t r) { return c->rep_aux + c->rep_tw * r; }
+uint32_t* rep_work(gossip_ctx* c, uint32_t r) {
+    return reinterpret_cast<uint32_t*>(c->rep_aux + c->rep_tw * (c->hist_cap + 1) + c->rep_hw * c->hist_cap) + 16ull * r;
+}
+uint32_t* rep_lstn(gossip_ctx* c, uint32_t r) {
+    return reinterpret_cast<uint32_t*>(c->rep_aux + c->rep_tw * (c->hist_cap + 1) + c->rep_hw * c->hist_cap +
+                                       8ull * c->hist_cap) + 4ull * r;
+}
+
 RoundArgs make_args(gossip_ctx* c) {
     RoundArgs a{};
     a.rp = c->rp;
@@ -592,7 +607,7 @@ RoundArgs make_args(gossip_ctx* c) {
     // k_apply_remote -- mark the tiles of the peers they activate; round 5, before which a block swept every
     // tile in every push round: config 4 as 8 parts, ≈ 1.2 ms of kernels per near-empty round)
     if (c->tact[0]) {
-        a.tcur = c->tact[c->tcur];
+        a.tcur = c->replaying ? rep_tact(c, c->rep_round) : c->tact[c->tcur];
         // the marked-tile sweep only for a nearly empty frontier (it walks 64 tiles per wave in turn;
         // at a 1.3 % frontier, 57 % of the tiles, the full sweep was faster: 3.1 against 4.4 ms)
         a.tsparse = c->tact_ok && c->frontier_est * 500 < c->n_local ? 1u : 0u;
@@ -600,16 +615,16 @@ RoundArgs make_args(gossip_ctx* c) {
         // round): kept only where the next frontier is likely small -- a tiny frontier, or a shrinking one
         const bool small = c->frontier_est * 500 < c->n_local ||
                            (c->frontier_est < c->prev_frontier_est && c->frontier_est * 100 < c->n_local);
-        a.tnx = small ? c->tact[c->tcur ^ 1] : nullptr;
+        a.tnx = small ? (c->replaying ? rep_tact(c, c->rep_round + 1) : c->tact[c->tcur ^ 1]) : nullptr;
         c->tact_marked = small;
     }
     a.send = c->send;
     a.miss = c->miss;
-    a.st = c->st;
+    a.st = c->replaying ? c->d_hist + (uint64_t)c->rep_round * kStatLines : c->st;
     a.cov = c->cov_hist ? c->cov_hist + (uint64_t)c->round * 64 * c->Wp : nullptr;
     a.chunks = c->chunks;
     a.n_chunks = c->n_chunks;
-    a.hacc = c->hacc;
+    a.hacc = c->replaying && c->hacc ? c->rep_aux + c->rep_tw * (c->hist_cap + 1) + c->rep_hw * c->rep_round : c->hacc;
     a.row_step = c->row_step;
     a.row_q = c->row_q;
     a.row_grid = c->row_grid;
@@ -1034,7 +1049,7 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
     // the previous round booked this round's source side (late pull rounds): those lines are this round's
     const bool booked = c->pre_booked;
     c->pre_booked = false;
-    if (booked) std::swap(c->st, c->st_pre);
+    if (booked && !c->replaying) std::swap(c->st, c->st_pre);  // (replayed: the booking went to this round's row)
     RoundArgs a = make_args(c);
     const uint32_t pw = pack_w(c);
     if (c->cfg.rejoin_threshold) {  // restarts first: a peer dying this round cannot restart in it
@@ -1281,17 +1296,17 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
         c->dgone_next = c->round + 1;
     }
     a.src_booked = booked ? 1u : 0u;
-    a.st = c->st;
-    a.st_pre = c->cur_pre ? c->st_pre : nullptr;
+    a.st = c->replaying ? c->d_hist + (uint64_t)c->rep_round * kStatLines : c->st;
+    a.st_pre = !c->cur_pre ? nullptr : c->replaying ? c->d_hist + (uint64_t)(c->rep_round + 1) * kStatLines : c->st_pre;
     a.lst_out = c->cur_lst_out >= 0 ? c->lst[c->cur_lst_out] : nullptr;
-    a.lst_n = c->cur_lst_out >= 0 ? c->d_lst_n + c->cur_lst_out : nullptr;
+    a.lst_n = c->cur_lst_out < 0 ? nullptr : c->replaying ? rep_lstn(c, c->rep_round) : c->d_lst_n + c->cur_lst_out;
     a.lst_cap = c->lst_cap;
     c->last_pull = pull;
     c->last_bin = bin;
     c->last_front = false;
     if (pull) {
         if (a.tcur) {  // pull / binned rounds set no tile marks: this round's go, the next push round scans
-            HIPCHK(queue_zero(c, a.tcur, tact_bytes(c)));
+            if (!c->replaying) HIPCHK(queue_zero(c, a.tcur, tact_bytes(c)));
             a.tcur = a.tnx = nullptr;
             a.tsparse = 0;
         }
@@ -1473,7 +1488,7 @@ gossip_status round_compute(gossip_ctx* c) {
         // whole-array clear from a 5 % frontier (config 4 round 4: 17 %; round 3, 1.25 %, clears per peer)
         p.clear_all = c->pb_clear_all && c->frontier_est * 20 >= c->n_local ? 1u : 0u;
         c->cur_clear_all = p.clear_all != 0;
-        if (a.tcur) HIPCHK(queue_zero(c, a.tcur, tact_bytes(c)));  // unread marks go
+        if (a.tcur && !c->replaying) HIPCHK(queue_zero(c, a.tcur, tact_bytes(c)));  // unread marks go
         HIPCHK(timed(c, "pb_scatter", [&] { return launch_pb_scatter(a, p, c->any_dead, c->W, c->stream); }));
         HIPCHK(timed(c, "pb_split", [&] { return launch_pb_split(p, c->stream); }));
         HIPCHK(timed(c, "pb_apply", [&] { return launch_pb_apply(a, p, c->stream); }));
@@ -1481,7 +1496,7 @@ gossip_status round_compute(gossip_ctx* c) {
     }
     // k_pull_heavy's per-row accumulators, cleared with the round's first kernel
     const bool hz = c->hacc && c->n_chunks && (c->cur_list || c->last_bin || c->last_pull);
-    if (hz) HIPCHK(queue_zero(c, c->hacc, c->n_chunks * c->Wp * sizeof(uint64_t)));
+    if (hz && !c->replaying) HIPCHK(queue_zero(c, c->hacc, c->n_chunks * c->Wp * sizeof(uint64_t)));
     if (c->cur_list) {
         // nx holds the new words of the round before last: its list's rows (and the heavy rows) if that was
         // a list round, anything otherwise
@@ -1498,9 +1513,10 @@ gossip_status round_compute(gossip_ctx* c) {
     if (c->last_bin) {
         if (c->apply_persist && c->bin_stream && !c->d_work)
             HIPCHK(hipMalloc((void**)&c->d_work, 8 * sizeof(uint32_t)));
-        if (c->apply_persist && c->bin_stream)  // the apply's bin counters, zeroed with the round's first launch
+        if (c->apply_persist && c->bin_stream && !c->replaying)  // the apply's bin counters, zeroed with the round's first launch
             HIPCHK(queue_zero(c, c->d_work, 8 * sizeof(uint32_t)));
         BinArgs b = bin_args(c, c->bins_first, src_stats(c));
+        if (b.work && c->replaying) b.work = rep_work(c, c->rep_round);
         // every bin is needy while more than one (peer, message) pair per peer is missing: no check pass
         b.needy_check = c->cur_missing > c->n_local && c->needy_skip ? 0u : 1u;
         if (c->stage_n && c->bins.stages == c->stage_n) {
@@ -1556,7 +1572,7 @@ gossip_status round_compute(gossip_ctx* c) {
     if (c->cfg.extra_cap)
         HIPCHK(timed(c, "push_extra", [&] { return launch_push_extra(a, pw, c->any_dead, remote, c->stream); }));
     HIPCHK(timed(c, "push_heavy", [&] { return launch_push_heavy(a, pw, c->any_dead, remote, c->stream); }));
-    if (a.tcur && !a.tsparse) HIPCHK(queue_zero(c, a.tcur, tact_bytes(c)));  // unread marks go
+    if (a.tcur && !a.tsparse && !c->replaying) HIPCHK(queue_zero(c, a.tcur, tact_bytes(c)));  // unread marks go
     HIPCHK(timed(c, "push_light", [&] { return launch_push_light(a, pw, c->any_dead, remote, c->stream); }));
     if (c->cur_arec) {
         HIPCHK(hipMemcpyAsync(c->h_counts, c->d_counts, c->world * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
@@ -1574,8 +1590,7 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
     if (c->replaying && c->last_st_round != c->round) {  // the recorded sums; the lines go to the history
         // copied to the history and cleared by the next round's first launch (the zero batch); whatever is
         // queued before goes out first (a queued clear of these lines would run before their copy)
-        HIPCHK(flush_zero(c));
-        HIPCHK(queue_zero(c, c->st, kStatLines * sizeof(DevStats), c->d_hist + (uint64_t)c->rep_round * kStatLines));
+        // (the round's kernels wrote its lines straight into its row of the history)
         c->last_st = c->rec_st[c->rep_round];
         c->lst_out_n = c->rec_lst[c->rep_round];
         c->last_st_round = c->round;
@@ -1774,13 +1789,25 @@ gossip_status step_round(gossip_ctx* c, gossip_round_stats* out);
 // copied to d_hist; then one read of them, checked field by field against the recording.
 gossip_status replay_run(gossip_ctx* c, gossip_round_stats* per_round, uint32_t cap, uint32_t* rounds) {
     const uint32_t R = (uint32_t)c->rec_st.size();
-    if (c->hist_cap < R) {
+    const uint64_t tw = c->tact[0] ? tact_bytes(c) / 8 : 0, hw = c->hacc ? c->n_chunks * c->Wp : 0;
+    if (c->hist_cap != R || c->rep_tw != tw || c->rep_hw != hw) {  // (the rows below are laid out for R rounds)
         hipFree(c->d_hist);
         c->d_hist = nullptr;
         c->hist_cap = 0;
-        HIPCHK(hipMalloc((void**)&c->d_hist, (uint64_t)R * kStatLines * sizeof(DevStats)));
+        hipFree(c->rep_aux);
+        c->rep_aux = nullptr;
+        // rows 0..R (a round may book the next one's source side into row R)
+        HIPCHK(hipMalloc((void**)&c->d_hist, (uint64_t)(R + 1) * kStatLines * sizeof(DevStats)));
+        c->rep_tw = tw;
+        c->rep_hw = hw;
+        // tile marks (R + 1 rows), heavy accumulators, 16 apply counters and 4 list counters (u32) per round
+        c->rep_aux_words = c->rep_tw * (R + 1) + c->rep_hw * R + 8ull * R + 2ull * R + 1;
+        HIPCHK(hipMalloc((void**)&c->rep_aux, c->rep_aux_words * sizeof(uint64_t)));
         c->hist_cap = R;
     }
+    HIPCHK(flush_zero(c));
+    HIPCHK(hipMemsetAsync(c->d_hist, 0, (uint64_t)(R + 1) * kStatLines * sizeof(DevStats), c->stream));
+    HIPCHK(hipMemsetAsync(c->rep_aux, 0, c->rep_aux_words * sizeof(uint64_t), c->stream));
     c->replaying = true;
     uint32_t k = 0;
     gossip_status s = GOSSIP_OK;
@@ -1799,7 +1826,7 @@ gossip_status replay_run(gossip_ctx* c, gossip_round_stats* per_round, uint32_t 
         return s;
     }
     std::vector<DevStats> h((uint64_t)R * kStatLines);
-    HIPCHK(flush_zero(c));  // (the last round's lines are still queued for the history)
+    HIPCHK(flush_zero(c));
     HIPCHK(hipMemcpyAsync(h.data(), c->d_hist, h.size() * sizeof(DevStats), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     bool same = k == R && c->finished;
@@ -2044,6 +2071,7 @@ void gossip_destroy(gossip_ctx* c) {
     hipFree(c->d_probe);
     hipFree(c->d_work);
     hipFree(c->d_hist);
+    hipFree(c->rep_aux);
     hipFree(c->d_part);
     hipFree(c->d_toff);
     hipFree(c->sx_pos);
