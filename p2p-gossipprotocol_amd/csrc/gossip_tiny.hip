@@ -45,20 +45,29 @@ __device__ __forceinline__ void tiny_reduce(unsigned long long (&v)[kTFields], u
     constexpr int kWaves = kB / 64;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if constexpr (kB == 64) {
-        // one wave: the lanes' values through LDS, then lane f sums field f (its 64 loads in flight together).
-        // Shuffle trees waited for every permute of every field (66 round trips, ~3 us of a 4 us round).
-        __shared__ unsigned long long tr[64 * kTFields];
+        // one wave: the lanes' values through LDS (field-major rows padded by two words, so the summing
+        // lanes' 16-B reads fall in different banks), then lane f sums row f with four accumulators, its
+        // loads in flight together.  Shuffle trees waited for every permute of every field (66 round trips,
+        // ~3 us of a 4 us round); LDS atomics into one word per field serialised the lanes (0.17 ms a run).
+        constexpr int kRow = 66;
+        __shared__ unsigned long long tr[kTFields * kRow];
 #pragma unroll
         for (int f = 0; f < kTFields; ++f) {
-            tr[lane * kTFields + f] = v[f];
+            tr[f * kRow + lane] = v[f];
             v[f] = 0;
         }
         __syncthreads();
         if (lane < kTFields) {
-            unsigned long long s = 0;
+            const unsigned long long* row = tr + lane * kRow;
+            unsigned long long a0 = 0, a1 = 0, a2 = 0, a3 = 0;
 #pragma unroll
-            for (int i = 0; i < 64; ++i) s += tr[i * kTFields + lane];
-            tot[lane] = s;
+            for (int i = 0; i < 64; i += 4) {
+                a0 += row[i];
+                a1 += row[i + 1];
+                a2 += row[i + 2];
+                a3 += row[i + 3];
+            }
+            tot[lane] = (a0 + a1) + (a2 + a3);
         }
         __syncthreads();
         return;

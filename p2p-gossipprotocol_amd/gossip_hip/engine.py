@@ -203,6 +203,17 @@ class Engine:
         check(self._L.gossip_run(self._ctx, buf, cap, C.byref(rounds)), "gossip_run")
         return [buf[i].as_dict() for i in range(min(rounds.value, cap))]
 
+    def run_into(self, cap: int = 4096) -> int:
+        """gossip_run into a buffer kept across calls; returns the rounds run (their stats: last_stats())."""
+        if getattr(self, "_run_buf", None) is None or len(self._run_buf) < cap:
+            self._run_buf, self._run_n = (RoundStats * cap)(), C.c_uint32()
+        check(self._L.gossip_run(self._ctx, self._run_buf, cap, C.byref(self._run_n)), "gossip_run")
+        return self._run_n.value
+
+    def last_stats(self) -> list[dict]:
+        """The rounds of the last run_into(), as run() returns them."""
+        return [self._run_buf[i].as_dict() for i in range(min(self._run_n.value, len(self._run_buf)))]
+
     # partitioned phases (see distributed.py)
     def set_exchange(self, send_ptr: int, recv_ptr: int, part_begins) -> None:
         pb = np.ascontiguousarray(part_begins, dtype=np.uint64)
@@ -409,6 +420,17 @@ class Group:
         rounds = C.c_uint32()
         check(self._L.gossip_group_run(self._g, buf, cap, C.byref(rounds)), "gossip_group_run")
         return [buf[i].as_dict() for i in range(min(rounds.value, cap))]
+
+    def run_into(self, cap: int = 4096) -> int:
+        """gossip_group_run into a buffer kept across calls; returns the rounds run (their stats: last_stats())."""
+        if getattr(self, "_run_buf", None) is None or len(self._run_buf) < cap:
+            self._run_buf, self._run_n = (RoundStats * cap)(), C.c_uint32()
+        check(self._L.gossip_group_run(self._g, self._run_buf, cap, C.byref(self._run_n)), "gossip_group_run")
+        return self._run_n.value
+
+    def last_stats(self) -> list[dict]:
+        """The rounds of the last run_into(), as run() returns them."""
+        return [self._run_buf[i].as_dict() for i in range(min(self._run_n.value, len(self._run_buf)))]
 
     def read_seen(self) -> np.ndarray:
         out = np.zeros((self.n_peers, self.W), dtype=np.uint64)
