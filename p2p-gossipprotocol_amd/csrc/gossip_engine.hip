@@ -655,6 +655,9 @@ RoundArgs make_args(gossip_ctx* c) {
 // Upload a host-built CSR and derive the heavy-row chunk list.
 gossip_status install_graph(gossip_ctx* c, uint64_t* d_rp, uint32_t* d_col, uint64_t m) {
     free_graph(c);
+    // the next reset clears nw / nx whole (the last run's list rows and heavy rows were the old overlay's)
+    c->lin_idx[0] = c->lin_idx[1] = -1;
+    c->bufs_zero = false;
     c->heavy = c->heavy_req;  // layout key: the chunk list, bins and blocked segments below all use it
     c->rp = d_rp;
     c->col = d_col;
@@ -2299,6 +2302,17 @@ gossip_status gossip_reset(gossip_ctx* c) {
         c->bufs_zero = true;
     } else {
         HIPCHK(launch_zero_words(c->seen, words, s));
+        if (!c->bufs_zero && !c->in_round && c->lin_idx[0] >= 0 && c->lin_idx[1] >= 0) {
+            // the last two rounds pulled needy lists: each wrote only its list's rows and the heavy rows into a
+            // buffer cleared before it (the list rounds' contract: one word per peer, nothing injected or
+            // killed later), so those rows are all that is left -- nw holds the last round's, nx the one's
+            // before (config 4: two 2 GB fills, 0.94 ms of a step, became two list clears)
+            RoundArgs a = make_args(c);
+            HIPCHK(launch_list_zero(a, c->lst[c->lin_idx[1]], c->lin_n[1], s));
+            a.nx = c->nw;
+            HIPCHK(launch_list_zero(a, c->lst[c->lin_idx[0]], c->lin_n[0], s));
+            c->bufs_zero = true;
+        }
         if (!c->bufs_zero) {  // (a run that ended normally left both zero)
             HIPCHK(launch_zero_words(c->nw, words, s));
             HIPCHK(launch_zero_words(c->nx, words, s));
