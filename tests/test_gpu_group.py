@@ -138,3 +138,20 @@ def test_group_rejects_mixed_devices():
     from gossip_hip import GossipError
     with pytest.raises(GossipError):
         Group(1 << 12, 64, [0, 0, 1])
+
+
+def test_group_run_into_keeps_stats_in_a_reused_buffer(oracle):
+    """Group.run_into (bench's timed steps): gossip_group_run into a buffer kept
+    across calls, the per-round stats read after the run -- the oracle's rounds,
+    run after run."""
+    w = config(2, 1 << 15, pick=oracle.pick_origins)
+    rp, col = oracle.gen_workload(w)
+    ref = oracle.simulate_workload(w, rp, col)
+    with Group(w.n, w.n_msgs, [0, 0], **w.engine_kwargs()) as g:
+        g.build_graph()
+        g.inject(w.origins, w.inject_rounds)
+        for _ in range(2):
+            g.reset()
+            assert g.run_into() == len(ref["stats"])
+            assert g.last_stats() == ref["stats"]
+        assert np.array_equal(g.read_seen(), ref["seen"])

@@ -593,3 +593,10 @@ def test_recorded_schedule_replay(oracle, idx, n):
             e.reset()
             _compare(e, ref, w)
         assert e.kernel_bytes("#replayed_runs") == 3
+        # bench's timed steps: the run's stats left in a buffer kept across calls, read afterwards
+        e.set_tuning("replay", 1)
+        for _ in range(3):
+            e.reset()
+            assert e.run_into() == len(ref["stats"])
+            assert e.last_stats() == ref["stats"]
+        assert np.array_equal(e.read_seen(), ref["seen"])
