@@ -295,8 +295,8 @@ class Ranked(Single):
         from gossip_hip import Engine, comm_unique_id, partition_edges
         self.dist, self.world, self.rank = dist, world, rank
         # blocks of about equal work (the powerlaw overlay's edges sit at the low ids), as gossip_group_create
-        part = partition_edges(w.n, w.n_msgs, world, **{k: v for k, v in tune.items() if k != "tuning"},
-                               **w.engine_kwargs())
+        kw = {**{k: v for k, v in tune.items() if k != "tuning"}, **w.engine_kwargs()}  # (one dict: no duplicate keys)
+        part = partition_edges(w.n, w.n_msgs, world, **kw)
         self.eng = Engine(w.n, w.n_msgs, device=dev, part=(part[rank], part[rank + 1]), **tune, **w.engine_kwargs())
         self.eng.build_graph()
         self.eng.inject(w.origins, w.inject_rounds)

@@ -34,6 +34,8 @@ typedef int gossip_status;
 #define GOSSIP_ENODEV (-5)  /* no gfx950 device visible */
 #define GOSSIP_EOVERFLOW (-6) /* report buffer overflowed (reports dropped) */
 #define GOSSIP_ESTALL (-8)    /* device work gave up waiting (a bounded spin tripped): results incomplete */
+#define GOSSIP_EBOUNDS (-9)   /* checked-index build only (make checked): a kernel index passed its bound;
+                                 gossip_last_error names the site, the index and the bound */
 
 /* Overlay models. */
 #define GOSSIP_GRAPH_POWERLAW 1      /* scale overlay: power-law pick (peer.cpp:219-222), skewed
@@ -49,8 +51,8 @@ typedef int gossip_status;
 #define GOSSIP_FLAG_NO_BLOCKED 32u      /* no propagation-blocked push rounds (saves ~22 B per edge of records) */
 #define GOSSIP_FLAG_FORCE_BLOCKED 64u   /* every push or binned round runs propagation-blocked where it can
                                            (single partition, one word per peer, slot layout) */
-#define GOSSIP_FLAG_UNIFORM_PARTITION 128u /* gossip_group_create: blocks of ceil(n/parts) peers instead of
-                                              gossip_partition_edges */
+#define GOSSIP_FLAG_UNIFORM_PARTITION 128u /* gossip_group_create: blocks of ceil(n/parts) peers, rounded up to
+                                              whole 64-peer tiles, instead of gossip_partition_edges */
 
 /*
  * Replaces: NetworkConfig's parsed values (config.cpp:31-42,93-96) plus the
@@ -264,8 +266,9 @@ typedef struct gossip_group gossip_group;
 gossip_status gossip_group_create(const gossip_config* cfg, uint32_t n_parts, const int32_t* devices,
                                   gossip_group** out);
 /* The same with the caller's partition: begins[0] = 0 < begins[1] < ... < begins[n_parts] = n_peers, every
- * block starting on a whole 64-peer tile (gossip_group_create: gossip_partition_edges, or gossip_partition
- * under GOSSIP_FLAG_UNIFORM_PARTITION). */
+ * block starting on a whole 64-peer tile (gossip_group_create: gossip_partition_edges; blocks of ceil(n/parts)
+ * rounded up to whole tiles for other overlays, under GOSSIP_FLAG_UNIFORM_PARTITION, or when n_peers < 64 parts
+ * -- GOSSIP_EINVAL if that leaves a part empty). */
 gossip_status gossip_group_create_parts(const gossip_config* cfg, uint32_t n_parts, const int32_t* devices,
                                         const uint64_t* begins, gossip_group** out);
 void gossip_group_destroy(gossip_group* g);

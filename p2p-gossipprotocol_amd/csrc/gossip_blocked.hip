@@ -933,7 +933,7 @@ __global__ __launch_bounds__(256) void k_px_pack(PbArgs p, uint32_t world, uint3
 
 hipError_t build_px(const uint64_t* rp, const uint32_t* col, uint64_t n_local, uint64_t n_global, uint32_t heavy,
                     const HeavyChunk* chunks, uint64_t n_chunks, const uint64_t* part, uint32_t world, uint32_t own,
-                    uint64_t cap_records, hipStream_t s, PbState* out, std::string* err) {
+                    hipStream_t s, PbState* out, std::string* err) {
     PbState st;
     uint32_t* d_cnt = nullptr;
     auto bail = [&](hipError_t e, const char* what) {
@@ -974,7 +974,6 @@ hipError_t build_px(const uint64_t* rp, const uint32_t* col, uint64_t n_local, u
     // records, gossip_dist.hip)
     uint64_t stride = 0;
     for (uint32_t q = 0; q < world; ++q) stride = std::max(stride, per_q[q]);
-    (void)cap_records;
     st.rec_stride = std::max<uint64_t>(stride, 1);
     st.n1 = n1;
     size_t free_b = 0, total_b = 0;

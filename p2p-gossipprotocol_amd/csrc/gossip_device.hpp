@@ -24,6 +24,27 @@ __device__ __forceinline__ uint64_t bin_chunk_ve(const BinArgs& b, uint64_t c, u
     return max(vb, min(min(vb + b.chunk, (c / b.cps + 1) * b.seg), n));
 }
 
+// Checked-index build (`make checked`: -DGOSSIP_CHECKED, build/checked/libgossip_hip.so).  GOSSIP_IDX(a, site,
+// i, bound) is i in the product build; the checked build records the first index at or past its bound in a.chk
+// ({trips, site, index, bound}) and substitutes 0, so the access stays inside the buffer and the run ends with
+// GOSSIP_EBOUNDS naming the site instead of a fault that depends on what the allocator placed after the buffer.
+#ifdef GOSSIP_CHECKED
+__device__ __forceinline__ uint64_t chk_idx(unsigned long long* chk, uint32_t site, uint64_t i, uint64_t bound) {
+    if (i < bound) return i;
+    if (chk && atomicAdd(&chk[0], 1ull) == 0ull) {
+        chk[1] = site;
+        chk[2] = i;
+        chk[3] = bound;
+    }
+    return 0;
+}
+#define GOSSIP_IDX(a, site, i, bound) chk_idx((a).chk, (site), (uint64_t)(i), (uint64_t)(bound))
+constexpr bool kChecked = true;
+#else
+#define GOSSIP_IDX(a, site, i, bound) ((uint64_t)(i))
+constexpr bool kChecked = false;
+#endif
+
 // the bits a peer can still learn: messages injected so far (at P = 1 the ones whose origin was alive to
 // inject them -- a never-injected message kept every row of config 5 scanning to its end)
 __device__ __forceinline__ uint64_t injm_full(const RoundArgs& a, int w) {

@@ -53,7 +53,7 @@ namespace gossip {
 
 namespace {
 
-constexpr int kStatSlots = 13;  // all-reduced stat fields (see pack_stats)
+constexpr int kStatSlots = 15;  // all-reduced stat fields (see pack_stats)
 
 struct DistRank {
     gossip_ctx* ctx = nullptr;
@@ -97,6 +97,10 @@ struct DistDriver {
     // schedule state, from global stats (identical on every rank)
     uint64_t prev_new = 0, injected = 0, cum_digest = 0, cum_covered = 0;
     uint64_t front = 0;  // this round's frontier (the peers the last round activated, all ranks)
+    // stages of a binned round's staged all-gather: the count every rank asked for at the last stats all-reduce
+    // when they all asked for the same, else 1 (one process per GPU: a rank whose bin layout failed, or tuned
+    // differently, would post other send/recv sizes than its peers -- a hang or a corrupt gather buffer)
+    uint32_t stages = 1;
     bool finished = false;
     std::vector<int32_t> modes;
 };
@@ -726,7 +730,8 @@ void pack_stats(DistRank& r, uint64_t* v) {
     const gossip_round_stats& s = r.local;
     const uint64_t f[kStatSlots] = {s.frontier, s.traversals, s.deliveries, s.undelivered, s.new_receipts,
                                     s.injected, s.died,       s.reports,    s.reconnects,  s.rejoined,
-                                    s.digest,   s.covered,    ctx_frontier_est(r.ctx)};
+                                    s.digest,   s.covered,    ctx_frontier_est(r.ctx),
+                                    ctx_stages(r.ctx), (uint64_t)ctx_stages(r.ctx) * ctx_stages(r.ctx)};
     std::memcpy(v, f, sizeof(f));
 }
 
@@ -799,8 +804,7 @@ gossip_status dist_step(DistDriver* d, gossip_round_stats* out) {
         const bool compact = d->world > 1 && d->front * 1000 < (uint64_t)gpm * d->n;
         // a binned round with a whole-slice exchange goes out in stages under its scatter (every rank has a
         // streamed bin layout and asks for the same number of stages)
-        uint32_t S = mode == GOSSIP_MODE_BIN && !compact && d->world > 1 ? ctx_stages(d->ranks[0].ctx) : 1u;
-        for (auto& r : d->ranks) S = ctx_stages(r.ctx) == S ? S : 1u;
+        const uint32_t S = mode == GOSSIP_MODE_BIN && !compact && d->world > 1 ? d->stages : 1u;
         if ((s = dbg_sync(d, compact ? "compact_gather" : S > 1 ? "staged_gather" : "all_gather",
                           compact ? compact_gather(d) : S > 1 ? staged_gather(d, S) : all_gather(d))))
             return s;
@@ -841,6 +845,10 @@ gossip_status dist_step(DistDriver* d, gossip_round_stats* out) {
     d->cum_digest += g[10];
     d->cum_covered += g[11];
     d->front = g[12];
+    // every rank asked for the same stage count iff sum(S)^2 == world * sum(S^2) (equality in Cauchy-Schwarz);
+    // every rank computes this from the same sums, so all take the same exchange in the next binned round
+    d->stages = g[13] % d->world == 0 && g[13] * g[13] == (uint64_t)d->world * g[14]
+                    ? (uint32_t)std::min<uint64_t>(g[13] / d->world, kMaxStages) : 1u;
     o.digest = d->cum_digest;
     o.covered = d->cum_covered;
     o.duplicates = o.deliveries - o.new_receipts;
@@ -948,6 +956,7 @@ gossip_status dist_step_ctx(gossip_ctx* c, gossip_round_stats* out) {
 
 void dist_reset(DistDriver* d) {
     d->prev_new = d->injected = d->cum_digest = d->cum_covered = d->front = 0;
+    d->stages = 1;
     d->finished = false;
     d->modes.clear();
 }
@@ -1017,7 +1026,7 @@ gossip_status gossip_partition_edges(const gossip_config* cfg, uint32_t world, u
         }
         uint64_t x = ((uint64_t)(hi * (double)n) + 63) / 64 * 64;
         x = std::max<uint64_t>(x, begins[q - 1] + 64);                  // non-empty, whole tiles
-        x = std::min<uint64_t>(x, n - (uint64_t)(world - q) * 64 / 64 * 64);  // room for the blocks after it
+        x = std::min<uint64_t>(x, (n - (uint64_t)(world - q) * 64) / 64 * 64);  // room for the blocks after it
         begins[q] = x;
     }
     begins[world] = n;
@@ -1127,6 +1136,18 @@ gossip_status gossip_group_create(const gossip_config* cfg, uint32_t n_parts, co
     gossip_status s = cfg->flags & GOSSIP_FLAG_UNIFORM_PARTITION ? gossip_partition(cfg->n_peers, n_parts, part.data())
                                                                  : gossip_partition_edges(cfg, n_parts, part.data());
     if (s) return s;
+    // gossip_group_create_parts takes blocks that start on whole 64-peer tiles; the uniform blocks (ref_bootstrap
+    // overlays, GOSSIP_FLAG_UNIFORM_PARTITION, or fewer than 64 peers per block) are ceil(n/P) peers, so they
+    // are rounded up to whole tiles here
+    bool tiles = true;
+    for (uint32_t q = 0; q < n_parts; ++q) tiles &= part[q] % 64 == 0;
+    if (!tiles) {
+        const uint64_t n = cfg->n_peers, chunk = ((n + n_parts - 1) / n_parts + 63) / 64 * 64;
+        for (uint32_t q = 0; q <= n_parts; ++q) part[q] = std::min<uint64_t>((uint64_t)q * chunk, n);
+        for (uint32_t q = 0; q < n_parts; ++q)
+            if (part[q + 1] <= part[q])
+                return set_error(GOSSIP_EINVAL, "n_peers too small: every part needs whole 64-peer tiles");
+    }
     return gossip_group_create_parts(cfg, n_parts, devices, part.data(), out);
 }
 

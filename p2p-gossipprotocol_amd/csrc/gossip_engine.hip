@@ -628,6 +628,7 @@ RoundArgs make_args(gossip_ctx* c) {
     a.row_step = c->row_step;
     a.row_q = c->row_q;
     a.row_grid = c->row_grid;
+    a.chk = reinterpret_cast<unsigned long long*>(c->inj_live + kMaxWords);
     a.inj_live = c->world <= 1 && c->n_local == c->n ? c->inj_live : nullptr;  // a partition injects its own only
     a.n_local = c->n_local;
     a.begin = c->begin;
@@ -1253,7 +1254,7 @@ gossip_status round_begin(gossip_ctx* c, bool remote, int requested, int* mode) 
                 build_px(c->rp, c->col, c->n_local, c->n, c->heavy, c->chunks, c->n_chunks, c->part_begins.data(),
                          c->world, (uint32_t)(std::find(c->part_begins.begin(), c->part_begins.end(), c->begin) -
                                               c->part_begins.begin()),
-                         (uint64_t)c->world * c->n_local, c->stream, &c->px, &err);
+                         c->stream, &c->px, &err);
             if (e == hipSuccess) {
                 c->px_state = 1;  // (d_part: set with the sparse exchange, gossip_set_sparse)
             } else if (e == hipErrorOutOfMemory || e == hipErrorInvalidValue) {
@@ -1589,6 +1590,27 @@ gossip_status round_compute(gossip_ctx* c) {
     return GOSSIP_OK;
 }
 
+// Checked-index build (GOSSIP_CHECKED): the first index a kernel found past its bound since the last check
+// (gossip_device.hpp GOSSIP_IDX), reported once and cleared.  The product build reads nothing.
+gossip_status check_bounds(gossip_ctx* c) {
+#ifdef GOSSIP_CHECKED
+    unsigned long long h[4] = {};
+    unsigned long long* d = reinterpret_cast<unsigned long long*>(c->inj_live + kMaxWords);
+    HIPCHK(hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (!h[0]) return GOSSIP_OK;
+    HIPCHK(hipMemsetAsync(d, 0, sizeof(h), c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    char msg[192];
+    std::snprintf(msg, sizeof(msg), "round %u: %llu indices past their bounds; first: site %llu, index %llu, bound %llu",
+                  c->round, h[0], h[1], h[2], h[3]);
+    return fail(GOSSIP_EBOUNDS, msg);
+#else
+    (void)c;
+    return GOSSIP_OK;
+#endif
+}
+
 gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative) {
     if (c->replaying && c->last_st_round != c->round) {  // the recorded sums; the lines go to the history
         // copied to the history and cleared by the next round's first launch (the zero batch); whatever is
@@ -1608,6 +1630,7 @@ gossip_status read_slot(gossip_ctx* c, gossip_round_stats* out, bool cumulative)
                                   c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         HIPCHK(queue_zero(c, c->st, kStatLines * sizeof(DevStats)));  // cleared with the next round's first launch
+        if (gossip_status cs = check_bounds(c)) return cs;
         if (c->cur_pb || c->cur_px) {
             // bit 4: a wave gave up waiting for its staging generation (gossip_stage.hpp, kStageSpin: the
             // protocol always progresses, so this means a bug, not load); bits 1/2: a record region that
@@ -1848,6 +1871,10 @@ gossip_status replay_run(gossip_ctx* c, gossip_round_stats* per_round, uint32_t 
         for (int f = 0; same && f < kStatFields; ++f)
             same = f == 11 || f == 14 || f == 15 || f == 18 || f == 19 || x[f] == y[f];
     }
+    if (gossip_status cs = check_bounds(c)) {
+        rec_drop(c);
+        return cs;
+    }
     if (same && any_pb) {
         uint32_t e = 0;
         HIPCHK(hipMemcpy(&e, c->pb.err, sizeof(e), hipMemcpyDeviceToHost));
@@ -1878,6 +1905,7 @@ const char* gossip_strerror(gossip_status s) {
         case GOSSIP_EOVERFLOW: return "report buffer overflow";
         case GOSSIP_ECOMM: return "RCCL error";
         case GOSSIP_ESTALL: return "device work stalled";
+        case GOSSIP_EBOUNDS: return "index past its bound (checked build)";
         default: return "unknown status";
     }
 }
@@ -1948,7 +1976,9 @@ gossip_status gossip_create(const gossip_config* cfg, gossip_ctx** out) {
         return bail("stats", err);
     if ((err = hipHostMalloc((void**)&c->h_st, kStatLines * sizeof(DevStats))) != hipSuccess) return bail("pinned stats", err);
     if ((err = hipMalloc((void**)&c->n_reports, sizeof(unsigned long long))) != hipSuccess) return bail("nrep", err);
-    if ((err = hipMalloc((void**)&c->inj_live, kMaxWords * sizeof(uint64_t))) != hipSuccess) return bail("inj", err);
+    // (+4 words: the checked-index build's record, RoundArgs.chk, behind the injected messages)
+    if ((err = hipMalloc((void**)&c->inj_live, (kMaxWords + 4) * sizeof(uint64_t))) != hipSuccess) return bail("inj", err);
+    if ((err = hipMemset(c->inj_live + kMaxWords, 0, 4 * sizeof(uint64_t))) != hipSuccess) return bail("chk", err);
     if (c->cfg.extra_cap) {
         if (c->cfg.extra_cap > 64) {
             free_state(c);

@@ -344,6 +344,19 @@ struct RoundArgs {
     uint32_t row_step;             // k_pull_rows: neighbour words gathered per row per step (1 or 2)
     uint32_t row_q;                // k_pull_rows: queue entries per wave (128; 256: "row_queue", A/B)
     uint32_t row_grid;             // k_pull_rows: workgroups (0: kMaxGrid; "row_grid", A/B)
+    unsigned long long* chk;       // checked-index build (GOSSIP_CHECKED): {trips, site, index, bound} of the
+                                   // first index past its bound (gossip_device.hpp GOSSIP_IDX); unused otherwise
+};
+
+// GOSSIP_IDX sites (the checked-index build reports the first one that trips)
+enum : uint32_t {
+    kChkStreamDirect = 1,  // k_bin_stream, scatter_direct: a chunk's source word read from the gather buffer
+    kChkStreamSlice,       // k_bin_stream: a chunk-local source in the LDS slice
+    kChkStageSrc,          // scatter_stage: a source word staged from nw_src
+    kChkStreamVal,         // k_bin_stream: a value slot
+    kChkApplyRecord,       // k_apply_records: a record's peer in the block
+    kChkPullGather,        // k_pull_rows / k_pull_heavy: a neighbour's word in nw_src
+    kChkApplyRemote,       // k_apply_remote: a received word of the block
 };
 
 // Re-bootstrap draw (handleDeadPeer peer.cpp:398-404 -> selectAndConnectPeers
@@ -470,11 +483,12 @@ PbArgs pb_args(const PbState& p);
 hipError_t launch_pb_scatter(const RoundArgs& a, const PbArgs& p, bool check_alive, uint32_t wd, hipStream_t s);
 // A vertex block's sparse push rounds as records (P > 1, one word per peer): level 1 with the destination
 // blocks as its coarse bins and the own block delivered at once; its segments' capacities from the block's
-// edge counts.  hipErrorInvalidValue: a destination's records could outgrow its slot of the exchange buffer
-// (cap_records each; the staging push stays).
+// edge counts.  The records for one destination can outnumber its block: the receivers grow their record
+// buffers to a round's records (exchange_records, gossip_dist.hip).  hipErrorInvalidValue: world outside
+// [2, kPbCoarseMax] or n_global >= 2^32 (the staging push stays).
 hipError_t build_px(const uint64_t* rp, const uint32_t* col, uint64_t n_local, uint64_t n_global, uint32_t heavy,
                     const HeavyChunk* chunks, uint64_t n_chunks, const uint64_t* part, uint32_t world, uint32_t own,
-                    uint64_t cap_records, hipStream_t s, PbState* out, std::string* err);
+                    hipStream_t s, PbState* out, std::string* err);
 // the record buffer of the sparse push round in flight ({peer, words} per record, stride records per destination
 // block): the staging push's compaction (the exchange's seg buffer) or the record push's own (gossip_dist.hip)
 void ctx_send_records(gossip_ctx* c, const uint64_t** base, uint64_t* stride);

@@ -730,7 +730,8 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
         for (int j = 0; j < kRowB; ++j)
 #pragma unroll
             for (int w = 0; w < W; ++w)  // unconditional (a select would sink the load into a branch)
-                x[j][w] = a.nw_src[(ok[j] ? (uint64_t)u[j] : 0) * W + w] & (ok[j] ? ~0ull : 0ull);
+                x[j][w] = a.nw_src[GOSSIP_IDX(a, kChkPullGather, (ok[j] ? (uint64_t)u[j] : 0) * W + w, a.n_src * W)] &
+                          (ok[j] ? ~0ull : 0ull);
 #pragma unroll
         for (int j = 0; j < kRowB; ++j) acc.gathered += ok[j];
         bool done = true;
@@ -836,7 +837,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_heavy(RoundArgs a) {
                 if (!skip) {
 #pragma unroll
                     for (int w = 0; w < W; ++w)
-                        if (need[w]) part[w] |= a.nw_src[(uint64_t)u * W + w] & need[w];
+                        if (need[w]) part[w] |= a.nw_src[GOSSIP_IDX(a, kChkPullGather, (uint64_t)u * W + w, a.n_src * W)] & need[w];
                 }
             }
             if (a.heavy_exit && (++batch % kHeavyExitEvery) == 0 && e0 + 64 < ch.e1) {
@@ -1017,7 +1018,7 @@ __device__ __forceinline__ void scatter_stage(const RoundArgs& a, const BinArgs&
 #pragma unroll
     for (int k = 0; k < kSliceIt; ++k) {
         const uint64_t i = threadIdx.x + (uint64_t)k * kSB;
-        r[k] = i < nwords ? a.nw_src[vb * W + i] : 0ull;
+        r[k] = i < nwords ? a.nw_src[GOSSIP_IDX(a, kChkStageSrc, vb * W + i, a.n_src * W)] : 0ull;
     }
     __syncthreads();  // previous unit's readers are done with the slice
 #pragma unroll
@@ -1447,7 +1448,8 @@ __global__ __launch_bounds__(kSB) void k_bin_stream(RoundArgs a, BinArgs b, uint
         // (b.split_direct: a split chunk's later units, whose first unit stages the chunk and books its stats)
         const bool direct = (b.direct && !(vb < a.end && bin_chunk_ve(b, un.c, a.n_src) > a.begin)) ||
                             (b.split_direct && !un.first);  // block-uniform
-        const uint64_t* src = a.nw_src + vb * W;
+        const uint64_t ve = bin_chunk_ve(b, un.c, a.n_src);  // (the checked build's bound of a source)
+        (void)ve;
         if (!direct) {
             scatter_stage<W, COV, kCW, kSB>(a, b, un, wd, slice, live_s, cov_s, acc);
             __syncthreads();
@@ -1457,7 +1459,10 @@ __global__ __launch_bounds__(kSB) void k_bin_stream(RoundArgs a, BinArgs b, uint
         // the word source as a compile-time choice (a select would issue both loads)
         auto pieces = [&](auto dir) {
         constexpr bool kDirect = decltype(dir)::value;
-        auto word = [&](uint64_t u) { return kDirect ? src[u] : (uint64_t)slice[u]; };
+        auto word = [&](uint64_t u) {
+            return kDirect ? a.nw_src[GOSSIP_IDX(a, kChkStreamDirect, vb * W + u, ve * W)]
+                           : (uint64_t)slice[GOSSIP_IDX(a, kChkStreamSlice, u, (ve - vb) * W)];
+        };
         // Software-pipelined: the cb entries of a lane's next batch are loaded before the current batch's
         // words are stored.  vmcnt counts loads and stores in issue order, so a batch whose loads follow the
         // previous batch's stores waits for those stores' acknowledgements as well; issued one batch ahead,
@@ -1483,10 +1488,19 @@ __global__ __launch_bounds__(kSB) void k_bin_stream(RoundArgs a, BinArgs b, uint
                 for (int j = 0; j < kU; ++j) {
                     const uint64_t k = kb + (uint64_t)j * kSB;
                     if (k >= k1) break;
-                    const uint32_t u0 = sv[j] & (kRunStart - 1u), u1 = (sv[j] >> 16) & (kRunStart - 1u);
+                    const uint64_t e = 2 * k;
+                    // A piece cut by the unit's ends holds an entry of the neighbouring unit in cb order --
+                    // another chunk's local source id (e = p0 - 1 when p0 is odd, e + 1 = p1 when p1 is odd;
+                    // k in [k0, k1) keeps e + 1 >= p0 and e < p1).  Staged, that id only indexes the LDS slice
+                    // (any chunk-local id is < kCW) and its word is dropped below; read directly from the
+                    // gather buffer it addressed up to a chunk past this chunk's sources: past the buffer's
+                    // end for the last chunk of the ids (the illegal access of test_group_dense_exchange_
+                    // forms_equal_oracle[3-100003-3-direct], round 5).  Such an entry reads source 0 instead.
+                    constexpr bool kMask = kDirect || kChecked;
+                    const uint32_t u0 = kMask && e < un.p0 ? 0u : sv[j] & (kRunStart - 1u);
+                    const uint32_t u1 = kMask && e + 1 >= un.p1 ? 0u : (sv[j] >> 16) & (kRunStart - 1u);
                     const uint64_t x0 = word(u0);
                     const uint64_t x1 = word(u1);
-                    const uint64_t e = 2 * k;
                     if (e >= un.p0 && e + 2 <= un.p1) {
                         u64x2 y;
                         y.x = x0;
@@ -2397,7 +2411,8 @@ __global__ __launch_bounds__(kBlock) void k_apply_remote(RoundArgs a, const uint
 #pragma unroll
         for (int w = 0; w < W; ++w) {
             uint64_t inc = 0;
-            for (uint32_t p = 0; p < world; ++p) inc |= recv[((uint64_t)p * stride + v) * W + w];
+            for (uint32_t p = 0; p < world; ++p)
+                inc |= recv[GOSSIP_IDX(a, kChkApplyRemote, ((uint64_t)p * stride + v) * W + w, (uint64_t)world * stride * W)];
             if (!inc) continue;
             const uint64_t cur = a.seen[v * W + w];
             if (a.defer) {  // seen is folded in by k_commit_nx: this round's local receipts are in nx
@@ -2531,7 +2546,7 @@ __global__ __launch_bounds__(kBlock) void k_apply_records(RoundArgs a, const uin
     Acc acc;
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n_rec; i += (uint64_t)gridDim.x * kBlock) {
         const uint64_t* r = rec + i * (1 + W);
-        const uint64_t lv = r[0] - a.begin;
+        const uint64_t lv = GOSSIP_IDX(a, kChkApplyRecord, r[0] - a.begin, a.n_local);
         unsigned long long* sp = reinterpret_cast<unsigned long long*>(a.seen) + lv * W;
 #pragma unroll
         for (int w = 0; w < W; ++w) {

@@ -34,6 +34,7 @@ FLAG_NO_BIN = 8
 FLAG_FORCE_BIN = 16
 FLAG_NO_BLOCKED = 32
 FLAG_FORCE_BLOCKED = 64
+FLAG_UNIFORM_PARTITION = 128
 MODE_AUTO = -1
 MODE_PUSH = 0
 MODE_PULL = 1

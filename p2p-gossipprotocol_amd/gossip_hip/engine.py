@@ -73,7 +73,7 @@ def make_config(n_peers: int, n_msgs: int, *, rng_seed: int = 0, graph: str = "p
                 part: tuple[int, int] = (0, 0), report_capacity: int = 0, mode: str = "auto",
                 pull_permille: int = 0, front_permille: int = 0, bin_permille: int = 0, bins: bool = True,
                 extra_cap: int = 0, list_cap: int = 0, rejoin_threshold: int = 0, blocked: str = "auto",
-                blocked_permille: int = 0) -> GossipConfig:
+                blocked_permille: int = 0, uniform_partition: bool = False) -> GossipConfig:
     """gossip_config from keyword arguments (the fields of include/gossip/gossip.h)."""
     cfg = GossipConfig()
     cfg.n_peers = n_peers
@@ -91,7 +91,8 @@ def make_config(n_peers: int, n_msgs: int, *, rng_seed: int = 0, graph: str = "p
     cfg.device = device
     cfg.flags = (_abi.FLAG_COVERAGE_HISTORY if coverage_history else 0) | (0 if bins else _abi.FLAG_NO_BIN) | {
         "auto": 0, "push": _abi.FLAG_FORCE_PUSH, "pull": _abi.FLAG_FORCE_PULL, "bin": _abi.FLAG_FORCE_BIN}[mode] | {
-        "auto": 0, "off": _abi.FLAG_NO_BLOCKED, "force": _abi.FLAG_FORCE_BLOCKED}[blocked]
+        "auto": 0, "off": _abi.FLAG_NO_BLOCKED, "force": _abi.FLAG_FORCE_BLOCKED}[blocked] | (
+        _abi.FLAG_UNIFORM_PARTITION if uniform_partition else 0)
     cfg.report_capacity = report_capacity
     cfg.pull_permille = pull_permille
     cfg.front_permille = front_permille
@@ -211,7 +212,9 @@ class Engine:
         return self._run_n.value
 
     def last_stats(self) -> list[dict]:
-        """The rounds of the last run_into(), as run() returns them."""
+        """The rounds of the last run_into(), as run() returns them ([] before the first)."""
+        if getattr(self, "_run_buf", None) is None:
+            return []
         return [self._run_buf[i].as_dict() for i in range(min(self._run_n.value, len(self._run_buf)))]
 
     # partitioned phases (see distributed.py)
@@ -429,7 +432,9 @@ class Group:
         return self._run_n.value
 
     def last_stats(self) -> list[dict]:
-        """The rounds of the last run_into(), as run() returns them."""
+        """The rounds of the last run_into(), as run() returns them ([] before the first)."""
+        if getattr(self, "_run_buf", None) is None:
+            return []
         return [self._run_buf[i].as_dict() for i in range(min(self._run_n.value, len(self._run_buf)))]
 
     def read_seen(self) -> np.ndarray:

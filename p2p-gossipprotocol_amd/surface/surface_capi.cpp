@@ -84,6 +84,48 @@ int gossip_surface_seed(const char* ops, char* out, size_t cap) {
     }
 }
 
+// gossip_json from every field (a received message's bytes rebuilt from what it carries)
+int gossip_surface_gossip_json(const char* content, const char* hash, int msg_number, const char* ip, int port,
+                               const char* timestamp, char* out, size_t cap) {
+    return put(gossip::gossip_json(content, hash, msg_number, ip, port, timestamp), out, cap);
+}
+
+// peer_list_json of entries "<ip> <port> <lastSeen>", one per line, in the given order
+int gossip_surface_peer_list(const char* entries, char* out, size_t cap) {
+    std::vector<PeerInfo> peers;
+    std::istringstream in(entries ? entries : "");
+    std::string ip;
+    int port = 0;
+    long long t = 0;
+    while (in >> ip >> port >> t)
+        peers.push_back(PeerInfo{ip, port, std::chrono::system_clock::time_point(std::chrono::seconds(t))});
+    return put(gossip::peer_list_json(peers), out, cap);
+}
+
+// gossip_surface_seed with the seed's log: start() and every request logged to <logdir>/seed_8000_output.txt
+int gossip_surface_seed_logged(const char* ops, const char* logdir, char* out, size_t cap) {
+    try {
+        SeedNode seed("127.0.0.1", 8000);
+        std::istringstream in(ops ? ops : "");
+        std::string line, res;
+        bool started = false;
+        while (std::getline(in, line)) {
+            const size_t sp = line.find(' ');
+            if (sp == std::string::npos) continue;
+            seed.setClock(std::stoll(line.substr(0, sp)));
+            if (!started) {
+                seed.setLogDir(logdir ? logdir : "");
+                seed.start();
+                started = true;
+            }
+            res += seed.handleRequest(line.substr(sp + 1)) + "\n";
+        }
+        return put(res, out, cap);
+    } catch (const std::exception&) {
+        return -2;
+    }
+}
+
 int gossip_surface_log(int seed_style, long long t, const char* msg, char* out, size_t cap) {
     return put(seed_style ? gossip::seed_log_line((std::time_t)t, msg) : gossip::peer_log_line((std::time_t)t, msg), out,
                cap);

@@ -155,3 +155,64 @@ def test_group_run_into_keeps_stats_in_a_reused_buffer(oracle):
             assert g.run_into() == len(ref["stats"])
             assert g.last_stats() == ref["stats"]
         assert np.array_equal(g.read_seen(), ref["seen"])
+
+
+def _ref_bootstrap_workload(n):
+    """The literal bootstrap overlay (config 1's model, n <= 4096) at n peers: 64 messages from peers spread over
+    the ids at round 0, peer 3 killed at round 12, pings every 15 rounds -- config 1 sends 10 messages per peer,
+    more than 512 at n > 51."""
+    from dataclasses import replace
+    w = config(1, 8)
+    o = (np.arange(64, dtype=np.uint32) * (n // 64)).astype(np.uint32)
+    return replace(w, n=n, n_msgs=64, origins=o, inject_rounds=np.zeros(64, dtype=np.uint32),
+                   name=f"ref_bootstrap_{n}")
+
+
+@pytest.mark.parametrize("n,P", [(4000, 2), (1001, 3)])
+def test_group_ref_bootstrap_blocks_round_up_to_tiles(oracle, n, P):
+    """gossip_group_create on an overlay other than powerlaw cuts ceil(n/P) blocks rounded up to whole 64-peer
+    tiles (gossip_group_create_parts takes only tile-aligned blocks; round 5 returned EINVAL here):
+    the literal bootstrap DAG at a peer count off a tile boundary gives the oracle's run."""
+    import ctypes as C
+    w = _ref_bootstrap_workload(n)
+    rp, col = oracle.gen_workload(w)
+    ref = oracle.simulate_workload(w, rp, col)
+    rp = np.asarray(rp, dtype=np.uint64)
+    col = np.asarray(col, dtype=np.uint32)
+    with Group(w.n, w.n_msgs, [0] * P, **w.engine_kwargs()) as g:
+        # the literal DAG is generated single-partition only: each block loads its rows (gossip_load_csr)
+        b = [0]
+        for p in range(P):
+            b.append(b[-1] + g.shape(p)["n_local"])
+        assert all(x % 64 == 0 for x in b[:-1]) and b[-1] == n
+        for p in range(P):
+            lrp = np.ascontiguousarray(rp[b[p]:b[p + 1] + 1] - rp[b[p]])
+            lcol = np.ascontiguousarray(col[rp[b[p]]:rp[b[p + 1]]])
+            st = g._L.gossip_load_csr(g.part_ctx(p), lrp.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                      lcol.ctypes.data_as(C.POINTER(C.c_uint32)), lrp.size - 1, int(lrp[-1]))
+            assert st == 0, g._L.gossip_last_error().decode()
+        g.inject(w.origins, w.inject_rounds)
+        g.schedule_kills([k[0] for k in w.kills], [k[1] for k in w.kills])
+        g.reset()
+        stats = g.run()
+        assert stats == ref["stats"]
+        assert np.array_equal(g.read_seen(), ref["seen"])
+        assert np.array_equal(g.reports(), ref["reports"])
+
+
+def test_group_uniform_partition_rounds_up_to_tiles(oracle):
+    """GOSSIP_FLAG_UNIFORM_PARTITION with ceil(n/P) off a tile (100,003 / 3 = 33,335): tile-aligned blocks, the
+    oracle's run."""
+    w = config(3, 100_003, pick=oracle.pick_origins)
+    rp, col = oracle.gen_workload(w)
+    ref = oracle.simulate_workload(w, rp, col)
+    stats, seen, reps, again = _run_group(w, [0] * 3, uniform_partition=True)
+    assert stats == ref["stats"]
+    assert np.array_equal(seen, ref["seen"])
+    assert again == stats
+
+
+def test_group_too_small_for_whole_tiles_is_einval():
+    from gossip_hip import GossipError
+    with pytest.raises(GossipError, match="64-peer tiles"):
+        Group(100, 64, [0, 0, 0], graph="ref_bootstrap")  # 64-peer blocks: [0, 64, 100, 100]

@@ -19,6 +19,16 @@ def test_blocks_are_contiguous_tiles(P):
     assert all(x % 64 == 0 for x in b[:-1])
 
 
+@pytest.mark.parametrize("n,P", [(191, 2), (200, 3), (1000, 8), (4097, 4), (1 << 14 | 5, 8)])
+def test_small_blocks_off_a_tile_stay_whole_tiles(n, P):
+    """n % 64 != 0: the room kept for the blocks after a boundary is a whole number of tiles too (round 5
+    capped a boundary at n - 64 (P - q), off a tile -- [0, 127, 191] -- which gossip_group_create_parts rejects)."""
+    b = partition_edges(n, 64, P)
+    assert b[0] == 0 and b[-1] == n and all(b[q + 1] > b[q] for q in range(P))
+    if n >= 64 * P:
+        assert all(x % 64 == 0 for x in b[:-1]), b
+
+
 def test_other_overlays_and_tiny_ones_get_uniform_blocks():
     assert partition_edges(4096, 64, 4, graph="ref_bootstrap") == partition(4096, 4)
     assert partition_edges(100, 64, 3) == partition(100, 3)  # fewer than 64 peers per block
