@@ -1,7 +1,8 @@
 // info.hpp -- drop-in PeerInfo / PeerInfoHash (reference: info.hpp:6-39).
-// The reference serialises PeerInfo with nlohmann::json (absent from this
-// image); the wire form {"ip","lastSeen","port"} (sorted keys, compact) is
-// produced by gossip/formats.hpp instead.
+// The reference serialises PeerInfo with nlohmann::json (info.hpp:23-39); the
+// surface does not depend on it: the wire form {"ip","lastSeen","port"} (sorted
+// keys, compact) is produced by gossip/formats.hpp, byte-exact against the
+// reference's own serialiser (tests/test_ref_wire.py).
 #pragma once
 
 #include <chrono>

@@ -6,12 +6,14 @@
  * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use it,
  * and only as the checker / the timed CPU baseline.
  *
- * The reference (PareenShah27/P2P-GossipProtocol @ 2025-02-25) is not
- * buildable (nlohmann/json absent, broken Makefile, deadlock at
- * peer.cpp:280->283->126), so this file restates the
- * *intended* semantics of peer.cpp as the deterministic round model of
- * DESIGN.md section 2 ("round contract").  Each function cites the reference
- * lines it follows.
+ * The reference (PareenShah27/P2P-GossipProtocol @ 2025-02-25) compiles here
+ * from its sources with the image's nlohmann/json 3.1.1 (oracle/Makefile ref;
+ * its own Makefile is broken, F1), but its hot path cannot run: a peer stops
+ * at its first receipt (peer.cpp:280->283->126, F3, observed in
+ * tests/golden/ref_wire.json).  So this file restates the *intended*
+ * semantics of peer.cpp as the deterministic round model of DESIGN.md
+ * section 2 ("round contract").  Each function cites the reference lines it
+ * follows.
  *
  * Parity pinning: Philox4x32-10 is pinned by the Random123 KATs
  * (tests/golden/philox_kat.json); the ref_bootstrap generator by the
@@ -20,7 +22,10 @@
  * (tests/golden/hand_graphs.json) and by two independent drivers
  * (literal message-list driver vs 64-bit-mask driver) that must agree.
  * The NetworkConfig restatement is pinned against the real reference
- * config.cpp compiled into oracle/_ref/ (tests/golden/config_cases.json).
+ * config.cpp compiled into oracle/_ref/ (tests/golden/config_cases.json);
+ * the seed registry and the wire and log formats of the surface against the
+ * reference's seed.cpp / peer.cpp / info.hpp run here (tests/golden/
+ * ref_wire.json).
  */
 #ifndef GOSSIP_ORACLE_H
 #define GOSSIP_ORACLE_H

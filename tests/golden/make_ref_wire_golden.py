@@ -1,0 +1,267 @@
+"""Regenerates ref_wire.json from the REAL reference, run here (TEST INFRASTRUCTURE ONLY; the build container
+holds /root/reference, the GPU box does not -- the committed JSON is what the tests read).
+
+`make -C oracle ref` compiles the reference's own sources where they lie under /root/reference, with the image's
+real nlohmann/json 3.1.1 (/opt/conda/include/json.hpp), into oracle/_ref/:
+
+1. registry: ref_registry_driver runs a script of SeedNode::addPeer / handleDeadNode / getPeerList calls
+   (seed.cpp:153-178) and json(PeerInfo).dump() (info.hpp:23-39); its outputs, stdout and seed log are stored.
+2. tcp: the reference's seed (ref_seed: SeedNode::start, seed.cpp:25-151) and the reference's program
+   (peer_network: main.cpp + wrapper.cpp + peer.cpp + seed.cpp + config.cpp) on 127.0.0.1.  A recording proxy
+   in front of the seed keeps every request and reply; listeners registered as peers keep what the reference
+   peer sends them.  Stored: the peer's register bytes (peer.cpp:176-180), the seed's peer_list replies
+   (seed.cpp:120-125), the gossip messages the peer generated and broadcast (peer.cpp:297-318,357-379), what
+   happened when a listener sent the peer a gossip message (F3: the receiving thread locks messageMutex at
+   peer.cpp:280 and again in logToFile at :283 -> :126), the seed's handling of a dead_node request
+   (seed.cpp:130-138,158-167), both log files and the program's stdout.
+
+Timestamps of the live run are the wall clock of this container; the tests rebuild every byte string from the
+fields it carries.  usage: python3 tests/golden/make_ref_wire_golden.py
+"""
+import json
+import os
+import signal
+import socket
+import subprocess
+import sys
+import tempfile
+import threading
+import time
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+REPO = HERE.parent.parent
+REF = REPO / "oracle" / "_ref"
+PEER_PORT = 5000            # the reference's hard-coded local port (config.cpp:39)
+PEER_IP = "192.168.99.96"   # ... and address (config.cpp:38)
+EPOCH = 1740441600
+
+
+def compact(obj) -> bytes:
+    return json.dumps(obj, sort_keys=True, separators=(",", ":")).encode()
+
+
+# ---------------------------------------------------------------------------------------------------------
+def registry_case() -> dict:
+    script = [f"add 127.0.0.1 {5000 + i} {EPOCH + i}" for i in range(8)]
+    script += ["list", f"add 127.0.0.1 5002 {EPOCH + 100}", "list",           # a second registration keeps the key
+               "dead 127.0.0.1 5003", "dead 127.0.0.1 5003", "dead 10.0.0.9 1",  # erase once, then no-ops
+               "list", f"add 127.0.0.1 5003 {EPOCH + 200}", "list",             # a removed peer registers again
+               f"peer 127.0.0.1 5000 {EPOCH}", f"peer {PEER_IP} {PEER_PORT} 0", "peer 10.1.2.3 65535 4102444800",
+               'peer a"b\\c 7 1']
+    with tempfile.TemporaryDirectory() as td:
+        r = subprocess.run([str(REF / "ref_registry_driver")], input="\n".join(script) + "\n", capture_output=True,
+                           text=True, cwd=td, check=True, timeout=60)
+        log = (Path(td) / "seed_7999_output.txt").read_text() if (Path(td) / "seed_7999_output.txt").exists() else ""
+    results = [ln[1:] for ln in r.stdout.splitlines() if ln.startswith("@")]
+    stdout = [ln for ln in r.stdout.splitlines() if not ln.startswith("@")]
+    assert len(results) == len(script), (results, script)
+    return {"script": script, "results": results, "stdout": stdout, "log": log}
+
+
+# ---------------------------------------------------------------------------------------------------------
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def wait_port(port: int, timeout: float = 10.0) -> None:
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        try:
+            with socket.create_connection(("127.0.0.1", port), timeout=0.5):
+                return
+        except OSError:
+            time.sleep(0.05)
+    raise RuntimeError(f"port {port} never opened")
+
+
+class Proxy(threading.Thread):
+    """Forwards every connection to the seed and records each chunk in both directions."""
+
+    def __init__(self, seed_port: int):
+        super().__init__(daemon=True)
+        self.seed_port = seed_port
+        self.srv = socket.socket()
+        self.srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        self.srv.bind(("127.0.0.1", 0))
+        self.srv.listen(16)
+        self.port = self.srv.getsockname()[1]
+        self.log: list[dict] = []
+        self.lock = threading.Lock()
+
+    def run(self):
+        while True:
+            try:
+                c, _ = self.srv.accept()
+            except OSError:
+                return
+            threading.Thread(target=self.pair, args=(c,), daemon=True).start()
+
+    def pair(self, c):
+        s = socket.create_connection(("127.0.0.1", self.seed_port))
+        conn = {"requests": [], "replies": []}
+        with self.lock:
+            self.log.append(conn)
+
+        def pump(a, b, key):
+            while True:
+                try:
+                    d = a.recv(65536)
+                except OSError:
+                    d = b""
+                if not d:
+                    try:
+                        b.shutdown(socket.SHUT_WR)
+                    except OSError:
+                        pass
+                    return
+                with self.lock:
+                    conn[key].append(d.decode())
+                b.sendall(d)
+
+        t = threading.Thread(target=pump, args=(s, c, "replies"), daemon=True)
+        t.start()
+        pump(c, s, "requests")
+
+
+class Listener(threading.Thread):
+    """A peer address the seed hands out: records every byte the reference peer sends it, per connection."""
+
+    def __init__(self):
+        super().__init__(daemon=True)
+        self.srv = socket.socket()
+        self.srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        self.srv.bind(("127.0.0.1", 0))
+        self.srv.listen(64)
+        self.port = self.srv.getsockname()[1]
+        self.chunks: list[tuple[float, str]] = []
+        self.conns = 0
+        self.lock = threading.Lock()
+
+    def run(self):
+        while True:
+            try:
+                c, _ = self.srv.accept()
+            except OSError:
+                return
+            with self.lock:
+                self.conns += 1
+            threading.Thread(target=self.read, args=(c,), daemon=True).start()
+
+    def read(self, c):
+        while True:
+            try:
+                d = c.recv(65536)
+            except OSError:
+                return
+            if not d:
+                return
+            with self.lock:
+                self.chunks.append((time.time(), d.decode()))
+
+
+def request(port: int, payload: bytes, reply: bool) -> str:
+    with socket.create_connection(("127.0.0.1", port), timeout=5) as s:
+        s.sendall(payload)
+        if not reply:
+            time.sleep(0.3)
+            return ""
+        return s.recv(65536).decode()
+
+
+def tcp_case() -> dict:
+    with tempfile.TemporaryDirectory() as td:
+        seed_port = free_port()
+        seed = subprocess.Popen([str(REF / "ref_seed"), str(seed_port)], cwd=td, stdout=subprocess.PIPE,
+                                stderr=subprocess.STDOUT, text=True, start_new_session=True)
+        peer = None
+        try:
+            wait_port(seed_port)
+            proxy = Proxy(seed_port)
+            proxy.start()
+            listeners = [Listener() for _ in range(6)]
+            for li in listeners:
+                li.start()
+            # the listeners register first (the harness's requests, compact sorted JSON as nlohmann dumps it)
+            reg_replies = []
+            for li in listeners:
+                reg_replies.append(request(proxy.port, compact({"ip": "127.0.0.1", "port": li.port,
+                                                                "type": "register"}), True))
+                time.sleep(1.05)  # distinct lastSeen seconds
+            cfg = Path(td) / "network.txt"
+            cfg.write_text(f"127.0.0.1:{proxy.port}\n")
+            peer = subprocess.Popen([str(REF / "peer_network"), str(cfg)], cwd=td, stdout=subprocess.PIPE,
+                                    stderr=subprocess.STDOUT, text=True, start_new_session=True)
+            t_start = time.time()
+            # messageGenerationLoop: message 0 at once, then one every 5 s (peer.cpp:357-378)
+            time.sleep(7.0)
+            got_before = {li.port: list(li.chunks) for li in listeners}
+            # a listener the peer connected to sends it a gossip message (as broadcastMessage formats one);
+            # the receiving thread takes messageMutex (peer.cpp:280) and logToFile takes it again (:283 -> :126)
+            target = next(li for li in listeners if li.chunks)
+            m0 = json.loads(target.chunks[0][1])
+            probe = {"content": "Message from 127.0.0.1:%d" % target.port, "hash": "0" * 64, "msg_number": 0,
+                     "source_ip": "127.0.0.1", "source_port": target.port, "timestamp": str(int(time.time() * 1e9)),
+                     "type": "gossip"}
+            t_probe = time.time()
+            request(PEER_PORT, compact(probe), False)
+            time.sleep(9.0)  # two more generation ticks would have come by now
+            got_after = {li.port: [c for c in li.chunks if c[0] > t_probe] for li in listeners}
+            # the seed: a dead_node request for the first listener, then one more registration
+            dead = listeners[0]
+            request(proxy.port, compact({"dead_ip": "127.0.0.1", "dead_port": dead.port, "type": "dead_node"}), False)
+            late = Listener()
+            late.start()
+            late_reply = request(proxy.port, compact({"ip": "127.0.0.1", "port": late.port, "type": "register"}), True)
+            elapsed = time.time() - t_start
+        finally:
+            for p in (peer, seed):
+                if p is not None:
+                    try:
+                        os.killpg(p.pid, signal.SIGKILL)
+                    except ProcessLookupError:
+                        pass
+                    p.wait(timeout=10)
+        peer_out = peer.stdout.read() if peer else ""
+        seed_out = seed.stdout.read()
+        peer_log = (Path(td) / f"peer_{PEER_PORT}_output.txt").read_text()
+        seed_log = (Path(td) / f"seed_{seed_port}_output.txt").read_text()
+    peer_conn = [c for c in proxy.log if any(f'"ip":"{PEER_IP}"' in r for r in c["requests"])]
+    return {
+        "seed_port": seed_port, "proxy_port": proxy.port, "peer_ip": PEER_IP, "peer_port": PEER_PORT,
+        "listeners": [li.port for li in listeners], "late_listener": late.port, "dead_listener": dead.port,
+        "listener_register_replies": reg_replies,
+        "peer_register_request": peer_conn[0]["requests"] if peer_conn else [],
+        "peer_register_reply": peer_conn[0]["replies"] if peer_conn else [],
+        "connections_per_listener": {str(li.port): li.conns for li in listeners},
+        "gossip_received_before_probe": {str(k): [c[1] for c in v] for k, v in got_before.items()},
+        "probe": json.dumps(probe, sort_keys=True, separators=(",", ":")), "probe_target": target.port,
+        "probe_first_message_seen": m0,
+        "gossip_received_after_probe": {str(k): [c[1] for c in v] for k, v in got_after.items()},
+        "late_register_reply": late_reply,
+        "seed_log": seed_log, "peer_log": peer_log, "peer_stdout": peer_out, "seed_stdout": seed_out,
+        "elapsed_s": round(elapsed, 2),
+    }
+
+
+def main():
+    for tool in ("ref_registry_driver", "ref_seed", "peer_network"):
+        if not (REF / tool).exists():
+            sys.exit(f"{REF / tool} missing: run `make -C oracle ref` (needs /root/reference and nlohmann/json)")
+    out = {
+        "source": "the reference compiled by oracle/Makefile (ref target) with nlohmann/json 3.1.1 "
+                  "(/opt/conda/include/json.hpp) and OpenSSL libcrypto; tests/golden/make_ref_wire_golden.py",
+        "registry": registry_case(),
+        "tcp": tcp_case(),
+    }
+    (HERE / "ref_wire.json").write_text(json.dumps(out, indent=1) + "\n")
+    t = out["tcp"]
+    print("registry results:", len(out["registry"]["results"]), "| peer register:", t["peer_register_request"],
+          "| gossip before probe:", {k: len(v) for k, v in t["gossip_received_before_probe"].items()},
+          "| after:", {k: len(v) for k, v in t["gossip_received_after_probe"].items()}, "| elapsed", t["elapsed_s"])
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,219 @@
+"""CPU tests of the drop-in surface against the REAL reference, run in the build container
+(tests/golden/ref_wire.json, made by tests/golden/make_ref_wire_golden.py from the reference's seed.cpp,
+peer.cpp, info.hpp, main.cpp, wrapper.cpp and config.cpp compiled by oracle/Makefile with the image's
+nlohmann/json 3.1.1 and OpenSSL):
+
+- A2, the seed registry (seed.cpp:153-178): the reference's SeedNode driven through a script of registrations
+  and dead-node reports, and the reference seed over TCP; the surface SeedNode given the same requests holds
+  the same peers with the same lastSeen after every step (compared as sets: the reference iterates an
+  unordered_map), prints and logs the same lines (seed.cpp:59,127-137,163-165,180-188).
+- (f)1, the wire formats: the reference peer's register request (peer.cpp:176-180), the seed's peer_list
+  replies (seed.cpp:120-125, info.hpp:26-32), the gossip messages the reference peer generated and broadcast
+  (peer.cpp:297-307,357-367) with their SHA-256 labels (peer.cpp:135-159) and every log line, byte for byte.
+- F3: the reference peer stops at its first receipt -- recorded, so the hot path's own parity stays
+  pinned to the round model, not to a run of the reference.
+"""
+import calendar
+import ctypes as C
+import json
+import subprocess
+import time
+from pathlib import Path
+
+import pytest
+
+REPO = Path(__file__).resolve().parent.parent
+BUILD = REPO / "p2p-gossipprotocol_amd" / "build"
+WIRE = json.loads((REPO / "tests" / "golden" / "ref_wire.json").read_text())
+
+
+@pytest.fixture(scope="module")
+def surf():
+    L = C.CDLL(str(BUILD / "libgossip_surface.so"))
+    for name in ("gossip_surface_gossip_json", "gossip_surface_peer_list", "gossip_surface_seed_logged",
+                 "gossip_surface_hash", "gossip_surface_register", "gossip_surface_dead_node", "gossip_surface_log"):
+        getattr(L, name).restype = C.c_int
+    return L
+
+
+def _call(fn, *args):
+    buf = C.create_string_buffer(1 << 18)
+    assert fn(*args, buf, C.c_size_t(len(buf))) == 0
+    return buf.value.decode()
+
+
+def _entries(reply: str) -> set:
+    return {(p["ip"], p["port"], p["lastSeen"]) for p in json.loads(reply)["peers"]}
+
+
+def _log_pairs(text: str, sep: str):
+    """A reference log -- ctime(t) (its '\\n' included) + sep + message + '\\n' per entry -- as (t, message)."""
+    lines = text.split("\n")
+    assert lines[-1] == ""
+    out = []
+    for i in range(0, len(lines) - 1, 2):
+        t = calendar.timegm(time.strptime(lines[i], "%a %b %d %H:%M:%S %Y"))  # the container's clock is UTC
+        assert lines[i + 1].startswith(sep)
+        out.append((t, lines[i + 1][len(sep):]))
+    return out
+
+
+# ---- A2: the registry ---------------------------------------------------------------------------------
+def _surface_ops(script):
+    """The reference driver's script as surface SeedNode requests ('<clock> <json>')."""
+    ops, lists = [], []
+    for cmd in script:
+        w = cmd.split()
+        if w[0] == "add":
+            ops.append(f"{w[3]} " + json.dumps({"ip": w[1], "port": int(w[2]), "type": "register"}))
+            lists.append(len(ops) - 1)  # a register answers with the list after it
+        elif w[0] == "dead":
+            ops.append("0 " + json.dumps({"dead_ip": w[1], "dead_port": int(w[2]), "type": "dead_node"}))
+    return ops, lists
+
+
+def test_registry_removals_match_reference_seed(surf, tmp_path, capfd):
+    """The whole script: a dead-node report erases a registered peer once, printing and logging "Removed dead
+    peer" (seed.cpp:162-165); a second report, or one for a peer never registered, does nothing."""
+    reg = WIRE["registry"]
+    ops, _ = _surface_ops(reg["script"])
+    _call(surf.gossip_surface_seed_logged, "\n".join(ops).encode(), str(tmp_path).encode())
+    printed = [ln for ln in capfd.readouterr().out.splitlines() if ln.startswith("Removed dead peer")]
+    assert printed == reg["stdout"]
+    # (the reference driver calls addPeer directly, so its log holds only the removal)
+    ref_msgs = [m for _, m in _log_pairs(reg["log"], "")]
+    ours = [m for _, m in _log_pairs((tmp_path / "seed_8000_output.txt").read_text(), "")]
+    assert ref_msgs == [m for m in ours if m.startswith("Removed dead peer")]
+
+
+def test_registry_state_after_each_list(surf):
+    """The same script, each "list" answered by a fresh surface seed replaying the commands before it plus one
+    probe registration, minus the probe: every reference getPeerList (seed.cpp:169-178) as a set."""
+    reg = WIRE["registry"]
+    for i, (cmd, res) in enumerate(zip(reg["script"], reg["results"])):
+        if cmd != "list":
+            continue
+        ops, _ = _surface_ops(reg["script"][:i])
+        probe = "9 " + json.dumps({"ip": "203.0.113.1", "port": 1, "type": "register"})
+        out = _call(surf.gossip_surface_seed_logged, "\n".join(ops + [probe]).encode(), b"").split("\n")
+        got = _entries(out[len(ops)]) - {("203.0.113.1", 1, 9)}
+        assert got == _entries(res), cmd
+
+
+def test_peer_info_json_matches_nlohmann(surf):
+    """json(PeerInfo).dump() (info.hpp:23-33, nlohmann 3.1.1): sorted keys, compact, lastSeen as time_t, the ip
+    escaped as nlohmann escapes it; and the whole register reply {"peers":[...],"type":"peer_list"}."""
+    reg = WIRE["registry"]
+    for cmd, res in zip(reg["script"], reg["results"]):
+        w = cmd.split()
+        if w[0] == "peer":
+            one = _call(surf.gossip_surface_peer_list, f"{w[1]} {w[2]} {w[3]}".encode())
+            assert one == '{"peers":[' + res + '],"type":"peer_list"}'
+        elif w[0] == "list":
+            ent = "\n".join(f'{p["ip"]} {p["port"]} {p["lastSeen"]}' for p in json.loads(res)["peers"])
+            assert _call(surf.gossip_surface_peer_list, ent.encode()) == res
+
+
+# ---- the wire, over TCP -----------------------------------------------------------------------------------
+def test_register_request_is_reference_peers(surf):
+    t = WIRE["tcp"]
+    assert t["peer_register_request"] == [_call(surf.gossip_surface_register, t["peer_ip"].encode(), t["peer_port"])]
+
+
+def test_peer_list_replies_are_reference_seeds(surf):
+    """Every peer_list the reference seed sent (to the listeners, to the reference peer, after a dead_node),
+    rebuilt by peer_list_json from its own entries in its order: the same bytes."""
+    t = WIRE["tcp"]
+    replies = t["listener_register_replies"] + t["peer_register_reply"] + [t["late_register_reply"]]
+    assert len(replies) == len(t["listeners"]) + 2
+    for r in replies:
+        ent = "\n".join(f'{p["ip"]} {p["port"]} {p["lastSeen"]}' for p in json.loads(r)["peers"])
+        assert _call(surf.gossip_surface_peer_list, ent.encode()) == r
+
+
+def test_seed_over_tcp_matches_surface_seed(surf, tmp_path):
+    """The reference seed's requests in arrival order, replayed into the surface SeedNode at the reference's
+    clock (a registration's second is its entry's lastSeen in the reply): the same peer set after every
+    registration, the dead listener gone, and the same log messages in order (less "New client connection
+    accepted", which the reference logs per TCP connection in handleClient, seed.cpp:94-96)."""
+    t = WIRE["tcp"]
+    regs = [(p, r) for p, r in zip(t["listeners"], t["listener_register_replies"])]
+    peer_reply = t["peer_register_reply"][0]
+    ops, want = [], []
+    for port, reply in regs:
+        ts = next(p["lastSeen"] for p in json.loads(reply)["peers"] if p["port"] == port)
+        ops.append(f"{ts} " + json.dumps({"ip": "127.0.0.1", "port": port, "type": "register"}))
+        want.append(_entries(reply))
+    ts = next(p["lastSeen"] for p in json.loads(peer_reply)["peers"] if p["port"] == t["peer_port"])
+    ops.append(f"{ts} " + t["peer_register_request"][0])
+    want.append(_entries(peer_reply))
+    ops.append(f"{ts} " + json.dumps({"dead_ip": "127.0.0.1", "dead_port": t["dead_listener"], "type": "dead_node"}))
+    want.append(None)
+    late = json.loads(t["late_register_reply"])["peers"]
+    ts = next(p["lastSeen"] for p in late if p["port"] == t["late_listener"])
+    ops.append(f"{ts} " + json.dumps({"ip": "127.0.0.1", "port": t["late_listener"], "type": "register"}))
+    want.append(_entries(t["late_register_reply"]))
+    out = _call(surf.gossip_surface_seed_logged, "\n".join(ops).encode(), str(tmp_path).encode()).split("\n")
+    for o, w in zip(out, want):
+        if w is None:
+            assert o == ""
+        else:
+            assert _entries(o) == w
+    assert ("127.0.0.1", t["dead_listener"]) not in {(a, b) for a, b, _ in _entries(out[len(ops) - 1])}
+    ref = [m for _, m in _log_pairs(t["seed_log"], "") if m != "New client connection accepted"]
+    ref = [m.replace(f"port {t['seed_port']}", "port 8000") for m in ref]
+    ours = [m for _, m in _log_pairs((tmp_path / "seed_8000_output.txt").read_text(), "")]
+    assert ours == ref
+
+
+def test_gossip_messages_are_reference_peers(surf):
+    """The messages the reference peer generated (messageGenerationLoop, peer.cpp:357-378) as its listener
+    received them: content "Message from <ip>:<port>", the SHA-256 label of content || timestamp || source ip
+    (peer.cpp:135-159, OpenSSL), and gossip_json of the fields -- the same bytes (peer.cpp:298-307)."""
+    t = WIRE["tcp"]
+    got = [m for v in t["gossip_received_before_probe"].values() for m in v]
+    assert len(got) >= 2
+    for raw in got:
+        m = json.loads(raw)
+        assert m["content"] == f'Message from {t["peer_ip"]}:{t["peer_port"]}'
+        assert len(m["timestamp"]) == 19  # nanoseconds since the epoch (peer.cpp:361)
+        assert _call(surf.gossip_surface_hash, m["content"].encode(), m["timestamp"].encode(),
+                     m["source_ip"].encode()) == m["hash"]
+        assert _call(surf.gossip_surface_gossip_json, m["content"].encode(), m["hash"].encode(), m["msg_number"],
+                     m["source_ip"].encode(), m["source_port"], m["timestamp"].encode()) == raw
+    assert sorted(json.loads(r)["msg_number"] for r in got) == list(range(len(got)))
+
+
+def test_log_lines_are_reference_bytes(surf):
+    """Every line of the reference peer's and seed's logs (peer.cpp:125-133: ctime + ": " + msg; seed.cpp:180-188:
+    ctime + msg) rebuilt by the surface from (time, message)."""
+    t = WIRE["tcp"]
+    for text, style, sep in ((t["peer_log"], 0, ": "), (t["seed_log"], 1, "")):
+        rebuilt = "".join(_call(surf.gossip_surface_log, style, C.c_longlong(ts), m.encode())
+                          for ts, m in _log_pairs(text, sep))
+        assert rebuilt == text
+
+
+def test_reference_peer_stops_at_its_first_receipt():
+    """F3, observed: after a listener sent the reference peer one gossip message, the peer logged nothing for it
+    ("Received new message" never appears: handleClient holds messageMutex, peer.cpp:280, and logToFile locks it
+    again, :283 -> :126) and generated nothing more (messageGenerationLoop blocks on the same mutex, :370),
+    where it had sent a message every 5 s before."""
+    t = WIRE["tcp"]
+    before = sum(len(v) for v in t["gossip_received_before_probe"].values())
+    after = sum(len(v) for v in t["gossip_received_after_probe"].values())
+    assert before >= 2 and after == 0
+    assert "Received new message" not in t["peer_log"]
+    assert t["peer_log"].count("Generated message") == before
+
+
+def test_cli_prints_the_reference_programs_lines(tmp_path):
+    """gossip_peer_network prints what the reference's main.cpp printed for the same network.txt, up to
+    "Starting peer node..." (main.cpp:43-57; the reference then blocks in its accept loop)."""
+    t = WIRE["tcp"]
+    cfg = tmp_path / "network.txt"
+    cfg.write_text(f"127.0.0.1:{t['proxy_port']}\n")
+    r = subprocess.run([str(BUILD / "gossip_peer_network"), str(cfg)], capture_output=True, text=True, timeout=120)
+    want = t["peer_stdout"]
+    assert want.endswith("Starting peer node...\n")
+    assert r.stdout[:len(want)] == want
