@@ -34,7 +34,11 @@ REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO / "p2p-gossipprotocol_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-XGMI_LINK_GBS = 153.0  # one xGMI link, each direction; a GPU of the 8-GPU node has 7 (one to each other GPU)
+# One xGMI link of the 8-GPU node (a GPU has 7, one to each other GPU).  AMD quotes MI355X's Infinity Fabric as 7
+# links and 1075.2 GB/s aggregate, 153.6 GB/s a link, without saying whether that is each way or both ways
+# together (MI300X's 128 GB/s a link is both ways, 64 each way).  The projection reports both readings:
+XGMI_LINK_GBS = 153.6       # ... 153.6 GB/s each way (the upper bound)
+XGMI_LINK_GBS_HALF = 76.8   # ... 153.6 GB/s both ways together: 76.8 each way (the lower bound)
 DENSE_KERNELS = ("bin_scatter", "bin_apply", "pull_heavy")  # the device work of a binned round
 
 
@@ -393,14 +397,20 @@ def link_projection(run, k_ms, k_b, timed_steps: int, dist) -> dict:
     world = run.parts if dist is None else run.world
     if world < 2:
         return {}
-    link = max(sum(x[k] for k in EXCHANGES) for x in k_b) / timed_steps / ((world - 1) * XGMI_LINK_GBS * 1e9) * 1e3
-    out = {"exchange_link_ms_per_step": round(link, 3),
+    gb = max(sum(x[k] for k in EXCHANGES) for x in k_b) / timed_steps / 1e9  # the busiest rank's GB per step
+    link = gb / ((world - 1) * XGMI_LINK_GBS) * 1e3
+    link_lo = gb / ((world - 1) * XGMI_LINK_GBS_HALF) * 1e3
+    out = {"exchange_gb_per_step_busiest_rank": round(gb, 3),
+           "exchange_link_ms_per_step": round(link, 3),
+           "exchange_link_ms_per_step_half_rate": round(link_lo, 3),
            "exchange_link_model": f"max over ranks of the bytes a rank receives per step / ({world - 1} links x "
-                                  f"{XGMI_LINK_GBS:.0f} GB/s)"}
+                                  f"{XGMI_LINK_GBS} GB/s each way); _half_rate: {XGMI_LINK_GBS_HALF} GB/s each way "
+                                  "(AMD's 153.6 GB/s a link read as both ways together)"}
     if run.parts > 1 and run.n_gpus == 1:
         part_k = [sum(x[k][0] for k in KERNELS) / timed_steps for x in k_ms]
         out.update({"part_kernel_ms_per_step": [round(v, 3) for v in part_k],
                     "projected_ms_per_step": round(max(part_k) + link, 3),
+                    "projected_ms_per_step_half_rate": round(max(part_k) + link_lo, 3),
                     "projected_model": "slowest part's kernels + exchange_link_ms_per_step, no overlap, no host time"})
     return out
 

@@ -369,7 +369,11 @@ gossip_status gossip_kernel_bytes(gossip_ctx* ctx, const char* kernel, double* b
  * by the record push, below it records appended by the push; -1 never; 5
  * per 100 000 default), "row_queue" (128 default or 256: the row pull's
  * queue entries per wave), "row_grid" (the row pull's workgroups; 0 default:
- * those resident at once).
+ * those resident at once), "blocked_marks" (1 default: a narrow blocked
+ * round -- under 5 % frontier, after a round that kept its tile marks -- reads
+ * the new words of marked tiles only in level 1; 0: every tile),
+ * "blocked_clear_all" (1 default: wide blocked rounds clear every new word in
+ * level 2; 0: level 1 clears the words it consumes).
  * Layout keys
  * apply at the next gossip_build_graph / gossip_load_csr ("list_cap": at the
  * next chain of needy-list rounds, never inside one).  GOSSIP_EINVAL: unknown key. */

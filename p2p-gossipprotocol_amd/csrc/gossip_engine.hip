@@ -235,6 +235,7 @@ struct gossip_ctx {
     uint64_t cur_missing = 0;    // (peer, message) pairs still missing at the round's push start (round_begin)
     uint32_t apply_pipe = 2;     // "apply_pipe": the streamed apply's pipeline shape (0-3; 2 measured best)
     bool pb_clear_all = true;    // "blocked_clear_all": wide blocked rounds clear new words whole in level 2
+    bool pb_marks = true;        // "blocked_marks": narrow blocked rounds' level 1 sweeps the marked tiles only
     bool cur_clear_all = false;  // (the round in flight does)
     bool scatter_direct = false; // "scatter_direct": a vertex block's scatter reads other blocks' words directly
     bool scatter_small = false;  // "scatter_small": the streamed scatter's small-chunk instance where chunks fit it
@@ -1492,8 +1493,11 @@ gossip_status round_compute(gossip_ctx* c) {
         // whole-array clear from a 5 % frontier (config 4 round 4: 17 %; round 3, 1.25 %, clears per peer)
         p.clear_all = c->pb_clear_all && c->frontier_est * 20 >= c->n_local ? 1u : 0u;
         c->cur_clear_all = p.clear_all != 0;
-        if (a.tcur && !c->replaying) HIPCHK(queue_zero(c, a.tcur, tact_bytes(c)));  // unread marks go
+        // narrow rounds with valid marks: level 1 reads the marked tiles' new words only (config 4 round 3)
+        p.marks = c->pb_marks && c->tact_ok && a.tcur && c->frontier_est * 20 < c->n_local
+                      ? reinterpret_cast<const unsigned long long*>(a.tcur) : nullptr;
         HIPCHK(timed(c, "pb_scatter", [&] { return launch_pb_scatter(a, p, c->any_dead, c->W, c->stream); }));
+        if (a.tcur && !c->replaying) HIPCHK(queue_zero(c, a.tcur, tact_bytes(c)));  // read: cleared before the split
         HIPCHK(timed(c, "pb_split", [&] { return launch_pb_split(p, c->stream); }));
         HIPCHK(timed(c, "pb_apply", [&] { return launch_pb_apply(a, p, c->stream); }));
         return GOSSIP_OK;
@@ -2054,6 +2058,7 @@ gossip_status gossip_set_tuning(gossip_ctx* c, const char* key, int64_t value) {
     else if (k == "apply_wide") c->apply_wide = value != 0;
     else if (k == "scatter_small") c->scatter_small = value != 0;
     else if (k == "blocked_clear_all") c->pb_clear_all = value != 0;
+    else if (k == "blocked_marks") c->pb_marks = value != 0;
     else if (k == "apply_pipe") {
         if (value < 0 || value > 3) return fail(GOSSIP_EINVAL, "apply_pipe must be 0..3");
         c->apply_pipe = (uint32_t)value;

@@ -231,6 +231,8 @@ struct PbArgs {
     uint32_t clear_all;       // a wide frontier: the split clears every new word in whole pieces, and level 1
                               // clears none (scattered 8-B clears of a dense frontier cost a read-modify-write
                               // per touched sector)
+    const unsigned long long* marks;  // narrow rounds with valid tile marks (RoundArgs.tcur: every tile with new
+                              // words marked): level 1 reads the new words of marked tiles only; null: every tile
     uint64_t n_local;
 };
 

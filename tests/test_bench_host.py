@@ -125,4 +125,7 @@ def test_link_projection():
     assert out["exchange_link_ms_per_step"] == pytest.approx(link, abs=1e-3)
     assert out["part_kernel_ms_per_step"] == [1.0, 2.0, 3.0, 4.0]
     assert out["projected_ms_per_step"] == pytest.approx(4.0 + link, abs=1e-3)
+    # the other reading of AMD's 153.6 GB/s a link (both ways together): twice the link time
+    assert out["exchange_link_ms_per_step_half_rate"] == pytest.approx(2 * link, abs=2e-3)
+    assert out["projected_ms_per_step_half_rate"] == pytest.approx(4.0 + 2 * link, abs=2e-3)
     assert b.link_projection(FakeRun(1, 1, []), k_ms[:1], k_b[:1], 2, None) == {}

@@ -88,7 +88,7 @@ def test_workload_parity(oracle, idx, n, mode):
         assert e.run() == first
 
 
-@pytest.mark.parametrize("blocked", ["force", "auto", "force_hubs", "auto_dense"])
+@pytest.mark.parametrize("blocked", ["force", "auto", "force_hubs", "auto_dense", "force_plain"])
 @pytest.mark.parametrize("idx,n", [(2, 1 << 16), (3, 1 << 18), (5, 1 << 16), (5, 50_000), (3, 1 << 20)])
 def test_blocked_push_parity(oracle, idx, n, blocked):
     """Propagation-blocked push rounds (gossip_blocked.hip): every push and binned
@@ -98,8 +98,11 @@ def test_blocked_push_parity(oracle, idx, n, blocked):
     targets are undelivered sends, peer.cpp:312).  force_hubs: the leading tiles
     of in-degree > 1024 (twice the mean) take level 1's direct deliveries (at config 4's size only
     the real hubs do); auto_dense: the binned rounds under 30 % run blocked as at
-    config 4's size."""
+    config 4's size; force_plain: without round 6's marked-tile level 1 of narrow rounds (the default
+    wherever the frontier is under 5 % and the tile marks are kept)."""
     tuning = {}
+    if blocked == "force_plain":
+        tuning.update(blocked_marks=0)
     if blocked == "force_hubs":
         tuning["blocked_direct_in"] = 1024
     if blocked == "auto_dense":

@@ -73,3 +73,38 @@ def test_cli_partitioned_network(oracle, tmp_path, n_gpus):
     assert [(x["round"], x["frontier"], x["deliveries"], x["new_receipts"], x["died"], x["reports"], x["covered"])
             for x in rounds] == [(s["round"], s["frontier"], s["deliveries"], s["new_receipts"], s["died"],
                                   s["reports"], s["covered"]) for s in ref["stats"]]
+
+
+def _ref_wire():
+    return json.loads((Path(__file__).resolve().parent / "golden" / "ref_wire.json").read_text())
+
+
+@pytest.mark.parametrize("idx", [0, 1])
+def test_engine_registry_matches_reference_seed(oracle, idx):
+    """The engine's seed registry after a whole run (registrations, then the run's dead-node reports -- A2, A10)
+    against the REAL reference SeedNode fed the same registrations and reports (tests/golden/ref_wire.json,
+    made by tests/golden/make_ref_wire_golden.py from seed.cpp compiled with nlohmann/json 3.1.1): the same
+    peers, and as many first removals as the reference printed "Removed dead peer" lines (seed.cpp:162-165)."""
+    import numpy as np
+    from dataclasses import replace
+
+    from gossip_hip import Engine
+    run = _ref_wire()["registry_runs"][idx]
+    w = config(1, 8)
+    if idx == 1:  # the same workload make_ref_wire_golden.py ran
+        w = replace(w, n=300, n_msgs=64, origins=(np.arange(64, dtype=np.uint32) * 4),
+                    inject_rounds=np.zeros(64, dtype=np.uint32), churn_threshold=int(0.03 * 2 ** 32), ping_every=3,
+                    max_missed=2, min_rounds=20, kills=[(7, 1), (150, 4)], name="ref_bootstrap_300_churn")
+    assert w.name == run["workload"] and w.n == run["n"]
+    with Engine(w.n, w.n_msgs, device=0, **w.engine_kwargs()) as e:
+        e.build_graph()
+        e.inject(w.origins, w.inject_rounds)
+        if w.kills:
+            e.schedule_kills([k[0] for k in w.kills], [k[1] for k in w.kills])
+        e.reset()
+        stats = e.run()
+        reg = e.registered()
+        assert len(e.reports()) == run["reports"]
+    ref = {(p["ip"], p["port"]) for p in json.loads(run["reference_final_list"])["peers"]}
+    assert {("127.0.0.1", 5000 + i) for i in range(w.n) if reg[i]} == ref
+    assert sum(s["seed_removals"] for s in stats) == len(run["reference_removed"])

@@ -181,7 +181,10 @@ def test_gossip_messages_are_reference_peers(surf):
                      m["source_ip"].encode()) == m["hash"]
         assert _call(surf.gossip_surface_gossip_json, m["content"].encode(), m["hash"].encode(), m["msg_number"],
                      m["source_ip"].encode(), m["source_port"], m["timestamp"].encode()) == raw
-    assert sorted(json.loads(r)["msg_number"] for r in got) == list(range(len(got)))
+    # broadcastMessage sends each generated message to every connected peer (peer.cpp:310-316): every listener
+    # the reference peer connected to got messages 0, 1, ... in order
+    for port, msgs in t["gossip_received_before_probe"].items():
+        assert [json.loads(r)["msg_number"] for r in msgs] == list(range(len(msgs)))
 
 
 def test_log_lines_are_reference_bytes(surf):
@@ -204,7 +207,8 @@ def test_reference_peer_stops_at_its_first_receipt():
     after = sum(len(v) for v in t["gossip_received_after_probe"].values())
     assert before >= 2 and after == 0
     assert "Received new message" not in t["peer_log"]
-    assert t["peer_log"].count("Generated message") == before
+    per_listener = {len(v) for v in t["gossip_received_before_probe"].values() if v}
+    assert len(per_listener) == 1 and t["peer_log"].count("Generated message") == per_listener.pop()
 
 
 def test_cli_prints_the_reference_programs_lines(tmp_path):
@@ -217,3 +221,17 @@ def test_cli_prints_the_reference_programs_lines(tmp_path):
     want = t["peer_stdout"]
     assert want.endswith("Starting peer node...\n")
     assert r.stdout[:len(want)] == want
+
+
+# ---- A2 + A10 over whole runs ----------------------------------------------------------------------------
+@pytest.mark.parametrize("run", WIRE["registry_runs"], ids=lambda r: r["workload"])
+def test_oracle_registry_matches_reference_seed_over_a_run(run):
+    """Every peer of a run registers (peer.cpp:67-72 -> seed.cpp:109-117), then the oracle's dead-node reports go
+    to the reference SeedNode in report order (seed.cpp:130-138 -> :158-167): the reference's final peers are the
+    peers the oracle's registry holds, and its "Removed dead peer" lines are the oracle's seed removals.  (The
+    engine's registry and removals equal the oracle's in the GPU parity suite, and the reference's directly in
+    tests/test_gpu_surface.py::test_engine_registry_matches_reference_seed.)"""
+    ref = {(p["ip"], p["port"]) for p in json.loads(run["reference_final_list"])["peers"]}
+    ora = {("127.0.0.1", 5000 + i) for i, r in enumerate(run["oracle_registered"]) if r}
+    assert ref == ora
+    assert len(run["reference_removed"]) == run["oracle_seed_removals"]

@@ -18,6 +18,8 @@
 #   prof:<config>            rocprofv3 kernel trace + stats of the bench command, FETCH_SIZE and WRITE_SIZE passes
 #   pmcrounds:<config>[:..]  the same three passes over tools/round_profile.py (tuning args as rounds)
 #   ab:<config>:<kernel>:<reps>:<arm>:<arm>...  tools/ab_kernel.py, arms (k=v,k=v or -) alternated in one process
+#   libab:<config>:<kernel>:<rounds>:<libA>:<libB>  two builds of libgossip_hip (paths under the repo), one
+#                            tools/ab_kernel.py process each, alternated <rounds> times (A B A B ...)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 OUT=$1; shift
@@ -91,6 +93,15 @@ for step in "$@"; do
       f=$O/ab_c${a[1]}.txt
       timeout -k 10 600 python3 -u tools/ab_kernel.py "${a[@]:1}" > $f 2>&1 || fail $step $f
       tail -20 $f | cut -c1-220 ;;
+    libab)
+      f=$O/libab_c${a[1]}_${a[2]}.txt
+      for ((k = 0; k < ${a[3]}; k++)); do
+        for L in "${a[4]}" "${a[5]}"; do
+          echo "== $L" >> $f
+          GOSSIP_HIP_LIB=$PWD/$L timeout -k 10 300 python3 -u tools/ab_kernel.py ${a[1]} ${a[2]} 3 - >> $f 2>&1 || fail $step $f
+        done
+      done
+      grep -E "^== |median" $f | paste - - | cut -c1-160 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
