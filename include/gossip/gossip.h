@@ -330,6 +330,7 @@ gossip_status gossip_kernel_bytes(gossip_ctx* ctx, const char* kernel, double* b
  * small overlays run round by round), "full_liveness" (ping every edge instead
  * of the closed form), "defer_permille" (-1 auto), "bin_stream" (the binned
  * layout: -1 / 1 streamed, the default; 0 the slot layout), "pull_first2", "in_flight", "heavy_exit", "heavy_degree"
+ * (layout: rows longer than this are heavy; -1 auto, 256, or 512 on overlays of >= 2^27 peers)
  * (layout), "heavy_chunk", "bin_front_permille", "bin_words", "bin_chunk", "val_tune"
  * (-1 auto, 0, 1, 2 = print), "src_stats" (who books a binned round's source
  * side: -1 auto = 1 the scatter, 0 the apply), "blocked_bin_slots"

@@ -259,7 +259,8 @@ struct gossip_ctx {
     bool send_dirty = false;     // the dense staging buffer holds a dense push round's masks
     uint32_t heavy = kHeavyDegree;      // light/heavy row threshold of the resident overlay (its chunks, bins and
                                         // blocked segments were laid out with it)
-    uint32_t heavy_req = kHeavyDegree;  // "heavy_degree": the threshold of the next build
+    uint32_t heavy_req = 0;             // "heavy_degree": the threshold of the next build (0: kHeavyDegree, or
+                                        // kHeavyDegreeLarge on overlays of >= kHeavyLargePeers peers)
     uint64_t frontier_est = 0;   // activated peers of the previous round
     std::vector<uint64_t> inj_prefix;  // per sorted injection: cumulative mask words
     uint64_t cum_digest = 0, cum_covered = 0;
@@ -660,7 +661,8 @@ gossip_status install_graph(gossip_ctx* c, uint64_t* d_rp, uint32_t* d_col, uint
     // the next reset clears nw / nx whole (the last run's list rows and heavy rows were the old overlay's)
     c->lin_idx[0] = c->lin_idx[1] = -1;
     c->bufs_zero = false;
-    c->heavy = c->heavy_req;  // layout key: the chunk list, bins and blocked segments below all use it
+    // layout key: the chunk list, bins and blocked segments below all use it
+    c->heavy = c->heavy_req ? c->heavy_req : c->n >= kHeavyLargePeers ? kHeavyDegreeLarge : kHeavyDegree;
     c->rp = d_rp;
     c->col = d_col;
     c->n_edges = m;
@@ -2032,7 +2034,7 @@ gossip_status gossip_set_tuning(gossip_ctx* c, const char* key, int64_t value) {
     else if (k == "pull_first2") c->first_ok = value != 0;
     else if (k == "in_flight") c->flight_ok = value != 0;
     else if (k == "heavy_exit") c->heavy_exit = value != 0;
-    else if (k == "heavy_degree") c->heavy_req = std::max<uint32_t>(1u, u);
+    else if (k == "heavy_degree") c->heavy_req = value < 0 ? 0u : std::max<uint32_t>(1u, u);
     else if (k == "heavy_chunk") c->heavy_chunk = u;
     else if (k == "bin_front_permille") c->bin_front_pm = u;
     else if (k == "bin_words") c->bin_words_req = u;

@@ -30,6 +30,9 @@ struct TraceRange {
 
 constexpr uint32_t kMaskedEdge = 0x80000000u;  // col[e] bit 31: edge dropped by liveness (peer.cpp:388)
 constexpr uint32_t kHeavyDegree = 256;         // default: rows longer than this go to the edge-chunked kernels
+constexpr uint32_t kHeavyDegreeLarge = 512;    // ... on overlays of kHeavyLargePeers peers or more (round 6, config 4:
+constexpr uint64_t kHeavyLargePeers = 1ull << 27;  // 44.05 -> 43.47 ms per step in one process; config 5 at 2^26
+                                               // measured 21.80 -> 22.02 and keeps 256)
 constexpr uint32_t kHeavyChunk = 1024;         // edges per heavy chunk (one wave); 256 below 2^22 owned peers
 constexpr int kBlock = 256;                    // 4 waves of 64
 constexpr int kMaxWords = 8;                   // M <= 512 concurrent messages
@@ -359,6 +362,10 @@ enum : uint32_t {
     kChkApplyRecord,       // k_apply_records: a record's peer in the block
     kChkPullGather,        // k_pull_rows / k_pull_heavy: a neighbour's word in nw_src
     kChkApplyRemote,       // k_apply_remote: a received word of the block
+    kChkPushSeen,          // push: a local delivery's seen word
+    kChkRecordOut,         // push at P > 1: an appended record's place in its destination block's slice
+    kChkListRow,           // k_pull_list: a listed row
+    kChkApplyVal,          // k_bin_apply_runs: a slot's value (its cb position)
 };
 
 // Re-bootstrap draw (handleDeadPeer peer.cpp:398-404 -> selectAndConnectPeers

@@ -142,7 +142,8 @@ __device__ __forceinline__ void append_records(const RoundArgs& a, bool want, ui
         base = ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(base >> 32), lead) << 32) |
                (uint32_t)__shfl((int)(uint32_t)base, lead);
         if (want && q == qq) {
-            uint64_t* rec = a.rec_out + (qq * a.rec_stride + base + (uint64_t)__popcll(grp & ((1ull << lane) - 1))) * 2;
+            const uint64_t k = base + (uint64_t)__popcll(grp & ((1ull << lane) - 1));
+            uint64_t* rec = a.rec_out + (qq * a.rec_stride + GOSSIP_IDX(a, kChkRecordOut, k, a.rec_stride)) * 2;
             rec[0] = c;
             rec[1] = m;
         }
@@ -189,7 +190,7 @@ __device__ __forceinline__ void deliver(const RoundArgs& a, uint32_t c, const ui
     const uint64_t lv = (uint64_t)(c - (uint32_t)a.begin);
     uint64_t cur[W];
 #pragma unroll
-    for (int w = 0; w < W; ++w) cur[w] = m[w] ? a.seen[lv * W + w] : ~0ull;
+    for (int w = 0; w < W; ++w) cur[w] = m[w] ? a.seen[GOSSIP_IDX(a, kChkPushSeen, lv * W + w, a.n_local * W)] : ~0ull;
     deliver_local<W>(a, lv, m, cur, acc);
 }
 
@@ -247,7 +248,8 @@ __device__ __forceinline__ void deliver_batch(const RoundArgs& a, const uint32_t
     for (int j = 0; j < kU; ++j)
 #pragma unroll
         for (int w = 0; w < W; ++w) {
-            const uint64_t x = a.seen[loc[j] ? (uint64_t)(c[j] - (uint32_t)a.begin) * W + w : 0];
+            const uint64_t x =
+                a.seen[GOSSIP_IDX(a, kChkPushSeen, loc[j] ? (uint64_t)(c[j] - (uint32_t)a.begin) * W + w : 0, a.n_local * W)];
             cur[j][w] = x | (loc[j] && m[j][w] ? 0ull : ~0ull);  // (a select would sink the load into a branch)
         }
     // the test-and-sets, every atomic of a phase issued before any result is used
@@ -934,7 +936,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_list(RoundArgs a, const uint32_
     const uint64_t inj_all = injm_full(a, 0), inj_now = injm(a, 0);
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n_pad; i += stride) {
         const bool in = i < n;
-        const uint32_t v = in ? lst[i] : 0u;
+        const uint32_t v = in ? (uint32_t)GOSSIP_IDX(a, kChkListRow, lst[i], a.n_local) : 0u;
         const uint64_t sv = in ? a.seen[v] : ~0ull;
         const uint64_t need = inj_all & ~sv;  // every bit the peer lacks ...
         const uint64_t want = need & inj_now;  // ... and of those, the ones in some new word this round
@@ -1670,7 +1672,7 @@ __global__ __launch_bounds__(kB) void k_bin_apply_runs(RoundArgs a, BinArgs b, u
                     const uint64_t q = grp(i, j) * 64 + lane;
                     const uint64_t p = valid(i, j) ? (uint64_t)((uint32_t)q - off[st][j]) : 0;  // the slot's cb position
 #pragma unroll
-                    for (int w = 0; w < W; ++w) x[st][j][w] = b.val[p * W + w];
+                    for (int w = 0; w < W; ++w) x[st][j][w] = b.val[GOSSIP_IDX(a, kChkApplyVal, p * W + w, b.n_binned * W)];
                 }
             };
             auto fold = [&](int st, uint32_t i) {

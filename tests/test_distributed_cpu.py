@@ -4,7 +4,6 @@ Checks P-invariance: the partitioned run equals the single-partition run
 (stats per round, seen sets, dead-node reports, seed removals)."""
 import json
 import os
-import socket
 import sys
 from pathlib import Path
 
@@ -15,15 +14,7 @@ import torch.multiprocessing as mp
 REPO = Path(__file__).resolve().parent.parent
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
-def _worker(rank, world, port, idx, n, out_dir, pull, sparse):
+def _worker(rank, world, rdzv, idx, n, out_dir, pull, sparse):
     sys.path[:0] = [str(REPO / "p2p-gossipprotocol_amd"), str(REPO / "tests")]
     import torch
     import torch.distributed as dist
@@ -32,7 +23,8 @@ def _worker(rank, world, port, idx, n, out_dir, pull, sparse):
     from gossip_hip.distributed import PartitionedRun, partition
     from gossip_hip.workloads import config
 
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    # a file rendezvous: nothing to bind (a free port picked by the parent could be taken before rank 0 binds it)
+    dist.init_process_group("gloo", init_method=f"file://{rdzv}", rank=rank, world_size=world)
     orc = oracle_ref.Oracle(REPO / "oracle" / "_build" / "libgossip_oracle.so")
     w = config(idx, n, pick=orc.pick_origins)
     rp, col = orc.gen_workload(w, threads=1)
@@ -58,7 +50,8 @@ def _worker(rank, world, port, idx, n, out_dir, pull, sparse):
 @pytest.mark.parametrize("idx,n", [(2, 3000), (5, 4096), (3, 2048)])
 def test_partitioned_equals_single(oracle, tmp_path, world, idx, n, pull, sparse):
     from gossip_hip.workloads import config
-    mp.spawn(_worker, args=(world, _free_port(), idx, n, str(tmp_path), pull, sparse), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, str(tmp_path / "rdzv"), idx, n, str(tmp_path), pull, sparse), nprocs=world,
+             join=True)
     out = json.loads((tmp_path / "out.json").read_text())
     seen = np.load(tmp_path / "seen.npy")
     w = config(idx, n, pick=oracle.pick_origins)

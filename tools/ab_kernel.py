@@ -28,7 +28,6 @@ defaults = {"row_grid": 0, "row_queue": 128, "apply_pipe": 2, "pull_first2": 1, 
 e.reset()
 e.run()
 e.enable_timing(True)
-KHEAVY = 256  # kHeavyDegree (gossip_internal.hpp)
 LAYOUT = ("bin_words", "bin_chunk", "scatter_units", "heavy_degree", "heavy_chunk")
 res = [[] for _ in arms]
 if kern == "step":
@@ -36,7 +35,7 @@ if kern == "step":
 for rep in range(reps):
     for i, a in enumerate(arms):
         for k in keys:
-            e.set_tuning(k, a.get(k, defaults.get(k, -1 if k not in LAYOUT else (KHEAVY if k == "heavy_degree" else 0))))
+            e.set_tuning(k, a.get(k, defaults.get(k, -1 if k not in LAYOUT or k == "heavy_degree" else 0)))
         if any(k in LAYOUT for k in keys):
             e.build_graph()
             e.inject(w.origins, w.inject_rounds)

@@ -9,6 +9,7 @@
 #   suite                    pytest -m gpu (the whole GPU suite, skip reasons on record)
 #   tests:<file>[:<k expr>]  one GPU test file (optionally -k)
 #   checked                  the partitioned suites against build/checked/libgossip_hip.so (GOSSIP_EBOUNDS on)
+#   checkedall               the whole GPU suite against the checked build
 #   evidence                 round 6's bounds evidence: the dense-exchange group tests against the checked build
 #                            of round 5's stream kernel (build/checked_unfixed, tools/experiments/
 #                            r06_unmasked_stream_entries.patch); failures are the record, not an error
@@ -57,6 +58,10 @@ for step in "$@"; do
         $PYT tests/test_gpu_group.py tests/test_gpu_partitioned.py tests/test_gpu_parity.py -m gpu > $O/checked.log 2>&1 \
         || fail $step $O/checked.log
       tail -1 $O/checked.log ;;
+    checkedall)
+      GOSSIP_HIP_LIB=$PWD/p2p-gossipprotocol_amd/build/checked/libgossip_hip.so timeout -k 10 1100 \
+        $PYT tests -m gpu > $O/checked_all.log 2>&1 || fail $step $O/checked_all.log
+      tail -1 $O/checked_all.log ;;
     evidence)
       GOSSIP_HIP_LIB=$PWD/p2p-gossipprotocol_amd/build/checked_unfixed/libgossip_hip.so timeout -k 10 600 \
         python3 -u -m pytest -q -rf --timeout 200 --timeout-method thread tests/test_gpu_group.py -m gpu \
