@@ -373,7 +373,9 @@ gossip_status gossip_kernel_bytes(gossip_ctx* ctx, const char* kernel, double* b
  * those resident at once), "blocked_marks" (1 default: a narrow blocked
  * round -- under 5 % frontier, after a round that kept its tile marks -- reads
  * the new words of marked tiles only in level 1; 0: every tile),
- * "blocked_clear_all" (1 default: wide blocked rounds clear every new word in
+ * "heavy_side" (1 default: at P = 1 a binned round's heavy-row pull runs on a
+ * second stream beside the scatter and k_heavy_commit applies its finds after
+ * the apply; 0: the pull after the apply), "blocked_clear_all" (1 default: wide blocked rounds clear every new word in
  * level 2; 0: level 1 clears the words it consumes).
  * Layout keys
  * apply at the next gossip_build_graph / gossip_load_csr ("list_cap": at the

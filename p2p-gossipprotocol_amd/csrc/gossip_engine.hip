@@ -77,6 +77,9 @@ struct gossip_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     bool own_stream = false;
+    // binned rounds at P = 1: the heavy rows' pull on a second stream beside the scatter (round 6)
+    hipStream_t aux = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     uint64_t n = 0, begin = 0, end = 0, n_local = 0;
     uint32_t M = 0, W = 0, Wp = 0;
 
@@ -236,6 +239,7 @@ struct gossip_ctx {
     uint32_t apply_pipe = 2;     // "apply_pipe": the streamed apply's pipeline shape (0-3; 2 measured best)
     bool pb_clear_all = true;    // "blocked_clear_all": wide blocked rounds clear new words whole in level 2
     bool pb_marks = true;        // "blocked_marks": narrow blocked rounds' level 1 sweeps the marked tiles only
+    bool heavy_side = true;      // "heavy_side": a binned round's heavy-row pull beside its scatter (P = 1)
     bool cur_clear_all = false;  // (the round in flight does)
     bool scatter_direct = false; // "scatter_direct": a vertex block's scatter reads other blocks' words directly
     bool scatter_small = false;  // "scatter_small": the streamed scatter's small-chunk instance where chunks fit it
@@ -1527,6 +1531,23 @@ gossip_status round_compute(gossip_ctx* c) {
             HIPCHK(queue_zero(c, c->d_work, 8 * sizeof(uint32_t)));
         BinArgs b = bin_args(c, c->bins_first, src_stats(c));
         if (b.work && c->replaying) b.work = rep_work(c, c->rep_round);
+        // the heavy rows' pull on the second stream, beside the scatter (it reads seen and the new words, which
+        // the scatter leaves alone, and ORs its finds into hacc); k_heavy_commit applies them after the apply,
+        // whose whole-tile stores rewrite the heavy rows' seen and nx words
+        const bool side = c->heavy_side && c->n_chunks && c->hacc && !a.st_pre && c->world <= 1 && hz;
+        if (side) {
+            if (!c->aux) HIPCHK(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+            if (!c->ev_fork) HIPCHK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+            if (!c->ev_join) HIPCHK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+            HIPCHK(flush_zero(c));  // (the round's clears -- hacc among them -- before the fork)
+            HIPCHK(hipEventRecord(c->ev_fork, c->stream));
+            HIPCHK(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+            void* tok = nullptr;
+            ctx_timer_start_on(c, c->aux, &tok);
+            HIPCHK(launch_pull_heavy(a, pw, c->aux, true, true));
+            ctx_timer_stop_on(c, "pull_heavy", c->aux, tok);
+            HIPCHK(hipEventRecord(c->ev_join, c->aux));
+        }
         // every bin is needy while more than one (peer, message) pair per peer is missing: no check pass
         b.needy_check = c->cur_missing > c->n_local && c->needy_skip ? 0u : 1u;
         if (c->stage_n && c->bins.stages == c->stage_n) {
@@ -1546,7 +1567,15 @@ gossip_status round_compute(gossip_ctx* c) {
         }
         HIPCHK(timed(c, "bin_apply", [&] { return launch_bin_apply(a, b, pw, c->stream); }));
         c->bins_first = false;
-        HIPCHK(timed(c, "pull_heavy", [&] { return launch_pull_heavy(a, pw, c->stream, hz); }));
+        if (side) {
+            // (timed from before the join: a wait for the side stream counts in the round's critical path)
+            HIPCHK(timed(c, "heavy_commit", [&] {
+                const hipError_t e = hipStreamWaitEvent(c->stream, c->ev_join, 0);
+                return e != hipSuccess ? e : launch_heavy_commit(a, pw, c->stream);
+            }));
+        } else {
+            HIPCHK(timed(c, "pull_heavy", [&] { return launch_pull_heavy(a, pw, c->stream, hz); }));
+        }
         return GOSSIP_OK;
     }
     if (c->last_pull) {
@@ -2061,6 +2090,7 @@ gossip_status gossip_set_tuning(gossip_ctx* c, const char* key, int64_t value) {
     else if (k == "scatter_small") c->scatter_small = value != 0;
     else if (k == "blocked_clear_all") c->pb_clear_all = value != 0;
     else if (k == "blocked_marks") c->pb_marks = value != 0;
+    else if (k == "heavy_side") c->heavy_side = value != 0;
     else if (k == "apply_pipe") {
         if (value < 0 || value > 3) return fail(GOSSIP_EINVAL, "apply_pipe must be 0..3");
         c->apply_pipe = (uint32_t)value;
@@ -2116,6 +2146,12 @@ void gossip_destroy(gossip_ctx* c) {
     hipFree(c->d_toff);
     hipFree(c->sx_pos);
     hipFree(c->sx_tmp);
+    if (c->aux) {
+        hipStreamSynchronize(c->aux);
+        hipStreamDestroy(c->aux);
+    }
+    if (c->ev_fork) hipEventDestroy(c->ev_fork);
+    if (c->ev_join) hipEventDestroy(c->ev_join);
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
     if (c->dist && c->dist_owned) gossip::dist_free(c->dist);
     delete c;

@@ -408,7 +408,10 @@ hipError_t launch_push_heavy(const RoundArgs& a, uint32_t W, bool check_alive, b
 hipError_t launch_push_light(const RoundArgs& a, uint32_t W, bool check_alive, bool remote, hipStream_t s);
 hipError_t launch_frontier_bits(const RoundArgs& a, uint32_t W, hipStream_t s);
 hipError_t launch_pull_rows(const RoundArgs& a, uint32_t W, hipStream_t s);
-hipError_t launch_pull_heavy(const RoundArgs& a, uint32_t W, hipStream_t s, bool hacc_zeroed = false);
+// defer: the rows' finds only ORed into hacc (binned rounds, run beside the scatter); launch_heavy_commit applies
+// them after the apply
+hipError_t launch_pull_heavy(const RoundArgs& a, uint32_t W, hipStream_t s, bool hacc_zeroed = false, bool defer = false);
+hipError_t launch_heavy_commit(const RoundArgs& a, uint32_t W, hipStream_t s);
 // late pull rounds over a needy list (one word per peer): the stale new words of the round before last
 // cleared (by its list, or n_local words), then the list's rows pulled
 hipError_t launch_list_zero(const RoundArgs& a, const uint32_t* lst, uint32_t n, hipStream_t s);

@@ -804,7 +804,11 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
     }
 }
 
-template <int W>
+// kDefer (binned rounds, P = 1; round 6): the chunks only OR what they found into their row's hacc word, and
+// k_heavy_commit applies the rows after the apply -- so the heavy rows' pull runs on a second stream beside the
+// binned round's scatter (it reads seen and the new words, which the scatter does not write) instead of after
+// the apply (whose whole-tile stores rewrite the heavy rows' seen and nx words).
+template <int W, bool kDefer = false>
 __global__ __launch_bounds__(kBlock) void k_pull_heavy(RoundArgs a) {
     Acc acc;
     PreAcc pre;
@@ -872,6 +876,15 @@ __global__ __launch_bounds__(kBlock) void k_pull_heavy(RoundArgs a) {
 #pragma unroll
             for (int off = 32; off > 0; off >>= 1) part[w] |= __shfl_xor(part[w], off);
         }
+        if (kDefer) {  // the row's bits: k_heavy_commit tests them against seen after the apply
+            if (lane == 0)
+#pragma unroll
+                for (int w = 0; w < W; ++w)
+                    if (part[w] & ~pub[w])
+                        atomicOr(reinterpret_cast<unsigned long long*>(a.hacc) + (uint64_t)ch.first * W + w,
+                                 (unsigned long long)part[w]);
+            continue;
+        }
         if (lane == 0) {
 #pragma unroll
             for (int w = 0; w < W; ++w) {
@@ -903,6 +916,33 @@ __global__ __launch_bounds__(kBlock) void k_pull_heavy(RoundArgs a) {
     acc.htrav = acc.pulled;  // heavy-row edges scanned
     acc.pulled = 0;
     flush_pre(pre, a.st_pre);
+    flush(acc, a.st);
+}
+
+// After a binned round's apply: the deferred heavy rows (k_pull_heavy<W, true>), one thread per row -- handleClient's
+// test-and-set of what the row's chunks found (peer.cpp:277-285).  The apply wrote the heavy rows' nx words (zero:
+// their in-edges have no slots); a row's words are ORed in here.
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_heavy_commit(RoundArgs a) {
+    Acc acc;
+    for (uint64_t ci = (uint64_t)blockIdx.x * kBlock + threadIdx.x; ci < a.n_chunks; ci += (uint64_t)gridDim.x * kBlock) {
+        const HeavyChunk ch = a.chunks[ci];
+        if (ch.first != ci) continue;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            const uint64_t x = a.hacc[ci * W + w];
+            if (!x) continue;
+            const uint64_t sv = a.seen[(uint64_t)ch.v * W + w];
+            const uint64_t fr = x & ~sv;
+            acc.fresh_or[w] |= fr;
+            if (!fr) continue;
+            a.seen[(uint64_t)ch.v * W + w] = sv | fr;
+            const uint64_t onx = a.nx[(uint64_t)ch.v * W + w];
+            a.nx[(uint64_t)ch.v * W + w] = onx | fr;
+            acc.activated += onx == 0;
+            acc.fresh += (unsigned long long)__popcll(fr);
+        }
+    }
     flush(acc, a.st);
 }
 
@@ -2812,13 +2852,27 @@ hipError_t launch_pull_rows(const RoundArgs& a, uint32_t W_, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_pull_heavy(const RoundArgs& a, uint32_t W_, hipStream_t s, bool hacc_zeroed) {
+hipError_t launch_pull_heavy(const RoundArgs& a, uint32_t W_, hipStream_t s, bool hacc_zeroed, bool defer) {
     if (!a.n_chunks) return hipSuccess;
     if (a.hacc && !hacc_zeroed) {
         const hipError_t e = hipMemsetAsync(a.hacc, 0, a.n_chunks * wp_of(W_) * sizeof(uint64_t), s);
         if (e != hipSuccess) return e;
     }
-    GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_pull_heavy<W>, dim3(grid_for(a.n_chunks, kWavesPerBlock)),
+    if (defer) {
+        if (!a.hacc) return hipErrorInvalidValue;
+        GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_pull_heavy<W, true>),
+                                                       dim3(grid_for(a.n_chunks, kWavesPerBlock)), dim3(kBlock), 0,
+                                                       s, a));
+    } else {
+        GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_pull_heavy<W>, dim3(grid_for(a.n_chunks, kWavesPerBlock)),
+                                                       dim3(kBlock), 0, s, a));
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_heavy_commit(const RoundArgs& a, uint32_t W_, hipStream_t s) {
+    if (!a.n_chunks) return hipSuccess;
+    GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL(k_heavy_commit<W>, dim3(grid_for(a.n_chunks, kBlock)),
                                                    dim3(kBlock), 0, s, a));
     return hipGetLastError();
 }

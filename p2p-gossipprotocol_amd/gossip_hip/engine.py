@@ -18,7 +18,11 @@ from ._abi import DeadReport, GossipConfig, RoundStats, check
 _GRAPHS = {"powerlaw": _abi.GRAPH_POWERLAW, "ref_bootstrap": _abi.GRAPH_REF_BOOTSTRAP}
 KERNELS = ("push_light", "push_heavy", "push_extra", "src_count", "frontier_bits", "pull_light", "pull_heavy", "pull_list", "list_zero", "bin_scatter",
            "bin_apply", "pb_scatter", "pb_split", "pb_apply", "liveness", "rebootstrap", "rejoin", "churn", "kills",
-           "inject", "apply_remote", "commit", "compact_send", "px_scatter", "tiny")
+           "inject", "apply_remote", "commit", "compact_send", "px_scatter", "tiny", "heavy_commit")
+# kernels that run on a ctx's second stream beside others (binned rounds at P = 1: the heavy rows' pull beside the
+# scatter); a round's critical path counts them only when the round has no join (heavy_commit, whose timer covers
+# the wait for the side stream)
+SIDE_KERNELS = ("pull_heavy",)
 # exchange steps of partitioned rounds, timed on each part's stream (gossip_dist.hip; bytes = received per part)
 EXCHANGES = ("all_gather", "all_to_all", "records")
 

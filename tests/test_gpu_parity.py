@@ -345,7 +345,7 @@ _VARIANTS = {"defer_1": ({"defer_permille": 1}, {"blocked": "off"}), "stream": (
              "no_lists": ({"list_rounds": 0}, {}), "needy_test": ({"bin_needy_skip": 0}, {}),
              "stream_needy_test": ({"bin_stream": 1, "bin_needy_skip": 0}, {}),
              "apply_pipe_1": ({"apply_pipe": 1}, {}), "apply_pipe_2": ({"apply_pipe": 2}, {}),
-             "apply_pipe_3": ({"apply_pipe": 3}, {}),
+             "apply_pipe_3": ({"apply_pipe": 3}, {}), "heavy_after_apply": ({"heavy_side": 0}, {}),
              "scatter_small": ({"scatter_small": 1}, {}),
              "small_kernels": ({"bin_words": 1024, "bin_chunk": 1024, "scatter_small": 1}, {}),
              "split_units": ({"scatter_units": 4096}, {}),

@@ -9,7 +9,8 @@ from gossip_hip.workloads import config  # noqa: E402
 
 K = ("push_light", "push_heavy", "pull_light", "pull_heavy", "frontier_bits", "bin_scatter", "bin_apply", "inject",
      "liveness", "churn", "kills", "src_count", "rebootstrap", "push_extra", "commit",
-     "pb_scatter", "pb_split", "pb_apply", "pull_list", "list_zero", "px_scatter", "compact_send", "apply_remote")
+     "pb_scatter", "pb_split", "pb_apply", "pull_list", "list_zero", "px_scatter", "compact_send", "apply_remote",
+     "heavy_commit")
 w = config(int(sys.argv[1]) if len(sys.argv) > 1 else 4)
 kw = dict(a.split("=", 1) for a in sys.argv[2:])  # extra engine options, e.g. blocked=off
 kw = {k: (int(v) if v.lstrip("-").isdigit() else v) for k, v in kw.items()}
