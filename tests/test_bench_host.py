@@ -129,3 +129,14 @@ def test_link_projection():
     assert out["exchange_link_ms_per_step_half_rate"] == pytest.approx(2 * link, abs=2e-3)
     assert out["projected_ms_per_step_half_rate"] == pytest.approx(4.0 + 2 * link, abs=2e-3)
     assert b.link_projection(FakeRun(1, 1, []), k_ms[:1], k_b[:1], 2, None) == {}
+
+
+def test_critical_path_of_side_stream_kernels():
+    """A round's critical-path device time: the heavy rows' pull beside a binned round's scatter counts only when
+    the round has no heavy_commit (whose timer covers the join)."""
+    b = _bench()
+    from gossip_hip.engine import KERNELS
+    binned = {"bin_scatter": 5.0, "bin_apply": 6.0, "pull_heavy": 4.0, "heavy_commit": 0.1}
+    assert b.critical(binned, KERNELS) == pytest.approx(11.1)
+    assert b.critical({"bin_scatter": 5.0, "bin_apply": 6.0, "pull_heavy": 0.4}, KERNELS) == pytest.approx(11.4)
+    assert b.critical({"push_light": 0.2, "push_heavy": 0.1, "churn": 0.1}, KERNELS) == pytest.approx(0.4)
