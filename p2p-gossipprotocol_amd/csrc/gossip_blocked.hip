@@ -379,6 +379,12 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_scatter(RoundArgs a, PbArgs p, 
 // level 2: slice sl of coarse bin k -- the segments of level-1 workgroups
 // [sl * kPbGrid / kPbSlices, (sl + 1) * kPbGrid / kPbSlices) -> the bin's fine bins
 // ---------------------------------------------------------------------------
+// kRot (blocked_pipe, round 6): the next batch of records is loaded while this one is staged, into the other of
+// two register sets (the loop unrolled by two, so no set is copied while its loads are in flight), from clamped
+// addresses whatever the batch's end -- validity is applied where the records are used.  (Round 6's first try
+// loaded `in ? record : pad` and copied the next batch's registers into the current ones at the loop's end: the
+// select and the copies made every batch wait for the loads just issued, and it measured no gain.)
+template <bool kRot>
 __global__ __launch_bounds__(kPbBlock) void k_pb_split(PbArgs p) {
     constexpr uint32_t kN = 128;  // search table (>= kPbFineMax, a power of two)
     static_assert(kPbFineMax <= kN, "fine bins per coarse bin");
@@ -449,7 +455,7 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_split(PbArgs p) {
             atomicOr(p.err, 2u);
         }
     };
-    {
+    if (!kRot) {
         const uint32_t n = ps_s[kSeg];
         for (uint32_t i0 = (uint32_t)wave * 64 * kPbU; i0 < n; i0 += kPbBlock * kPbU) {  // wave-uniform
             uint32_t d[kPbU], f[kPbU], dl[kPbU];
@@ -471,6 +477,45 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_split(PbArgs p) {
                 dl[j] = d[j] - flo_s[f[j]];
             }
             stage<kPbU, kPbB2, kPbH2>(tk_s, wr_s, gn_s, bd_s, bw_s, f, dl, x, rec, flush2, p.err);
+        }
+    } else {
+        const uint32_t n = ps_s[kSeg];
+        constexpr uint32_t kStep = kPbBlock * kPbU;
+        auto load = [&](uint32_t i0, uint32_t (&d)[kPbU], unsigned long long (&x)[kPbU]) {
+#pragma unroll
+            for (int j = 0; j < kPbU; ++j) {
+                const uint32_t i = min(i0 + j * 64 + lane, n - 1);  // (n > 0 here) clamped: read, not used
+                const uint32_t sg = find_bin<kSeg>(ps_s, i);       // ps_s[sg] <= i < ps_s[sg + 1]
+                const uint64_t at = sb_s[sg] + (i - ps_s[sg]);
+                d[j] = p.r1_dst[at];
+                x[j] = p.r1_w[at];
+            }
+        };
+        auto use = [&](uint32_t i0, const uint32_t (&d)[kPbU], const unsigned long long (&x)[kPbU]) {
+            uint32_t f[kPbU], dl[kPbU];
+            unsigned long long xv[kPbU];
+            bool rec[kPbU];
+#pragma unroll
+            for (int j = 0; j < kPbU; ++j) {
+                rec[j] = i0 + j * 64 + lane < n && d[j] != kPbPad;
+                f[j] = rec[j] ? find_bin<kN>(flo_s, d[j]) : 0u;
+                dl[j] = d[j] - flo_s[f[j]];
+                xv[j] = x[j];
+            }
+            stage<kPbU, kPbB2, kPbH2>(tk_s, wr_s, gn_s, bd_s, bw_s, f, dl, xv, rec, flush2, p.err);
+        };
+        uint32_t dA[kPbU], dB[kPbU];
+        unsigned long long xA[kPbU], xB[kPbU];
+        uint32_t i0 = (uint32_t)wave * 64 * kPbU;
+        if (i0 < n) load(i0, dA, xA);
+        while (i0 < n) {  // wave-uniform
+            load(i0 + kStep, dB, xB);  // (clamped: the last batch's prefetch reads record n - 1 again)
+            use(i0, dA, xA);
+            i0 += kStep;
+            if (i0 >= n) break;
+            load(i0 + kStep, dA, xA);
+            use(i0, dB, xB);
+            i0 += kStep;
         }
     }
 
@@ -502,6 +547,10 @@ __global__ __launch_bounds__(kPbBlock) void k_pb_split(PbArgs p) {
 // 3's 53.5 M records).
 // ---------------------------------------------------------------------------
 constexpr int kPbApplyGrid = 256;  // one per CU (the accumulator takes most of the LDS)
+// kRot (blocked_pipe): the record loop as k_pb_split's -- two register sets in turn, clamped loads, and the
+// destinations read as the 32-bit word of their pair (a u16 load compared as a 16-bit value kept a separate
+// zero-extension, which waited for the load where it was issued)
+template <bool kRot>
 __global__ __launch_bounds__(1024) void k_pb_apply(RoundArgs a, PbArgs p) {
     __shared__ unsigned long long acc_s[kBinWords];
     __shared__ uint32_t meta_s[2][3 * kPbSlices + 2];  // per bin: s2_len[4], s2_base lo/hi [8], f_lo, f_lo + 1
@@ -547,7 +596,45 @@ __global__ __launch_bounds__(1024) void k_pb_apply(RoundArgs a, PbArgs p) {
         }
         // the records of the bin's kPbSlices segments (one virtual array: prefix sums ps), kPbU per thread,
         // the next batch's loads in flight while this one is folded
-        {
+        if (kRot) {
+            auto pos = [&](uint32_t vi) {  // the record's position (vi < total)
+                uint32_t sg = 0;
+#pragma unroll
+                for (uint32_t s = 1; s < kPbSlices; ++s) sg += vi >= ps[s];
+                return sb[sg] + (vi - ps[sg]);
+            };
+            const uint32_t* r2d = reinterpret_cast<const uint32_t*>(p.r2_dst);
+            auto load = [&](uint32_t v0_, uint32_t (&d)[kPbU], unsigned long long (&w)[kPbU]) {
+#pragma unroll
+                for (int j = 0; j < kPbU; ++j) {
+                    const uint64_t at = pos(min(v0_ + j * 1024, total - 1));  // clamped: read, not used
+                    d[j] = r2d[at >> 1];
+                    w[j] = p.r2_w[at];
+                }
+            };
+            auto fold = [&](uint32_t v0_, const uint32_t (&d)[kPbU], const unsigned long long (&w)[kPbU]) {
+#pragma unroll
+                for (int j = 0; j < kPbU; ++j) {
+                    const uint32_t vi = v0_ + j * 1024;
+                    const uint32_t dd = (d[j] >> ((uint32_t)(pos(min(vi, total - 1)) & 1) * 16)) & 0xFFFFu;
+                    if (vi < total && dd != 0xFFFFu) atomicOr(&acc_s[dd], w[j]);  // ds_or_b64
+                }
+            };
+            constexpr uint32_t kStep = 1024 * kPbU;
+            uint32_t dA[kPbU], dB[kPbU];
+            unsigned long long wA[kPbU], wB[kPbU];
+            uint32_t vb = threadIdx.x;
+            load(vb, dA, wA);
+            while (vb < total) {
+                load(vb + kStep, dB, wB);
+                fold(vb, dA, wA);
+                vb += kStep;
+                if (vb >= total) break;
+                load(vb + kStep, dA, wA);
+                fold(vb, dB, wB);
+                vb += kStep;
+            }
+        } else {
             auto load = [&](uint32_t v0_, uint16_t (&d)[kPbU], unsigned long long (&w)[kPbU]) {
 #pragma unroll
                 for (int j = 0; j < kPbU; ++j) {
@@ -1035,14 +1122,16 @@ hipError_t launch_pb_scatter(const RoundArgs& a, const PbArgs& p, bool check_ali
 }
 
 hipError_t launch_pb_split(const PbArgs& p, hipStream_t s) {
-    hipLaunchKernelGGL(k_pb_split, dim3(p.n_coarse * kPbSlices), dim3(kPbBlock), 0, s, p);
+    if (p.pipe) hipLaunchKernelGGL(k_pb_split<true>, dim3(p.n_coarse * kPbSlices), dim3(kPbBlock), 0, s, p);
+    else hipLaunchKernelGGL(k_pb_split<false>, dim3(p.n_coarse * kPbSlices), dim3(kPbBlock), 0, s, p);
     return hipGetLastError();
 }
 
 hipError_t launch_pb_apply(const RoundArgs& a, const PbArgs& p, hipStream_t s) {
     if (!p.n_fine) return hipSuccess;
     const unsigned g = (unsigned)std::min<uint64_t>(p.n_fine, kPbApplyGrid);
-    hipLaunchKernelGGL(k_pb_apply, dim3(g), dim3(1024), 0, s, a, p);
+    if (p.pipe) hipLaunchKernelGGL(k_pb_apply<true>, dim3(g), dim3(1024), 0, s, a, p);
+    else hipLaunchKernelGGL(k_pb_apply<false>, dim3(g), dim3(1024), 0, s, a, p);
     return hipGetLastError();
 }
 

@@ -56,6 +56,33 @@ __device__ __forceinline__ uint64_t injm_full(const RoundArgs& a, int w) {
 __device__ __forceinline__ uint64_t injm(const RoundArgs& a, int w) {
     return injm_full(a, w) & (a.use_flight ? a.in_flight[w] : ~0ull);
 }
+__device__ __forceinline__ uint64_t sgpr64(uint64_t x) {  // a wave-uniform value, kept in scalar registers
+    return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
+}
+// Both masks of a round, read once at a kernel's start (round 6).  Read where they were used, inside a
+// sweep or a finish loop, inj_live is a global load the compiler cannot hoist past the loop's stores to
+// seen and nx, and the wait for it (vmcnt(0)) also waited for every load the loop had put in flight ahead:
+// k_pull_rows's next-tile prefetch, the binned apply's whole-bin seen loads.
+template <int W>
+struct InjMasks {
+    uint64_t full[W], cur[W];
+    __device__ __forceinline__ explicit InjMasks(const RoundArgs& a) {
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            full[w] = sgpr64(injm_full(a, w));
+            cur[w] = sgpr64(injm(a, w));
+        }
+    }
+    // word i % W's mask for a lane-varying i (a select chain: no register-array indexing)
+    __device__ __forceinline__ uint64_t cur_at(uint32_t wi) const {
+        uint64_t m = cur[0];
+#pragma unroll
+        for (int w = 1; w < W; ++w)
+            if (wi == (uint32_t)w) m = cur[w];
+        return m;
+    }
+};
 
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
 #pragma unroll

@@ -219,6 +219,7 @@ struct gossip_ctx {
                                           // exchange {tile bitmap, packed non-zero words} (gossip_dist.hip)
     uint32_t row_step = 1;                // "pull_step": k_pull_rows's neighbour words per row per step
     uint32_t row_q = 128, row_grid = 0;   // "row_queue" / "row_grid": k_pull_rows's queue and grid (A/B)
+    uint32_t row_pre = 1;                 // "row_prefetch": k_pull_rows's tiles in flight per wave (1 or 2)
                                           // (config 4 round 7: 2 -> 1, 180 -> 101 M gathers, 6.6-6.8 ->
                                           // 5.4-5.7 ms; most rows stop at their first neighbour)
     bool bin_stream = false;      // streamed binned layout (chosen in prepare_bins)
@@ -236,9 +237,11 @@ struct gossip_ctx {
     bool cur_defer = false;       // this round defers: advance() folds nx into seen
     bool full_liveness = false;  // "full_liveness": ping every edge each ping round (A/B against closed form)
     uint64_t cur_missing = 0;    // (peer, message) pairs still missing at the round's push start (round_begin)
-    uint32_t apply_pipe = 2;     // "apply_pipe": the streamed apply's pipeline shape (0-3; 2 measured best)
+    uint32_t apply_pipe = 5;     // "apply_pipe": the streamed apply's pipeline shape (0-8; round 6: 5, the
+                                 // contiguous-group shape with every load two iterations ahead, measured best)
     bool pb_clear_all = true;    // "blocked_clear_all": wide blocked rounds clear new words whole in level 2
     bool pb_marks = true;        // "blocked_marks": narrow blocked rounds' level 1 sweeps the marked tiles only
+    bool pb_pipe = true;         // "blocked_pipe": the split's and the blocked apply's record loops pipelined
     bool heavy_side = true;      // "heavy_side": a binned round's heavy-row pull beside its scatter (P = 1)
     bool cur_clear_all = false;  // (the round in flight does)
     bool scatter_direct = false; // "scatter_direct": a vertex block's scatter reads other blocks' words directly
@@ -633,6 +636,7 @@ RoundArgs make_args(gossip_ctx* c) {
     a.hacc = c->replaying && c->hacc ? c->rep_aux + c->rep_tw * (c->hist_cap + 1) + c->rep_hw * c->rep_round : c->hacc;
     a.row_step = c->row_step;
     a.row_q = c->row_q;
+    a.row_pre = c->row_pre;
     a.row_grid = c->row_grid;
     a.chk = reinterpret_cast<unsigned long long*>(c->inj_live + kMaxWords);
     a.inj_live = c->world <= 1 && c->n_local == c->n ? c->inj_live : nullptr;  // a partition injects its own only
@@ -1492,6 +1496,7 @@ gossip_status round_compute(gossip_ctx* c) {
     TraceRange tr("%s", c->last_bin ? "binned" : c->last_pull ? "pull" : c->cur_pb ? "push (blocked)" : c->cur_sparse ? "push (sparse exchange)" : "push");
     if (c->cur_pb) {
         PbArgs p = pb_args(c->pb);
+        p.pipe = c->pb_pipe ? 1u : 0u;
         p.chunks = c->chunks;
         p.n_chunks = c->n_chunks;
         p.nw = reinterpret_cast<unsigned long long*>(c->nw);
@@ -2083,6 +2088,7 @@ gossip_status gossip_set_tuning(gossip_ctx* c, const char* key, int64_t value) {
     else if (k == "replay") c->replay_req = value != 0;
     else if (k == "scatter_direct") c->scatter_direct = value != 0;
     else if (k == "row_queue") c->row_q = value == 256 ? 256u : 128u;
+    else if (k == "row_prefetch") c->row_pre = value == 2 ? 2u : 1u;
     else if (k == "row_grid") c->row_grid = u;
     else if (k == "scatter_units") c->scatter_units = u;
     else if (k == "scatter_split_direct") c->split_direct = value != 0;
@@ -2090,9 +2096,10 @@ gossip_status gossip_set_tuning(gossip_ctx* c, const char* key, int64_t value) {
     else if (k == "scatter_small") c->scatter_small = value != 0;
     else if (k == "blocked_clear_all") c->pb_clear_all = value != 0;
     else if (k == "blocked_marks") c->pb_marks = value != 0;
+    else if (k == "blocked_pipe") c->pb_pipe = value != 0;
     else if (k == "heavy_side") c->heavy_side = value != 0;
     else if (k == "apply_pipe") {
-        if (value < 0 || value > 3) return fail(GOSSIP_EINVAL, "apply_pipe must be 0..3");
+        if (value < 0 || value > 8) return fail(GOSSIP_EINVAL, "apply_pipe must be 0..8");
         c->apply_pipe = (uint32_t)value;
     }
     else if (k == "apply_persist") c->apply_persist = value != 0;

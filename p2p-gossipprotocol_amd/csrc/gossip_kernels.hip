@@ -536,10 +536,14 @@ __global__ __launch_bounds__(kBlock) void k_frontier_bits(RoundArgs a) {
 // for whole rows) -- or at its end.  Finished lanes take the next row:
 // fr = (OR of the scanned neighbours) & need, and a row that stops early
 // already holds all of need.
-template <int W, bool COV, bool FRONT, int kRowB, int kRowQ = 128>  // kRowB: edges per lane per step; kRowQ: queue entries per wave
+// kTiles (round 6, "row_prefetch" 2): two tiles' words and row bounds in flight per wave, in two buffers taken in
+// turn (each reloaded right after its sweep, so no buffer is copied while its loads are in flight).  With one
+// buffer the next tile's loads were copied into the current tile's registers at the loop's end, a wait for
+// loads issued in the same iteration: one memory round trip per swept tile and wave.
+template <int W, bool COV, bool FRONT, int kRowB, int kRowQ = 128, int kTiles = 1>  // kRowB: edges per lane per step; kRowQ: queue entries per wave
 // (116 VGPRs, four waves per SIMD.  Launch bounds asking five or six spill to scratch and ran round 7 at
 // 5.9-6.1 and 8.3-8.6 ms against 4.8-5.1: the sweep and the row state do not fit 96 or 80 registers.)
-__global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) {
+__global__ __launch_bounds__(kBlock, kTiles == 2 ? 4 : 1) void k_pull_rows(RoundArgs a, uint32_t wd) {
     __shared__ unsigned int cov_s[COV ? 64 * W : 1];
     __shared__ uint32_t q_v[kWavesPerBlock][kRowQ];
     __shared__ uint32_t q_d[kWavesPerBlock][kRowQ];
@@ -553,6 +557,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
     }
     Acc acc;
     PreAcc pre;
+    const InjMasks<W> im(a);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint32_t* qv = q_v[wv];
     uint32_t* lq = q_lst[wv];
@@ -612,9 +617,9 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
             if (a.fold && vv && m[w]) a.seen[v * W + w] = sv;
             // nd: every bit the peer lacks (the row's final seen word is rebuilt from it); a row is queued
             // only if one of them is in flight this round
-            nd[w] = va ? injm_full(a, w) & ~sv : 0ull;
+            nd[w] = va ? im.full[w] & ~sv : 0ull;
             act |= m[w] != 0;
-            needy |= (nd[w] & injm(a, w)) != 0;
+            needy |= (nd[w] & im.cur[w]) != 0;
             // nx is written whole in a pull round; rows that learn rewrite it.  (Leaving a queued row's word to
             // its finish alone turned these whole-line stores into partial ones: round 7 5.2-5.7 against
             // 4.8-5.1 ms.)
@@ -664,11 +669,21 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
         }
         q_tail += (uint32_t)__popcll(bal);
     };
-    TileIn nxt;
+    TileIn nxt, alt;
     load_tile(t, nxt);
+    if (kTiles == 2) load_tile(t + nwaves, alt);
     while (true) {
-        // refill the queue while it has room for a whole tile
-        while (t < n_tiles && q_tail - q_head <= (uint32_t)(kRowQ - 64)) {
+        // refill the queue while it has room for a whole tile (kTiles 2: for two, swept as a pair -- straight-line
+        // code, so the wait before each sweep counts the other buffer's loads as still in flight)
+        while (t < n_tiles && q_tail - q_head <= (uint32_t)(kRowQ - 64 * kTiles)) {
+            if (kTiles == 2) {
+                sweep_tile(t, nxt);  // (a tile past the end sweeps nothing)
+                load_tile(t + 2 * nwaves, nxt);  // (clamped past the end)
+                sweep_tile(t + nwaves, alt);
+                load_tile(t + 3 * nwaves, alt);
+                t += 2 * nwaves;
+                continue;
+            }
             const TileIn cur = nxt;
             load_tile(t + nwaves, nxt);  // unconditional (clamped): the wait before the sweep can then count it
             sweep_tile(t, cur);
@@ -741,7 +756,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
         for (int w = 0; w < W; ++w) {
 #pragma unroll
             for (int j = 0; j < kRowB; ++j) got[w] |= x[j][w] & need[w];
-            done &= got[w] == (need[w] & injm(a, w));  // every bit it can still learn this round
+            done &= got[w] == (need[w] & im.cur[w]);  // every bit it can still learn this round
         }
         rk += kRowB;
         bool lacks = false;
@@ -754,9 +769,9 @@ __global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) 
                 acc.fresh_or[w] |= fr;
                 // still lacking a bit in flight: the only rows that can learn later (no injections: the next
                 // round's bits in flight are this round's receipts, a subset of this round's)
-                lacks |= (need[w] & injm(a, w) & ~fr) != 0;
+                lacks |= (need[w] & im.cur[w] & ~fr) != 0;
                 if (fr) {
-                    a.seen[(uint64_t)rv * W + w] = (injm_full(a, w) & ~need[w]) | fr;  // within inj_mask
+                    a.seen[(uint64_t)rv * W + w] = (im.full[w] & ~need[w]) | fr;  // within inj_mask
                     a.nx[(uint64_t)rv * W + w] = fr;
                     pc += (uint32_t)__popcll(fr);
                     if (a.st_pre && w < (int)wd) pre.digest += digest_weight(((uint64_t)a.begin + rv) * wd + w) * fr;
@@ -812,6 +827,7 @@ template <int W, bool kDefer = false>
 __global__ __launch_bounds__(kBlock) void k_pull_heavy(RoundArgs a) {
     Acc acc;
     PreAcc pre;
+    const InjMasks<W> im(a);
     const int lane = threadIdx.x & 63;
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
     for (uint64_t ci = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); ci < a.n_chunks; ci += nwaves) {
@@ -823,7 +839,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_heavy(RoundArgs a) {
             pub[w] = 0;
             // one lane reads, every lane uses the same value: the branch below stays wave-uniform
             const uint64_t s0 = __shfl(a.seen[(uint64_t)ch.v * W + w], 0);
-            need[w] = injm(a, w) & ~s0;
+            need[w] = im.cur[w] & ~s0;
             if (a.dead_mode && !bit_alive(a.alive, (uint32_t)(a.begin + ch.v))) need[w] = 0;  // dead: no receive
             part[w] = 0;
             any |= need[w] != 0;
@@ -1349,7 +1365,7 @@ __device__ __forceinline__ void bin_src_stats(const RoundArgs& a, const BinArgs&
 // rows: 0 here, OR-ed by k_pull_heavy afterwards).
 template <int W, int kWords, int kB>
 __device__ __forceinline__ void bin_finish(const RoundArgs& a, uint64_t v0, uint32_t nv,
-                                           const unsigned long long* acc_s, Acc& acc) {
+                                           const unsigned long long* acc_s, Acc& acc, const InjMasks<W>& im) {
     constexpr int kJ = (kWords + kB - 1) / kB;
     const uint32_t n = nv * W, n_pad = (n + 63) & ~63u;
     uint64_t sv[kJ], pv[kJ];
@@ -1367,7 +1383,7 @@ __device__ __forceinline__ void bin_finish(const RoundArgs& a, uint64_t v0, uint
         const uint64_t p = pv[j];
         const uint64_t s = sv[j] | p;
         const bool va = in && (!a.dead_mode || bit_alive(a.alive, (uint32_t)(a.begin + v0 + i / W)));  // dead: no receive
-        const uint64_t fr = va ? acc_s[i] & injm(a, i % W) & ~s : 0ull;
+        const uint64_t fr = va ? acc_s[i] & im.cur_at(i % W) & ~s : 0ull;
 #pragma unroll
         for (int w = 0; w < W; ++w)
             if (i % W == w) acc.fresh_or[w] |= fr;  // (constant register indices)
@@ -1390,6 +1406,7 @@ __global__ __launch_bounds__(kB) void k_bin_apply(RoundArgs a, BinArgs b, uint32
     __shared__ unsigned long long acc_s[kWords];
     __shared__ unsigned int cov_s[64 * W];
     Acc acc;
+    const InjMasks<W> im(a);
     const Bin bn = b.bins[blockIdx.x];
     const uint32_t nv = bn.v1 - bn.v0;
     const uint64_t v0 = bn.v0;
@@ -1407,7 +1424,7 @@ __global__ __launch_bounds__(kB) void k_bin_apply(RoundArgs a, BinArgs b, uint32
         acc_s[i] = 0ull;
         if (!b.needy_check) continue;
         const bool va = !a.dead_mode || bit_alive(a.alive, (uint32_t)(a.begin + v0 + i / W));
-        needy |= va && (injm(a, i % W) & ~(a.seen[v0 * W + i] | pend(i))) != 0;
+        needy |= va && (im.cur_at(i % W) & ~(a.seen[v0 * W + i] | pend(i))) != 0;
     }
     auto cov_out = [&] {
         if (b.src_stats || !a.cov) return;
@@ -1446,7 +1463,7 @@ __global__ __launch_bounds__(kB) void k_bin_apply(RoundArgs a, BinArgs b, uint32
         }
     }
     __syncthreads();
-    bin_finish<W, kWords, kB>(a, v0, nv, acc_s, acc);
+    bin_finish<W, kWords, kB>(a, v0, nv, acc_s, acc, im);
     flush<kB / 64>(acc, a.st);
     cov_out();
 }
@@ -1616,10 +1633,23 @@ __global__ __launch_bounds__(kSB) void k_bin_stream(RoundArgs a, BinArgs b, uint
 // round's words, a.fold).
 // Pipeline shape (kPipe, W = 1 only; others use 0): groups per stage kG, and how many iterations ahead
 // each load is issued -- bdst + ap_grp LA, ap_run LB, val LC (LA > LB > LC >= 1), kS = LA + 1 register sets.
-template <int W, int kPipe> struct ApplyPipe { static constexpr int kG = W == 1 ? 4 : W == 2 ? 2 : 1, LA = 3, LB = 2, LC = 1; };
-template <> struct ApplyPipe<1, 1> { static constexpr int kG = 2, LA = 5, LB = 3, LC = 1; };
-template <> struct ApplyPipe<1, 2> { static constexpr int kG = 2, LA = 5, LB = 4, LC = 2; };
-template <> struct ApplyPipe<1, 3> { static constexpr int kG = 2, LA = 6, LB = 5, LC = 3; };
+// kSeq (shapes 4-6, round 6): a wave's groups are one contiguous range of the bin instead of every kWaves-th
+// group, so the runs that start before a group are the wave's running count of run-start flags (a scalar: the
+// ballot's popcount), ap_grp is read once per wave and bin, and the group indices are scalars.  Strided, every
+// group's ap_grp word was a vector load and a register per stage, and the destinations came only one iteration
+// ahead of the run lookup that needs them (LA - LB = 1 in shapes 0, 2, 3).
+template <int W, int kPipe> struct ApplyPipe {
+    static constexpr int kG = W == 1 ? 4 : W == 2 ? 2 : 1, LA = 3, LB = 2, LC = 1;
+    static constexpr bool kSeq = false;
+};
+template <> struct ApplyPipe<1, 1> { static constexpr int kG = 2, LA = 5, LB = 3, LC = 1; static constexpr bool kSeq = false; };
+template <> struct ApplyPipe<1, 2> { static constexpr int kG = 2, LA = 5, LB = 4, LC = 2; static constexpr bool kSeq = false; };
+template <> struct ApplyPipe<1, 3> { static constexpr int kG = 2, LA = 6, LB = 5, LC = 3; static constexpr bool kSeq = false; };
+template <> struct ApplyPipe<1, 4> { static constexpr int kG = 2, LA = 5, LB = 4, LC = 2; static constexpr bool kSeq = true; };
+template <> struct ApplyPipe<1, 5> { static constexpr int kG = 2, LA = 6, LB = 4, LC = 2; static constexpr bool kSeq = true; };
+template <> struct ApplyPipe<1, 6> { static constexpr int kG = 2, LA = 7, LB = 5, LC = 3; static constexpr bool kSeq = true; };
+template <> struct ApplyPipe<1, 7> { static constexpr int kG = 2, LA = 8, LB = 5, LC = 2; static constexpr bool kSeq = true; };
+template <> struct ApplyPipe<1, 8> { static constexpr int kG = 2, LA = 7, LB = 4, LC = 2; static constexpr bool kSeq = true; };
 
 template <int W, int kWords, int kB, int kPipe = 0, bool kProbe = false>  // kProbe: apply_probe's clocks
 __global__ __launch_bounds__(kB) void k_bin_apply_runs(RoundArgs a, BinArgs b, uint32_t wd) {
@@ -1627,11 +1657,14 @@ __global__ __launch_bounds__(kB) void k_bin_apply_runs(RoundArgs a, BinArgs b, u
     constexpr int kG = ApplyPipe<W, kPipe>::kG;                      // groups per stage
     constexpr int LA = ApplyPipe<W, kPipe>::LA, LB = ApplyPipe<W, kPipe>::LB, LC = ApplyPipe<W, kPipe>::LC;
     constexpr int kS = LA + 1;                                        // stages in flight
+    constexpr bool kSeq = ApplyPipe<W, kPipe>::kSeq;
     static_assert(LA > LB && LB > LC && LC >= 1, "load lags");
     __shared__ unsigned long long acc_s[kWords];
     __shared__ unsigned int cov_s[64 * W];
     Acc acc;
+    const InjMasks<W> im(a);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wave_u = __builtin_amdgcn_readfirstlane(wave);  // (the same value, known wave-uniform)
     if (!b.src_stats && a.cov)
         for (uint32_t i = threadIdx.x; i < 64 * W; i += kB) cov_s[i] = 0;
     const unsigned long long upto = lane == 63 ? ~0ull : (2ull << lane) - 1;  // lanes 0..lane
@@ -1661,7 +1694,7 @@ __global__ __launch_bounds__(kB) void k_bin_apply_runs(RoundArgs a, BinArgs b, u
             acc_s[i] = 0ull;
             if (!b.needy_check) continue;
             const bool va = !a.dead_mode || bit_alive(a.alive, (uint32_t)(a.begin + v0 + i / W));
-            needy |= va && (injm(a, i % W) & ~(a.seen[v0 * W + i] | pend(i))) != 0;
+            needy |= va && (im.cur_at(i % W) & ~(a.seen[v0 * W + i] | pend(i))) != 0;
         }
         tick(kProbeInit);
         if (kProbe && threadIdx.x == 0) {
@@ -1678,13 +1711,19 @@ __global__ __launch_bounds__(kB) void k_bin_apply_runs(RoundArgs a, BinArgs b, u
         if (threadIdx.x == 0) acc.pulled += bn.s1 - bn.s0;  // slots scanned (byte accounting)
         if (bn.s1 > bn.s0) {
             const uint64_t g_lo = bn.s0 >> 6, g_hi = ((bn.s1 - 1) >> 6) + 1;
-            // this wave's groups: g_lo + wave + kWaves * t, t < n_t
-            const uint32_t n_t =
-                g_hi - g_lo > (uint64_t)wave ? (uint32_t)((g_hi - g_lo - wave + kWaves - 1) / kWaves) : 0u;
+            // this wave's groups: g_lo + wave + kWaves * t, t < n_t (kSeq: g_lo + t_lo + t, t < n_t)
+            const uint64_t n_g = g_hi - g_lo;
+            const uint64_t t_lo = kSeq ? n_g * (uint32_t)wave_u / kWaves : 0;
+            const uint32_t n_t = kSeq ? (uint32_t)(n_g * ((uint32_t)wave_u + 1) / kWaves - t_lo)
+                                 : n_g > (uint64_t)wave ? (uint32_t)((n_g - wave + kWaves - 1) / kWaves) : 0u;
             const uint32_t n_it = (n_t + kG - 1) / kG;
             uint32_t d[kS][kG], gr[kS][kG], off[kS][kG];
             uint64_t x[kS][kG][W];
-            auto grp = [&](uint32_t i, int j) { return g_lo + wave + (uint64_t)kWaves * (i * kG + j); };
+            // kSeq: the runs that start before the wave's next group (scalar)
+            uint32_t rc = kSeq && n_t ? __builtin_amdgcn_readfirstlane(b.ap_grp[g_lo + t_lo]) : 0u;
+            auto grp = [&](uint32_t i, int j) {
+                return kSeq ? g_lo + t_lo + (uint64_t)(i * kG + j) : g_lo + wave + (uint64_t)kWaves * (i * kG + j);
+            };
             auto valid = [&](uint32_t i, int j) {  // lane's slot belongs to the bin (and to this wave's groups)
                 const uint64_t g = grp(i, j), q = g * 64 + lane;
                 return i * kG + j < n_t && q >= bn.s0 && q < bn.s1;
@@ -1693,16 +1732,26 @@ __global__ __launch_bounds__(kB) void k_bin_apply_runs(RoundArgs a, BinArgs b, u
 #pragma unroll
                 for (int j = 0; j < kG; ++j) {
                     const uint64_t g = min(grp(i, j), g_hi - 1);
-                    d[st][j] = b.bdst[g * 64 + lane];
-                    gr[st][j] = b.ap_grp[g];
+                    // kSeq: the raw 32-bit word of the lane's slot pair, its half taken where it is used.  (A u16
+                    // load whose flag test the compiler narrowed to a 16-bit compare kept a separate zero-extension
+                    // in the load's own iteration, which waited for the load there: every iteration waited for its
+                    // own destinations, whatever the lags.)
+                    if (kSeq) d[st][j] = reinterpret_cast<const uint32_t*>(b.bdst)[(g * 64 + lane) >> 1];
+                    else d[st][j] = b.bdst[g * 64 + lane];
+                    if (!kSeq) gr[st][j] = b.ap_grp[g];
                 }
             };
             auto ld_b = [&](int st, uint32_t i) {  // the run of each slot -> its offset
 #pragma unroll
                 for (int j = 0; j < kG; ++j) {
+                    if (kSeq) d[st][j] = (d[st][j] >> ((lane & 1) * 16)) & 0xFFFFu;  // the lane's slot
                     const unsigned long long fl = __ballot((d[st][j] & kRunStart) != 0);
                     // a slot of the bin lies in a run that starts at or before it (run >= 0); others clamp
-                    const uint32_t run = min(gr[st][j] + (uint32_t)__popcll(fl & upto) - 1u, run_max);
+                    // (kSeq: stages come here in order, so rc counts the runs before group (i, j); a clamped
+                    // group past the wave's range adds garbage that only such groups see)
+                    const uint32_t g0 = kSeq ? rc : gr[st][j];
+                    if (kSeq) rc += (uint32_t)__popcll(fl);
+                    const uint32_t run = min(g0 + (uint32_t)__popcll(fl & upto) - 1u, run_max);
                     off[st][j] = b.ap_run[run];
                 }
             };
@@ -1746,7 +1795,7 @@ __global__ __launch_bounds__(kB) void k_bin_apply_runs(RoundArgs a, BinArgs b, u
         }
         __syncthreads();
         tick(kProbeSlots);
-        bin_finish<W, kWords, kB>(a, v0, nv, acc_s, acc);
+        bin_finish<W, kWords, kB>(a, v0, nv, acc_s, acc, im);
         tick(kProbeFinish);
     };
     // Rows of kApplyRow consecutive bins, row r to XCD group r % 8 (the blocks x + 8 i): member j of group x
@@ -2841,6 +2890,7 @@ hipError_t launch_pull_rows(const RoundArgs& a, uint32_t W_, hipStream_t s) {
 #define GOSSIP_ROWS(COV, FR)                                                                        \
     do {                                                                                            \
         if (a.row_step == 1 && a.row_q == 256 && W == 1 && !COV && !FR) go(k_pull_rows<W, COV, FR, 1, 256>); \
+        else if (a.row_step == 1 && a.row_pre == 2 && W == 1) go(k_pull_rows<1, COV, FR, 1, 256, 2>);      \
         else if (a.row_step == 1) go(k_pull_rows<W, COV, FR, 1>);                                   \
         else go(k_pull_rows<W, COV, FR, 2>);                                                        \
     } while (0)
@@ -2990,8 +3040,18 @@ hipError_t launch_bin_apply(const RoundArgs& a, const BinArgs& b, uint32_t W_, h
                 hipLaunchKernelGGL((k_bin_apply_runs<1, kBinWords, 1024, 1>), dim3(sgrid), dim3(1024), 0, s, a, b, wd);
             else if (b.apply_pipe == 2)
                 hipLaunchKernelGGL((k_bin_apply_runs<1, kBinWords, 1024, 2>), dim3(sgrid), dim3(1024), 0, s, a, b, wd);
-            else
+            else if (b.apply_pipe == 3)
                 hipLaunchKernelGGL((k_bin_apply_runs<1, kBinWords, 1024, 3>), dim3(sgrid), dim3(1024), 0, s, a, b, wd);
+            else if (b.apply_pipe == 4)
+                hipLaunchKernelGGL((k_bin_apply_runs<1, kBinWords, 1024, 4>), dim3(sgrid), dim3(1024), 0, s, a, b, wd);
+            else if (b.apply_pipe == 5)
+                hipLaunchKernelGGL((k_bin_apply_runs<1, kBinWords, 1024, 5>), dim3(sgrid), dim3(1024), 0, s, a, b, wd);
+            else if (b.apply_pipe == 6)
+                hipLaunchKernelGGL((k_bin_apply_runs<1, kBinWords, 1024, 6>), dim3(sgrid), dim3(1024), 0, s, a, b, wd);
+            else if (b.apply_pipe == 7)
+                hipLaunchKernelGGL((k_bin_apply_runs<1, kBinWords, 1024, 7>), dim3(sgrid), dim3(1024), 0, s, a, b, wd);
+            else
+                hipLaunchKernelGGL((k_bin_apply_runs<1, kBinWords, 1024, 8>), dim3(sgrid), dim3(1024), 0, s, a, b, wd);
         } else if (b.bin_words > kBinWords / 2) {
             GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_apply_runs<W, kBinWords, 1024>),
                                                            dim3(sgrid), dim3(1024), 0, s, a, b, wd));

@@ -346,6 +346,13 @@ _VARIANTS = {"defer_1": ({"defer_permille": 1}, {"blocked": "off"}), "stream": (
              "stream_needy_test": ({"bin_stream": 1, "bin_needy_skip": 0}, {}),
              "apply_pipe_1": ({"apply_pipe": 1}, {}), "apply_pipe_2": ({"apply_pipe": 2}, {}),
              "apply_pipe_3": ({"apply_pipe": 3}, {}), "heavy_after_apply": ({"heavy_side": 0}, {}),
+             # whole bins (the pipeline shapes only apply to them; overlays of <= 2^20 peers default to small bins)
+             "whole_bins_pipe_2": ({"bin_words": 18432, "apply_pipe": 2}, {}),
+             "whole_bins_pipe_4": ({"bin_words": 18432, "apply_pipe": 4}, {}),
+             "whole_bins_pipe_5": ({"bin_words": 18432, "apply_pipe": 5}, {}),
+             "whole_bins_pipe_6": ({"bin_words": 18432, "apply_pipe": 6}, {}),
+             "whole_bins_pipe_7": ({"bin_words": 18432, "apply_pipe": 7}, {}),
+             "whole_bins_pipe_8": ({"bin_words": 18432, "apply_pipe": 8}, {}),
              "scatter_small": ({"scatter_small": 1}, {}),
              "small_kernels": ({"bin_words": 1024, "bin_chunk": 1024, "scatter_small": 1}, {}),
              "split_units": ({"scatter_units": 4096}, {}),
@@ -353,6 +360,11 @@ _VARIANTS = {"defer_1": ({"defer_permille": 1}, {"blocked": "off"}), "stream": (
              "apply_wide": ({"bin_words": 2048, "apply_wide": 1}, {}),
              "apply_probe": ({"apply_probe": 1}, {}), "apply_one_per_bin": ({"apply_persist": 0}, {}), "slots_needy_test": ({"bin_stream": 0, "bin_needy_skip": 0}, {}),
              "blocked_dense": ({"blocked_bin_slots": 0}, {"blocked_permille": 1000}),
+             "blocked_dense_pipe": ({"blocked_bin_slots": 0, "blocked_pipe": 1}, {"blocked_permille": 1000}),
+             "blocked_unpiped": ({"blocked_pipe": 0}, {"blocked_permille": 1000}),
+             "row_prefetch_2": ({"row_prefetch": 2}, {}),
+             "row_prefetch_2_all_pull": ({"row_prefetch": 2}, {"bin_permille": 100000}),
+             "blocked_wide_pipe": ({"blocked_pipe": 1}, {"blocked_permille": 1000}),
              "blocked_dense_clear_peers": ({"blocked_bin_slots": 0, "blocked_clear_all": 0}, {"blocked_permille": 1000})}
 
 
