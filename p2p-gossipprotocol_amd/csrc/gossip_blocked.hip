@@ -94,6 +94,8 @@ struct PbAcc {
 // ---------------------------------------------------------------------------
 // level 1: workgroup w's share of the frontier's deliveries -> coarse-bin records
 // ---------------------------------------------------------------------------
+// (Round 6: the expansion's next batch loaded into a second register set without copies spilled at 128 VGPRs and
+// took level 1 from 5.56 to 7.99 ms per config-4 run; tools/experiments/r06_blocked_level1_expand_rotation.patch.)
 template <bool CA, bool COV>
 __global__ __launch_bounds__(kPbBlock) void k_pb_scatter(RoundArgs a, PbArgs p, uint32_t wd) {
     __shared__ uint32_t lo_s[kPbCoarse + 1];

@@ -219,7 +219,6 @@ struct gossip_ctx {
                                           // exchange {tile bitmap, packed non-zero words} (gossip_dist.hip)
     uint32_t row_step = 1;                // "pull_step": k_pull_rows's neighbour words per row per step
     uint32_t row_q = 128, row_grid = 0;   // "row_queue" / "row_grid": k_pull_rows's queue and grid (A/B)
-    uint32_t row_pre = 1;                 // "row_prefetch": k_pull_rows's tiles in flight per wave (1 or 2)
                                           // (config 4 round 7: 2 -> 1, 180 -> 101 M gathers, 6.6-6.8 ->
                                           // 5.4-5.7 ms; most rows stop at their first neighbour)
     bool bin_stream = false;      // streamed binned layout (chosen in prepare_bins)
@@ -636,7 +635,6 @@ RoundArgs make_args(gossip_ctx* c) {
     a.hacc = c->replaying && c->hacc ? c->rep_aux + c->rep_tw * (c->hist_cap + 1) + c->rep_hw * c->rep_round : c->hacc;
     a.row_step = c->row_step;
     a.row_q = c->row_q;
-    a.row_pre = c->row_pre;
     a.row_grid = c->row_grid;
     a.chk = reinterpret_cast<unsigned long long*>(c->inj_live + kMaxWords);
     a.inj_live = c->world <= 1 && c->n_local == c->n ? c->inj_live : nullptr;  // a partition injects its own only
@@ -2088,7 +2086,6 @@ gossip_status gossip_set_tuning(gossip_ctx* c, const char* key, int64_t value) {
     else if (k == "replay") c->replay_req = value != 0;
     else if (k == "scatter_direct") c->scatter_direct = value != 0;
     else if (k == "row_queue") c->row_q = value == 256 ? 256u : 128u;
-    else if (k == "row_prefetch") c->row_pre = value == 2 ? 2u : 1u;
     else if (k == "row_grid") c->row_grid = u;
     else if (k == "scatter_units") c->scatter_units = u;
     else if (k == "scatter_split_direct") c->split_direct = value != 0;

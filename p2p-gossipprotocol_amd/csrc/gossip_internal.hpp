@@ -237,7 +237,8 @@ struct PbArgs {
     const unsigned long long* marks;  // narrow rounds with valid tile marks (RoundArgs.tcur: every tile with new
                               // words marked): level 1 reads the new words of marked tiles only; null: every tile
     uint64_t n_local;
-    uint32_t pipe;            // "blocked_pipe": the split's and the apply's record loops pipelined (k_pb_split<true>)
+    uint32_t pipe;            // "blocked_pipe": the split's and the apply's record loops pipelined (k_pb_split<true>,
+                              // k_pb_apply<true>)
 };
 
 struct PbState {
@@ -349,7 +350,6 @@ struct RoundArgs {
     uint32_t src_booked;           // k_pull_rows: the sweep books no source side
     uint32_t row_step;             // k_pull_rows: neighbour words gathered per row per step (1 or 2)
     uint32_t row_q;                // k_pull_rows: queue entries per wave (128; 256: "row_queue", A/B)
-    uint32_t row_pre;              // k_pull_rows: tiles in flight per wave in the sweep (1 or 2: "row_prefetch")
     uint32_t row_grid;             // k_pull_rows: workgroups (0: kMaxGrid; "row_grid", A/B)
     unsigned long long* chk;       // checked-index build (GOSSIP_CHECKED): {trips, site, index, bound} of the
                                    // first index past its bound (gossip_device.hpp GOSSIP_IDX); unused otherwise

@@ -536,14 +536,10 @@ __global__ __launch_bounds__(kBlock) void k_frontier_bits(RoundArgs a) {
 // for whole rows) -- or at its end.  Finished lanes take the next row:
 // fr = (OR of the scanned neighbours) & need, and a row that stops early
 // already holds all of need.
-// kTiles (round 6, "row_prefetch" 2): two tiles' words and row bounds in flight per wave, in two buffers taken in
-// turn (each reloaded right after its sweep, so no buffer is copied while its loads are in flight).  With one
-// buffer the next tile's loads were copied into the current tile's registers at the loop's end, a wait for
-// loads issued in the same iteration: one memory round trip per swept tile and wave.
-template <int W, bool COV, bool FRONT, int kRowB, int kRowQ = 128, int kTiles = 1>  // kRowB: edges per lane per step; kRowQ: queue entries per wave
+template <int W, bool COV, bool FRONT, int kRowB, int kRowQ = 128>  // kRowB: edges per lane per step; kRowQ: queue entries per wave
 // (116 VGPRs, four waves per SIMD.  Launch bounds asking five or six spill to scratch and ran round 7 at
 // 5.9-6.1 and 8.3-8.6 ms against 4.8-5.1: the sweep and the row state do not fit 96 or 80 registers.)
-__global__ __launch_bounds__(kBlock, kTiles == 2 ? 4 : 1) void k_pull_rows(RoundArgs a, uint32_t wd) {
+__global__ __launch_bounds__(kBlock) void k_pull_rows(RoundArgs a, uint32_t wd) {
     __shared__ unsigned int cov_s[COV ? 64 * W : 1];
     __shared__ uint32_t q_v[kWavesPerBlock][kRowQ];
     __shared__ uint32_t q_d[kWavesPerBlock][kRowQ];
@@ -669,21 +665,13 @@ __global__ __launch_bounds__(kBlock, kTiles == 2 ? 4 : 1) void k_pull_rows(Round
         }
         q_tail += (uint32_t)__popcll(bal);
     };
-    TileIn nxt, alt;
+    // (Round 6 measured two tiles in flight per wave, swept as pairs from two buffers: 124-147 VGPRs, so three
+    // waves per SIMD or spills at four; round 7 4.94 -> 5.48 ms, tools/experiments/r06_row_pull_tile_pairs.patch.)
+    TileIn nxt;
     load_tile(t, nxt);
-    if (kTiles == 2) load_tile(t + nwaves, alt);
     while (true) {
-        // refill the queue while it has room for a whole tile (kTiles 2: for two, swept as a pair -- straight-line
-        // code, so the wait before each sweep counts the other buffer's loads as still in flight)
-        while (t < n_tiles && q_tail - q_head <= (uint32_t)(kRowQ - 64 * kTiles)) {
-            if (kTiles == 2) {
-                sweep_tile(t, nxt);  // (a tile past the end sweeps nothing)
-                load_tile(t + 2 * nwaves, nxt);  // (clamped past the end)
-                sweep_tile(t + nwaves, alt);
-                load_tile(t + 3 * nwaves, alt);
-                t += 2 * nwaves;
-                continue;
-            }
+        // refill the queue while it has room for a whole tile
+        while (t < n_tiles && q_tail - q_head <= (uint32_t)(kRowQ - 64)) {
             const TileIn cur = nxt;
             load_tile(t + nwaves, nxt);  // unconditional (clamped): the wait before the sweep can then count it
             sweep_tile(t, cur);
@@ -2890,7 +2878,6 @@ hipError_t launch_pull_rows(const RoundArgs& a, uint32_t W_, hipStream_t s) {
 #define GOSSIP_ROWS(COV, FR)                                                                        \
     do {                                                                                            \
         if (a.row_step == 1 && a.row_q == 256 && W == 1 && !COV && !FR) go(k_pull_rows<W, COV, FR, 1, 256>); \
-        else if (a.row_step == 1 && a.row_pre == 2 && W == 1) go(k_pull_rows<1, COV, FR, 1, 256, 2>);      \
         else if (a.row_step == 1) go(k_pull_rows<W, COV, FR, 1>);                                   \
         else go(k_pull_rows<W, COV, FR, 2>);                                                        \
     } while (0)

@@ -362,8 +362,6 @@ _VARIANTS = {"defer_1": ({"defer_permille": 1}, {"blocked": "off"}), "stream": (
              "blocked_dense": ({"blocked_bin_slots": 0}, {"blocked_permille": 1000}),
              "blocked_dense_pipe": ({"blocked_bin_slots": 0, "blocked_pipe": 1}, {"blocked_permille": 1000}),
              "blocked_unpiped": ({"blocked_pipe": 0}, {"blocked_permille": 1000}),
-             "row_prefetch_2": ({"row_prefetch": 2}, {}),
-             "row_prefetch_2_all_pull": ({"row_prefetch": 2}, {"bin_permille": 100000}),
              "blocked_wide_pipe": ({"blocked_pipe": 1}, {"blocked_permille": 1000}),
              "blocked_dense_clear_peers": ({"blocked_bin_slots": 0, "blocked_clear_all": 0}, {"blocked_permille": 1000})}
 
