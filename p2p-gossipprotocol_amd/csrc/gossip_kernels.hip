@@ -3051,8 +3051,11 @@ hipError_t launch_bin_apply(const RoundArgs& a, const BinArgs& b, uint32_t W_, h
             // 16 KB accumulators: eight 4-wave workgroups per CU (small bins of small overlays)
             GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_apply_runs<W, kSmallBinWords, 256>),
                                                            dim3(sgrid), dim3(256), 0, s, a, b, wd));
-        } else {
+        } else if (wp_of(W_) == 1) {
             // 72 KB accumulators: two 8-wave workgroups per CU, one's per-bin phases under the other's slots
+            // (one word: shape 5's contiguous groups)
+            hipLaunchKernelGGL((k_bin_apply_runs<1, kBinWords / 2, 512, 5>), dim3(sgrid), dim3(512), 0, s, a, b, wd);
+        } else {
             GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_apply_runs<W, kBinWords / 2, 512>),
                                                            dim3(sgrid), dim3(512), 0, s, a, b, wd));
         }
