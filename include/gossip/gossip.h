@@ -350,7 +350,9 @@ gossip_status gossip_kernel_bytes(gossip_ctx* ctx, const char* kernel, double* b
  * 1 default, 0 always test), "apply_pipe" (the streamed apply's load
  * pipeline shape, 0-8, A/B; default 5), "blocked_pipe" (1 default: the
  * blocked rounds' level-2 and apply record loops keep the next batch's loads
- * in flight; 0 the unpipelined loops), "apply_persist" (1 default: the
+ * in flight; 0 the unpipelined loops), "zero_fill" (1 default: the reset
+ * clears the seen and new-word arrays with the runtime's fill; 0 the
+ * library's own 16-B store kernel), "apply_persist" (1 default: the
  * streamed apply runs as resident workgroups taking bins from per-XCD
  * counters; 0: one workgroup per bin), "replay" (0: gossip_run never replays a
  * recorded schedule), "scatter_direct" (partitioned runs: a block's binned

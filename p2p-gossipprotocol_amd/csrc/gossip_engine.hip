@@ -241,6 +241,8 @@ struct gossip_ctx {
     bool pb_clear_all = true;    // "blocked_clear_all": wide blocked rounds clear new words whole in level 2
     bool pb_marks = true;        // "blocked_marks": narrow blocked rounds' level 1 sweeps the marked tiles only
     bool pb_pipe = true;         // "blocked_pipe": the split's and the blocked apply's record loops pipelined
+    bool zero_fill = true;       // "zero_fill": the reset clears its word arrays with hipMemsetAsync (0: k_zero2;
+                                 // round 6, arms alternated: config 4 42.34 -> 42.10 ms, config 2 4.36 -> 4.30)
     bool heavy_side = true;      // "heavy_side": a binned round's heavy-row pull beside its scatter (P = 1)
     bool cur_clear_all = false;  // (the round in flight does)
     bool scatter_direct = false; // "scatter_direct": a vertex block's scatter reads other blocks' words directly
@@ -2094,6 +2096,7 @@ gossip_status gossip_set_tuning(gossip_ctx* c, const char* key, int64_t value) {
     else if (k == "blocked_clear_all") c->pb_clear_all = value != 0;
     else if (k == "blocked_marks") c->pb_marks = value != 0;
     else if (k == "blocked_pipe") c->pb_pipe = value != 0;
+    else if (k == "zero_fill") c->zero_fill = value != 0;
     else if (k == "heavy_side") c->heavy_side = value != 0;
     else if (k == "apply_pipe") {
         if (value < 0 || value > 8) return fail(GOSSIP_EINVAL, "apply_pipe must be 0..8");
@@ -2378,7 +2381,7 @@ gossip_status gossip_reset(gossip_ctx* c) {
                                  c->tact[0], c->tact[1], c->st, s));
         c->bufs_zero = true;
     } else {
-        HIPCHK(launch_zero_words(c->seen, words, s));
+        HIPCHK(launch_zero_words(c->seen, words, s, c->zero_fill));
         if (!c->bufs_zero && !c->in_round && c->lin_idx[0] >= 0 && c->lin_idx[1] >= 0) {
             // the last two rounds pulled needy lists: each wrote only its list's rows and the heavy rows into a
             // buffer cleared before it (the list rounds' contract: one word per peer, nothing injected or
@@ -2391,8 +2394,8 @@ gossip_status gossip_reset(gossip_ctx* c) {
             c->bufs_zero = true;
         }
         if (!c->bufs_zero) {  // (a run that ended normally left both zero)
-            HIPCHK(launch_zero_words(c->nw, words, s));
-            HIPCHK(launch_zero_words(c->nx, words, s));
+            HIPCHK(launch_zero_words(c->nw, words, s, c->zero_fill));
+            HIPCHK(launch_zero_words(c->nx, words, s, c->zero_fill));
             c->bufs_zero = true;
         }
         for (int k = 0; k < 2; ++k) HIPCHK(hipMemsetAsync(c->tact[k], 0, tact_bytes(c), s));

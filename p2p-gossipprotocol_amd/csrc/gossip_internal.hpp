@@ -464,7 +464,7 @@ hipError_t launch_rejoin_select(const RoundArgs& a, const RebootArgs& r, const u
                                 const unsigned long long* n_list, uint64_t max_list, hipStream_t s);
 hipError_t launch_commit_nx(uint64_t* seen, const uint64_t* nx, uint64_t n_words, hipStream_t s);
 hipError_t launch_first2(const uint64_t* rp, const uint32_t* col, uint64_t n, uint64_t* out, hipStream_t s);
-hipError_t launch_zero_words(uint64_t* words, uint64_t n_words, hipStream_t s);
+hipError_t launch_zero_words(uint64_t* words, uint64_t n_words, hipStream_t s, bool fill);
 // up to kZeroRanges small device ranges (whole 32-bit words) cleared by one launch: a round's stat lines,
 // tile marks, heavy-row accumulators and list counters, instead of one fill each (config 2: 55 rounds a
 // step, ~7 us of GPU time and launch gap per fill)

@@ -354,6 +354,7 @@ _VARIANTS = {"defer_1": ({"defer_permille": 1}, {"blocked": "off"}), "stream": (
              "whole_bins_pipe_7": ({"bin_words": 18432, "apply_pipe": 7}, {}),
              "whole_bins_pipe_8": ({"bin_words": 18432, "apply_pipe": 8}, {}),
              "half_bins": ({"bin_words": 9216}, {}),
+             "zero_fill": ({"zero_fill": 1}, {}),
              "scatter_small": ({"scatter_small": 1}, {}),
              "small_kernels": ({"bin_words": 1024, "bin_chunk": 1024, "scatter_small": 1}, {}),
              "split_units": ({"scatter_units": 4096}, {}),

@@ -24,7 +24,8 @@ if w.kills:
     e.schedule_kills([k[0] for k in w.kills], [k[1] for k in w.kills])
 # the engine's defaults of the keys an arm may set (an arm leaves the others at these)
 defaults = {"row_grid": 0, "row_queue": 128, "apply_pipe": 5, "pull_first2": 1, "heavy_exit": 1, "bin_needy_skip": 1,
-            "apply_persist": 1, "in_flight": 1, "blocked_pipe": 1}
+            "apply_persist": 1, "in_flight": 1, "blocked_pipe": 1,
+            "zero_fill": 1}
 e.reset()
 e.run()
 e.enable_timing(True)
