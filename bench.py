@@ -510,8 +510,12 @@ def main():
         rounds_prof = per_round_profile(run, w.n)
         dense = [r for r in rounds_prof if r["mode"] == "bin"]
         alg = sum(r["alg_bytes"] for r in rounds_prof)
-        # the dominant kernel by device time (part 0's; every part runs the same schedule)
-        dom = max((k for k in KERNELS), key=lambda k: k_ms[0][k][0])
+        # the dominant kernel by device time (part 0's; every part runs the same schedule).  A side-stream kernel's
+        # events also time its wait for CUs beside the scatter (config 5's heavy-row pull: 0.94 ms per launch by
+        # events for 1.5 % of its design bytes), so it is not a candidate when it ran beside a join (critical())
+        from gossip_hip.engine import SIDE_KERNELS
+        side_used = k_ms[0].get("heavy_commit", (0.0, 0))[1] > 0
+        dom = max((k for k in KERNELS if not (side_used and k in SIDE_KERNELS)), key=lambda k: k_ms[0][k][0])
         ms, launches = k_ms[0][dom]
         # without the work-avoiding rounds: a pull round's 8(d) bytes out of the numerator and its kernel and
         # exchange time out of the step; a ping round's liveness bytes out of the numerator (its push or binned

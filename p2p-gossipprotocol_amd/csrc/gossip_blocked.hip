@@ -556,7 +556,13 @@ template <bool kRot>
 __global__ __launch_bounds__(1024) void k_pb_apply(RoundArgs a, PbArgs p) {
     __shared__ unsigned long long acc_s[kBinWords];
     __shared__ uint32_t meta_s[2][3 * kPbSlices + 2];  // per bin: s2_len[4], s2_base lo/hi [8], f_lo, f_lo + 1
+    // the bin's activated tiles (a.tnx bits), gathered in LDS and OR-ed into a.tnx once per bin (round 6: a
+    // read-then-atomic of the tnx word per activated tile inside the finish waited vmcnt(0) -- for the seen and
+    // nx stores just issued too -- up to 18 times per wave and bin)
+    constexpr uint32_t kMarkWords = (kBinWords / 64 + 63) / 64 + 1;
+    __shared__ unsigned long long tmark_s[kMarkWords];
     for (uint32_t i = threadIdx.x; i < kBinWords; i += 1024) acc_s[i] = 0ull;
+    if (threadIdx.x < kMarkWords) tmark_s[threadIdx.x] = 0ull;
     Acc acc;
     const int lane = threadIdx.x & 63;
     const uint64_t inj = injm(a, 0);
@@ -699,16 +705,19 @@ __global__ __launch_bounds__(1024) void k_pb_apply(RoundArgs a, PbArgs p) {
                 acc.activated++;
                 acc.fresh_or[0] |= fr;
             }
-            if (a.tnx) {  // the tile joins the next round's frontier tiles
-                if (b && lane == 0) {
-                    const uint64_t t = v >> 6;
-                    unsigned long long* tw = reinterpret_cast<unsigned long long*>(a.tnx) + (t >> 6);
-                    const unsigned long long tb = 1ull << (t & 63);
-                    if (!(*tw & tb)) atomicOr(tw, tb);
-                }
+            if (a.tnx && b && lane == 0) {  // the tile joins the next round's frontier tiles
+                const uint64_t t = v >> 6;
+                atomicOr(&tmark_s[(t >> 6) - ((uint64_t)v0 >> 12)], 1ull << (t & 63));  // (v0: a whole tile)
             }
         }
         __syncthreads();  // the accumulator is clear and the next segment table is in
+        if (a.tnx && threadIdx.x < kMarkWords) {
+            const unsigned long long m = tmark_s[threadIdx.x];
+            if (m) {
+                atomicOr(reinterpret_cast<unsigned long long*>(a.tnx) + ((uint64_t)v0 >> 12) + threadIdx.x, m);
+                tmark_s[threadIdx.x] = 0ull;  // (read and cleared by this thread alone; the next bin marks after
+            }                                  //  its record loop's barrier)
+        }
     }
     flush<1024 / 64>(acc, a.st);
 }
