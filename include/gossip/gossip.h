@@ -348,7 +348,7 @@ gossip_status gossip_kernel_bytes(gossip_ctx* ctx, const char* kernel, double* b
  * -1 default 600, 0 never, 1000 always), "bin_needy_skip" (binned rounds
  * with over one missing pair per peer skip the apply's per-bin needy test:
  * 1 default, 0 always test), "apply_pipe" (the streamed apply's load
- * pipeline shape, 0-8, A/B; default 5), "blocked_pipe" (1 default: the
+ * pipeline shape, 0-10, A/B; default 5), "blocked_pipe" (1 default: the
  * blocked rounds' level-2 and apply record loops keep the next batch's loads
  * in flight; 0 the unpipelined loops), "zero_fill" (1 default: the reset
  * clears the seen and new-word arrays with the runtime's fill; 0 the

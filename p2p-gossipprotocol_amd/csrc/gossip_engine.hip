@@ -236,7 +236,7 @@ struct gossip_ctx {
     bool cur_defer = false;       // this round defers: advance() folds nx into seen
     bool full_liveness = false;  // "full_liveness": ping every edge each ping round (A/B against closed form)
     uint64_t cur_missing = 0;    // (peer, message) pairs still missing at the round's push start (round_begin)
-    uint32_t apply_pipe = 5;     // "apply_pipe": the streamed apply's pipeline shape (0-8; round 6: 5, the
+    uint32_t apply_pipe = 5;     // "apply_pipe": the streamed apply's pipeline shape (0-10; round 6: 5, the
                                  // contiguous-group shape with every load two iterations ahead, measured best)
     bool pb_clear_all = true;    // "blocked_clear_all": wide blocked rounds clear new words whole in level 2
     bool pb_marks = true;        // "blocked_marks": narrow blocked rounds' level 1 sweeps the marked tiles only
@@ -2099,7 +2099,7 @@ gossip_status gossip_set_tuning(gossip_ctx* c, const char* key, int64_t value) {
     else if (k == "zero_fill") c->zero_fill = value != 0;
     else if (k == "heavy_side") c->heavy_side = value != 0;
     else if (k == "apply_pipe") {
-        if (value < 0 || value > 8) return fail(GOSSIP_EINVAL, "apply_pipe must be 0..8");
+        if (value < 0 || value > 10) return fail(GOSSIP_EINVAL, "apply_pipe must be 0..10");
         c->apply_pipe = (uint32_t)value;
     }
     else if (k == "apply_persist") c->apply_persist = value != 0;

@@ -1638,6 +1638,8 @@ template <> struct ApplyPipe<1, 5> { static constexpr int kG = 2, LA = 6, LB = 4
 template <> struct ApplyPipe<1, 6> { static constexpr int kG = 2, LA = 7, LB = 5, LC = 3; static constexpr bool kSeq = true; };
 template <> struct ApplyPipe<1, 7> { static constexpr int kG = 2, LA = 8, LB = 5, LC = 2; static constexpr bool kSeq = true; };
 template <> struct ApplyPipe<1, 8> { static constexpr int kG = 2, LA = 7, LB = 4, LC = 2; static constexpr bool kSeq = true; };
+template <> struct ApplyPipe<1, 9> { static constexpr int kG = 3, LA = 6, LB = 4, LC = 2; static constexpr bool kSeq = true; };
+template <> struct ApplyPipe<1, 10> { static constexpr int kG = 3, LA = 5, LB = 3, LC = 1; static constexpr bool kSeq = true; };
 
 template <int W, int kWords, int kB, int kPipe = 0, bool kProbe = false>  // kProbe: apply_probe's clocks
 __global__ __launch_bounds__(kB) void k_bin_apply_runs(RoundArgs a, BinArgs b, uint32_t wd) {
@@ -3037,8 +3039,12 @@ hipError_t launch_bin_apply(const RoundArgs& a, const BinArgs& b, uint32_t W_, h
                 hipLaunchKernelGGL((k_bin_apply_runs<1, kBinWords, 1024, 6>), dim3(sgrid), dim3(1024), 0, s, a, b, wd);
             else if (b.apply_pipe == 7)
                 hipLaunchKernelGGL((k_bin_apply_runs<1, kBinWords, 1024, 7>), dim3(sgrid), dim3(1024), 0, s, a, b, wd);
-            else
+            else if (b.apply_pipe == 8)
                 hipLaunchKernelGGL((k_bin_apply_runs<1, kBinWords, 1024, 8>), dim3(sgrid), dim3(1024), 0, s, a, b, wd);
+            else if (b.apply_pipe == 9)
+                hipLaunchKernelGGL((k_bin_apply_runs<1, kBinWords, 1024, 9>), dim3(sgrid), dim3(1024), 0, s, a, b, wd);
+            else
+                hipLaunchKernelGGL((k_bin_apply_runs<1, kBinWords, 1024, 10>), dim3(sgrid), dim3(1024), 0, s, a, b, wd);
         } else if (b.bin_words > kBinWords / 2) {
             GOSSIP_DISPATCH_W(wp_of(W_), hipLaunchKernelGGL((k_bin_apply_runs<W, kBinWords, 1024>),
                                                            dim3(sgrid), dim3(1024), 0, s, a, b, wd));

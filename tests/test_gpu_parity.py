@@ -353,6 +353,8 @@ _VARIANTS = {"defer_1": ({"defer_permille": 1}, {"blocked": "off"}), "stream": (
              "whole_bins_pipe_6": ({"bin_words": 18432, "apply_pipe": 6}, {}),
              "whole_bins_pipe_7": ({"bin_words": 18432, "apply_pipe": 7}, {}),
              "whole_bins_pipe_8": ({"bin_words": 18432, "apply_pipe": 8}, {}),
+             "whole_bins_pipe_9": ({"bin_words": 18432, "apply_pipe": 9}, {}),
+             "whole_bins_pipe_10": ({"bin_words": 18432, "apply_pipe": 10}, {}),
              "half_bins": ({"bin_words": 9216}, {}),
              "zero_fill": ({"zero_fill": 1}, {}),
              "scatter_small": ({"scatter_small": 1}, {}),
